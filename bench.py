@@ -1,0 +1,229 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json metric: 256x256 images/sec for T=1000 DDPM sampling (+ ms/UNet-step).
+
+One "step" = one reverse-diffusion step over the per-GPU batch: a full UNet forward on the HIP
+engine + the fused scheduler update (reference sample_ddpm.py:37-44).  The timed region runs
+EXACTLY --steps consecutive steps of the T=1000 schedule starting at t=999 (default 1000 = one
+complete sample, x_T -> x_0, including the final all-gather of x_0 when N>1); images/s =
+(images in flight) * (steps / T) / elapsed, so a full run is the literal job throughput.
+
+Workload (BASELINE config 2 at N=1, config 5 at N=8): S=256, 16 images per GPU (weak scaling),
+fp32, the default config.yaml UNet (110.08 M params) with keyed synthetic weights, Philox device
+noise keyed by (seed, global sample, step).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run (RCCL).
+Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
+  roofline      per-launch HIP events around every implicit-GEMM conv of one UNet forward; the
+                dominant kernel is conv_igemm_kernel<128,128> (fp32 MFMA) — achieved = its
+                algorithmic FLOPs per launch / its mean launch duration, against the 157.3 TF
+                fp32 MFMA peak (MI355X_MICROARCH.md).
+  cpu_baseline  the oracle's PyTorch-CPU restatement of the reference UNet step (N=1 only), on a
+                bounded sample (a few 256-px UNet steps), extrapolated x T.
+"""
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+GFLOP_PER_IMAGE_STEP_256 = 590.61  # SURVEY.md §8(d) algorithmic FLOPs (probe hook count)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=1000)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=16, help='images per GPU')
+    ap.add_argument('--size', type=int, default=256)
+    ap.add_argument('--timesteps', type=int, default=1000)
+    ap.add_argument('--seed', type=int, default=3455)
+    ap.add_argument('--graph', type=int, default=1, help='replay the UNet forward from a HIP graph')
+    ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-batch', type=int, default=2)
+    ap.add_argument('--cpu-steps', type=int, default=2)
+    return ap.parse_args()
+
+
+def roofline_leg(model, x, t_dev):
+    from weatherconverter_amd import kernels
+    torch.cuda.synchronize()
+    prof = kernels.profile_conv(True)
+    with torch.no_grad():
+        model(x, t_dev)
+    torch.cuda.synchronize()
+    kernels.profile_conv(False)
+    per = {}
+    for tile, flops, e0, e1 in prof:
+        d = per.setdefault(tile, [0, 0.0, 0.0])
+        d[0] += 1
+        d[1] += flops
+        d[2] += e0.elapsed_time(e1) * 1e-3
+    n, fl, sec = per['128x128']
+    mean_dur = sec / n
+    achieved = (fl / n) / mean_dur / 1e12
+    total_conv = sum(v[2] for v in per.values())
+    return {
+        'kernel': 'conv_igemm_kernel<128,128> (fp32 MFMA implicit-GEMM conv)',
+        'bound': 'mfma',
+        'achieved': round(achieved, 2),
+        'peak': FP32_PEAK_TFLOPS,
+        'unit': 'TFLOP/s',
+        'frac': round(achieved / FP32_PEAK_TFLOPS, 4),
+        'traffic': None,
+        'launches_per_step': n,
+        'mean_launch_ms': round(mean_dur * 1e3, 4),
+        'gflop_per_launch': round(fl / n / 1e9, 3),
+        'conv_share_of_event_time': round(sec / max(total_conv, 1e-12), 3),
+    }
+
+
+def cpu_baseline_leg(args):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle.unet_oracle import unet_forward, unet_state_dict_keys
+    from weatherconverter_amd.diffusion_model.config import model_config
+    from weatherconverter_amd.synthetic import synth_tensor
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    mc = model_config(args.size)
+    sd = {k: synth_tensor(k, s) for k, s in unet_state_dict_keys(mc).items()}
+    x = torch.randn((args.cpu_batch, 3, args.size, args.size), generator=torch.Generator().manual_seed(1))
+    t = torch.tensor([500])
+    with torch.no_grad():
+        unet_forward(sd, mc, x, t)  # warm
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            unet_forward(sd, mc, x, t)
+        dt = (time.perf_counter() - t0) / args.cpu_steps
+    return {
+        'value': round(args.cpu_batch / (dt * args.timesteps), 7),
+        'unit': 'images/s',
+        'cores': threads,
+        'kind': 'port',
+        'ms_per_step': round(dt * 1e3, 1),
+        'sample': f'oracle PyTorch-CPU UNet step (reference unet_base.Unet restated), {args.size}px, '
+                  f'B={args.cpu_batch}, {args.cpu_steps} timed steps after 1 warmup, extrapolated x{args.timesteps}'
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from weatherconverter_amd import kernels
+    from weatherconverter_amd.diffusion_model.config import model_config
+    from weatherconverter_amd.diffusion_model.models.unet_base import Unet
+    from weatherconverter_amd.diffusion_model.sample_ddpm import _GraphStep
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    from weatherconverter_amd.synthetic import init_synthetic_
+
+    mc = model_config(args.size)
+    model = Unet(mc)
+    init_synthetic_(model, seed=0)
+    model = model.to(dev).eval()
+    sched = LinearNoiseScheduler(args.timesteps, 0.0001, 0.02, device=dev)
+    B = args.batch
+    T = args.timesteps
+    K = min(args.steps, T)
+    sample0 = rank * B
+    shape = (B, mc.im_channels, mc.im_size, mc.im_size)
+    ts = torch.arange(T, device=dev, dtype=torch.long)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    with torch.no_grad():
+        x = kernels.philox_normal(shape, dev, args.seed, sample0=sample0, step=T)
+        runner = _GraphStep(model, x) if args.graph else None
+        fwd = runner if runner is not None else (lambda xx, tt: model(xx, tt))
+        nxt = torch.empty_like(x)
+        # untimed warmup: W steps from a scratch copy
+        xw = x.clone()
+        for j in range(args.warmup):
+            i = T - 1 - (j % T)
+            eps = fwd(xw, ts[i:i + 1])
+            sched.step(xw, eps, i, out=nxt, noise='philox', seed=args.seed, sample0=sample0)
+            xw, nxt = nxt, xw
+        del xw
+        gathered = None
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(T - 1, T - 1 - K, -1):
+            eps = fwd(x, ts[i:i + 1])
+            if i == 0:
+                sched.step(x, eps, 0, out=nxt)
+            else:
+                sched.step(x, eps, i, out=nxt, noise='philox', seed=args.seed, sample0=sample0)
+            x, nxt = nxt, x
+        if world > 1:
+            gathered = torch.empty((B * world, ) + shape[1:], device=dev)
+            dist.all_gather_into_tensor(gathered, x)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        finite = bool(torch.isfinite(x).all())
+
+        result = None
+        if rank == 0:
+            images = B * world * K / T
+            ms_step = elapsed / K * 1e3
+            unet_tflops = GFLOP_PER_IMAGE_STEP_256 * B / (ms_step * 1e-3) / 1e3 if args.size == 256 else None
+            result = {
+                'metric': '256x256 images/sec (T=1000 DDPM sample)',
+                'value': round(images / elapsed, 5),
+                'unit': 'images/s',
+                'n_gpus': world,
+                'steps': K,
+                'warmup': args.warmup,
+                'ms_per_step': round(ms_step, 3),
+                'higher_is_better': True,
+                'scaling': 'weak',
+                'vs_baseline': None,
+                'dtype': 'f32',
+                'data': 'synthetic (keyed random-init weights, Philox N(0,1) x_T and per-step noise)',
+                'config': {
+                    'workload': f'DDPM reverse sampling, UNet config.yaml @ {args.size}px, {B} images/GPU, '
+                                f'T={T}, {K} timed steps from t={T - 1}' + (' (complete sample)' if K == T else ''),
+                    'global_batch': B * world,
+                    'image_size': args.size,
+                    'timesteps': T,
+                    'parallelism': f'batch-sharded x{world}, 1 RCCL all-gather of x0' if world > 1 else 'single GPU',
+                    'hip_graph': bool(args.graph),
+                    'x_finite': finite,
+                },
+                'ms_per_unet_step': round(ms_step, 3),
+                'unet_step_tflops_algorithmic': round(unet_tflops, 2) if unet_tflops else None,
+            }
+            if not args.no_roofline:
+                result['roofline'] = roofline_leg(model, x, ts[500:501])
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            result['cpu_baseline'] = cpu_baseline_leg(args)
+        else:
+            result['cpu_baseline'] = None
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,171 @@
+/*
+ * wc_kernels.h — C ABI of the WeatherConverter MI355X (gfx950) hot-path kernels.
+ *
+ * The reference (xXCoffeeColaXc/WeatherConverter, 100 % Python) has no FFI of its own: its hot
+ * path is PyTorch eager ops called from the Python API listed in SURVEY.md §8(b).  Each entry
+ * point below replaces a group of those eager ops; the reference call site it stands in for is
+ * cited per function.  The Python drop-in layer (weatherconverter_amd/) binds these through ctypes
+ * (see INTEGRATION.md).
+ *
+ * Conventions
+ *  - All tensors are caller-owned device memory (torch storage).  Nothing here allocates or frees.
+ *  - Activations are NHWC fp32 "views": (ptr, C, ldc) where ldc >= C is the per-pixel stride in
+ *    floats, so channel slices of a wider buffer (the UNet skip concat) are addressed in place.
+ *  - Every function is asynchronous on the given hipStream_t (passed as void*) and never syncs.
+ *  - Return 0 on success, a positive hipError_t on a launch error, or a negative WC_E_* code when
+ *    a shape is outside what the kernel supports (the Python layer raises RuntimeError; there is
+ *    no silent fallback).
+ */
+#ifndef WC_KERNELS_H
+#define WC_KERNELS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WC_OK 0
+#define WC_E_SHAPE (-1)   /* unsupported shape / alignment */
+#define WC_E_ARG (-2)     /* null pointer or bad enum */
+
+/* ------------------------------------------------------------------------------------------ */
+/* Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32).                            */
+/* ------------------------------------------------------------------------------------------ */
+
+#define WC_MAX_TAPS 16
+
+/* One K-segment of the implicit GEMM: a source view read through `ntaps` spatial taps.  The K
+ * index of the packed weight is (kbase + tap * C + c). */
+typedef struct wc_conv_seg {
+    const float* src;   /* NHWC view base (already offset to its first channel) */
+    int C;              /* channels read from this view (multiple of 32) */
+    int ldc;            /* pixel stride of the view, floats */
+    int H, W;           /* spatial extent of the source */
+    int sy, sx;         /* stride of the input sampling grid */
+    int ntaps;          /* 1..WC_MAX_TAPS */
+    int dy[WC_MAX_TAPS];
+    int dx[WC_MAX_TAPS];
+    /* Optional fused GroupNorm-apply prologue: v = v*scale[b*C+c] + shift[b*C+c]; NULL = none. */
+    const float* scale;
+    const float* shift;
+    int silu;           /* apply SiLU after the affine (only meaningful with scale/shift) */
+    int kbase;          /* first K column of this segment in the packed weight */
+} wc_conv_seg;
+
+typedef struct wc_conv_args {
+    wc_conv_seg seg[2];
+    int nseg;
+    /* GEMM grid: M = B*Hm*Wm output positions, N output channels. */
+    int B, Hm, Wm;
+    int N;
+    const float* w;     /* packed weight [N][ldw] with K contiguous */
+    int ldw;
+    const float* bias;  /* [N] or NULL */
+    const float* temb;  /* per-(batch, n) add, temb[b*temb_ld + n]; temb_ld = 0 broadcasts */
+    int temb_ld;
+    const float* res;   /* residual view added in the epilogue (same spatial map as out) or NULL */
+    int ldres;
+    float* out;         /* output view */
+    int ldo;
+    int Ho, Wo;         /* output spatial extent */
+    int osy, osx, ooy, oox; /* output position = (my*osy + ooy, mx*osx + oox) */
+    int out_nchw;       /* 1: write out[(b*N + n)*Ho*Wo + oy*Wo + ox] (ldo ignored) */
+} wc_conv_args;
+
+/* Replaces: nn.Conv2d 3x3/1x1/4x4-s2 and nn.ConvTranspose2d (per output parity), the GN+SiLU
+ * prologue of nn.Sequential(GroupNorm, SiLU, Conv2d), the temb broadcast add, the 1x1
+ * residual_input_conv and the residual add — unet_base.py:87-109,123-129,146-150,333-334,348
+ * and the attention in/out projections of nn.MultiheadAttention (unet_base.py:115,159). */
+int wc_conv_igemm(const wc_conv_args* args, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Number of per-batch pixel splits used by wc_gn_stats for a given shape (partials sizing). */
+int wc_gn_num_splits(int B, int HW, int C);
+/* partials: float[B][splits][groups][2] (mean, M2 of the split), count derivable from shape. */
+int wc_gn_stats(const float* x, int B, int HW, int C, int ldc, int groups, float* partials,
+                void* stream);
+/* Combine partials → per-(b, c) affine: scale = rstd*gamma, shift = beta - mean*rstd*gamma. */
+int wc_gn_finalize(const float* partials, int B, int HW, int C, int groups, const float* gamma,
+                   const float* beta, float eps, float* scale, float* shift, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Flash attention, fp32 MFMA (replaces nn.MultiheadAttention's softmax(QK^T/sqrt(d))V,        */
+/* unet_base.py:115,159,214,257,320,365).                                                      */
+/* ------------------------------------------------------------------------------------------ */
+
+/* qkv: [B*N][ld_qkv] rows holding q | k | v (C each, head h at columns h*d); out: [B*N][ld_out]. */
+int wc_attention_fwd(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
+                     int heads, float scale, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Time embedding: sinusoid + t_proj MLP + every ResBlock's SiLU→Linear projection in one launch */
+/* (replaces get_time_embedding unet_base.py:7-30, t_proj :395-397,462, t_emb_layers :98-100). */
+/* ------------------------------------------------------------------------------------------ */
+
+/* t: int64[nt]; w1,b1,w2,b2: t_proj Linear weights [D][D]/[D]; proj_w: concatenated rows
+ * [P][D], proj_b: [P]; out: [nt][P].  D = temb_dim (even, <= 256). */
+int wc_temb(const int64_t* t, int nt, int D, const float* w1, const float* b1, const float* w2,
+            const float* b2, const float* proj_w, const float* proj_b, int P, float* out,
+            void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Stem / head                                                                                 */
+/* ------------------------------------------------------------------------------------------ */
+
+/* conv_in: NCHW input (B, Cin<=4, H, W) → NHWC view, 3x3 pad 1 (unet_base.py:400,456). */
+int wc_conv_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* b,
+               int Cout, float* out, int ldo, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Scheduler (linear_noise_scheduler.py)                                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Noise source for the reverse step. */
+#define WC_NOISE_NONE 0     /* t == 0: x' = mean */
+#define WC_NOISE_TENSOR 1   /* z given as a device tensor (torch-CPU-compatible mode) */
+#define WC_NOISE_PHILOX 2   /* z generated in-kernel: Philox4x32-10(seed, sample, step) */
+
+/* x_out = (x - coef_eps*eps ... ) exactly as sample_prev_timestep (:96-116) /
+ * sample_prev_timestep2 (:63-77):  mean = (x - (beta*eps)/s1m) / sqrt_alpha;  x' = mean + sigma*z.
+ * sz_out == NULL: x_out = x' (fused sampling step).  sz_out != NULL: x_out = mean and
+ * sz_out = sigma*z, the (mean, sigma) pair the reference method returns.
+ * The per-step scalars are computed on the host in fp32 exactly as the reference computes them.
+ * Elements are NCHW (B, C, H, W) contiguous; Philox noise is keyed by the GLOBAL sample index
+ * (sample0 + b) so results do not depend on how samples are sharded over ranks. */
+int wc_ddpm_step(const float* x, const float* eps, const float* z, float* x_out, float* sz_out,
+                 int64_t B,
+                 int64_t per_sample, float beta, float s1m, float sqrt_alpha, float sigma,
+                 int noise_mode, uint64_t seed, int64_t sample0, int64_t step, void* stream);
+
+/* add_noise / add_noise2 (:30-61): out = a[t_b]*x0 + b[t_b]*noise with per-sample coefficients
+ * (coef_a/coef_b: float[B], already gathered for each sample's t on the device). */
+int wc_add_noise(const float* x0, const float* noise, const float* coef_a, const float* coef_b,
+                 float* out, int64_t B, int64_t per_sample, void* stream);
+
+/* Standard normal fill, Philox4x32-10 keyed by (seed, sample0 + b, step); out is (B, per_sample). */
+int wc_philox_normal(float* out, int64_t B, int64_t per_sample, uint64_t seed, int64_t sample0,
+                     int64_t step, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Semantic-gradient guidance update (sgg/sgg.py:16-22, seg_model/inference.py:39-43)          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* grad: (nb, 3, 4S, 4S) input-gradient of the segmenter loss; mu, sigma: (nb, 3, S, S).
+ * m[y][x] = sqrt(sum_c (avgpool4(grad)_c * std_c)^2); mu_hat = mu + lambda*sigma*m;
+ * xt = mu_hat + sigma.  `sum_batch` = 1 reproduces the reference's batch-1 squeeze semantics
+ * for nb > 1 (D4: the magnitude sums over the batch axis too).  mag_out (optional) receives m. */
+int wc_sgg_update(const float* grad, const float* mu, const float* sigma, float* xt_out,
+                  float* mag_out, int nb, int S, float lambda_, double std0, double std1,
+                  double std2, int sum_batch, void* stream);
+
+/* Library identification (for the CPU load test). */
+const char* wc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WC_KERNELS_H */

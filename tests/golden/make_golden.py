@@ -1,0 +1,154 @@
+"""Generate golden vectors by importing the REFERENCE (xXCoffeeColaXc/WeatherConverter) on CPU.
+
+Run in the build container only (the reference does not exist on the GPU box):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--reference /root/reference]
+
+Outputs (committed; inputs are regenerated from seeds, weights from the keyed recipe in
+weatherconverter_amd/synthetic.py, so only outputs + digests are stored):
+  manifest.json         state_dict key->shape for the 64/128/256 default configs and the tiny config
+  sched.npz             scheduler tables (T=50, T=1000), reverse-step / add_noise vectors
+  temb.npz              get_time_embedding for several t
+  unet_tiny.npz         tiny-config Unet forward, B=2, shared t and per-sample t
+  unet_64.npz           64-px default-config Unet forward, B=2 (config 1 model)
+  unet_256.npz          256-px default-config Unet forward, B=1 (BASELINE architecture)
+  traj_64_T50.npz       config 1: 64 px, B=2, T=50 reverse trajectory (sample_ddpm.py:35-44 loop)
+The reference modules imported: diffusion_model.models.unet_base, diffusion_model.scheduler.
+linear_noise_scheduler, diffusion_model.config.models.  ``Tensor.cuda`` is shimmed to a no-op
+(unet_base.py:461 hard-codes .cuda()); nothing in the reference is modified.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from weatherconverter_amd.synthetic import synthetic_images, synthetic_state_dict, state_dict_digest  # noqa: E402
+
+TINY = dict(name='ddpm', im_channels=3, im_size=32, down_channels=[32, 64, 64, 128], mid_channels=[128, 128, 64],
+            down_sample=[True, True, False], time_emb_dim=128, num_down_layers=2, num_mid_layers=1,
+            num_up_layers=2, num_heads=4, attn_resolutions=[16, 8])
+
+
+def default_model(ref_models, im_size):
+    import yaml
+    with open(os.path.join(ROOT, 'weatherconverter_amd/diffusion_model/config/config.yaml')) as fh:
+        m = yaml.safe_load(fh)['model']
+    m['im_size'] = im_size
+    return ref_models.ModelConfig(**m)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--reference', default='/root/reference')
+    ap.add_argument('--skip-traj', action='store_true')
+    args = ap.parse_args()
+    sys.path.insert(0, args.reference)
+    torch.Tensor.cuda = lambda self, *a, **k: self  # harness shim for unet_base.py:461
+    torch.set_num_threads(8)
+    from diffusion_model.config import models as ref_models
+    from diffusion_model.models.unet_base import Unet, get_time_embedding
+    from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+
+    out = {}
+    # ------------------------------------------------------------- manifest
+    manifest = {}
+    cfgs = {'tiny': ref_models.ModelConfig(**TINY)}
+    for s in (64, 128, 256):
+        cfgs[f'default_{s}'] = default_model(ref_models, s)
+    for name, mc in cfgs.items():
+        net = Unet(mc)
+        manifest[name] = {'config': mc.model_dump(), 'keys': [[k, list(v.shape)] for k, v in net.state_dict().items()]}
+    with open(os.path.join(HERE, 'manifest.json'), 'w') as fh:
+        json.dump(manifest, fh)
+    print('manifest:', {k: len(v['keys']) for k, v in manifest.items()})
+
+    # ------------------------------------------------------------- scheduler
+    sched = {}
+    for T in (50, 1000):
+        s = LinearNoiseScheduler(T, 0.0001, 0.02)
+        for n in ('betas', 'alphas', 'alpha_cum_prod', 'sqrt_alpha_cum_prod', 'one_minus_cum_prod',
+                  'sqrt_one_minus_alpha_cum_prod'):
+            sched[f'T{T}_{n}'] = getattr(s, n).numpy()
+    s = LinearNoiseScheduler(1000, 0.0001, 0.02)
+    g = torch.Generator().manual_seed(11)
+    xt = torch.randn((2, 3, 16, 16), generator=g) * 3
+    eps = torch.randn((2, 3, 16, 16), generator=g)
+    sched['step_xt'] = xt.numpy()
+    sched['step_eps'] = eps.numpy()
+    for t in (0, 1, 37, 500, 999):
+        torch.manual_seed(1000 + t)
+        mean, sz, _ = s.sample_prev_timestep(xt, eps, torch.as_tensor(t))
+        sched[f'step{t}_mean'] = mean.numpy()
+        if sz is not None:
+            sched[f'step{t}_sigz'] = sz.numpy()
+            torch.manual_seed(1000 + t)
+            sched[f'step{t}_z'] = torch.randn(xt.shape).numpy()
+    tb = torch.tensor([3, 3])
+    torch.manual_seed(77)
+    mean2, sz2, _ = s.sample_prev_timestep2(xt, eps, tb)
+    sched['step2_t'] = tb.numpy()
+    sched['step2_mean'] = mean2.numpy()
+    sched['step2_sigz'] = sz2.numpy()
+    torch.manual_seed(77)
+    sched['step2_z'] = torch.randn(xt.shape).numpy()
+    tn = torch.tensor([5, 880])
+    sched['addnoise_t'] = tn.numpy()
+    sched['addnoise_out'] = s.add_noise(xt, eps, tn).numpy()
+    sched['addnoise2_out'] = s.add_noise2(xt, eps, tn).numpy()
+    np.savez(os.path.join(HERE, 'sched.npz'), **sched)
+
+    # ------------------------------------------------------------- time embedding
+    ts = torch.tensor([0, 1, 17, 500, 999])
+    np.savez(os.path.join(HERE, 'temb.npz'), t=ts.numpy(), emb=get_time_embedding(ts, 128).numpy())
+
+    # ------------------------------------------------------------- UNet forwards
+    def run_forward(mc, B, t, xseed, wseed=0):
+        net = Unet(mc)
+        sd = synthetic_state_dict(net.state_dict(), seed=wseed)
+        net.load_state_dict(sd)
+        net.eval()
+        x = synthetic_images((B, mc.im_channels, mc.im_size, mc.im_size), seed=xseed)
+        with torch.no_grad():
+            y = net(x, torch.as_tensor(t))
+        return net, y, state_dict_digest(sd)
+
+    net, y1, dg = run_forward(cfgs['tiny'], 2, [7], 101)
+    _, y2, _ = run_forward(cfgs['tiny'], 2, [3, 900], 102)
+    np.savez(os.path.join(HERE, 'unet_tiny.npz'), y_shared_t=y1.numpy(), y_batch_t=y2.numpy(), digest=dg)
+    print('tiny done', float(y1.abs().max()))
+    _, y64, dg64 = run_forward(cfgs['default_64'], 2, [37], 201)
+    np.savez(os.path.join(HERE, 'unet_64.npz'), y=y64.numpy(), digest=dg64)
+    print('64 done', float(y64.abs().max()))
+    _, y256, dg256 = run_forward(cfgs['default_256'], 1, [611], 301)
+    np.savez(os.path.join(HERE, 'unet_256.npz'), y=y256.numpy(), digest=dg256)
+    print('256 done', float(y256.abs().max()))
+
+    # ------------------------------------------------------------- config-1 trajectory
+    if not args.skip_traj:
+        mc = cfgs['default_64']
+        net = Unet(mc)
+        net.load_state_dict(synthetic_state_dict(net.state_dict(), seed=0))
+        net.eval()
+        s50 = LinearNoiseScheduler(50, 0.0001, 0.02)
+        torch.manual_seed(3455)
+        xt = torch.randn((2, 3, 64, 64))  # sample_ddpm.py:35-36
+        eps_first = None
+        with torch.no_grad():
+            for i in reversed(range(50)):  # sample_ddpm.py:37-44
+                noise_pred = net(xt, torch.as_tensor(i).unsqueeze(0))
+                if eps_first is None:
+                    eps_first = noise_pred.clone()
+                mean, sigma, _ = s50.sample_prev_timestep(xt, noise_pred, torch.as_tensor(i))
+                xt = mean + sigma if i != 0 else mean
+        np.savez(os.path.join(HERE, 'traj_64_T50.npz'), x0=xt.numpy(), eps_first=eps_first.numpy(), seed=3455)
+        print('traj done', float(xt.abs().max()))
+
+
+if __name__ == '__main__':
+    main()

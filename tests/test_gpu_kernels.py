@@ -1,0 +1,293 @@
+"""GPU: every HIP kernel against a PyTorch fp32 CPU reference of the same op (or the golden vectors).
+
+Stated tolerance for fp32 kernels: relative L2 <= 1e-5; the scheduler and forward
+noising kernels must be bit-exact with the reference's torch ops.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN, rel_l2
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope='module')
+def K():
+    from weatherconverter_amd import kernels
+    kernels._native.load()
+    return kernels
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def _gn_affine_ref(x, gamma, beta, G=8, eps=1e-5):
+    B, C = x.shape[:2]
+    xg = x.double().reshape(B, G, -1)
+    mean = xg.mean(-1)
+    var = xg.var(-1, unbiased=False)
+    rstd = 1.0 / torch.sqrt(var + eps)
+    rstd_c = rstd.repeat_interleave(C // G, dim=1)
+    mean_c = mean.repeat_interleave(C // G, dim=1)
+    scale = rstd_c * gamma.double()
+    shift = beta.double() - mean_c * scale
+    return scale.float(), shift.float()
+
+
+@pytest.mark.parametrize('B,H,W,C,offset', [(2, 12, 12, 64, 3.0), (3, 33, 17, 96, 0.0), (1, 64, 64, 256, 50.0)])
+def test_gn_affine(K, B, H, W, C, offset):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn((B, C, H, W), generator=g) * 2 + offset
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    sc, sh = K.gn_affine(K.View.full(_nhwc(x).cuda()), gamma.cuda(), beta.cuda())
+    y = x * sc.cpu()[:, :, None, None] + sh.cpu()[:, :, None, None]
+    ref = F.group_norm(x, 8, gamma, beta, 1e-5)
+    assert rel_l2(y, ref) < TOL
+
+
+def test_gn_affine_strided_view(K):
+    """GN of a channel slice [C, 2C) of a wider NHWC buffer (the skip-concat layout)."""
+    g = torch.Generator().manual_seed(2)
+    buf = torch.randn((2, 16, 16, 128), generator=g)
+    gamma, beta = torch.ones(64), torch.zeros(64)
+    sc, sh = K.gn_affine(K.View(buf.cuda(), 64, 64), gamma.cuda(), beta.cuda())
+    x = _nchw(buf[..., 64:])
+    y = x * sc.cpu()[:, :, None, None] + sh.cpu()[:, :, None, None]
+    assert rel_l2(y, F.group_norm(x, 8, gamma, beta, 1e-5)) < TOL
+
+
+def _pack(w):
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+TAPS3 = [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]
+
+
+@pytest.mark.parametrize('B,H,W,Ci,Co', [(2, 12, 12, 64, 96), (1, 16, 16, 32, 64), (2, 9, 20, 128, 128),
+                                         (1, 32, 32, 64, 256), (2, 8, 8, 96, 3)])
+def test_conv3x3_gn_silu_temb_residual(K, B, H, W, Ci, Co):
+    """ResBlock conv2 shape: SiLU(GN-affine(h)) * W3x3 + b + temb + conv1x1(x) (2 K-segments)."""
+    g = torch.Generator().manual_seed(3)
+    h = torch.randn((B, Ci, H, W), generator=g)
+    x2 = torch.randn((B, 32, H, W), generator=g)
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    wr = torch.randn((Co, 32, 1, 1), generator=g) / 32**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    temb = torch.randn((B, Co), generator=g)
+    sc = 1 + 0.2 * torch.randn((B, Ci), generator=g)
+    sh = 0.2 * torch.randn((B, Ci), generator=g)
+    a = F.silu(h * sc[:, :, None, None] + sh[:, :, None, None])
+    ref = F.conv2d(a, w, b, padding=1) + temb[:, :, None, None] + F.conv2d(x2, wr)
+    wp = torch.cat([_pack(w), wr.reshape(Co, 32)], 1).contiguous().cuda()
+    out = torch.empty((B, H, W, Co)).cuda()
+    K.conv_igemm([K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=True),
+                  K.Seg(K.View.full(_nhwc(x2).cuda()), [(0, 0)], kbase=9 * Ci)], wp, b.cuda(), K.View.full(out),
+                 Hm=H, Wm=W, temb=temb.cuda(), temb_ld=Co)
+    assert rel_l2(_nchw(out.cpu()), ref) < TOL
+
+
+def test_conv3x3_nchw_head(K):
+    """conv_out: GN+SiLU prologue, 64->3, NCHW store."""
+    g = torch.Generator().manual_seed(4)
+    B, H, W, Ci = 2, 40, 40, 64
+    h = torch.randn((B, Ci, H, W), generator=g)
+    w = torch.randn((3, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    b = torch.randn(3, generator=g)
+    sc = torch.rand((B, Ci), generator=g) + 0.5
+    sh = torch.randn((B, Ci), generator=g) * 0.1
+    ref = F.conv2d(F.silu(h * sc[:, :, None, None] + sh[:, :, None, None]), w, b, padding=1)
+    out = torch.empty((B, 3, H, W)).cuda()
+    K.conv_igemm([K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=True)],
+                 _pack(w).cuda(), b.cuda(), None, Hm=H, Wm=W, out_nchw=out)
+    assert rel_l2(out.cpu(), ref) < TOL
+
+
+def test_down_conv_4x4_s2(K):
+    g = torch.Generator().manual_seed(5)
+    B, H, W, C = 2, 24, 24, 64
+    x = torch.randn((B, C, H, W), generator=g)
+    w = torch.randn((C, C, 4, 4), generator=g) / (C * 16)**0.5
+    b = torch.randn(C, generator=g) * 0.1
+    ref = F.conv2d(x, w, b, stride=2, padding=1)
+    out = torch.empty((B, H // 2, W // 2, C)).cuda()
+    taps = [(ky - 1, kx - 1) for ky in range(4) for kx in range(4)]
+    K.conv_igemm([K.Seg(K.View.full(_nhwc(x).cuda()), taps, stride=2)], _pack(w).cuda(), b.cuda(), K.View.full(out),
+                 Hm=H // 2, Wm=W // 2)
+    assert rel_l2(_nchw(out.cpu()), ref) < TOL
+
+
+def test_conv_transpose_4x4_s2_into_concat_slice(K):
+    from weatherconverter_amd.diffusion_model.models.engine import pack_convT
+    g = torch.Generator().manual_seed(6)
+    B, H, W, C = 2, 8, 10, 64
+    x = torch.randn((B, C, H, W), generator=g)
+    wt = torch.randn((C, C, 4, 4), generator=g) / (C * 4)**0.5
+    b = torch.randn(C, generator=g) * 0.1
+    ref = F.conv_transpose2d(x, wt, b, stride=2, padding=1)
+    buf = torch.zeros((B, 2 * H, 2 * W, 2 * C)).cuda()
+    dst = K.View(buf, 0, C)
+    xin = K.View.full(_nhwc(x).cuda())
+    for py in (0, 1):
+        for px in (0, 1):
+            taps, wp = pack_convT(wt, py, px)
+            K.conv_igemm([K.Seg(xin, taps)], wp.cuda(), b.cuda(), dst, Hm=H, Wm=W, out_map=(2, 2, py, px))
+    got = _nchw(buf[..., :C].cpu())
+    assert rel_l2(got, ref) < TOL
+    assert torch.count_nonzero(buf[..., C:]) == 0  # the skip half is untouched
+
+
+def test_linear_gn_prologue_residual_epilogue(K):
+    """in_proj with GN-apply prologue and out_proj with in-place residual epilogue."""
+    g = torch.Generator().manual_seed(7)
+    B, H, W, C = 2, 8, 8, 128
+    y = torch.randn((B, H, W, C), generator=g)
+    o = torch.randn((B, H, W, C), generator=g)
+    w = torch.randn((C, C), generator=g) / C**0.5
+    b = torch.randn(C, generator=g)
+    yc = y.cuda()
+    K.conv_igemm([K.Seg(K.View.full(o.cuda()), [(0, 0)])], w.cuda(), b.cuda(), K.View.full(yc), Hm=H, Wm=W,
+                 res=K.View.full(yc))
+    ref = y + F.linear(o, w, b)
+    assert rel_l2(yc.cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize('B,N,C', [(2, 64, 64), (2, 100, 128), (1, 256, 256), (2, 1024, 512), (1, 1024, 768),
+                                   (1, 4096, 128), (1, 300, 768)])
+def test_attention(K, B, N, C):
+    from oracle.unet_oracle import mha
+    g = torch.Generator().manual_seed(8)
+    qkv = torch.randn((B, N, 3 * C), generator=g)
+    heads = 4
+    d = C // heads
+    q, k, v = qkv.split(C, -1)
+    q = q.reshape(B, N, heads, d).transpose(1, 2)
+    k = k.reshape(B, N, heads, d).transpose(1, 2)
+    v = v.reshape(B, N, heads, d).transpose(1, 2)
+    ref = (torch.softmax((q * d**-0.5) @ k.transpose(-1, -2), -1) @ v).transpose(1, 2).reshape(B, N, C)
+    out = torch.empty((B * N, C)).cuda()
+    K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads)
+    assert rel_l2(out.cpu().reshape(B, N, C), ref) < TOL
+    del mha
+
+
+def test_attention_spiky_scores(K):
+    """A dominant key forces the running max to jump mid-sequence (online-softmax rescale path)."""
+    g = torch.Generator().manual_seed(9)
+    B, N, C, heads = 1, 512, 256, 4
+    d = C // heads
+    qkv = torch.randn((B, N, 3 * C), generator=g)
+    qkv[0, 400, C:2 * C] *= 25.0  # key 400 large in every head
+    q, k, v = qkv.split(C, -1)
+    q = q.reshape(B, N, heads, d).transpose(1, 2)
+    k = k.reshape(B, N, heads, d).transpose(1, 2)
+    v = v.reshape(B, N, heads, d).transpose(1, 2)
+    ref = (torch.softmax((q.double() * d**-0.5) @ k.double().transpose(-1, -2), -1) @ v.double())
+    ref = ref.transpose(1, 2).reshape(B, N, C)
+    out = torch.empty((B * N, C)).cuda()
+    K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads)
+    assert rel_l2(out.cpu().reshape(B, N, C), ref) < TOL
+
+
+def test_time_embedding_and_projections(K):
+    from oracle.unet_oracle import time_embedding
+    g = torch.Generator().manual_seed(10)
+    D, P = 128, 1000
+    w1, w2 = torch.randn((D, D), generator=g) / D**0.5, torch.randn((D, D), generator=g) / D**0.5
+    b1, b2 = torch.randn(D, generator=g) * 0.1, torch.randn(D, generator=g) * 0.1
+    pw, pb = torch.randn((P, D), generator=g) / D**0.5, torch.randn(P, generator=g) * 0.1
+    t = torch.tensor([0, 1, 17, 500, 999])
+    e = time_embedding(t, D)
+    h = F.linear(F.silu(F.linear(e, w1, b1)), w2, b2)
+    ref = F.linear(F.silu(h), pw, pb)
+    out = K.temb(t.cuda(), w1.cuda(), b1.cuda(), w2.cuda(), b2.cuda(), pw.cuda(), pb.cuda())
+    assert rel_l2(out.cpu(), ref) < TOL
+
+
+def test_conv_in_nchw_to_nhwc(K):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((2, 3, 33, 31), generator=g)
+    w = torch.randn((64, 3, 3, 3), generator=g) / 27**0.5
+    b = torch.randn(64, generator=g) * 0.1
+    buf = torch.zeros((2, 33, 31, 128)).cuda()
+    K.conv_in(x.cuda(), w.cuda(), b.cuda(), K.View(buf, 64, 64))
+    assert rel_l2(_nchw(buf[..., 64:].cpu()), F.conv2d(x, w, b, padding=1)) < TOL
+    assert torch.count_nonzero(buf[..., :64]) == 0
+
+
+def test_ddpm_step_bitwise_vs_reference(K):
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    gd = np.load(os.path.join(GOLDEN, 'sched.npz'))
+    s = LinearNoiseScheduler(1000, 0.0001, 0.02)
+    xt, eps = torch.from_numpy(gd['step_xt']).cuda(), torch.from_numpy(gd['step_eps']).cuda()
+    for t in (0, 1, 37, 500, 999):
+        z = torch.from_numpy(gd[f'step{t}_z']) if t else None
+        mean, sz, none = s.sample_prev_timestep(xt, eps, torch.as_tensor(t), z=z)
+        assert none is None
+        assert np.array_equal(mean.cpu().numpy(), gd[f'step{t}_mean']), t
+        if t:
+            assert np.array_equal(sz.cpu().numpy(), gd[f'step{t}_sigz']), t
+            fused = s.step(xt, eps, t, z=z.cuda())
+            assert np.array_equal(fused.cpu().numpy(), gd[f'step{t}_mean'] + gd[f'step{t}_sigz'])
+        else:
+            assert sz is None
+    mean2, sz2, _ = s.sample_prev_timestep2(xt, eps, torch.from_numpy(gd['step2_t']),
+                                            z=torch.from_numpy(gd['step2_z']))
+    assert np.array_equal(mean2.cpu().numpy(), gd['step2_mean'])
+    assert np.array_equal(sz2.cpu().numpy(), gd['step2_sigz'])
+    tn = torch.from_numpy(gd['addnoise_t'])
+    assert np.array_equal(s.add_noise(xt, eps, tn).cpu().numpy(), gd['addnoise_out'])
+    assert np.array_equal(s.add_noise2(xt, eps, tn).cpu().numpy(), gd['addnoise2_out'])
+
+
+def test_ddpm_step_reference_rng_stream(K):
+    """Default noise = torch.randn on the CPU generator, drawn exactly as the reference (:110)."""
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    gd = np.load(os.path.join(GOLDEN, 'sched.npz'))
+    s = LinearNoiseScheduler(1000, 0.0001, 0.02)
+    xt, eps = torch.from_numpy(gd['step_xt']).cuda(), torch.from_numpy(gd['step_eps']).cuda()
+    torch.manual_seed(1000 + 37)
+    _, sz, _ = s.sample_prev_timestep(xt, eps, 37)
+    assert np.array_equal(sz.cpu().numpy(), gd['step37_sigz'])
+
+
+def test_philox_shard_invariant_and_normal(K):
+    a = K.philox_normal((4, 3, 32, 32), 'cuda', seed=1234, sample0=0, step=7)
+    b = K.philox_normal((2, 3, 32, 32), 'cuda', seed=1234, sample0=2, step=7)
+    assert torch.equal(a[2:], b)
+    c = K.philox_normal((4, 3, 32, 32), 'cuda', seed=1234, sample0=0, step=8)
+    assert not torch.equal(a, c)
+    big = K.philox_normal((64, 3, 64, 64), 'cuda', seed=5, step=1).double()
+    assert abs(float(big.mean())) < 5e-3 and abs(float(big.std()) - 1) < 5e-3
+    assert abs(float((big**3).mean())) < 2e-2 and abs(float((big**4).mean()) - 3) < 3e-2
+
+
+@pytest.mark.parametrize('nb,S,batch_axis', [(1, 32, False), (2, 16, False), (2, 16, True)])
+def test_sgg_update(K, nb, S, batch_axis):
+    g = torch.Generator().manual_seed(12)
+    grad = torch.randn((nb, 3, 4 * S, 4 * S), generator=g) * 1e-3
+    mu = torch.randn((nb, 3, S, S), generator=g)
+    sigma = torch.randn((nb, 3, S, S), generator=g) * 0.1
+    xt, mag = K.sgg_update(grad.cuda(), mu.cuda(), sigma.cuda(), 60.0, batch_axis_sum=batch_axis)
+    p = F.avg_pool2d(grad, 4, 4).double() * torch.tensor([0.229, 0.224, 0.225], dtype=torch.float64)[:, None, None]
+    if batch_axis:  # reference semantics at nb > 1 (squeeze(0) no-op, numpy sum over axis 0 = batch)
+        m_ref = p.pow(2).sum(0).sqrt()[None]  # (1, 3, S, S)
+        assert rel_l2(mag.cpu(), m_ref[0]) < 1e-6
+    else:
+        m_ref = p.pow(2).sum(1, keepdim=True).sqrt()  # (nb, 1, S, S)
+        assert rel_l2(mag.cpu(), m_ref[:, 0]) < 1e-6
+    ref = mu.double() + (60.0 * sigma).double() * m_ref + sigma.double()
+    assert rel_l2(xt.cpu(), ref) < 1e-6
+    if nb == 1:
+        from oracle.scheduler_oracle import gsg_update
+        assert rel_l2(xt.cpu(), gsg_update(grad, mu, sigma, 60.0)) < 1e-6

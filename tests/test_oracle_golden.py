@@ -1,0 +1,114 @@
+"""CPU: pin the oracle (oracle/) against golden vectors captured from the reference import.
+
+Tolerances: the oracle restates the reference op for op with the same torch CPU kernels except
+nn.MultiheadAttention's fused fast path, so forwards agree to ~1e-7 relative; we assert 1e-6.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, rel_l2
+from oracle.scheduler_oracle import OracleScheduler, gsg_update, sample_loop
+from oracle.unet_oracle import time_embedding, unet_forward, unet_state_dict_keys
+from weatherconverter_amd.diffusion_model.config import ModelConfig
+from weatherconverter_amd.synthetic import state_dict_digest, synth_tensor, synthetic_images
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, 'manifest.json')))
+
+
+def _sd(mc, seed=0):
+    return {k: synth_tensor(k, s, seed=seed) for k, s in unet_state_dict_keys(mc).items()}
+
+
+@pytest.mark.parametrize('name', ['tiny', 'default_64', 'default_128', 'default_256'])
+def test_oracle_key_layout_matches_reference(name):
+    m = MANIFEST[name]
+    mc = ModelConfig(**m['config'])
+    ours = unet_state_dict_keys(mc)
+    ref = {k: tuple(s) for k, s in m['keys']}
+    assert ours == ref
+
+
+def test_scheduler_tables():
+    g = np.load(os.path.join(GOLDEN, 'sched.npz'))
+    for T in (50, 1000):
+        s = OracleScheduler(T, 0.0001, 0.02)
+        for n in ('betas', 'alphas', 'alpha_cum_prod', 'sqrt_alpha_cum_prod', 'one_minus_cum_prod',
+                  'sqrt_one_minus_alpha_cum_prod'):
+            assert np.array_equal(getattr(s, n).numpy(), g[f'T{T}_{n}']), (T, n)
+
+
+def test_scheduler_steps_bitwise():
+    g = np.load(os.path.join(GOLDEN, 'sched.npz'))
+    s = OracleScheduler(1000, 0.0001, 0.02)
+    xt, eps = torch.from_numpy(g['step_xt']), torch.from_numpy(g['step_eps'])
+    for t in (0, 1, 37, 500, 999):
+        z = torch.from_numpy(g[f'step{t}_z']) if t else None
+        mean, sz = s.sample_prev_timestep(xt, eps, t, z=z)
+        assert np.array_equal(mean.numpy(), g[f'step{t}_mean'])
+        if t:
+            assert np.array_equal(sz.numpy(), g[f'step{t}_sigz'])
+    mean2, sz2 = s.sample_prev_timestep2(xt, eps, torch.from_numpy(g['step2_t']), z=torch.from_numpy(g['step2_z']))
+    assert np.array_equal(mean2.numpy(), g['step2_mean'])
+    assert np.array_equal(sz2.numpy(), g['step2_sigz'])
+    assert np.array_equal(s.add_noise(xt, eps, torch.from_numpy(g['addnoise_t'])).numpy(), g['addnoise_out'])
+
+
+def test_time_embedding_bitwise():
+    g = np.load(os.path.join(GOLDEN, 'temb.npz'))
+    assert np.array_equal(time_embedding(torch.from_numpy(g['t']), 128).numpy(), g['emb'])
+
+
+def _forward_case(name, fixture, key, B, t, xseed):
+    mc = ModelConfig(**MANIFEST[name]['config'])
+    sd = _sd(mc)
+    g = np.load(os.path.join(GOLDEN, fixture))
+    assert state_dict_digest(sd) == str(g['digest'])
+    x = synthetic_images((B, mc.im_channels, mc.im_size, mc.im_size), seed=xseed)
+    with torch.no_grad():
+        y = unet_forward(sd, mc, x, torch.as_tensor(t))
+    return rel_l2(y, g[key])
+
+
+def test_oracle_unet_tiny():
+    assert _forward_case('tiny', 'unet_tiny.npz', 'y_shared_t', 2, [7], 101) < 1e-6
+    assert _forward_case('tiny', 'unet_tiny.npz', 'y_batch_t', 2, [3, 900], 102) < 1e-6
+
+
+def test_oracle_unet_64():
+    assert _forward_case('default_64', 'unet_64.npz', 'y', 2, [37], 201) < 1e-6
+
+
+def test_oracle_unet_256():
+    assert _forward_case('default_256', 'unet_256.npz', 'y', 1, [611], 301) < 1e-6
+
+
+@pytest.mark.slow
+def test_oracle_trajectory_config1():
+    """Config 1 (64 px, B=2, T=50) trajectory through the restated loop (sample_ddpm.py:35-44)."""
+    mc = ModelConfig(**MANIFEST['default_64']['config'])
+    sd = _sd(mc)
+    g = np.load(os.path.join(GOLDEN, 'traj_64_T50.npz'))
+    s = OracleScheduler(50, 0.0001, 0.02)
+    torch.manual_seed(int(g['seed']))
+    x_T = torch.randn((2, 3, 64, 64))
+    with torch.no_grad():
+        x0 = sample_loop(lambda x, t: unet_forward(sd, mc, x, t), s, x_T)
+    assert rel_l2(x0, g['x0']) < 1e-5
+
+
+def test_gsg_update_math():
+    """apply_gsg update on a synthetic gradient: float64 result, batch-1 semantics (sgg.py:18-22)."""
+    g = torch.Generator().manual_seed(5)
+    grad = torch.randn((1, 3, 32, 32), generator=g) * 1e-3
+    mu = torch.randn((1, 3, 8, 8), generator=g)
+    sigma = torch.randn((1, 3, 8, 8), generator=g) * 0.1
+    xt = gsg_update(grad, mu, sigma, 60.0)
+    assert xt.dtype == torch.float64 and xt.shape == (1, 3, 8, 8)
+    pooled = grad.reshape(1, 3, 8, 4, 8, 4).mean(dim=(3, 5)).double()
+    mag = (pooled[0] * torch.tensor([0.229, 0.224, 0.225], dtype=torch.float64)[:, None, None]).pow(2).sum(0).sqrt()
+    ref = mu.double() + (60.0 * sigma).double() * mag + sigma.double()
+    assert torch.allclose(xt, ref, rtol=1e-6, atol=1e-9)

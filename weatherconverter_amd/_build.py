@@ -1,0 +1,66 @@
+"""Build ``libwc_kernels.so`` in-tree with hipcc for gfx950.
+
+The library is a plain C-ABI shared object (no torch symbols), loaded through ctypes by
+``weatherconverter_amd._native``.  It links the HIP runtime by soname (``libamdhip64.so.7``); at run
+time the copy torch already loaded is reused, so there is exactly one HIP runtime per process.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+LIBDIR = os.path.join(HERE, 'lib')
+LIBNAME = 'libwc_kernels.so'
+LIB_PATH = os.path.join(LIBDIR, LIBNAME)
+ROOT = os.path.dirname(HERE)
+
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = os.environ.get('WC_OFFLOAD_ARCH', 'gfx950')
+
+SOURCES = ['wc_conv.hip', 'wc_gn.hip', 'wc_attention.hip', 'wc_misc.hip']
+HEADERS = ['wc_common.hpp']
+
+CFLAGS = [
+    '-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-munsafe-fp-atomics',
+    '-I', os.path.join(ROOT, 'include'), '-Wno-unused-result'
+]
+
+
+def _stale(obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'wc_kernels.h')]
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        obj = os.path.join(LIBDIR, 'obj', src.replace('.hip', '.o'))
+        objs.append(obj)
+        if force or _stale(obj, [sp] + hdrs):
+            jobs.append([HIPCC] + CFLAGS + ['-c', sp, '-o', obj])
+
+    def run(cmd):
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed:\n{" ".join(cmd)}\n{r.stdout}\n{r.stderr}')
+        return r
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        list(ex.map(run, jobs))
+    if jobs or force or _stale(LIB_PATH, objs):
+        run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', LIB_PATH] + objs)
+    return LIB_PATH
+
+
+if __name__ == '__main__':
+    print(build(verbose='-v' in sys.argv, force='-f' in sys.argv))

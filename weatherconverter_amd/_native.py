@@ -1,0 +1,102 @@
+"""ctypes binding of ``libwc_kernels.so`` (the C ABI declared in ``include/wc_kernels.h``).
+
+There is deliberately no CPU fallback: every product entry point goes through these kernels and a
+missing or failing library raises.  ``torch`` is imported before the library is opened so the HIP
+runtime torch ships (soname ``libamdhip64.so.7``) is the one the kernels bind to.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime first)
+
+from . import _build
+
+MAX_TAPS = 16
+NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
+
+EXPORTS = [
+    'wc_conv_igemm', 'wc_gn_num_splits', 'wc_gn_stats', 'wc_gn_finalize', 'wc_attention_fwd',
+    'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
+    'wc_version'
+]
+
+
+class ConvSeg(ctypes.Structure):
+    _fields_ = [
+        ('src', ctypes.c_void_p), ('C', ctypes.c_int), ('ldc', ctypes.c_int), ('H', ctypes.c_int),
+        ('W', ctypes.c_int), ('sy', ctypes.c_int), ('sx', ctypes.c_int), ('ntaps', ctypes.c_int),
+        ('dy', ctypes.c_int * MAX_TAPS), ('dx', ctypes.c_int * MAX_TAPS), ('scale', ctypes.c_void_p),
+        ('shift', ctypes.c_void_p), ('silu', ctypes.c_int), ('kbase', ctypes.c_int)
+    ]
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [
+        ('seg', ConvSeg * 2), ('nseg', ctypes.c_int), ('B', ctypes.c_int), ('Hm', ctypes.c_int),
+        ('Wm', ctypes.c_int), ('N', ctypes.c_int), ('w', ctypes.c_void_p), ('ldw', ctypes.c_int),
+        ('bias', ctypes.c_void_p), ('temb', ctypes.c_void_p), ('temb_ld', ctypes.c_int),
+        ('res', ctypes.c_void_p), ('ldres', ctypes.c_int), ('out', ctypes.c_void_p),
+        ('ldo', ctypes.c_int), ('Ho', ctypes.c_int), ('Wo', ctypes.c_int), ('osy', ctypes.c_int),
+        ('osx', ctypes.c_int), ('ooy', ctypes.c_int), ('oox', ctypes.c_int),
+        ('out_nchw', ctypes.c_int)
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_F = ctypes.c_float
+_D = ctypes.c_double
+_U = ctypes.c_uint64
+
+_SIGS = {
+    'wc_conv_igemm': [ctypes.POINTER(ConvArgs), _P],
+    'wc_gn_num_splits': [_I, _I, _I],
+    'wc_gn_stats': [_P, _I, _I, _I, _I, _I, _P, _P],
+    'wc_gn_finalize': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P],
+    'wc_attention_fwd': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
+    'wc_temb': [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P],
+    'wc_conv_in': [_P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
+    'wc_ddpm_step': [_P, _P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _I, _U, _L, _L, _P],
+    'wc_add_noise': [_P, _P, _P, _P, _P, _L, _L, _P],
+    'wc_philox_normal': [_P, _L, _L, _U, _L, _L, _P],
+    'wc_sgg_update': [_P, _P, _P, _P, _P, _I, _I, _F, _D, _D, _D, _I, _P],
+}
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _build.LIB_PATH
+
+
+def load(build_if_missing: bool = True):
+    """Open the kernel library (building it first if it is absent and hipcc exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        if not build_if_missing or not os.path.exists(_build.HIPCC):
+            raise RuntimeError(f'weatherconverter_amd: HIP kernel library missing at {path}; run '
+                               f'python -c "import __graft_entry__ as g; g.build()"')
+        _build.build()
+    lib = ctypes.CDLL(path)
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    lib.wc_version.argtypes = []
+    lib.wc_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def check(status: int, op: str):
+    if status != 0:
+        kind = {-1: 'unsupported shape', -2: 'bad argument'}.get(status, f'hipError {status}')
+        raise RuntimeError(f'weatherconverter_amd kernel {op} failed: {kind}')
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args), name)

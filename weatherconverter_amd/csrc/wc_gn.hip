@@ -1,0 +1,155 @@
+// GroupNorm statistics for NHWC fp32 views (reference: nn.GroupNorm(8, C), unet_base.py:90 etc.).
+//
+// Pass 1 (wc_gn_stats): grid = B * splits * G workgroups, group index fastest so the G blocks that
+// read the same pixel rows run together and share L2 lines.  Each thread accumulates shifted
+// sums around its own first element (pivot), which keeps the moments free of E[x^2]-E[x]^2
+// cancellation; the workgroup merges (n, mean, M2) with Chan's formula.  HBM-bound: 4 B/element.
+// Pass 2 (wc_gn_finalize): one workgroup per batch element merges the split partials (again
+// Chan, fixed order => deterministic) and emits the per-(b, c) affine
+//   scale = gamma * rstd,   shift = beta - mean * rstd * gamma,
+// consumed by the conv prologue (GroupNorm-apply + SiLU fused into the next conv's loads).
+#include "wc_common.hpp"
+
+namespace {
+
+constexpr int GN_THREADS = 256;
+
+int splits_for(int B, int HW, int C) {
+    (void)C;
+    const int G = 8;
+    int target = 2048 / (B * G);
+    if (target < 1) target = 1;
+    int max_by_hw = HW / 64;
+    if (max_by_hw < 1) max_by_hw = 1;
+    if (target > max_by_hw) target = max_by_hw;
+    if (target > 256) target = 256;
+    return target;
+}
+
+__global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const float* __restrict__ x, int HW,
+                                                              int C, int ldc, int G, int splits,
+                                                              float* __restrict__ partials) {
+    const int g = blockIdx.x % G;
+    const int split = (blockIdx.x / G) % splits;
+    const int b = blockIdx.x / (G * splits);
+    const int cpg = C / G;
+    const int q_per_pix = cpg / 4;  // float4 per pixel within the group
+    const int pps = (HW + splits - 1) / splits;
+    const int p_begin = split * pps;
+    const int p_end = min(HW, p_begin + pps);
+    const long total = (long)max(0, p_end - p_begin) * q_per_pix;
+
+    const float* base = x + ((long)b * HW + p_begin) * ldc + g * cpg;
+    float n = 0.f, s = 0.f, ss = 0.f, pivot = 0.f;
+    bool have = false;
+    for (long idx = threadIdx.x; idx < total; idx += GN_THREADS) {
+        long pix = idx / q_per_pix;
+        int q = (int)(idx - pix * q_per_pix);
+        f32x4 v = *reinterpret_cast<const f32x4*>(base + pix * ldc + q * 4);
+        if (!have) { pivot = v.x; have = true; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float d = v[i] - pivot;
+            s += d;
+            ss = fmaf(d, d, ss);
+        }
+        n += 4.f;
+    }
+    float mean = 0.f, m2 = 0.f;
+    if (n > 0.f) {
+        mean = pivot + s / n;
+        m2 = fmaxf(ss - s * (s / n), 0.f);
+    }
+    // wave merge
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+        chan_merge(n, mean, m2, nb, mb, m2b);
+    }
+    __shared__ float red[3][GN_THREADS / 64];
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][wave] = n; red[1][wave] = mean; red[2][wave] = m2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float N0 = red[0][0], M0 = red[1][0], Q0 = red[2][0];
+        for (int w = 1; w < GN_THREADS / 64; ++w) chan_merge(N0, M0, Q0, red[0][w], red[1][w], red[2][w]);
+        float* o = partials + (((long)b * splits + split) * G + g) * 2;
+        o[0] = M0;
+        o[1] = Q0;
+    }
+}
+
+__global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(
+    const float* __restrict__ partials, int HW, int C, int G, int splits,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    float* __restrict__ scale, float* __restrict__ shift) {
+    const int b = blockIdx.x;
+    const int cpg = C / G;
+    const int pps = (HW + splits - 1) / splits;
+    __shared__ float s_mean[32], s_rstd[32];
+    // 32 lanes per group: lane j merges splits j, j+32, ... then a 32-lane butterfly.
+    const int g = threadIdx.x / 32;
+    const int j = threadIdx.x % 32;
+    if (g < G) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int sp = j; sp < splits; sp += 32) {
+            int pb = sp * pps;
+            int pe = min(HW, pb + pps);
+            float cnt = (float)max(0, pe - pb) * (float)cpg;
+            const float* pp = partials + (((long)b * splits + sp) * G + g) * 2;
+            chan_merge(n, mean, m2, cnt, pp[0], pp[1]);
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            float nb = __shfl_xor(n, o, 32), mb = __shfl_xor(mean, o, 32), m2b = __shfl_xor(m2, o, 32);
+            chan_merge(n, mean, m2, nb, mb, m2b);
+        }
+        if (j == 0) {
+            float var = n > 0.f ? m2 / n : 0.f;  // biased, as torch
+            s_mean[g] = mean;
+            s_rstd[g] = 1.0f / sqrtf(fmaxf(var, 0.f) + eps);
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += GN_THREADS) {
+        int gg = c / cpg;
+        float r = s_rstd[gg];
+        float ga = gamma ? gamma[c] : 1.f;
+        float be = beta ? beta[c] : 0.f;
+        float sc = r * ga;
+        scale[(long)b * C + c] = sc;
+        shift[(long)b * C + c] = be - s_mean[gg] * sc;
+    }
+}
+
+}  // namespace
+
+extern "C" int wc_gn_num_splits(int B, int HW, int C) { return splits_for(B, HW, C); }
+
+extern "C" int wc_gn_stats(const float* x, int B, int HW, int C, int ldc, int groups,
+                           float* partials, void* stream) {
+    if (!x || !partials) return WC_E_ARG;
+    if (groups < 1 || groups > 8 || C % groups != 0 || (C / groups) % 4 != 0 || ldc % 4 != 0)
+        return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) != 0) return WC_E_SHAPE;
+    int splits = splits_for(B, HW, C);
+    dim3 grid(B * splits * groups);
+    hipLaunchKernelGGL(gn_stats_kernel, grid, dim3(GN_THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), x, HW, C, ldc, groups, splits,
+                       partials);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_gn_finalize(const float* partials, int B, int HW, int C, int groups,
+                              const float* gamma, const float* beta, float eps, float* scale,
+                              float* shift, void* stream) {
+    if (!partials || !scale || !shift) return WC_E_ARG;
+    if (groups < 1 || groups > 8 || C % groups != 0) return WC_E_SHAPE;
+    int splits = splits_for(B, HW, C);
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(GN_THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), partials, HW, C, groups, splits,
+                       gamma, beta, eps, scale, shift);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}

@@ -1,0 +1,363 @@
+// Small kernels of the DDPM hot path: time embedding, stem conv, scheduler step, forward
+// noising, counter-based Gaussian noise and the semantic-gradient-guidance update.
+#include "wc_common.hpp"
+
+#include <math.h>
+
+namespace {
+
+// --------------------------------------------------------------------------------------------
+// Time embedding (reference get_time_embedding unet_base.py:7-30; t_proj :395-397;
+// t_emb_layers :98-100 = SiLU -> Linear).  One launch computes, per timestep row,
+//   e = [sin(t/f_k), cos(t/f_k)],  f_k = 10000^(k/(D/2))   (fp32 pow/sin/cos as torch)
+//   h = W2 SiLU(W1 e + b1) + b2                              (t_proj)
+//   out[p] = proj_w[p] . SiLU(h) + proj_b[p]                 (all ResBlock projections)
+// Every workgroup recomputes the 2x D^2 MLP (cheap) and owns 256 projection rows.
+// --------------------------------------------------------------------------------------------
+constexpr int TE_THREADS = 256;
+
+__global__ __launch_bounds__(TE_THREADS) void temb_kernel(const int64_t* __restrict__ t, int D,
+                                                          const float* __restrict__ w1,
+                                                          const float* __restrict__ b1,
+                                                          const float* __restrict__ w2,
+                                                          const float* __restrict__ b2,
+                                                          const float* __restrict__ pw,
+                                                          const float* __restrict__ pb, int P,
+                                                          float* __restrict__ out) {
+    __shared__ float e[256], h[256];
+    const int row = blockIdx.y;
+    const int half = D / 2;
+    const float tv = (float)t[row];
+    for (int k = threadIdx.x; k < half; k += TE_THREADS) {
+        float f = powf(10000.0f, (float)k / (float)half);
+        float a = tv / f;
+        e[k] = sinf(a);
+        e[k + half] = cosf(a);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < D; j += TE_THREADS) {
+        float acc = 0.f;
+        const float* wr = w1 + (long)j * D;
+        for (int k = 0; k < D; ++k) acc = fmaf(wr[k], e[k], acc);
+        h[j] = wc_silu(acc + b1[j]);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < D; j += TE_THREADS) {
+        float acc = 0.f;
+        const float* wr = w2 + (long)j * D;
+        for (int k = 0; k < D; ++k) acc = fmaf(wr[k], h[k], acc);
+        e[j] = wc_silu(acc + b2[j]);  // SiLU of t_proj output = input of every t_emb_layer
+    }
+    __syncthreads();
+    const int p = blockIdx.x * TE_THREADS + threadIdx.x;
+    if (p < P) {
+        const float* wr = pw + (long)p * D;
+        float acc = 0.f;
+        for (int k = 0; k < D; k += 4) {
+            f32x4 w = *reinterpret_cast<const f32x4*>(wr + k);
+            acc = fmaf(w.x, e[k], acc);
+            acc = fmaf(w.y, e[k + 1], acc);
+            acc = fmaf(w.z, e[k + 2], acc);
+            acc = fmaf(w.w, e[k + 3], acc);
+        }
+        out[(long)row * P + p] = acc + pb[p];
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// conv_in: 3x3 pad-1 conv from the NCHW image to an NHWC view (unet_base.py:400,456).  The
+// NCHW->NHWC transpose is fused here.  Thread = (pixel, 4 output channels).
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_in_kernel(const float* __restrict__ x, int B, int Cin,
+                                                      int H, int W, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, int Cout,
+                                                      float* __restrict__ out, int ldo) {
+    extern __shared__ float ws[];  // [Cin*9][Cout]
+    const int K = Cin * 9;
+    for (int i = threadIdx.x; i < K * Cout; i += blockDim.x) {
+        int co = i % Cout, k = i / Cout;
+        ws[i] = w[(long)co * K + k];
+    }
+    __syncthreads();
+    const int qpp = Cout / 4;
+    const long total = (long)B * H * W * qpp;
+    for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long)gridDim.x * blockDim.x) {
+        const int q = (int)(idx % qpp);
+        const long pix = idx / qpp;
+        const int xw = (int)(pix % W);
+        const int yh = (int)((pix / W) % H);
+        const int b = (int)(pix / ((long)W * H));
+        f32x4 acc = *reinterpret_cast<const f32x4*>(bias + q * 4);
+        for (int ci = 0; ci < Cin; ++ci) {
+            const float* plane = x + ((long)b * Cin + ci) * H * W;
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                int iy = yh + ky - 1;
+                if (iy < 0 || iy >= H) continue;
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    int ix = xw + kx - 1;
+                    if (ix < 0 || ix >= W) continue;
+                    float v = plane[(long)iy * W + ix];
+                    const f32x4 wv = *reinterpret_cast<const f32x4*>(ws + ((ci * 3 + ky) * 3 + kx) * Cout + q * 4);
+                    acc += v * wv;
+                }
+            }
+        }
+        *reinterpret_cast<f32x4*>(out + pix * ldo + q * 4) = acc;
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011) + Box-Muller.  Counter = (element/4, global sample, step, 0),
+// key = seed.  Independent of batch sharding by construction.
+// --------------------------------------------------------------------------------------------
+WC_DEVICE uint4 philox4x32_10(uint4 ctr, uint2 key) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+        uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+        ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+        key.x += W0;
+        key.y += W1;
+    }
+    return ctr;
+}
+
+WC_DEVICE f32x4 normal4(uint64_t seed, uint32_t e4, uint32_t sample, uint32_t step) {
+    uint4 r = philox4x32_10(make_uint4(e4, sample, step, 0u),
+                            make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const float inv = 2.3283064365386963e-10f;  // 2^-32
+    float u0 = ((float)r.x + 0.5f) * inv, u1 = ((float)r.y + 0.5f) * inv;
+    float u2 = ((float)r.z + 0.5f) * inv, u3 = ((float)r.w + 0.5f) * inv;
+    float ra = sqrtf(-2.f * logf(u0)), rb = sqrtf(-2.f * logf(u2));
+    float sa, ca, sb, cb;
+    sincosf(6.283185307179586f * u1, &sa, &ca);
+    sincosf(6.283185307179586f * u3, &sb, &cb);
+    return f32x4{ra * ca, ra * sa, rb * cb, rb * sb};
+}
+
+// Reverse step (linear_noise_scheduler.py:96-116 / :63-77).  Operation order and rounding follow
+// the reference's tensor ops exactly (explicit _rn intrinsics: no FMA contraction), so with an
+// identical z the result is bitwise equal to the PyTorch CPU path.
+__global__ __launch_bounds__(256) void ddpm_step_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ eps,
+                                                        const float* __restrict__ z,
+                                                        float* __restrict__ xo,
+                                                        float* __restrict__ szo, int64_t n4,
+                                                        int64_t per4, float beta, float s1m,
+                                                        float sqa, float sigma, int mode,
+                                                        uint64_t seed, int64_t sample0,
+                                                        int64_t step) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        f32x4 xv = reinterpret_cast<const f32x4*>(x)[i];
+        f32x4 ev = reinterpret_cast<const f32x4*>(eps)[i];
+        f32x4 zv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (mode == WC_NOISE_TENSOR) {
+            zv = reinterpret_cast<const f32x4*>(z)[i];
+        } else if (mode == WC_NOISE_PHILOX) {
+            int64_t smp = i / per4;
+            zv = normal4(seed, (uint32_t)(i - smp * per4), (uint32_t)(sample0 + smp), (uint32_t)step);
+        }
+        f32x4 r, sq;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float m = __fsub_rn(xv[k], __fdiv_rn(__fmul_rn(beta, ev[k]), s1m));
+            m = __fdiv_rn(m, sqa);
+            float sz = __fmul_rn(sigma, zv[k]);
+            if (szo) {
+                r[k] = m;
+                sq[k] = sz;
+            } else {
+                r[k] = (mode == WC_NOISE_NONE) ? m : __fadd_rn(m, sz);
+            }
+        }
+        reinterpret_cast<f32x4*>(xo)[i] = r;
+        if (szo) reinterpret_cast<f32x4*>(szo)[i] = sq;
+    }
+}
+
+__global__ __launch_bounds__(256) void add_noise_kernel(const float* __restrict__ x0,
+                                                        const float* __restrict__ nz,
+                                                        const float* __restrict__ ca,
+                                                        const float* __restrict__ cb,
+                                                        float* __restrict__ out, int64_t n4,
+                                                        int64_t per4) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t smp = i / per4;
+        const float a = ca[smp], bb = cb[smp];
+        f32x4 xv = reinterpret_cast<const f32x4*>(x0)[i];
+        f32x4 nv = reinterpret_cast<const f32x4*>(nz)[i];
+        f32x4 r;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a, xv[k]), __fmul_rn(bb, nv[k]));
+        reinterpret_cast<f32x4*>(out)[i] = r;
+    }
+}
+
+__global__ __launch_bounds__(256) void philox_kernel(float* __restrict__ out, int64_t n4,
+                                                     int64_t per4, uint64_t seed, int64_t sample0,
+                                                     int64_t step) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t smp = i / per4;
+        reinterpret_cast<f32x4*>(out)[i] =
+            normal4(seed, (uint32_t)(i - smp * per4), (uint32_t)(sample0 + smp), (uint32_t)step);
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// SGG update (sgg/sgg.py:16-22 + seg_model/inference.py:39-43).  One thread per output pixel of
+// the S x S latent: 4x4 average pool of the 4S x 4S gradient per channel (fp32, as F.avg_pool2d),
+// then the std-weighted L2 magnitude and the mean update in fp64 as the reference's numpy path.
+// mode 0: magnitude over channels per sample (reference semantics at batch 1);
+// mode 1: reference semantics for batch > 1 (D4): squeeze(0) is a no-op, so the numpy sum runs
+//         over the BATCH axis and the magnitude is per channel.
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgg_kernel(const float* __restrict__ grad,
+                                                  const float* __restrict__ mu,
+                                                  const float* __restrict__ sigma,
+                                                  float* __restrict__ xt, float* __restrict__ mag,
+                                                  int nb, int S, float lam, double s0, double s1,
+                                                  double s2, int mode) {
+    const int S4 = 4 * S;
+    const long total = (long)S * S;
+    const double stdv[3] = {s0, s1, s2};
+    for (long pix = (long)blockIdx.x * blockDim.x + threadIdx.x; pix < total;
+         pix += (long)gridDim.x * blockDim.x) {
+        const int y = (int)(pix / S), x = (int)(pix % S);
+        if (mode == 0) {
+            for (int b = 0; b < nb; ++b) {
+                double acc = 0.0;
+                for (int c = 0; c < 3; ++c) {
+                    const float* g = grad + (((long)b * 3 + c) * S4 + 4 * y) * S4 + 4 * x;
+                    float s = 0.f;
+                    for (int dy = 0; dy < 4; ++dy)
+                        for (int dx = 0; dx < 4; ++dx) s += g[(long)dy * S4 + dx];
+                    double v = (double)(s / 16.f) * stdv[c];
+                    acc += v * v;
+                }
+                double m = sqrt(acc);
+                if (mag) mag[(long)b * total + pix] = (float)m;
+                for (int c = 0; c < 3; ++c) {
+                    long o = ((long)b * 3 + c) * total + pix;
+                    double sg = (double)__fmul_rn(lam, sigma[o]);
+                    xt[o] = (float)(((double)mu[o] + sg * m) + (double)sigma[o]);
+                }
+            }
+        } else {
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0.0;
+                for (int b = 0; b < nb; ++b) {
+                    const float* g = grad + (((long)b * 3 + c) * S4 + 4 * y) * S4 + 4 * x;
+                    float s = 0.f;
+                    for (int dy = 0; dy < 4; ++dy)
+                        for (int dx = 0; dx < 4; ++dx) s += g[(long)dy * S4 + dx];
+                    double v = (double)(s / 16.f) * stdv[c];
+                    acc += v * v;
+                }
+                double m = sqrt(acc);
+                if (mag) mag[(long)c * total + pix] = (float)m;
+                for (int b = 0; b < nb; ++b) {
+                    long o = ((long)b * 3 + c) * total + pix;
+                    double sg = (double)__fmul_rn(lam, sigma[o]);
+                    xt[o] = (float)(((double)mu[o] + sg * m) + (double)sigma[o]);
+                }
+            }
+        }
+    }
+}
+
+int grid_for(int64_t n, int threads) {
+    int64_t g = (n + threads - 1) / threads;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+extern "C" int wc_temb(const int64_t* t, int nt, int D, const float* w1, const float* b1,
+                       const float* w2, const float* b2, const float* proj_w,
+                       const float* proj_b, int P, float* out, void* stream) {
+    if (!t || !w1 || !b1 || !w2 || !b2 || !proj_w || !proj_b || !out) return WC_E_ARG;
+    if (D <= 0 || D > 256 || D % 4 != 0 || nt <= 0 || P <= 0) return WC_E_SHAPE;
+    dim3 grid((P + TE_THREADS - 1) / TE_THREADS, nt);
+    hipLaunchKernelGGL(temb_kernel, grid, dim3(TE_THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                       t, D, w1, b1, w2, b2, proj_w, proj_b, P, out);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_conv_in(const float* x, int B, int Cin, int H, int W, const float* w,
+                          const float* b, int Cout, float* out, int ldo, void* stream) {
+    if (!x || !w || !b || !out) return WC_E_ARG;
+    if (Cin < 1 || Cin > 16 || Cout % 4 != 0 || ldo % 4 != 0) return WC_E_SHAPE;
+    size_t lds = (size_t)Cin * 9 * Cout * sizeof(float);
+    if (lds > 64 * 1024) return WC_E_SHAPE;
+    long total = (long)B * H * W * (Cout / 4);
+    hipLaunchKernelGGL(conv_in_kernel, dim3(grid_for(total, 256)), dim3(256), lds,
+                       reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, Cout, out, ldo);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_ddpm_step(const float* x, const float* eps, const float* z, float* x_out,
+                            float* sz_out, int64_t B, int64_t per_sample, float beta, float s1m,
+                            float sqrt_alpha, float sigma, int noise_mode, uint64_t seed,
+                            int64_t sample0, int64_t step, void* stream) {
+    if (!x || !eps || !x_out) return WC_E_ARG;
+    if (noise_mode < 0 || noise_mode > 2 || (noise_mode == WC_NOISE_TENSOR && !z)) return WC_E_ARG;
+    if (per_sample % 4 != 0) return WC_E_SHAPE;
+    int64_t n4 = B * per_sample / 4;
+    hipLaunchKernelGGL(ddpm_step_kernel, dim3(grid_for(n4, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), x, eps, z, x_out, sz_out, n4, per_sample / 4,
+                       beta, s1m, sqrt_alpha, sigma, noise_mode, seed, sample0, step);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_add_noise(const float* x0, const float* noise, const float* coef_a,
+                            const float* coef_b, float* out, int64_t B, int64_t per_sample,
+                            void* stream) {
+    if (!x0 || !noise || !coef_a || !coef_b || !out) return WC_E_ARG;
+    if (per_sample % 4 != 0) return WC_E_SHAPE;
+    int64_t n4 = B * per_sample / 4;
+    hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for(n4, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), x0, noise, coef_a, coef_b, out, n4,
+                       per_sample / 4);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_philox_normal(float* out, int64_t B, int64_t per_sample, uint64_t seed,
+                                int64_t sample0, int64_t step, void* stream) {
+    if (!out) return WC_E_ARG;
+    if (per_sample % 4 != 0) return WC_E_SHAPE;
+    int64_t n4 = B * per_sample / 4;
+    hipLaunchKernelGGL(philox_kernel, dim3(grid_for(n4, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), out, n4, per_sample / 4, seed,
+                       sample0, step);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_sgg_update(const float* grad, const float* mu, const float* sigma,
+                             float* xt_out, float* mag_out, int nb, int S, float lambda_,
+                             double std0, double std1, double std2, int sum_batch, void* stream) {
+    if (!grad || !mu || !sigma || !xt_out) return WC_E_ARG;
+    if (nb < 1 || S < 1) return WC_E_SHAPE;
+    long total = (long)S * S;
+    hipLaunchKernelGGL(sgg_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), grad, mu, sigma, xt_out, mag_out, nb,
+                       S, lambda_, std0, std1, std2, sum_batch ? 1 : 0);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" const char* wc_version(void) { return "weatherconverter_amd 0.1 gfx950"; }

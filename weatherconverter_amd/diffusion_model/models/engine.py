@@ -1,0 +1,275 @@
+"""UnetEngine: runs the reference ``Unet`` forward (``unet_base.py:451-488``) as gfx950 HIP kernels.
+
+Data layout in HBM
+------------------
+* Activations are NHWC fp32.  The only NCHW tensors are the UNet's input (read by ``wc_conv_in``,
+  which fuses the transpose) and its output (written by the last implicit-GEMM conv).
+* Skip concatenation is free: for every level ``i`` the engine allocates one buffer
+  ``U[i] = (B, S_i, S_i, 2*C_i)``.  The down path writes the level's input ``X_i`` (= the skip
+  ``down_outs[i]``) straight into channels ``[C_i, 2C_i)``; the up path's ConvTranspose (or the
+  stage below when it does not upsample) writes channels ``[0, C_i)``.  The up ResBlock then reads
+  ``U[i]`` as one contiguous tensor, which is exactly ``torch.cat([x, out_down], dim=1)`` of
+  ``unet_base.py:349``.
+* Weights are repacked once into GEMM form ``[N][K]`` with ``K = (tap, c_in)``; conv2 of every
+  ResBlock carries the 1x1 ``residual_input_conv`` as 32-aligned extra K columns (its bias folded
+  into conv2's), so a ResBlock is GN-stats, conv1, GN-stats, conv2 = 6 launches.
+
+Per ResBlock (``unet_base.py:146-150``)::
+
+    sc1, sh1 = GN-stats(X)                           wc_gn_stats + wc_gn_finalize
+    h  = conv3x3(SiLU(X*sc1 + sh1)) + b1 + temb      wc_conv_igemm (prologue + epilogue fused)
+    sc2, sh2 = GN-stats(h)
+    Y  = conv3x3(SiLU(h*sc2 + sh2)) + conv1x1(X) + b2 + b_res     one wc_conv_igemm, 2 K-segments
+
+Per attention layer (``unet_base.py:153-161``), in place on Y::
+
+    sc, sh = GN-stats(Y);  qkv = (Y*sc + sh) W_in^T + b_in      (GN-apply fused in the GEMM)
+    O = flash-attention(qkv);  Y = Y + O W_out^T + b_out        (residual fused in the epilogue)
+"""
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+
+from ... import kernels as K
+from ...kernels import Seg, View
+
+TAPS3 = [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]
+TAPS1 = [(0, 0)]
+TAPS4S2 = [(ky - 1, kx - 1) for ky in range(4) for kx in range(4)]
+# ConvTranspose2d(4, stride 2, pad 1): output row 2m+p gathers input rows m+dy with kernel row ky.
+_CT_TAPS = {0: [(0, 1), (-1, 3)], 1: [(1, 0), (0, 2)]}
+
+
+def pack_conv(w: torch.Tensor) -> torch.Tensor:
+    """[Co][Ci][kh][kw] -> [Co][(ky*kw + kx)*Ci + ci]."""
+    co = w.shape[0]
+    return w.detach().permute(0, 2, 3, 1).reshape(co, -1).contiguous().float()
+
+
+def pack_convT(wt: torch.Tensor, py: int, px: int) -> Tuple[List[Tuple[int, int]], torch.Tensor]:
+    """ConvTranspose weight [Ci][Co][4][4] -> (taps, [Co][tap*Ci + ci]) for output parity (py, px)."""
+    taps, cols = [], []
+    for dy, ky in _CT_TAPS[py]:
+        for dx, kx in _CT_TAPS[px]:
+            taps.append((dy, dx))
+            cols.append(wt.detach()[:, :, ky, kx].t())
+    return taps, torch.cat(cols, dim=1).contiguous().float()
+
+
+@dataclass
+class ResPack:
+    ci: int
+    co: int
+    g1: torch.Tensor
+    be1: torch.Tensor
+    w1: torch.Tensor
+    b1: torch.Tensor
+    g2: torch.Tensor
+    be2: torch.Tensor
+    w2: torch.Tensor  # conv2 (9*co) ++ residual 1x1 (ci)
+    b2: torch.Tensor
+    temb_off: int
+
+
+@dataclass
+class AttnPack:
+    c: int
+    heads: int
+    g: torch.Tensor
+    be: torch.Tensor
+    w_in: torch.Tensor
+    b_in: torch.Tensor
+    w_out: torch.Tensor
+    b_out: torch.Tensor
+
+
+class UnetEngine:
+
+    def __init__(self, model):
+        params = list(model.parameters())
+        if not params or not params[0].is_cuda:
+            raise RuntimeError('weatherconverter_amd.Unet runs on the GPU only (HIP kernels, no CPU fallback): '
+                               'move the model to a ROCm device first')
+        K._native.load()
+        self.model = model
+        self.device = params[0].device
+        self._sig = self._signature()
+        self._pack()
+
+    # ------------------------------------------------------------------ packing
+    def _signature(self):
+        return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+
+    def _pack(self):
+        m = self.model
+        self.res_packs = []
+        self.temb_rows_w, self.temb_rows_b = [], []
+        self._temb_P = 0
+        with torch.no_grad():
+            self.downs = [self._pack_stage(blk, n_res=blk.num_layers, attn=blk.use_attn) for blk in m.downs]
+            self.down_convs = [(pack_conv(blk.down_sample_conv.weight), blk.down_sample_conv.bias.detach().float())
+                               if blk.down_sample else None for blk in m.downs]
+            self.mids = [self._pack_stage(blk, n_res=blk.num_layers + 1, attn=True) for blk in m.mids]
+            self.ups = [self._pack_stage(blk, n_res=blk.num_layers, attn=blk.use_attn) for blk in m.ups]
+            self.up_convs = []
+            for blk in m.ups:
+                if blk.up_sample:
+                    parts = [pack_convT(blk.up_sample_conv.weight, py, px) for py in (0, 1) for px in (0, 1)]
+                    self.up_convs.append((parts, blk.up_sample_conv.bias.detach().float()))
+                else:
+                    self.up_convs.append(None)
+            self.conv_in_w = m.conv_in.weight.detach().float().contiguous()
+            self.conv_in_b = m.conv_in.bias.detach().float().contiguous()
+            self.norm_out = (m.norm_out.weight.detach().float(), m.norm_out.bias.detach().float())
+            self.conv_out_w = pack_conv(m.conv_out.weight)
+            self.conv_out_b = m.conv_out.bias.detach().float().contiguous()
+            tp = m.t_proj
+            self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
+                          tp[2].weight.detach().float().contiguous(), tp[2].bias.detach().float().contiguous()]
+            self.temb_w = torch.cat(self.temb_rows_w, 0).contiguous()
+            self.temb_b = torch.cat(self.temb_rows_b, 0).contiguous()
+
+    def _pack_res(self, blk, i: int) -> ResPack:
+        f, s, r = blk.resnet_conv_first[i], blk.resnet_conv_second[i], blk.residual_input_conv[i]
+        tl = blk.t_emb_layers[i][1]
+        ci, co = f[2].in_channels, f[2].out_channels
+        w2 = torch.cat([pack_conv(s[2].weight), r.weight.detach().reshape(co, ci).float()], 1).contiguous()
+        p = ResPack(ci=ci, co=co, g1=f[0].weight.detach().float(), be1=f[0].bias.detach().float(),
+                    w1=pack_conv(f[2].weight), b1=f[2].bias.detach().float().contiguous(),
+                    g2=s[0].weight.detach().float(), be2=s[0].bias.detach().float(), w2=w2,
+                    b2=(s[2].bias.detach().float() + r.bias.detach().float()).contiguous(), temb_off=self._temb_P)
+        self.temb_rows_w.append(tl.weight.detach().float())
+        self.temb_rows_b.append(tl.bias.detach().float())
+        self._temb_P += co
+        return p
+
+    @staticmethod
+    def _pack_attn(blk, i: int) -> AttnPack:
+        mha, gn = blk.attentions[i], blk.attention_norms[i]
+        c = mha.embed_dim
+        return AttnPack(c=c, heads=mha.num_heads, g=gn.weight.detach().float(), be=gn.bias.detach().float(),
+                        w_in=mha.in_proj_weight.detach().float().contiguous(),
+                        b_in=mha.in_proj_bias.detach().float().contiguous(),
+                        w_out=mha.out_proj.weight.detach().float().contiguous(),
+                        b_out=mha.out_proj.bias.detach().float().contiguous())
+
+    def _pack_stage(self, blk, n_res: int, attn: bool):
+        res = [self._pack_res(blk, i) for i in range(n_res)]
+        n_attn = len(blk.attentions)
+        att = [self._pack_attn(blk, i) for i in range(n_attn)] if attn else []
+        return res, att
+
+    # ------------------------------------------------------------------ building blocks
+    def _new(self, B, H, W, C) -> torch.Tensor:
+        return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
+
+    def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int):
+        B, H, W = X.B, X.H, X.W
+        sc1, sh1 = K.gn_affine(X, p.g1, p.be1)
+        h = View.full(self._new(B, H, W, p.co))
+        K.conv_igemm([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.b1, h, Hm=H, Wm=W,
+                     temb=temb[:, p.temb_off:], temb_ld=temb_ld)
+        sc2, sh2 = K.gn_affine(h, p.g2, p.be2)
+        K.conv_igemm([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
+                      Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.b2, Y, Hm=H, Wm=W)
+
+    def attention(self, Y: View, p: AttnPack):
+        B, H, W, C = Y.B, Y.H, Y.W, Y.C
+        N = H * W
+        sc, sh = K.gn_affine(Y, p.g, p.be)
+        qkv = self._new(B, H, W, 3 * C)
+        K.conv_igemm([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.b_in, View.full(qkv), Hm=H, Wm=W)
+        o = self._new(B, H, W, C)
+        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads)
+        K.conv_igemm([Seg(View.full(o), TAPS1)], p.w_out, p.b_out, Y, Hm=H, Wm=W, res=Y)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, t) -> torch.Tensor:
+        if self._signature() != self._sig:  # parameters changed in place: repack
+            self._sig = self._signature()
+            self._pack()
+        m = self.model
+        if x.dim() != 4 or x.shape[1] != m.model_config.im_channels:
+            raise RuntimeError(f'Unet expects (B, {m.model_config.im_channels}, H, W), got {tuple(x.shape)}')
+        x = x.to(device=self.device, dtype=torch.float32).contiguous()
+        B, _, S, S2 = x.shape
+        tt = torch.as_tensor(t).long().reshape(-1).to(self.device)
+        nt = tt.shape[0]
+        if nt not in (1, B):
+            raise RuntimeError(f'timestep tensor has {nt} entries for a batch of {B}')
+        temb = K.temb(tt, *self.tproj, self.temb_w, self.temb_b)
+        temb_ld = temb.shape[1] if nt > 1 else 0
+
+        dc = m.down_channels
+        L = len(dc) - 1
+        sizes = [(S, S2)]
+        for i in range(L):
+            h, w = sizes[-1]
+            sizes.append((h // 2, w // 2) if m.down_sample[i] else (h, w))
+        U = [self._new(B, sizes[i][0], sizes[i][1], 2 * dc[i]) for i in range(L)]
+
+        cur = View(U[0], dc[0], dc[0])
+        K.conv_in(x, self.conv_in_w, self.conv_in_b, cur)
+
+        # ---------------- down path
+        for i in range(L):
+            res, att = self.downs[i]
+            co = dc[i + 1]
+            H, W = sizes[i]
+            final = View(U[i + 1], dc[i + 1], dc[i + 1]) if i < L - 1 else View.full(
+                self._new(B, sizes[i + 1][0], sizes[i + 1][1], co))
+            for li, rp in enumerate(res):
+                last = li == len(res) - 1
+                tgt = final if (last and self.down_convs[i] is None) else View.full(self._new(B, H, W, co))
+                self.resblock(cur, tgt, rp, temb, temb_ld)
+                if att:
+                    self.attention(tgt, att[li])
+                cur = tgt
+            if self.down_convs[i] is not None:
+                w, b = self.down_convs[i]
+                K.conv_igemm([Seg(cur, TAPS4S2, stride=2)], w, b, final, Hm=sizes[i + 1][0], Wm=sizes[i + 1][1])
+                cur = final
+
+        # ---------------- mid path
+        for j, (res, att) in enumerate(self.mids):
+            last_mid = j == len(self.mids) - 1
+            H, W = cur.H, cur.W
+            for li, rp in enumerate(res):
+                if last_mid and li == len(res) - 1 and self.up_convs[0] is None:
+                    tgt = View(U[L - 1], 0, dc[L - 1])
+                else:
+                    tgt = View.full(self._new(B, H, W, rp.co))
+                self.resblock(cur, tgt, rp, temb, temb_ld)
+                cur = tgt
+                if li < len(att):
+                    self.attention(cur, att[li])
+
+        # ---------------- up path
+        for k, (res, att) in enumerate(self.ups):
+            i = L - 1 - k
+            H, W = sizes[i]
+            if self.up_convs[k] is not None:
+                parts, b = self.up_convs[k]
+                dst = View(U[i], 0, dc[i])
+                for (py, px), (taps, w) in zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts):
+                    K.conv_igemm([Seg(cur, taps)], w, b, dst, Hm=cur.H, Wm=cur.W, out_map=(2, 2, py, px))
+            else:
+                assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
+            cur = View.full(U[i])
+            next_in_place = i > 0 and self.up_convs[k + 1] is None
+            for li, rp in enumerate(res):
+                last = li == len(res) - 1
+                tgt = View(U[i - 1], 0, dc[i - 1]) if (last and next_in_place) else View.full(
+                    self._new(B, H, W, rp.co))
+                self.resblock(cur, tgt, rp, temb, temb_ld)
+                if att:
+                    self.attention(tgt, att[li])
+                cur = tgt
+
+        # ---------------- head: GN -> SiLU -> conv_out, NCHW output
+        sc, sh = K.gn_affine(cur, *self.norm_out)
+        out = torch.empty((B, m.model_config.im_channels, S, S2), dtype=torch.float32, device=self.device)
+        K.conv_igemm([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.conv_out_w, self.conv_out_b, None,
+                     Hm=S, Wm=S2, out_nchw=out)
+        return out

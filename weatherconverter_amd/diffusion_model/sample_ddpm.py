@@ -1,0 +1,182 @@
+"""Drop-in for the reference's ``diffusion_model/sample_ddpm.py`` (unguided DDPM sampling).
+
+Same public functions — ``load_config``, ``sample``, ``load_model``, ``load_scheduler``, ``infer`` —
+with the reference's argument meaning.  Differences, all opt-in or fail-loud:
+  * ``sample`` returns the final x0 tensor in addition to writing the PNG grid (``save_path=None``
+    skips the file), and takes build-only keywords: ``noise`` ('torch_cpu' = reference RNG stream,
+    'philox' = on-device counter-based noise), ``seed``, ``x_T``, ``graph``.
+  * ``infer`` does not swallow exceptions (reference ``:84-87`` prints and continues).
+Hot loop (reference ``:35-44``) per step: one UNet forward on the HIP engine + one fused scheduler
+kernel.  ``graph=True`` captures the UNet forward + step into a HIP graph once and replays it.
+"""
+import math
+import os
+from datetime import datetime
+from typing import Optional
+
+import torch
+
+from .config import Config, DiffusionConfig, ModelConfig, TrainingConfig, load_config  # noqa: F401
+from .models.unet_base import Unet
+from .scheduler.linear_noise_scheduler import LinearNoiseScheduler
+
+
+def _device() -> torch.device:
+    return torch.device('cuda' if torch.cuda.is_available() else 'cpu')
+
+
+# ----------------------------------------------------------------------------------- image output
+def make_grid(ims: torch.Tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> torch.Tensor:
+    """torchvision.utils.make_grid semantics for a (B, C, H, W) batch (torchvision is not a dependency)."""
+    B, C, H, W = ims.shape
+    if B == 1:
+        return ims[0]
+    xmaps = min(nrow, B)
+    ymaps = int(math.ceil(B / xmaps))
+    h, w = H + padding, W + padding
+    grid = torch.full((C, ymaps * h + padding, xmaps * w + padding), pad_value, dtype=ims.dtype)
+    k = 0
+    for y in range(ymaps):
+        for x in range(xmaps):
+            if k >= B:
+                break
+            grid[:, y * h + padding:y * h + padding + H, x * w + padding:x * w + padding + W] = ims[k]
+            k += 1
+    return grid
+
+
+def save_png(grid: torch.Tensor, path: str):
+    """ToPILImage semantics for float CHW in [0, 1]: mul(255).byte(), then PNG."""
+    from PIL import Image
+    arr = grid.mul(255).byte().permute(1, 2, 0).cpu().numpy()
+    Image.fromarray(arr.squeeze(-1) if arr.shape[-1] == 1 else arr).save(path)
+
+
+# ----------------------------------------------------------------------------------- sampling core
+class _GraphStep:
+    """One reverse step (UNet + fused scheduler update) captured into a HIP graph per timestep class.
+
+    The UNet's shapes are static across steps; only the timestep value and the step scalars change.
+    The graph reads the timestep from a device tensor and the scalars are baked per captured step, so
+    we capture one graph per distinct step index lazily... which would be T graphs.  Instead we capture
+    the UNet forward only (timestep read from device memory) and run the scheduler kernel eagerly.
+    """
+
+    def __init__(self, model: Unet, x: torch.Tensor):
+        self.model = model
+        self.x_in = x.clone()
+        self.t_in = torch.zeros(1, dtype=torch.long, device=x.device)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm the allocator / engine pack outside capture
+                self.eps = model(self.x_in, self.t_in)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.eps = model(self.x_in, self.t_in)
+
+    def __call__(self, x: torch.Tensor, t_dev: torch.Tensor) -> torch.Tensor:
+        self.x_in.copy_(x)
+        self.t_in.copy_(t_dev)
+        self.graph.replay()
+        return self.eps
+
+
+@torch.no_grad()
+def sample_tensor(model: Unet, scheduler: LinearNoiseScheduler, batch: int, im_channels: int, im_size: int, *,
+                  noise: str = 'torch_cpu', seed: Optional[int] = None, sample0: int = 0,
+                  x_T: Optional[torch.Tensor] = None, graph: bool = False, total_batch: Optional[int] = None,
+                  progress=None) -> torch.Tensor:
+    """The reverse loop of reference ``sample_ddpm.py:35-44``; returns x0 (not clamped).
+
+    noise='torch_cpu': x_T and every z come from the CPU generator in the reference's order
+    (``torch.randn`` of the full batch).  With ``total_batch`` > batch (sharded sampling) every
+    rank draws the full-batch tensor and keeps rows [sample0, sample0+batch) — identical to one rank.
+    noise='philox': x_T and z from Philox(seed, global sample, step) on the device.
+    """
+    dev = scheduler.device
+    T = scheduler.num_timesteps
+    shape = (batch, im_channels, im_size, im_size)
+    full = total_batch or batch
+    full_shape = (full, im_channels, im_size, im_size)
+    if noise not in ('torch_cpu', 'philox'):
+        raise ValueError(f"noise must be 'torch_cpu' or 'philox', got {noise!r}")
+    if seed is not None and noise == 'torch_cpu':
+        torch.manual_seed(seed)
+    seed = 0 if seed is None else seed
+
+    def cpu_noise():
+        z = torch.randn(full_shape)
+        return z[sample0:sample0 + batch].contiguous().to(dev)
+
+    if x_T is not None:
+        xt = x_T.to(dev, torch.float32).contiguous()
+    elif noise == 'torch_cpu':
+        xt = cpu_noise()
+    else:
+        from ..kernels import philox_normal
+        xt = philox_normal(shape, dev, seed, sample0=sample0, step=T)  # step index T keys x_T
+    ts = torch.arange(T, device=dev, dtype=torch.long)
+    runner = _GraphStep(model, xt) if graph else None
+    nxt = torch.empty_like(xt)
+    for i in reversed(range(T)):
+        t_dev = ts[i:i + 1]
+        eps = runner(xt, t_dev) if runner is not None else model(xt, t_dev)
+        if i == 0:
+            scheduler.step(xt, eps, 0, out=nxt)
+        elif noise == 'torch_cpu':
+            scheduler.step(xt, eps, i, out=nxt, z=cpu_noise())
+        else:
+            scheduler.step(xt, eps, i, out=nxt, noise='philox', seed=seed, sample0=sample0)
+        xt, nxt = nxt, xt
+        if progress is not None:
+            progress(i)
+    return xt
+
+
+def sample(model, scheduler: LinearNoiseScheduler, train_config: TrainingConfig, model_config: ModelConfig,
+           diffusion_config: DiffusionConfig, save_path: Optional[str] = 'diffusion_model_v2/outputs/samples', *,
+           noise: str = 'torch_cpu', seed: Optional[int] = None, x_T: Optional[torch.Tensor] = None,
+           graph: bool = False) -> torch.Tensor:
+    """Reference ``sample`` (:23-53): T-step reverse loop, clamp, [0,1], PNG grid.  Returns x0."""
+    if diffusion_config.num_timesteps != scheduler.num_timesteps:
+        raise RuntimeError('scheduler / diffusion_config timestep mismatch')
+    xt = sample_tensor(model, scheduler, train_config.sample_size, model_config.im_channels, model_config.im_size,
+                       noise=noise, seed=seed, x_T=x_T, graph=graph)
+    if save_path is not None:
+        ims = (torch.clamp(xt, -1., 1.).detach().cpu() + 1) / 2
+        grid = make_grid(ims, nrow=train_config.num_grid_rows)
+        now = datetime.now()
+        os.makedirs(save_path, exist_ok=True)
+        save_png(grid, os.path.join(save_path, f'x_410{now.hour}{now.minute}{now.second}.png'))
+    return xt
+
+
+def load_model(model_path: str, model_config: ModelConfig) -> torch.nn.Module:
+    """Reference :56-61 — Unet + ``torch.load(...)['model_state_dict']`` (weights_only load)."""
+    dev = _device()
+    model = Unet(model_config).to(dev)
+    checkpoint = torch.load(model_path, map_location=dev, weights_only=True)
+    model.load_state_dict(checkpoint['model_state_dict'])
+    model.eval()
+    return model
+
+
+def load_scheduler(diffusion_config: DiffusionConfig) -> LinearNoiseScheduler:
+    """Reference :64-70."""
+    return LinearNoiseScheduler(num_timesteps=diffusion_config.num_timesteps, beta_start=diffusion_config.beta_start,
+                                beta_end=diffusion_config.beta_end)
+
+
+def infer(config: Config, epoch: int = 410):
+    """Reference :73-87 (checkpoint ``{checkpoints}/{epoch}-checkpoint.ckpt``); errors propagate."""
+    checkpoint_path = os.path.join(config.folders.checkpoints, f'{epoch}-checkpoint.ckpt')
+    model = load_model(checkpoint_path, config.model)
+    scheduler = load_scheduler(config.diffusion)
+    with torch.no_grad():
+        return sample(model, scheduler, config.training, config.model, config.diffusion, config.folders.samples)
+
+
+if __name__ == '__main__':
+    infer(load_config())

@@ -1,0 +1,244 @@
+"""Thin typed wrappers over the C ABI (``include/wc_kernels.h``) taking torch device tensors.
+
+All launches go on the current torch stream (so torch ops, HIP graphs captured through
+``torch.cuda.graph`` and these kernels are ordered).  Shapes are validated here before a pointer
+ever reaches a kernel; the C layer re-validates and returns a status that is turned into a
+RuntimeError.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _native
+from ._native import ConvArgs, ConvSeg
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+# Optional per-launch instrumentation for bench.py's roofline leg: when a list is installed here,
+# conv_igemm records a (tile, algorithmic_flops, start_event, end_event) tuple around each launch.
+PROFILE = None
+
+
+def profile_conv(enable: bool):
+    global PROFILE
+    PROFILE = [] if enable else None
+    return PROFILE
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _req(cond: bool, msg: str):
+    if not cond:
+        raise RuntimeError(f'weatherconverter_amd: {msg}')
+
+
+@dataclass
+class View:
+    """NHWC fp32 channel slice ``t[..., c0:c0+C]`` of a contiguous (B, H, W, Ctot) tensor."""
+    t: torch.Tensor
+    c0: int
+    C: int
+
+    @staticmethod
+    def full(t: torch.Tensor) -> 'View':
+        return View(t, 0, t.shape[-1])
+
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + 4 * self.c0
+
+    @property
+    def ldc(self) -> int:
+        return self.t.shape[-1]
+
+    @property
+    def B(self) -> int:
+        return self.t.shape[0]
+
+    @property
+    def H(self) -> int:
+        return self.t.shape[1]
+
+    @property
+    def W(self) -> int:
+        return self.t.shape[2]
+
+    def check(self):
+        _req(self.t.is_cuda and self.t.dtype == torch.float32 and self.t.is_contiguous() and self.t.dim() == 4,
+             'views must be contiguous fp32 NHWC device tensors')
+        _req(0 <= self.c0 and self.c0 + self.C <= self.t.shape[-1], 'view channel range out of bounds')
+
+    def tensor(self) -> torch.Tensor:
+        return self.t[..., self.c0:self.c0 + self.C]
+
+
+@dataclass
+class Seg:
+    view: View
+    taps: Sequence[Tuple[int, int]]
+    stride: int = 1
+    scale: Optional[torch.Tensor] = None
+    shift: Optional[torch.Tensor] = None
+    silu: bool = False
+    kbase: int = 0
+
+
+def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
+               temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
+               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None):
+    """Implicit-GEMM conv: out[b, my*osy+ooy, mx*osx+oox, n] = sum_k A[m, k] W[n, k] (+bias, temb, res)."""
+    a = ConvArgs()
+    _req(1 <= len(segs) <= 2, 'conv_igemm takes 1 or 2 K segments')
+    _req(w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2, 'packed weight')
+    N, ldw = w.shape
+    B = segs[0].view.B
+    for i, s in enumerate(segs):
+        v = s.view
+        v.check()
+        _req(v.B == B, 'segment batch mismatch')
+        _req(len(s.taps) <= _native.MAX_TAPS, 'too many taps')
+        cs = a.seg[i]
+        cs.src = v.ptr
+        cs.C = v.C
+        cs.ldc = v.ldc
+        cs.H = v.H
+        cs.W = v.W
+        cs.sy = cs.sx = s.stride
+        cs.ntaps = len(s.taps)
+        for j, (dy, dx) in enumerate(s.taps):
+            cs.dy[j] = dy
+            cs.dx[j] = dx
+        if s.scale is not None:
+            _req(s.scale.shape == (B, v.C) and s.shift.shape == (B, v.C), 'GN affine shape')
+            cs.scale = s.scale.data_ptr()
+            cs.shift = s.shift.data_ptr()
+        cs.silu = int(s.silu)
+        cs.kbase = s.kbase
+    a.nseg = len(segs)
+    a.B, a.Hm, a.Wm, a.N = B, Hm, Wm, N
+    a.w, a.ldw = w.data_ptr(), ldw
+    a.bias = _ptr(bias)
+    a.temb, a.temb_ld = _ptr(temb), temb_ld
+    if res is not None:
+        res.check()
+        a.res, a.ldres = res.ptr, res.ldc
+    a.osy, a.osx, a.ooy, a.oox = out_map
+    if out_nchw is not None:
+        _req(out_nchw.is_contiguous() and out_nchw.shape[0] == B and out_nchw.shape[1] == N, 'NCHW output shape')
+        a.out = out_nchw.data_ptr()
+        a.ldo = 0
+        a.Ho, a.Wo = out_nchw.shape[2], out_nchw.shape[3]
+        a.out_nchw = 1
+    else:
+        out.check()
+        _req(out.C == N and out.B == B, 'output view shape')
+        a.out, a.ldo, a.Ho, a.Wo = out.ptr, out.ldc, out.H, out.W
+    if PROFILE is None:
+        _native.call('wc_conv_igemm', ctypes.byref(a), _stream())
+        return
+    ktot = sum(len(sg.taps) * sg.view.C for sg in segs)
+    flops = 2.0 * B * Hm * Wm * N * ktot
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _native.call('wc_conv_igemm', ctypes.byref(a), _stream())
+    e1.record()
+    PROFILE.append(('256x64' if N <= 64 else '128x128', flops, e0, e1))
+
+
+def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float = 1e-5,
+              groups: int = 8) -> Tuple[torch.Tensor, torch.Tensor]:
+    """GroupNorm statistics of a view -> per-(b, c) (scale, shift) so that GN(x) = x*scale + shift."""
+    v.check()
+    B, HW, C = v.B, v.H * v.W, v.C
+    lib = _native.load()
+    splits = lib.wc_gn_num_splits(B, HW, C)
+    part = torch.empty((B, splits, groups, 2), dtype=torch.float32, device=v.t.device)
+    scale = torch.empty((B, C), dtype=torch.float32, device=v.t.device)
+    shift = torch.empty_like(scale)
+    s = _stream()
+    _native.call('wc_gn_stats', v.ptr, B, HW, C, v.ldc, groups, part.data_ptr(), s)
+    _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps,
+                 scale.data_ptr(), shift.data_ptr(), s)
+    return scale, shift
+
+
+def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int):
+    _req(qkv.shape == (B * N, 3 * C) and qkv.is_contiguous(), 'qkv shape')
+    _req(out.shape == (B * N, C) and out.is_contiguous(), 'attention output shape')
+    d = C // heads
+    _native.call('wc_attention_fwd', qkv.data_ptr(), 3 * C, out.data_ptr(), C, B, N, C, heads, float(d)**-0.5,
+                 _stream())
+
+
+def temb(t: torch.Tensor, w1, b1, w2, b2, proj_w, proj_b) -> torch.Tensor:
+    _req(t.dtype == torch.int64 and t.is_cuda and t.dim() == 1, 'timesteps must be a 1-D int64 device tensor')
+    nt = t.shape[0]
+    D = w1.shape[0]
+    P = proj_w.shape[0]
+    out = torch.empty((nt, P), dtype=torch.float32, device=t.device)
+    _native.call('wc_temb', t.data_ptr(), nt, D, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                 proj_w.data_ptr(), proj_b.data_ptr(), P, out.data_ptr(), _stream())
+    return out
+
+
+def conv_in(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: View):
+    _req(x.is_contiguous() and x.dtype == torch.float32 and x.dim() == 4, 'conv_in input must be NCHW fp32')
+    B, Cin, H, W = x.shape
+    out.check()
+    _req(out.H == H and out.W == W and out.B == B, 'conv_in output view shape')
+    _native.call('wc_conv_in', x.data_ptr(), B, Cin, H, W, w.data_ptr(), b.data_ptr(), out.C, out.ptr, out.ldc,
+                 _stream())
+
+
+def ddpm_step(x: torch.Tensor, eps: torch.Tensor, out: torch.Tensor, beta: float, s1m: float, sqrt_alpha: float,
+              sigma: float, *, z: Optional[torch.Tensor] = None, mode: int = _native.NOISE_NONE, seed: int = 0,
+              sample0: int = 0, step: int = 0, sz_out: Optional[torch.Tensor] = None):
+    _req(x.shape == eps.shape == out.shape and x.is_contiguous() and eps.is_contiguous() and out.is_contiguous(),
+         'ddpm_step shapes')
+    if mode == _native.NOISE_TENSOR:
+        _req(z is not None and z.shape == x.shape and z.is_contiguous() and z.is_cuda, 'noise tensor shape')
+    B = x.shape[0]
+    per = x.numel() // B
+    if sz_out is not None:
+        _req(sz_out.shape == x.shape and sz_out.is_contiguous(), 'sz_out shape')
+    _native.call('wc_ddpm_step', x.data_ptr(), eps.data_ptr(), _ptr(z), out.data_ptr(), _ptr(sz_out), B, per, beta, s1m,
+                 sqrt_alpha, sigma, mode, seed & ((1 << 64) - 1), sample0, step, _stream())
+
+
+def add_noise(x0: torch.Tensor, noise: torch.Tensor, coef_a: torch.Tensor, coef_b: torch.Tensor) -> torch.Tensor:
+    _req(x0.shape == noise.shape and x0.is_contiguous() and noise.is_contiguous(), 'add_noise shapes')
+    B = x0.shape[0]
+    _req(coef_a.numel() == B and coef_b.numel() == B, 'add_noise coefficient count')
+    out = torch.empty_like(x0)
+    _native.call('wc_add_noise', x0.data_ptr(), noise.data_ptr(), coef_a.contiguous().data_ptr(),
+                 coef_b.contiguous().data_ptr(), out.data_ptr(), B, x0.numel() // B, _stream())
+    return out
+
+
+def philox_normal(shape, device, seed: int, sample0: int = 0, step: int = 0) -> torch.Tensor:
+    out = torch.empty(shape, dtype=torch.float32, device=device)
+    B = shape[0]
+    _native.call('wc_philox_normal', out.data_ptr(), B, out.numel() // B, seed & ((1 << 64) - 1), sample0, step,
+                 _stream())
+    return out
+
+
+def sgg_update(grad: torch.Tensor, mu: torch.Tensor, sigma: torch.Tensor, lam: float,
+               std=(0.229, 0.224, 0.225), batch_axis_sum: bool = False):
+    """Returns (xt, magnitude) — see include/wc_kernels.h wc_sgg_update."""
+    nb, c3, S, S2 = mu.shape
+    _req(c3 == 3 and S == S2 and sigma.shape == mu.shape, 'mu/sigma must be (nb, 3, S, S)')
+    _req(grad.shape == (nb, 3, 4 * S, 4 * S), 'grad must be (nb, 3, 4S, 4S)')
+    grad, mu, sigma = grad.contiguous(), mu.contiguous(), sigma.contiguous()
+    xt = torch.empty_like(mu)
+    mag = torch.empty((3 if batch_axis_sum else nb, S, S), dtype=torch.float32, device=mu.device)
+    _native.call('wc_sgg_update', grad.data_ptr(), mu.data_ptr(), sigma.data_ptr(), xt.data_ptr(), mag.data_ptr(),
+                 nb, S, float(lam), float(std[0]), float(std[1]), float(std[2]), int(batch_axis_sum), _stream())
+    return xt, mag

@@ -70,7 +70,7 @@ def test_unet_256_batch16_rows_match_singletons():
     assert torch.isfinite(y).all()
     g = np.load(os.path.join(GOLDEN, 'unet_256.npz'))
     assert rel_l2(y[:1].cpu(), g['y']) < 1e-5
-    assert rel_l2(y[:1], y0) < 1e-6 and rel_l2(y[9:10], y9) < 1e-6
+    assert rel_l2(y[:1], y0) < 1e-5 and rel_l2(y[9:10], y9) < 1e-5
 
 
 def test_trajectory_config1_reference_rng():

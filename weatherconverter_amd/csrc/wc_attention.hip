@@ -215,7 +215,12 @@ extern "C" int wc_attention_fwd(const float* qkv, int ld_qkv, float* out, int ld
     const int D = C / heads;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     switch (D) {
+        case 8: return launch_att<8>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
         case 16: return launch_att<16>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 24: return launch_att<24>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 48: return launch_att<48>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 96: return launch_att<96>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 160: return launch_att<160>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
         case 32: return launch_att<32>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
         case 64: return launch_att<64>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
         case 128: return launch_att<128>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);

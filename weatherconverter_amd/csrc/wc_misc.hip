@@ -141,8 +141,9 @@ WC_DEVICE f32x4 normal4(uint64_t seed, uint32_t e4, uint32_t sample, uint32_t st
 }
 
 // Reverse step (linear_noise_scheduler.py:96-116 / :63-77).  Operation order and rounding follow
-// the reference's tensor ops exactly (explicit _rn intrinsics: no FMA contraction), so with an
-// identical z the result is bitwise equal to the PyTorch CPU path.
+// the reference's tensor ops exactly (IEEE division, FP contraction pinned off: sigma*z is rounded
+// before the add, as the reference's separate tensor ops), so with identical tables and z the
+// result is bitwise equal to the PyTorch CPU path.
 __global__ __launch_bounds__(256) void ddpm_step_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ eps,
                                                         const float* __restrict__ z,
@@ -152,6 +153,7 @@ __global__ __launch_bounds__(256) void ddpm_step_kernel(const float* __restrict_
                                                         float sqa, float sigma, int mode,
                                                         uint64_t seed, int64_t sample0,
                                                         int64_t step) {
+#pragma clang fp contract(off)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * blockDim.x) {
         f32x4 xv = reinterpret_cast<const f32x4*>(x)[i];
@@ -187,6 +189,7 @@ __global__ __launch_bounds__(256) void add_noise_kernel(const float* __restrict_
                                                         const float* __restrict__ cb,
                                                         float* __restrict__ out, int64_t n4,
                                                         int64_t per4) {
+#pragma clang fp contract(off)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * blockDim.x) {
         int64_t smp = i / per4;

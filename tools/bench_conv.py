@@ -1,0 +1,95 @@
+"""Micro-benchmark of wc_conv_igemm / wc_attention_fwd on the 256-px UNet shapes (B=16), with a
+correctness spot check against torch fp32 on the GPU (torch conv: tf32 disabled)."""
+import argparse
+import sys
+import os
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from weatherconverter_amd import kernels as K  # noqa: E402
+
+TAPS3 = [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]
+
+
+def timeit(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False):
+    g = torch.Generator(device='cuda').manual_seed(0)
+    x = torch.randn((B, H, H, Ci), device='cuda', generator=g)
+    w = torch.randn((Co, 9 * Ci + res), device='cuda', generator=g) / (9 * Ci)**0.5
+    b = torch.randn(Co, device='cuda', generator=g)
+    sc = torch.rand((B, Ci), device='cuda', generator=g) + 0.5
+    sh = torch.randn((B, Ci), device='cuda', generator=g) * 0.1
+    out = torch.empty((B, H, H, Co), device='cuda')
+    segs = [K.Seg(K.View.full(x), TAPS3, scale=sc if prologue else None, shift=sh if prologue else None,
+                  silu=prologue)]
+    if res:
+        xr = torch.randn((B, H, H, res), device='cuda', generator=g)
+        segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=9 * Ci))
+    fn = lambda: K.conv_igemm(segs, w, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
+    t = timeit(fn)
+    fl = 2.0 * B * H * H * Co * (9 * Ci + res)
+    err = None
+    if check:
+        xx = x.permute(0, 3, 1, 2)
+        a = F.silu(xx * sc[:, :, None, None] + sh[:, :, None, None]) if prologue else xx
+        wt = w[:, :9 * Ci].reshape(Co, 3, 3, Ci).permute(0, 3, 1, 2)
+        torch.backends.cudnn.allow_tf32 = False
+        ref = F.conv2d(a, wt, b, padding=1)
+        if res:
+            ref = ref + F.conv2d(xr.permute(0, 3, 1, 2), w[:, 9 * Ci:].reshape(Co, res, 1, 1))
+        fn()
+        torch.cuda.synchronize()
+        got = out.permute(0, 3, 1, 2)
+        err = float((got.double() - ref.double()).norm() / ref.double().norm())
+    return t, fl / t / 1e12, err
+
+
+def attn_case(B, N, C):
+    qkv = torch.randn((B * N, 3 * C), device='cuda')
+    o = torch.empty((B * N, C), device='cuda')
+    t = timeit(lambda: K.attention(qkv, o, B, N, C, 4))
+    fl = 4.0 * B * N * N * C
+    return t, fl / t / 1e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--check', action='store_true')
+    ap.add_argument('--only', type=int, default=-1, help='run a single conv case (for PMC profiling)')
+    a = ap.parse_args()
+    K._native.load()
+    cases = [(16, 256, 128, 128, True, 0), (16, 256, 128, 128, True, 64), (16, 256, 64, 64, True, 0),
+             (16, 128, 256, 256, True, 0), (16, 64, 512, 512, True, 0), (16, 32, 768, 768, True, 0),
+             (16, 32, 1024, 256, True, 0), (16, 256, 64, 128, False, 0)]
+    tot_t = tot_f = 0
+    if a.only >= 0:
+        cases = [cases[a.only]]
+    for c in cases:
+        t, tf, err = conv_case(*c, check=a.check)
+        tot_t += t
+        tot_f += tf * t
+        print(f'conv B={c[0]} S={c[1]} {c[2]}->{c[3]} prologue={c[4]} res={c[5]}: {t*1e3:8.3f} ms  {tf:6.1f} TF/s'
+              + (f'  relL2={err:.2e}' if err is not None else ''), flush=True)
+    print(f'conv aggregate {tot_f / tot_t:.1f} TF/s')
+    if a.only >= 0:
+        return
+    for c in [(16, 4096, 512), (16, 1024, 768), (16, 1024, 512), (16, 4096, 128), (16, 1024, 256)]:
+        t, tf = attn_case(*c)
+        print(f'attn B={c[0]} N={c[1]} C={c[2]}: {t*1e3:8.3f} ms  {tf:6.1f} TF/s', flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -171,6 +171,7 @@ __global__ __launch_bounds__(256) void ddpm_step_kernel(const float* __restrict_
             float m = __fsub_rn(xv[k], __fdiv_rn(__fmul_rn(beta, ev[k]), s1m));
             m = __fdiv_rn(m, sqa);
             float sz = __fmul_rn(sigma, zv[k]);
+            asm volatile("" : "+v"(sz));  // sigma*z is rounded before the add (no FMA), as the reference
             if (szo) {
                 r[k] = m;
                 sq[k] = sz;
@@ -198,7 +199,11 @@ __global__ __launch_bounds__(256) void add_noise_kernel(const float* __restrict_
         f32x4 nv = reinterpret_cast<const f32x4*>(nz)[i];
         f32x4 r;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a, xv[k]), __fmul_rn(bb, nv[k]));
+        for (int k = 0; k < 4; ++k) {
+            float p0 = __fmul_rn(a, xv[k]), p1 = __fmul_rn(bb, nv[k]);
+            asm volatile("" : "+v"(p0), "+v"(p1));  // both products rounded before the add
+            r[k] = __fadd_rn(p0, p1);
+        }
         reinterpret_cast<f32x4*>(out)[i] = r;
     }
 }

@@ -36,18 +36,16 @@ constexpr unsigned OOB = 0x80000000u;  // byte offset past the SRD range -> load
 constexpr int SRD_BYTES = 0x7FFFFFFF;
 constexpr int SRD_FLAGS = 0x00020000;
 
-struct SegDev {
-    const float* src;
-    int C, ldc, H, W, sy, sx, ntaps, kbase;
-    int dy[WC_MAX_TAPS];
-    int dx[WC_MAX_TAPS];
+struct ConvDev {
+    // segment 0: the conv input, read through a kh x kw tap grid, optional GN prologue
+    const float* src0;
+    int C0, ldc0, H0, W0, sy, sx;
+    int kh, kw, ty0, tdy, tx0, tdx;  // tap (ky, kx) reads input (y*sy + ty0 + ky*tdy, x*sx + tx0 + kx*tdx)
     const float* scale;
     const float* shift;
-};
-
-struct ConvDev {
-    SegDev seg[2];
-    int nseg;
+    // segment 1 (optional): raw 1x1 input at the same pixel (the fused residual_input_conv)
+    const float* src1;
+    int C1, ldc1, kbase1;
     int B, Hm, Wm, N, M;
     const float* w;
     int ldw;
@@ -60,6 +58,7 @@ struct ConvDev {
     int ldo;
     int Ho, Wo, osy, osx, ooy, oox, out_nchw;
     int ident;    // output position == GEMM row (plain NHWC store)
+    int steps0;   // K-steps of segment 0
     int steps;    // total K-steps
     int ntiles_n; // N tiles
 };
@@ -114,104 +113,101 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
     const int n0 = tile_n * BN;
     const int HWm = p.Hm * p.Wm;
 
-    // ---- per-thread staging coordinates ----
+    // ---- per-thread staging coordinates (fixed for the whole K loop) ----
     const int q4 = tid & 7;     // 16-byte chunk (4 channels) within the 32-channel step
     const int prow = tid >> 3;  // 0..31
     const int wsw = ((q4 ^ ((prow >> 1) & 7)) << 2);  // swizzled column of this thread's writes
-    int pb[T::A_PER_T], py[T::A_PER_T], px[T::A_PER_T];
+    int pb[T::A_PER_T], ys[T::A_PER_T], xs[T::A_PER_T], org0[T::A_PER_T], org1[T::A_PER_T];
 #pragma unroll
     for (int j = 0; j < T::A_PER_T; ++j) {
-        int m = m0 + prow + 32 * j;
+        const int m = m0 + prow + 32 * j;
         if (m < p.M) {
-            int b = m / HWm;
-            int r = m - b * HWm;
+            const int b = m / HWm;
+            const int r = m - b * HWm;
+            const int y = r / p.Wm;
+            const int x = r - y * p.Wm;
             pb[j] = b;
-            py[j] = r / p.Wm;
-            px[j] = r - py[j] * p.Wm;
+            ys[j] = y * p.sy;
+            xs[j] = x * p.sx;
+            org0[j] = ((b * p.H0 + ys[j]) * p.W0 + xs[j]) * p.ldc0 + q4 * 4;
+            org1[j] = ((b * p.H0 + ys[j]) * p.W0 + xs[j]) * p.ldc1 + q4 * 4;
         } else {
-            pb[j] = -1; py[j] = -(1 << 20); px[j] = 0;  // never in range
+            pb[j] = -1; ys[j] = -(1 << 24); xs[j] = 0; org0[j] = 0; org1[j] = 0;  // never in range
         }
     }
     const int b_tile = m0 / HWm;  // the image of the whole tile when UNIB
 
-    // ---- scalar K-step state machine for the NEXT load ----
-    int ls = 0, ltap = 0, lc0 = 0;   // segment, tap, channel block of the next load
-    // per-segment, per-thread pixel origin offsets (floats) and sampling coordinates
-    int org[T::A_PER_T], ys[T::A_PER_T], xs[T::A_PER_T];
-    __amdgpu_buffer_rsrc_t srd_a = make_srd(p.seg[0].src);
-    __amdgpu_buffer_rsrc_t srd_w = make_srd(p.w);
-    __amdgpu_buffer_rsrc_t srd_sc = make_srd(PRO ? p.seg[0].scale : p.w);
-    __amdgpu_buffer_rsrc_t srd_sh = make_srd(PRO ? p.seg[0].shift : p.w);
-    int sH = p.seg[0].H, sW = p.seg[0].W, sldc = p.seg[0].ldc, sC = p.seg[0].C;
-    int sntaps = p.seg[0].ntaps, skbase = p.seg[0].kbase;
-
-    auto set_segment = [&](int s) {
-        const SegDev& sg = p.seg[s];
-        srd_a = make_srd(sg.src);
-        sH = sg.H; sW = sg.W; sldc = sg.ldc; sC = sg.C; sntaps = sg.ntaps; skbase = sg.kbase;
-#pragma unroll
-        for (int j = 0; j < T::A_PER_T; ++j) {
-            ys[j] = py[j] * sg.sy;
-            xs[j] = px[j] * sg.sx;
-            org[j] = pb[j] < 0 ? 0 : ((pb[j] * sg.H + ys[j]) * sg.W + xs[j]) * sg.ldc + q4 * 4;
-        }
-    };
-    set_segment(0);
+    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
+    const __amdgpu_buffer_rsrc_t srd1 = make_srd(p.src1 ? p.src1 : p.src0);
+    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.w);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.w);
 
     f32x4 ra[T::A_PER_T];
     f32x4 rb[T::B_PER_T];
     f32x4 rsc[UNIB ? 1 : T::A_PER_T], rsh[UNIB ? 1 : T::A_PER_T];
     unsigned aval = 0;
-    bool stage_pro = PRO != 0;  // whether the staged data (in ra) takes the prologue
 
-    auto load_step = [&]() {
-        const int dy = p.seg[ls].dy[ltap], dx = p.seg[ls].dx[ltap];
-        const int tap_off = (dy * sW + dx) * sldc + lc0;
+    // scalar state of the NEXT load in segment 0: tap (ky, kx) and channel block c0
+    int ky = 0, kx = 0, c0 = 0;
+
+    auto load_w = [&](int kcol) {
+#pragma unroll
+        for (int j = 0; j < T::B_PER_T; ++j) {
+            const int n = n0 + prow + 32 * j;
+            rb[j] = bload4(srdw, n < p.N ? (unsigned)(n * p.ldw + kcol) * 4u : OOB);
+        }
+    };
+    auto load0 = [&]() {
+        const int dy = p.ty0 + ky * p.tdy, dx = p.tx0 + kx * p.tdx;
+        const int tap_off = (dy * p.W0 + dx) * p.ldc0 + c0;
         aval = 0;
 #pragma unroll
         for (int j = 0; j < T::A_PER_T; ++j) {
             const int iy = ys[j] + dy, ix = xs[j] + dx;
-            const bool ok = (unsigned)iy < (unsigned)sH && (unsigned)ix < (unsigned)sW;
+            const bool ok = (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
             aval |= (ok ? 1u : 0u) << j;
-            ra[j] = bload4(srd_a, ok ? (unsigned)(org[j] + tap_off) * 4u : OOB);
+            ra[j] = bload4(srd0, ok ? (unsigned)(org0[j] + tap_off) * 4u : OOB);
         }
-        stage_pro = PRO != 0 && ls == 0;
         if constexpr (PRO != 0) {
-            if (ls == 0) {
-                const int c = lc0 + q4 * 4;
-                if constexpr (UNIB) {
-                    rsc[0] = bload4(srd_sc, (unsigned)(b_tile * sC + c) * 4u);
-                    rsh[0] = bload4(srd_sh, (unsigned)(b_tile * sC + c) * 4u);
-                } else {
+            const int c = c0 + q4 * 4;
+            if constexpr (UNIB) {
+                rsc[0] = bload4(srdsc, (unsigned)(b_tile * p.C0 + c) * 4u);
+                rsh[0] = bload4(srdsh, (unsigned)(b_tile * p.C0 + c) * 4u);
+            } else {
 #pragma unroll
-                    for (int j = 0; j < T::A_PER_T; ++j) {
-                        const unsigned o = pb[j] >= 0 ? (unsigned)(pb[j] * sC + c) * 4u : OOB;
-                        rsc[j] = bload4(srd_sc, o);
-                        rsh[j] = bload4(srd_sh, o);
-                    }
+                for (int j = 0; j < T::A_PER_T; ++j) {
+                    const unsigned o = pb[j] >= 0 ? (unsigned)(pb[j] * p.C0 + c) * 4u : OOB;
+                    rsc[j] = bload4(srdsc, o);
+                    rsh[j] = bload4(srdsh, o);
                 }
             }
         }
-        const int kcol = skbase + ltap * sC + lc0 + q4 * 4;
+        load_w((ky * p.kw + kx) * p.C0 + c0 + q4 * 4);
+        // advance (branch-free scalar selects)
+        c0 += BK;
+        const bool wc = c0 == p.C0;
+        c0 = wc ? 0 : c0;
+        kx += wc ? 1 : 0;
+        const bool wx = kx == p.kw;
+        kx = wx ? 0 : kx;
+        ky += wx ? 1 : 0;
+    };
+    int c1 = 0;  // next channel block of segment 1
+    auto load1 = [&]() {
+        aval = 0;
 #pragma unroll
-        for (int j = 0; j < T::B_PER_T; ++j) {
-            const int n = n0 + prow + 32 * j;
-            rb[j] = bload4(srd_w, n < p.N ? (unsigned)(n * p.ldw + kcol) * 4u : OOB);
+        for (int j = 0; j < T::A_PER_T; ++j) {
+            aval |= (pb[j] >= 0 ? 1u : 0u) << j;
+            ra[j] = bload4(srd1, pb[j] >= 0 ? (unsigned)(org1[j] + c1) * 4u : OOB);
         }
-        // advance the state machine (uniform scalar branches)
-        lc0 += BK;
-        if (lc0 == sC) {
-            lc0 = 0;
-            if (++ltap == sntaps) {
-                ltap = 0;
-                if (++ls < p.nseg) set_segment(ls);
-            }
-        }
+        load_w(p.kbase1 + c1 + q4 * 4);
+        c1 += BK;
     };
 
-    auto store_step = [&](float* buf) {
+    auto store = [&](float* buf, bool pro) {
         if constexpr (PRO != 0) {
-            if (stage_pro) {
+            if (pro) {
 #pragma unroll
                 for (int j = 0; j < T::A_PER_T; ++j) {
                     f32x4 v = ra[j] * rsc[UNIB ? 0 : j] + rsh[UNIB ? 0 : j];
@@ -251,20 +247,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
     const int a_row = (wm * 64 + l32) * BK;
     const int b_row = BM * BK + (wn * 64 + l32) * BK;
 
-    auto compute = [&](const float* buf) {
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(buf + a_row + koff[0]);
-        f32x4 a1 = *reinterpret_cast<const f32x4*>(buf + a_row + 32 * BK + koff[0]);
-        f32x4 b0 = *reinterpret_cast<const f32x4*>(buf + b_row + koff[0]);
-        f32x4 b1 = *reinterpret_cast<const f32x4*>(buf + b_row + 32 * BK + koff[0]);
+    // MFMAs of k-chunks [KQ0, KQ1) (4 channels each); fragments of chunk kq+1 are read under chunk kq.
+    f32x4 fa0, fa1, fb0, fb1;
+    auto frag = [&](const float* buf, int kq) {
+        fa0 = *reinterpret_cast<const f32x4*>(buf + a_row + koff[kq]);
+        fa1 = *reinterpret_cast<const f32x4*>(buf + a_row + 32 * BK + koff[kq]);
+        fb0 = *reinterpret_cast<const f32x4*>(buf + b_row + koff[kq]);
+        fb1 = *reinterpret_cast<const f32x4*>(buf + b_row + 32 * BK + koff[kq]);
+    };
+    auto compute = [&](const float* buf, int kq0, int kq1, bool prefetch_next_step_frag) {
 #pragma unroll
-        for (int kq = 0; kq < 4; ++kq) {
-            f32x4 na0, na1, nb0, nb1;
-            if (kq < 3) {  // prefetch the next chunk's fragments under this chunk's MFMAs
-                na0 = *reinterpret_cast<const f32x4*>(buf + a_row + koff[kq + 1]);
-                na1 = *reinterpret_cast<const f32x4*>(buf + a_row + 32 * BK + koff[kq + 1]);
-                nb0 = *reinterpret_cast<const f32x4*>(buf + b_row + koff[kq + 1]);
-                nb1 = *reinterpret_cast<const f32x4*>(buf + b_row + 32 * BK + koff[kq + 1]);
-            }
+        for (int kq = kq0; kq < kq1; ++kq) {
+            const f32x4 a0 = fa0, a1 = fa1, b0 = fb0, b1 = fb1;
+            if (kq < 3) frag(buf, kq + 1);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 acc[0][0] = mfma32(a0[j], b0[j], acc[0][0]);
@@ -272,23 +267,58 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
                 acc[1][0] = mfma32(a1[j], b0[j], acc[1][0]);
                 acc[1][1] = mfma32(a1[j], b1[j], acc[1][1]);
             }
-            if (kq < 3) { a0 = na0; a1 = na1; b0 = nb0; b1 = nb1; }
         }
+        (void)prefetch_next_step_frag;
     };
 
-    load_step();
-    store_step(lds);
-    __syncthreads();
+    // ---- K loop: one barrier per step; phase A loads segment 0, phase B segment 1 ----
+    // Per step: [next step's buffer loads] [MFMA chunks 0-1] [MFMA chunks 2-3 interleaved with the
+    // prologue VALU and the LDS writes of the next step, 1 MFMA : 5 VALU] [barrier].  The loads have
+    // 32 MFMAs (~2k cycles) to land before the interleaved half consumes them.
+#define WC_INTERLEAVE()                                                         \
+    do {                                                                        \
+        _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                     \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); /* MFMA */       \
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0); /* VALU */       \
+            if (i_ % 4 == 3)                                                    \
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0); /* DS wr */  \
+        }                                                                       \
+    } while (0)
 
-    for (int step = 0; step < p.steps; ++step) {
+    if (p.steps0 > 0) { load0(); store(lds, true); } else { load1(); store(lds, false); }
+    __syncthreads();
+    int step = 0;
+    for (; step < p.steps0 - 1; ++step) {
         float* cur = lds + (step & 1) * T::STAGE;
         float* nxt = lds + ((step & 1) ^ 1) * T::STAGE;
-        const bool more = step + 1 < p.steps;
-        if (more) load_step();
-        compute(cur);
-        if (more) store_step(nxt);
+        load0();
+        __builtin_amdgcn_sched_barrier(0);  // keep the next step's loads ahead of the MFMAs
+        frag(cur, 0);
+        compute(cur, 0, 2, false);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cur, 2, 4, false);
+        store(nxt, true);
+        WC_INTERLEAVE();
+        __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
     }
+    for (; step < p.steps - 1; ++step) {
+        float* cur = lds + (step & 1) * T::STAGE;
+        float* nxt = lds + ((step & 1) ^ 1) * T::STAGE;
+        load1();
+        __builtin_amdgcn_sched_barrier(0);
+        frag(cur, 0);
+        compute(cur, 0, 2, false);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cur, 2, 4, false);
+        store(nxt, false);
+        WC_INTERLEAVE();
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    }
+    frag(lds + (step & 1) * T::STAGE, 0);
+    compute(lds + (step & 1) * T::STAGE, 0, 4, false);
+#undef WC_INTERLEAVE
 
     // ---- epilogue ----
     const int HWo = p.Ho * p.Wo;
@@ -361,28 +391,43 @@ extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     if (!a || !a->w || !a->out) return WC_E_ARG;
     if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
     ConvDev d{};
-    long k = 0;
-    for (int s = 0; s < a->nseg; ++s) {
-        const wc_conv_seg& sg = a->seg[s];
-        if (!sg.src) return WC_E_ARG;
-        if (sg.C <= 0 || sg.C % BK != 0 || sg.ldc % 4 != 0) return WC_E_SHAPE;
-        if (sg.ntaps < 1 || sg.ntaps > WC_MAX_TAPS) return WC_E_SHAPE;
-        if ((reinterpret_cast<uintptr_t>(sg.src) & 15) != 0) return WC_E_SHAPE;
-        if ((sg.scale == nullptr) != (sg.shift == nullptr)) return WC_E_ARG;
-        if (s == 1 && sg.scale) return WC_E_ARG;  // the residual segment is read raw
-        // every byte offset the kernel forms must stay below the 2 GiB buffer range
-        if ((long)a->B * sg.H * sg.W * sg.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
-        SegDev& o = d.seg[s];
-        o.src = sg.src; o.C = sg.C; o.ldc = sg.ldc; o.H = sg.H; o.W = sg.W;
-        o.sy = sg.sy; o.sx = sg.sx; o.ntaps = sg.ntaps; o.kbase = sg.kbase;
-        for (int t = 0; t < sg.ntaps; ++t) { o.dy[t] = sg.dy[t]; o.dx[t] = sg.dx[t]; }
-        o.scale = sg.scale; o.shift = sg.shift;
-        if (sg.kbase + sg.ntaps * sg.C > a->ldw) return WC_E_SHAPE;
-        k += (long)sg.ntaps * sg.C;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src) return WC_E_ARG;
+    if (s0.C <= 0 || s0.C % BK != 0 || s0.ldc % 4 != 0) return WC_E_SHAPE;
+    if (s0.ntaps < 1 || s0.ntaps > WC_MAX_TAPS) return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(s0.src) & 15) != 0) return WC_E_SHAPE;
+    if ((s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
+    if (s0.kbase != 0) return WC_E_SHAPE;
+    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;  // 2 GiB SRD range
+    // the taps must form a kh x kw grid: tap t = (ty0 + (t / kw) * tdy, tx0 + (t % kw) * tdx)
+    int kw = 1;
+    while (kw < s0.ntaps && s0.dy[kw] == s0.dy[0]) ++kw;
+    if (s0.ntaps % kw != 0) return WC_E_SHAPE;
+    const int kh = s0.ntaps / kw;
+    const int tdx = kw > 1 ? s0.dx[1] - s0.dx[0] : 0;
+    const int tdy = kh > 1 ? s0.dy[kw] - s0.dy[0] : 0;
+    for (int t = 0; t < s0.ntaps; ++t)
+        if (s0.dy[t] != s0.dy[0] + (t / kw) * tdy || s0.dx[t] != s0.dx[0] + (t % kw) * tdx) return WC_E_SHAPE;
+    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.H0 = s0.H; d.W0 = s0.W; d.sy = s0.sy; d.sx = s0.sx;
+    d.kh = kh; d.kw = kw; d.ty0 = s0.dy[0]; d.tdy = tdy; d.tx0 = s0.dx[0]; d.tdx = tdx;
+    d.scale = s0.scale; d.shift = s0.shift;
+    long k = (long)s0.ntaps * s0.C;
+    if (a->nseg == 2) {
+        // the fused residual: raw 1x1 read of a view with the same spatial grid as segment 0
+        const wc_conv_seg& s1 = a->seg[1];
+        if (!s1.src || s1.scale) return WC_E_ARG;
+        if (s1.C <= 0 || s1.C % BK != 0 || s1.ldc % 4 != 0) return WC_E_SHAPE;
+        if ((reinterpret_cast<uintptr_t>(s1.src) & 15) != 0) return WC_E_SHAPE;
+        if (s1.ntaps != 1 || s1.dy[0] != 0 || s1.dx[0] != 0) return WC_E_SHAPE;
+        if (s1.H != s0.H || s1.W != s0.W || s1.sy != s0.sy || s1.sx != s0.sx) return WC_E_SHAPE;
+        if (s1.kbase != k) return WC_E_SHAPE;
+        if ((long)a->B * s1.H * s1.W * s1.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+        d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc; d.kbase1 = s1.kbase;
+        k += s1.C;
     }
+    if (k > a->ldw) return WC_E_SHAPE;
     if (a->ldw % 4 != 0 || (reinterpret_cast<uintptr_t>(a->w) & 15) != 0) return WC_E_SHAPE;
     if ((long)a->N * a->ldw * 4 >= (1L << 31)) return WC_E_SHAPE;
-    d.nseg = a->nseg;
     d.B = a->B; d.Hm = a->Hm; d.Wm = a->Wm; d.N = a->N;
     long M = (long)a->B * a->Hm * a->Wm;
     if (M <= 0 || M > (1L << 30) || a->N <= 0) return WC_E_SHAPE;
@@ -393,8 +438,9 @@ extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     d.out_nchw = a->out_nchw;
     d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
               a->Ho == a->Hm && a->Wo == a->Wm;
+    d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
     d.steps = (int)(k / BK);
-    const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
+    const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // 64-column outputs (C_out = 64 stages, the 3-channel head) use a 256x64 tile.
     if (a->N <= 64) return dispatch<256, 64>(d, pro, s);

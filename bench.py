@@ -14,9 +14,9 @@ noise keyed by (seed, global sample, step).
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run (RCCL).
 Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
   roofline      per-launch HIP events around every implicit-GEMM conv of one UNet forward; the
-                dominant kernel is conv_igemm_kernel<128,128> (fp32 MFMA) — achieved = its
-                algorithmic FLOPs per launch / its mean launch duration, against the 157.3 TF
-                fp32 MFMA peak (MI355X_MICROARCH.md).
+                dominant kernel is the conv_igemm_kernel instantiation with the most time (the
+                GN+SiLU-prologue 3x3 convs) — achieved = its algorithmic FLOPs per launch / its mean
+                launch duration, against the 157.3 TF fp32 MFMA peak (MI355X_MICROARCH.md).
   cpu_baseline  the oracle's PyTorch-CPU restatement of the reference UNet step (N=1 only), on a
                 bounded sample (a few 256-px UNet steps), extrapolated x T.
 """
@@ -64,12 +64,14 @@ def roofline_leg(model, x, t_dev):
         d[0] += 1
         d[1] += flops
         d[2] += e0.elapsed_time(e1) * 1e-3
-    n, fl, sec = per['128x128']
+    # dominant kernel = the conv_igemm instantiation with the most event time in one UNet forward
+    name = max(per, key=lambda k: per[k][2])
+    n, fl, sec = per[name]
     mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
     total_conv = sum(v[2] for v in per.values())
     return {
-        'kernel': 'conv_igemm_kernel<128,128> (fp32 MFMA implicit-GEMM conv)',
+        'kernel': name + ' (fp32 MFMA implicit-GEMM conv, GN+SiLU prologue)',
         'bound': 'mfma',
         'achieved': round(achieved, 2),
         'peak': FP32_PEAK_TFLOPS,
@@ -79,7 +81,7 @@ def roofline_leg(model, x, t_dev):
         'launches_per_step': n,
         'mean_launch_ms': round(mean_dur * 1e3, 4),
         'gflop_per_launch': round(fl / n / 1e9, 3),
-        'conv_share_of_event_time': round(sec / max(total_conv, 1e-12), 3),
+        'share_of_conv_event_time': round(sec / max(total_conv, 1e-12), 3),
     }
 
 

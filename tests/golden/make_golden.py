@@ -47,10 +47,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reference', default='/root/reference')
     ap.add_argument('--skip-traj', action='store_true')
+    ap.add_argument('--only-guided', action='store_true')
     args = ap.parse_args()
     sys.path.insert(0, args.reference)
     torch.Tensor.cuda = lambda self, *a, **k: self  # harness shim for unet_base.py:461
     torch.set_num_threads(8)
+    if args.only_guided:
+        return guided(args)
     from diffusion_model.config import models as ref_models
     from diffusion_model.models.unet_base import Unet, get_time_embedding
     from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
@@ -148,6 +151,55 @@ def main():
                 xt = mean + sigma if i != 0 else mean
         np.savez(os.path.join(HERE, 'traj_64_T50.npz'), x0=xt.numpy(), eps_first=eps_first.numpy(), seed=3455)
         print('traj done', float(xt.abs().max()))
+
+
+def guided(args):
+    """guided.npz + guided_manifest.json: DeepLabV3+ R101 OS16 (seg_model.network) logits and input
+    gradient, the apply_gsg update (sgg.py:16-22 + inference.py:39-53 restated: those modules import
+    torchvision, absent here), and the Swift-SRGAN generator (srgan_model.models)."""
+    import torch.nn.functional as F
+    from seg_model.network.modeling import deeplabv3plus_resnet101
+    from srgan_model.models import Generator
+    torch.set_num_threads(8)
+    out, manifest = {}, {}
+    seg = deeplabv3plus_resnet101(num_classes=19, output_stride=16, pretrained_backbone=False)
+    sd = synthetic_state_dict(seg.state_dict(), seed=0)
+    seg.load_state_dict(sd)
+    seg.eval()
+    manifest['deeplabv3plus_resnet101'] = [[k, list(v.shape)] for k, v in seg.state_dict().items()]
+    out['seg_digest'] = state_dict_digest(sd)
+    g = torch.Generator().manual_seed(41)
+    sr = torch.randn((1, 3, 32, 32), generator=g)
+    gt = torch.randint(0, 19, (1, 32, 32), generator=g)
+    gt[torch.rand((1, 32, 32), generator=g) < 0.05] = 255
+    x = sr.clone().requires_grad_(True)  # inference.py:118-152 restated
+    logits = seg(x)
+    loss = torch.nn.CrossEntropyLoss(ignore_index=255)(logits, gt.squeeze(1))
+    loss.backward()
+    out['sr'] = sr.numpy()
+    out['gt'] = gt.numpy()
+    out['logits'] = logits.detach().numpy()
+    out['grad'] = x.grad.numpy()
+    mu = torch.randn((1, 3, 8, 8), generator=g)
+    sigma = torch.randn((1, 3, 8, 8), generator=g) * 0.05
+    pooled = F.avg_pool2d(x.grad, kernel_size=4, stride=4)  # sgg.py:18
+    gn = pooled.squeeze(0).numpy() * np.array([0.229, 0.224, 0.225])[:, None, None]  # inference.py:39-42
+    mag = torch.from_numpy(np.sqrt(np.sum(gn**2, axis=0)))  # :43
+    out['mu'], out['sigma'] = mu.numpy(), sigma.numpy()
+    out['gsg_xt'] = ((mu + 60.0 * sigma * mag) + sigma).numpy()  # sgg.py:21-22, float64
+    gen = Generator(upscale_factor=4)
+    gsd = synthetic_state_dict(gen.state_dict(), seed=0)
+    gen.load_state_dict(gsd)
+    gen.eval()
+    manifest['srgan_generator'] = [[k, list(v.shape)] for k, v in gen.state_dict().items()]
+    out['srgan_digest'] = state_dict_digest(gsd)
+    lr = torch.rand((1, 3, 16, 16), generator=g)
+    with torch.no_grad():
+        out['srgan_in'], out['srgan_out'] = lr.numpy(), gen(lr).numpy()
+    np.savez(os.path.join(HERE, 'guided.npz'), **out)
+    with open(os.path.join(HERE, 'guided_manifest.json'), 'w') as fh:
+        json.dump(manifest, fh)
+    print('guided done', float(out['grad'].std()), float(np.abs(out['gsg_xt']).max()))
 
 
 if __name__ == '__main__':

@@ -149,7 +149,12 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
     e0.record()
     _native.call('wc_conv_igemm', ctypes.byref(a), _stream())
     e1.record()
-    PROFILE.append(('256x64' if N <= 64 else '128x128', flops, e0, e1))
+    # the kernel symbol wc_conv_igemm dispatches to (mirrors dispatch() in csrc/wc_conv.hip)
+    bm, bn = (256, 64) if N <= 64 else (128, 128)
+    s0 = segs[0]
+    pro = 0 if s0.scale is None else (2 if s0.silu else 1)
+    unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
+    PROFILE.append((f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}>', flops, e0, e1))
 
 
 def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float = 1e-5,

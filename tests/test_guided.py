@@ -90,11 +90,11 @@ def test_guided_translation_loop_modes():
     x = torch.rand((1, 3, 32, 32), generator=g) * 2 - 1
     gt = torch.randint(0, 19, (1, 128, 128), generator=g).cuda()
     noise = torch.randn((1, 3, 32, 32), generator=g)
-    kw = dict(N=6, t_start=torch.tensor([5]), noise=noise)
+    kw = dict(N=6, t_start=torch.tensor([5]), noise=noise, LAMBDA=1e6, return_latent=True)  # grads are ~1e-6
     torch.manual_seed(9)
-    ref = sample_with_sgg(x, unet, sched, seg, gt, gen, mode='reference', **kw)
+    ref, ref_lat = sample_with_sgg(x, unet, sched, seg, gt, gen, mode='reference', **kw)
     torch.manual_seed(9)
-    app = sample_with_sgg(x, unet, sched, seg, gt, gen, mode='applied', **kw)
+    app, app_lat = sample_with_sgg(x, unet, sched, seg, gt, gen, mode='applied', **kw)
     # plain DDPM from the same start and the same CPU noise stream
     torch.manual_seed(9)
     xt = sched.add_noise2(x.cuda(), noise.cuda(), torch.tensor([5]).cuda())
@@ -105,5 +105,5 @@ def test_guided_translation_loop_modes():
             xt = mu if i == 0 else (mu + sz)
         plain = gen(xt)
     assert ref.shape == (1, 3, 128, 128) and torch.isfinite(app).all()
-    assert rel_l2(ref, plain) < 1e-6
-    assert rel_l2(app, ref) > 1e-7
+    assert rel_l2(ref, plain) < 1e-6 and rel_l2(ref_lat, xt) < 1e-6
+    assert rel_l2(app_lat, ref_lat) > 1e-5  # the applied guidance moved the latent (ref vs plain < 1e-6)

@@ -24,7 +24,7 @@ from .srgan_model.models import inference as srgan_inference
 def sample_with_sgg(input_tensor: torch.Tensor, diff_model, diff_scheduler, seg_model, gt: torch.Tensor,
                     srgan_model, *, LAMBDA: float = 60.0, N: int = 500, mode: str = 'applied', use_lcg: bool = False,
                     t_start: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
-                    progress=None) -> torch.Tensor:
+                    progress=None, return_latent: bool = False):
     if mode not in ('reference', 'applied'):
         raise ValueError("mode must be 'reference' or 'applied'")
     dev = diff_scheduler.device
@@ -52,4 +52,5 @@ def sample_with_sgg(input_tensor: torch.Tensor, diff_model, diff_scheduler, seg_
             xt = (mu + sigma).contiguous()  # translation.py:90
         if progress is not None:
             progress(i)
-    return srgan_inference(srgan_model, xt)
+    sr_x0 = srgan_inference(srgan_model, xt)  # translation.py:95
+    return (sr_x0, xt) if return_latent else sr_x0

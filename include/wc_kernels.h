@@ -71,7 +71,13 @@ typedef struct wc_conv_args {
     int Ho, Wo;         /* output spatial extent */
     int osy, osx, ooy, oox; /* output position = (my*osy + ooy, mx*osx + oox) */
     int out_nchw;       /* 1: write out[(b*N + n)*Ho*Wo + oy*Wo + ox] (ldo ignored) */
+    int act;            /* epilogue activation after bias/temb, before the residual add:
+                           WC_ACT_NONE / WC_ACT_GELU (exact erf) / WC_ACT_SILU */
 } wc_conv_args;
+
+#define WC_ACT_NONE 0
+#define WC_ACT_GELU 1
+#define WC_ACT_SILU 2
 
 /* Replaces: nn.Conv2d 3x3/1x1/4x4-s2 and nn.ConvTranspose2d (per output parity), the GN+SiLU
  * prologue of nn.Sequential(GroupNorm, SiLU, Conv2d), the temb broadcast add, the 1x1
@@ -161,6 +167,24 @@ int wc_philox_normal(float* out, int64_t B, int64_t per_sample, uint64_t seed, i
 int wc_sgg_update(const float* grad, const float* mu, const float* sigma, float* xt_out,
                   float* mag_out, int nb, int S, float lambda_, double std0, double std1,
                   double std2, int sum_batch, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Older 128-px UNet (diffusion_model/models/old_modules.py:126-360)                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* nn.AvgPool2d(2) on an NHWC view (old_modules.py:185,192). */
+int wc_avgpool2x2(const float* in, int ldi, float* out, int ldo, int B, int H, int W, int C,
+                  void* stream);
+/* nn.Upsample(scale_factor=2, mode='bilinear'), align_corners=False (old_modules.py:219,222). */
+int wc_upsample2x_bilinear(const float* in, int ldi, float* out, int ldo, int B, int H, int W,
+                           int C, void* stream);
+/* nn.LayerNorm([C]) over the channels of P pixels (old_modules.py:80-85,90,93). */
+int wc_layernorm_channels(const float* in, int ldi, const float* gamma, const float* beta,
+                          float eps, float* out, int ldo, int64_t P, int C, void* stream);
+/* sinusoidal_embedding + nearest upsample (old_modules.py:283-317): out[pix][k] =
+ * sin(ang[k]*noise[b]) for k < K, cos(ang[k-K]*noise[b]) for K <= k < 2K. */
+int wc_noise_embed(const float* noise, const float* ang, int K, float* out, int ldo, int B,
+                   int HW, void* stream);
 
 /* Library identification (for the CPU load test). */
 const char* wc_version(void);

@@ -48,12 +48,15 @@ def main():
     ap.add_argument('--reference', default='/root/reference')
     ap.add_argument('--skip-traj', action='store_true')
     ap.add_argument('--only-guided', action='store_true')
+    ap.add_argument('--only-old', action='store_true')
     args = ap.parse_args()
     sys.path.insert(0, args.reference)
     torch.Tensor.cuda = lambda self, *a, **k: self  # harness shim for unet_base.py:461
     torch.set_num_threads(8)
     if args.only_guided:
         return guided(args)
+    if args.only_old:
+        return old_unet(args)
     from diffusion_model.config import models as ref_models
     from diffusion_model.models.unet_base import Unet, get_time_embedding
     from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
@@ -151,6 +154,36 @@ def main():
                 xt = mean + sigma if i != 0 else mean
         np.savez(os.path.join(HERE, 'traj_64_T50.npz'), x0=xt.numpy(), eps_first=eps_first.numpy(), seed=3455)
         print('traj done', float(xt.abs().max()))
+
+
+def old_unet(args):
+    """old_unet.npz: old_modules.UNet (128 px) forward and a sample_integrated.py:52-64 trajectory
+    (T=10 schedule, B=1, reference RNG stream), plus the key manifest."""
+    from diffusion_model.models.old_modules import UNet
+    from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    net = UNet()
+    sd = synthetic_state_dict(net.state_dict(), seed=0)
+    net.load_state_dict(sd)
+    net.eval()
+    out = {'digest': state_dict_digest(sd)}
+    x = synthetic_images((1, 3, 128, 128), seed=501)
+    lvl = torch.tensor([[[[0.2860]]]])
+    with torch.no_grad():
+        out['y'] = net(x, lvl).numpy()
+    s10 = LinearNoiseScheduler(10, 0.0001, 0.02)
+    torch.manual_seed(3455)
+    xt = torch.randn((1, 3, 128, 128))  # sample_integrated.py:52-53
+    with torch.no_grad():
+        for i in reversed(range(10)):  # :55-64
+            t = torch.full((xt.size(0), ), i, dtype=torch.long)
+            noise_pred = net(xt, s10.one_minus_cum_prod[t].view(-1, 1, 1, 1))
+            mean, sigma, _ = s10.sample_prev_timestep2(xt, noise_pred, t)
+            xt = mean + sigma if i != 0 else mean
+    out['traj_x0'] = xt.numpy()
+    np.savez(os.path.join(HERE, 'old_unet.npz'), **out)
+    with open(os.path.join(HERE, 'old_manifest.json'), 'w') as fh:
+        json.dump([[k, list(v.shape)] for k, v in net.state_dict().items()], fh)
+    print('old unet done', float(np.abs(out['y']).max()), float(np.abs(out['traj_x0']).max()))
 
 
 def guided(args):

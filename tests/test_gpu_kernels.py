@@ -317,3 +317,35 @@ def test_sgg_update(K, nb, S, batch_axis):
     if nb == 1:
         from oracle.scheduler_oracle import gsg_update
         assert rel_l2(xt.cpu(), gsg_update(grad, mu, sigma, 60.0)) < 1e-6
+
+
+def test_old_unet_helper_kernels(K):
+    """avg-pool 2x2, bilinear x2 (align_corners=False), channel LayerNorm, noise-level embedding and the
+    GELU epilogue against their torch ops (reference old_modules.py:80-94,185,219,283-317)."""
+    import math
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn((2, 96, 16, 12), generator=g)
+    xn = K.View.full(_nhwc(x).cuda())
+    pooled = K.View.full(torch.empty((2, 8, 6, 96)).cuda())
+    K.avgpool2x2(xn, pooled)
+    assert rel_l2(_nchw(pooled.t.cpu()), F.avg_pool2d(x, 2)) < 1e-6
+    buf = torch.zeros((2, 32, 24, 160)).cuda()
+    K.upsample2x_bilinear(xn, K.View(buf, 0, 96))
+    up = torch.nn.Upsample(scale_factor=2, mode='bilinear')(x)
+    assert rel_l2(_nchw(buf[..., :96].cpu()), up) < 1e-6
+    gam, bet = 1 + 0.1 * torch.randn(96, generator=g), 0.1 * torch.randn(96, generator=g)
+    ln = K.View.full(torch.empty((2, 16, 12, 96)).cuda())
+    K.layernorm_channels(xn, gam.cuda(), bet.cuda(), ln)
+    ref = F.layer_norm(_nhwc(x), [96], gam, bet)
+    assert rel_l2(ln.t.cpu(), ref) < 1e-6
+    lvl = torch.tensor([0.286, 0.9]).cuda()
+    ang = (2.0 * math.pi * torch.exp(torch.linspace(math.log(1.0), math.log(1000.0), 16))).float()
+    emb = torch.zeros((2, 4, 4, 64)).cuda()
+    K.noise_embed(lvl, ang.cuda(), K.View(emb, 32, 32))
+    ref = torch.cat([torch.sin(ang * lvl.cpu()[:, None]), torch.cos(ang * lvl.cpu()[:, None])], 1)
+    assert rel_l2(emb[:, 2, 3, 32:].cpu(), ref) < 1e-6 and torch.count_nonzero(emb[..., :32]) == 0
+    w = torch.randn((64, 96), generator=g) / 96**0.5
+    b = torch.randn(64, generator=g)
+    o = torch.empty((2, 16, 12, 64)).cuda()
+    K.conv_igemm([K.Seg(xn, [(0, 0)])], w.cuda(), b.cuda(), K.View.full(o), Hm=16, Wm=12, act=1)
+    assert rel_l2(o.cpu(), F.gelu(F.linear(_nhwc(x), w, b))) < 1e-5

@@ -17,8 +17,9 @@ NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 EXPORTS = [
     'wc_conv_igemm', 'wc_gn_num_splits', 'wc_gn_stats', 'wc_gn_finalize', 'wc_attention_fwd',
     'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
-    'wc_version'
+    'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed', 'wc_version'
 ]
+ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
 
 
 class ConvSeg(ctypes.Structure):
@@ -38,7 +39,7 @@ class ConvArgs(ctypes.Structure):
         ('res', ctypes.c_void_p), ('ldres', ctypes.c_int), ('out', ctypes.c_void_p),
         ('ldo', ctypes.c_int), ('Ho', ctypes.c_int), ('Wo', ctypes.c_int), ('osy', ctypes.c_int),
         ('osx', ctypes.c_int), ('ooy', ctypes.c_int), ('oox', ctypes.c_int),
-        ('out_nchw', ctypes.c_int)
+        ('out_nchw', ctypes.c_int), ('act', ctypes.c_int)
     ]
 
 
@@ -61,6 +62,10 @@ _SIGS = {
     'wc_add_noise': [_P, _P, _P, _P, _P, _L, _L, _P],
     'wc_philox_normal': [_P, _L, _L, _U, _L, _L, _P],
     'wc_sgg_update': [_P, _P, _P, _P, _P, _I, _I, _F, _D, _D, _D, _I, _P],
+    'wc_avgpool2x2': [_P, _I, _P, _I, _I, _I, _I, _I, _P],
+    'wc_upsample2x_bilinear': [_P, _I, _P, _I, _I, _I, _I, _I, _P],
+    'wc_layernorm_channels': [_P, _I, _P, _P, _F, _P, _I, _L, _I, _P],
+    'wc_noise_embed': [_P, _P, _I, _P, _I, _I, _I, _P],
 }
 
 _lib = None

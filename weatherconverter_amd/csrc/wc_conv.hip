@@ -58,6 +58,7 @@ struct ConvDev {
     int ldo;
     int Ho, Wo, osy, osx, ooy, oox, out_nchw;
     int ident;    // output position == GEMM row (plain NHWC store)
+    int act;      // epilogue activation (WC_ACT_*)
     int steps0;   // K-steps of segment 0
     int steps;    // total K-steps
     int ntiles_n; // N tiles
@@ -340,6 +341,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
                 int b = (HWm >= 32) ? b0 + (m >= bnd ? 1 : 0) : m / HWm;
                 float v = acc[mb][nb][r] + bn;
                 if (p.temb) v += p.temb[b * p.temb_ld + n];
+                if (p.act == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+                else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
                 if (p.ident) {
                     if (p.res) v += p.res[(long)m * p.ldres + n];
                     p.out[(long)m * p.ldo + n] = v;
@@ -436,6 +439,8 @@ extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo;
     d.Ho = a->Ho; d.Wo = a->Wo; d.osy = a->osy; d.osx = a->osx; d.ooy = a->ooy; d.oox = a->oox;
     d.out_nchw = a->out_nchw;
+    if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
+    d.act = a->act;
     d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
               a->Ho == a->Hm && a->Wo == a->Wm;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);

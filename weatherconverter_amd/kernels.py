@@ -92,7 +92,7 @@ class Seg:
 
 def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
-               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None):
+               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0):
     """Implicit-GEMM conv: out[b, my*osy+ooy, mx*osx+oox, n] = sum_k A[m, k] W[n, k] (+bias, temb, res)."""
     a = ConvArgs()
     _req(1 <= len(segs) <= 2, 'conv_igemm takes 1 or 2 K segments')
@@ -130,6 +130,7 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
         res.check()
         a.res, a.ldres = res.ptr, res.ldc
     a.osy, a.osx, a.ooy, a.oox = out_map
+    a.act = act
     if out_nchw is not None:
         _req(out_nchw.is_contiguous() and out_nchw.shape[0] == B and out_nchw.shape[1] == N, 'NCHW output shape')
         a.out = out_nchw.data_ptr()
@@ -247,3 +248,35 @@ def sgg_update(grad: torch.Tensor, mu: torch.Tensor, sigma: torch.Tensor, lam: f
     _native.call('wc_sgg_update', grad.data_ptr(), mu.data_ptr(), sigma.data_ptr(), xt.data_ptr(), mag.data_ptr(),
                  nb, S, float(lam), float(std[0]), float(std[1]), float(std[2]), int(batch_axis_sum), _stream())
     return xt, mag
+
+
+def avgpool2x2(x: View, out: View):
+    x.check()
+    out.check()
+    _req(out.H * 2 == x.H and out.W * 2 == x.W and out.C == x.C and out.B == x.B, 'avgpool2x2 shapes')
+    _native.call('wc_avgpool2x2', x.ptr, x.ldc, out.ptr, out.ldc, x.B, x.H, x.W, x.C, _stream())
+
+
+def upsample2x_bilinear(x: View, out: View):
+    x.check()
+    out.check()
+    _req(out.H == 2 * x.H and out.W == 2 * x.W and out.C == x.C and out.B == x.B, 'upsample2x shapes')
+    _native.call('wc_upsample2x_bilinear', x.ptr, x.ldc, out.ptr, out.ldc, x.B, x.H, x.W, x.C, _stream())
+
+
+def layernorm_channels(x: View, gamma: torch.Tensor, beta: torch.Tensor, out: View, eps: float = 1e-5):
+    x.check()
+    out.check()
+    _req(out.C == x.C and out.B * out.H * out.W == x.B * x.H * x.W, 'layernorm shapes')
+    _req(x.ldc == x.C or x.H * x.W > 0, 'layernorm view')
+    _native.call('wc_layernorm_channels', x.ptr, x.ldc, gamma.data_ptr(), beta.data_ptr(), eps, out.ptr, out.ldc,
+                 x.B * x.H * x.W, x.C, _stream())
+
+
+def noise_embed(noise: torch.Tensor, ang: torch.Tensor, out: View):
+    out.check()
+    K = ang.numel()
+    _req(out.C == 2 * K and noise.numel() == out.B and noise.is_contiguous() and ang.is_contiguous(),
+         'noise_embed shapes')
+    _native.call('wc_noise_embed', noise.data_ptr(), ang.data_ptr(), K, out.ptr, out.ldc, out.B, out.H * out.W,
+                 _stream())

@@ -13,10 +13,11 @@ noise keyed by (seed, global sample, step).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run (RCCL).
 Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
-  roofline      per-launch HIP events around every implicit-GEMM conv of one UNet forward; the
-                dominant kernel is the conv_igemm_kernel instantiation with the most time (the
-                GN+SiLU-prologue 3x3 convs) — achieved = its algorithmic FLOPs per launch / its mean
-                launch duration, against the 157.3 TF fp32 MFMA peak (MI355X_MICROARCH.md).
+  roofline      per-launch HIP events around every conv of one UNet forward; the dominant kernel
+                is the conv instantiation with the most time (the GN+SiLU-prologue 3x3 convs) —
+                achieved = its algorithmic (fp32-equivalent) FLOPs per launch / its mean launch
+                duration, against its own ceiling: 157.3 TF for the fp32-MFMA conv, 2516.6/6 =
+                419.4 TF for the bf16x6 conv (6 bf16 MFMAs per fp32 product; MI355X_MICROARCH.md).
   cpu_baseline  the oracle's PyTorch-CPU restatement of the reference UNet step (N=1 only), on a
                 bounded sample (a few 256-px UNet steps), extrapolated x T.
 """
@@ -29,6 +30,9 @@ import torch
 import torch.distributed as dist
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
+# bf16x6 conv: every fp32-equivalent 32x32x16 block costs 6 bf16 MFMAs, so its ceiling is the dense
+# bf16 MFMA peak (256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz = 2516.6 TF/s) / 6.
+BF16X6_PEAK_TFLOPS = round(2516.6 / 6, 1)
 HBM_PEAK_GBS = 8000.0
 GFLOP_PER_IMAGE_STEP_256 = 590.61  # SURVEY.md §8(d) algorithmic FLOPs (probe hook count)
 
@@ -70,18 +74,24 @@ def roofline_leg(model, x, t_dev):
     mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
     total_conv = sum(v[2] for v in per.values())
+    if name.startswith('conv3x3_x6'):
+        desc, peak = ' (bf16x6 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue)', BF16X6_PEAK_TFLOPS
+    else:
+        desc, peak = ' (fp32 MFMA implicit-GEMM conv, GN+SiLU prologue)', FP32_PEAK_TFLOPS
     return {
-        'kernel': name + ' (fp32 MFMA implicit-GEMM conv, GN+SiLU prologue)',
+        'kernel': name + desc,
         'bound': 'mfma',
         'achieved': round(achieved, 2),
-        'peak': FP32_PEAK_TFLOPS,
+        'peak': peak,
         'unit': 'TFLOP/s',
-        'frac': round(achieved / FP32_PEAK_TFLOPS, 4),
+        'frac': round(achieved / peak, 4),
         'traffic': None,
         'launches_per_step': n,
         'mean_launch_ms': round(mean_dur * 1e3, 4),
         'gflop_per_launch': round(fl / n / 1e9, 3),
         'share_of_conv_event_time': round(sec / max(total_conv, 1e-12), 3),
+        'conv_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1)}
+                         for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])},
     }
 
 

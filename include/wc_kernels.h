@@ -86,6 +86,26 @@ typedef struct wc_conv_args {
 int wc_conv_igemm(const wc_conv_args* args, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* 3x3 stride-1 convolution on bf16x6 split-precision MFMA (v_mfma_f32_32x32x16_bf16).         */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Every fp32 operand is split exactly into three bf16 pieces by truncation (v = v0 + v1 + v2,
+ * 8 significant bits each) and the products v_i*w_j with i + j <= 2 are accumulated in fp32.
+ * The dropped terms are < 3*2^-24 relative per product, the order of fp32 rounding.
+ *
+ * Same arguments as wc_conv_igemm, restricted to: segment 0 = 3x3 taps (-1..1 row-major) at
+ * stride 1 on an Hm x Wm grid equal to its source, C % 16 == 0; optional segment 1 = raw 1x1 at
+ * the same pixel, C % 16 == 0; plain NHWC output at the same grid; Hm % TH == 0 and
+ * Wm % 16 == 0 where TH = 8 (BN = 128) or 16 (BN = 64, used when N <= 64).
+ * args->w / ldw are ignored; w6 is the weight re-packed by the caller as
+ *   [ceil(N/BN)][steps][piece 3][k-half 2][BN][8] bf16 bit patterns,
+ * steps = 9*(C0/16) (channel-chunk major, tap minor) + C1/16, w6_bytes its size in bytes.
+ * Replaces the same reference layers as wc_conv_igemm's 3x3 case (unet_base.py:92,106). */
+int wc_conv3x3_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, void* stream);
+/* The output-channel tile (BN) wc_conv3x3_x6 uses for N output channels. */
+int wc_conv3x3_x6_tile_n(int N);
+
+/* ------------------------------------------------------------------------------------------ */
 /* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */
 /* ------------------------------------------------------------------------------------------ */
 

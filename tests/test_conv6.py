@@ -1,0 +1,147 @@
+"""bf16x6 split-precision 3x3 conv (csrc/wc_conv6.hip).
+
+CPU: the 3-piece bf16 split is exact, and the weight re-pack has the layout the kernel reads.
+GPU: the conv against a float64 PyTorch reference of the same op.  Stated tolerance: relative L2
+<= 1e-5 (the fp32 tolerance of SURVEY.md §8c) and, tighter, within 4x (+1e-7) of the error of the
+fp32-MFMA conv on the same inputs, i.e. fp32-class accuracy.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_l2
+
+TAPS3 = [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]
+
+
+def _bits_to_f32(p16: torch.Tensor) -> torch.Tensor:
+    return (p16.to(torch.int32) << 16).view(torch.float32)
+
+
+def test_split3_exact():
+    from weatherconverter_amd.kernels import split3_bits
+    g = torch.Generator().manual_seed(0)
+    x = torch.cat([torch.randn(100000, generator=g) * 10.0**e for e in range(-6, 7)])
+    x = torch.cat([x, torch.tensor([0.0, -0.0, 1.0, -1.0, 3.0e38, -1.17549435e-38, 1 / 3])])
+    p = split3_bits(x)
+    f = _bits_to_f32(p)
+    # exact: sum of the pieces in float64 reproduces x, and each piece is a bf16 value
+    assert torch.equal(f.double().sum(0), x.double())
+    assert torch.equal(f, _bits_to_f32((f.view(torch.int32) >> 16).to(torch.int16)))
+    # pieces shrink by >= 2^8: |p1| < 2^-7 |x|, |p2| < 2^-15 |x|
+    ax = x.abs().double()
+    assert bool((f[1].abs().double() <= ax * 2.0**-7).all()) and bool((f[2].abs().double() <= ax * 2.0**-15).all())
+
+
+@pytest.mark.parametrize('N,C0,C1', [(128, 64, 32), (64, 32, 0), (96, 48, 16), (256, 16, 64)])
+def test_pack_x6_layout(N, C0, C1):
+    """Unpack [tile][step][piece][half][BN][8] back to [N][9*C0 + C1] and compare exactly."""
+    from weatherconverter_amd.kernels import pack_x6
+    g = torch.Generator().manual_seed(1)
+    w = torch.randn((N, 9 * C0 + C1), generator=g)
+    x6 = pack_x6(w, C0, C1)
+    BN = x6.BN
+    assert BN == (64 if N <= 64 else 128)
+    T, S = x6.data.shape[0], x6.data.shape[1]
+    assert x6.data.shape == (T, S, 3, 2, BN, 8) and S == 9 * (C0 // 16) + C1 // 16
+    v = _bits_to_f32(x6.data).double().sum(2)  # (T, S, 2, BN, 8): sum of the pieces
+    v = v.permute(0, 3, 1, 2, 4).reshape(T * BN, S, 16)[:N]  # (n, step, k16)
+    s0 = v[:, :9 * (C0 // 16)].reshape(N, C0 // 16, 9, 16).permute(0, 2, 1, 3).reshape(N, 9 * C0)
+    s1 = v[:, 9 * (C0 // 16):].reshape(N, C1)
+    assert torch.equal(torch.cat([s0, s1], 1), w.double())
+    if N % BN:
+        assert not _bits_to_f32(x6.data).view(T, S, 3, 2, BN, 8)[-1, :, :, :, N % BN:].any()
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def _pack(w):
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+CASES = [
+    # B, H, W, Ci, Co, Cr (1x1 residual channels), prologue, act
+    (2, 16, 32, 64, 128, 32, 'silu', 0),
+    (1, 32, 32, 128, 64, 0, 'silu', 0),
+    (2, 8, 16, 96, 256, 64, 'affine', 0),
+    (1, 16, 16, 32, 96, 0, 'raw', 0),
+    (1, 16, 48, 64, 80, 0, 'silu', 1),
+    (2, 32, 16, 256, 128, 128, 'silu', 0),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr,pro,act', CASES)
+def test_conv3x3_x6_vs_float64(B, H, W, Ci, Co, Cr, pro, act):
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(7)
+    h = torch.randn((B, Ci, H, W), generator=g) * 1.5 + 0.3
+    x2 = torch.randn((B, max(Cr, 16), H, W), generator=g)
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    wr = torch.randn((Co, max(Cr, 16), 1, 1), generator=g) / max(Cr, 16)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    temb = torch.randn((B, Co), generator=g)
+    sc = 1 + 0.2 * torch.randn((B, Ci), generator=g)
+    sh = 0.2 * torch.randn((B, Ci), generator=g)
+    resv = torch.randn((B, H, W, Co), generator=g)
+
+    a = h.double()
+    if pro != 'raw':
+        a = a * sc.double()[:, :, None, None] + sh.double()[:, :, None, None]
+    if pro == 'silu':
+        a = F.silu(a)
+    ref = F.conv2d(a, w.double(), b.double(), padding=1) + temb.double()[:, :, None, None]
+    if Cr:
+        ref = ref + F.conv2d(x2.double(), wr.double())
+    if act == 1:
+        ref = F.gelu(ref)
+    ref = ref + _nchw(resv).double()
+
+    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=None if pro == 'raw' else sc.cuda(),
+                  shift=None if pro == 'raw' else sh.cuda(), silu=pro == 'silu')]
+    wp = _pack(w)
+    if Cr:
+        segs.append(K.Seg(K.View.full(_nhwc(x2).cuda()), [(0, 0)], kbase=9 * Ci))
+        wp = torch.cat([wp, wr.reshape(Co, Cr)], 1)
+    wp = wp.contiguous().cuda()
+    assert K.x6_eligible(segs, Co, H, W)
+    # output into a channel slice of a wider buffer (the skip-concat layout)
+    outs = {}
+    for mode in ('x6', 'fp32'):
+        buf = torch.full((B, H, W, Co + 32), 7.0, device='cuda')
+        out = K.View(buf, 16, Co)
+        kw = dict(Hm=H, Wm=W, temb=temb.cuda(), temb_ld=Co, res=K.View.full(resv.cuda()), act=act)
+        if mode == 'x6':
+            K.conv3x3_x6(segs, K.pack_x6(wp, Ci, Cr), b.cuda(), out, **kw)
+        else:
+            K.conv_igemm(segs, wp, b.cuda(), out, **kw)
+        torch.cuda.synchronize()
+        bc = buf.cpu()
+        assert bool((bc[..., :16] == 7.0).all()) and bool((bc[..., 16 + Co:] == 7.0).all())
+        outs[mode] = _nchw(bc[..., 16:16 + Co])
+    e6 = rel_l2(outs['x6'].double(), ref)
+    e32 = rel_l2(outs['fp32'].double(), ref)
+    assert e6 < 1e-5
+    assert e6 <= 4 * e32 + 1e-7, (e6, e32)
+
+
+@pytest.mark.gpu
+def test_conv3x3_x6_rejects_untiled_shape():
+    from weatherconverter_amd import kernels as K
+    h = torch.randn((1, 12, 16, 32), device='cuda')
+    segs = [K.Seg(K.View.full(h), TAPS3)]
+    assert not K.x6_eligible(segs, 128, 12, 16)  # H % 8 != 0
+    w6 = K.pack_x6(torch.randn((128, 9 * 32), device='cuda'), 32)
+    out = torch.empty((1, 12, 16, 128), device='cuda')
+    with pytest.raises(RuntimeError):
+        K.conv3x3_x6(segs, w6, None, K.View.full(out), Hm=12, Wm=16)

@@ -16,13 +16,15 @@ pytestmark = pytest.mark.gpu
 MANIFEST = json.load(open(os.path.join(GOLDEN, 'manifest.json')))
 
 
-def _model(name, seed=0):
+def _model(name, seed=0, precision=None):
     from weatherconverter_amd.diffusion_model.config import ModelConfig
     from weatherconverter_amd.diffusion_model.models.unet_base import Unet
     from weatherconverter_amd.synthetic import init_synthetic_
     mc = ModelConfig(**MANIFEST[name]['config'])
     net = Unet(mc)
     init_synthetic_(net, seed=seed)
+    if precision is not None:
+        net.set_conv_precision(precision)
     return mc, net.cuda().eval()
 
 
@@ -43,16 +45,18 @@ def test_unet_tiny_shared_and_per_sample_t():
     assert rel_l2(y2.cpu(), g['y_batch_t']) < 1e-5
 
 
-def test_unet_64_config1_model():
-    mc, net = _model('default_64')
+@pytest.mark.parametrize('precision', ['bf16x6', 'fp32'])
+def test_unet_64_config1_model(precision):
+    mc, net = _model('default_64', precision=precision)
     g = np.load(os.path.join(GOLDEN, 'unet_64.npz'))
     with torch.no_grad():
         y = net(_x(mc, 2, 201).cuda(), torch.tensor([37]).cuda())
     assert rel_l2(y.cpu(), g['y']) < 1e-5
 
 
-def test_unet_256_baseline_architecture():
-    mc, net = _model('default_256')
+@pytest.mark.parametrize('precision', ['bf16x6', 'fp32'])
+def test_unet_256_baseline_architecture(precision):
+    mc, net = _model('default_256', precision=precision)
     g = np.load(os.path.join(GOLDEN, 'unet_256.npz'))
     with torch.no_grad():
         y = net(_x(mc, 1, 301).cuda(), torch.tensor([611]).cuda())

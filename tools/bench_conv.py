@@ -25,7 +25,7 @@ def timeit(fn, iters=10):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
-def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False):
+def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32'):
     g = torch.Generator(device='cuda').manual_seed(0)
     x = torch.randn((B, H, H, Ci), device='cuda', generator=g)
     w = torch.randn((Co, 9 * Ci + res), device='cuda', generator=g) / (9 * Ci)**0.5
@@ -38,7 +38,11 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False):
     if res:
         xr = torch.randn((B, H, H, res), device='cuda', generator=g)
         segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=9 * Ci))
-    fn = lambda: K.conv_igemm(segs, w, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
+    if mode == 'x6':
+        w6 = K.pack_x6(w, Ci, res)
+        fn = lambda: K.conv3x3_x6(segs, w6, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
+    else:
+        fn = lambda: K.conv_igemm(segs, w, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
     t = timeit(fn)
     fl = 2.0 * B * H * H * Co * (9 * Ci + res)
     err = None
@@ -69,6 +73,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--check', action='store_true')
     ap.add_argument('--only', type=int, default=-1, help='run a single conv case (for PMC profiling)')
+    ap.add_argument('--modes', default='fp32,x6', help='conv arithmetic(s) to time: fp32, x6')
     a = ap.parse_args()
     K._native.load()
     cases = [(16, 256, 128, 128, True, 0), (16, 256, 128, 128, True, 64), (16, 256, 64, 64, True, 0),
@@ -77,13 +82,15 @@ def main():
     tot_t = tot_f = 0
     if a.only >= 0:
         cases = [cases[a.only]]
-    for c in cases:
-        t, tf, err = conv_case(*c, check=a.check)
-        tot_t += t
-        tot_f += tf * t
-        print(f'conv B={c[0]} S={c[1]} {c[2]}->{c[3]} prologue={c[4]} res={c[5]}: {t*1e3:8.3f} ms  {tf:6.1f} TF/s'
-              + (f'  relL2={err:.2e}' if err is not None else ''), flush=True)
-    print(f'conv aggregate {tot_f / tot_t:.1f} TF/s')
+    for mode in a.modes.split(','):
+        tot_t = tot_f = 0
+        for c in cases:
+            t, tf, err = conv_case(*c, check=a.check, mode=mode)
+            tot_t += t
+            tot_f += tf * t
+            print(f'{mode:4s} conv B={c[0]} S={c[1]} {c[2]}->{c[3]} prologue={c[4]} res={c[5]}: {t*1e3:8.3f} ms  '
+                  f'{tf:6.1f} TF/s' + (f'  relL2={err:.2e}' if err is not None else ''), flush=True)
+        print(f'{mode} conv aggregate {tot_f / tot_t:.1f} TF/s')
     if a.only >= 0:
         return
     for c in [(16, 4096, 512), (16, 1024, 768), (16, 1024, 512), (16, 4096, 128), (16, 1024, 256)]:

@@ -1,0 +1,455 @@
+// 3x3 stride-1 convolution on bf16x6 split-precision MFMA for gfx950.
+//
+// Precision.  Every fp32 operand v is split EXACTLY into three bf16 pieces by truncation:
+// v0 = v with the low 16 bits cleared, v1 = (v - v0) likewise, v2 = v - v0 - v1 (at most 8
+// significant bits, so it is exact in bf16).  The product a*w is accumulated as the six terms
+// a_i*w_j with i + j <= 2, each an exact bf16 x bf16 product summed in fp32 by
+// v_mfma_f32_32x32x16_bf16.  The dropped terms a1w2 + a2w1 + a2w2 are < 3*2^-24 |a w|, the size
+// of one fp32 rounding, so the result stays inside the fp32 tolerance of the reference conv.  A
+// 32x32x16 block costs 6 bf16 MFMAs (192 cycles) instead of 8 fp32 MFMAs (512 cycles): 2.67x the
+// fp32 MFMA rate (emulated-fp32 peak 2516.6 / 6 = 419.4 TF/s).
+//
+// Tiling (implicit GEMM, M = output pixels, N = output channels, K = (16-channel chunk, tap)).
+// A workgroup owns a TH x 16 pixel tile of one image and BN output channels; each of its 4 waves
+// owns 4 image rows x 16 columns (64 pixels) x 64 channels as 2 x 2 32x32 accumulators.
+//   * Per 16-channel chunk the (TH+2) x 18 input HALO is loaded once, GroupNorm-applied (+SiLU),
+//     zero-padded, split into its three bf16 pieces and written to LDS.  All 9 taps then read
+//     their A fragments from that one halo image at a constant per-tap offset, so the prologue
+//     VALU is paid (TH+2)*18/(TH*16) times per input element instead of 9 times.
+//   * A K-step is one (chunk, tap): the tap's 16 x BN weight pieces (pre-split and pre-laid-out
+//     by the host in the exact LDS order) are staged through registers one step ahead; one
+//     barrier per step.  The next chunk's halo is loaded at the chunk's first tap and written
+//     at its last, into the other halo buffer.
+//   * The fused 1x1 residual_input_conv (raw input, same pixel) runs as extra chunks with one
+//     tap (the halo centre).
+// LDS images.  Halo: [piece 3][k-half 2][pixel (TH+2)*18][8 bf16]; weights: [piece][k-half][BN]
+// [8 bf16].  The MFMA row -> pixel map is chosen so that each ds_read_b128 lane group
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) reads 16 consecutive pixels of one image row:
+// 16 distinct 16-byte slots, bank-conflict-free for every tap offset.
+//
+// Fused work (reference unet_base.py ResBlock, :87-109 / :146-150), as in wc_conv.hip:
+// prologue SiLU(v*scale[b,c] + shift[b,c]) with zero padding applied after it; epilogue
+// + bias[n] + temb[b,n], activation, + residual view, NHWC store.
+#include "wc_common.hpp"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int NT = 256;
+constexpr int HWD = 18;                // halo row width: 16 output columns + 2
+constexpr unsigned OOB = 0x80000000u;  // byte offset past the SRD range -> load returns 0
+constexpr int SRD_BYTES = 0x7FFFFFFF;
+constexpr int SRD_FLAGS = 0x00020000;
+
+struct X6Dev {
+    const float* src0;
+    int C0, ldc0;
+    const float* scale;
+    const float* shift;
+    const float* src1;
+    int C1, ldc1;
+    int B, H, W, N;
+    const void* w6;
+    const float* bias;
+    const float* temb;
+    int temb_ld;
+    const float* res;
+    int ldres;
+    float* out;
+    int ldo;
+    int act;
+    int nck0, nck1;  // 16-channel chunks of segment 0 (3x3) and segment 1 (1x1 residual)
+    int tiles_x, tiles_y, ntiles_n;
+};
+
+template <int TH, int BN>
+struct X6Tile {
+    static constexpr int BM = TH * 16;
+    static constexpr int WAVES_N = BN / 64;
+    static constexpr int WAVES_M = 4 / WAVES_N;
+    static_assert(WAVES_M * 64 == BM, "each wave owns 4 image rows x 16 columns");
+    static constexpr int HPIX = (TH + 2) * HWD;   // halo pixels
+    static constexpr int HPLANE = HPIX * 16;      // bytes of one (piece, k-half) halo plane
+    static constexpr int HSTAGE = 6 * HPLANE;     // one halo buffer
+    static constexpr int BPLANE = BN * 16;        // bytes of one (piece, k-half) weight plane
+    static constexpr int BSTAGE = 6 * BPLANE;     // one weight step
+    static constexpr int LDS = 2 * HSTAGE + 2 * BSTAGE;
+    static constexpr int H_ITEMS = HPIX * 4;      // float4 items of one halo chunk
+    static constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
+    static constexpr int B_ITEMS = BSTAGE / 16;   // 16-byte items of one weight step
+    static constexpr int B_PER_T = (B_ITEMS + NT - 1) / NT;
+};
+
+WC_DEVICE __amdgpu_buffer_rsrc_t make_srd(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, SRD_BYTES, SRD_FLAGS);
+}
+WC_DEVICE f32x4 bload_f4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+WC_DEVICE u32x4 bload_u4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+WC_DEVICE f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+WC_DEVICE float silu_fast(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+
+// High halves of two fp32 bit patterns packed into one dword: (hi16(hi) << 16) | hi16(lo).
+WC_DEVICE unsigned hi_pair(unsigned hi, unsigned lo) { return __builtin_amdgcn_perm(hi, lo, 0x07060302u); }
+
+// Exact three-piece bf16 split of 4 floats (see the header comment).
+// NOTE: bit-cast a scalar copy, never the subscript v[e] directly: hipcc (ROCm 7.2 clang) lowers
+// __builtin_bit_cast(unsigned, v[e]) of an ext_vector element to element 0 for every e
+// (tools/probes/bitcast_vector_element.hip reproduces it).
+WC_DEVICE void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+    unsigned u0[4], u1[4], u2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e];
+        const unsigned a = __float_as_uint(x);
+        const float r1 = x - __uint_as_float(a & 0xffff0000u);
+        const unsigned c = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(c & 0xffff0000u);
+        u0[e] = a;
+        u1[e] = c;
+        u2[e] = __float_as_uint(r2);
+    }
+    p0 = u32x2{hi_pair(u0[1], u0[0]), hi_pair(u0[3], u0[2])};
+    p1 = u32x2{hi_pair(u1[1], u1[0]), hi_pair(u1[3], u1[2])};
+    p2 = u32x2{hi_pair(u2[1], u2[0]), hi_pair(u2[3], u2[2])};
+}
+
+// MFMA row r (0..31) -> pixel (dy, dx) of a 2 x 16 strip: the ds_read_b128 lane group
+// {0-3, 12-15, 20-27} is row dy = 0, the group {4-11, 16-19, 28-31} row dy = 1.
+WC_DEVICE int row_dy(int r) { return ((r >= 4 && r < 12) || (r >= 16 && r < 20) || r >= 28) ? 1 : 0; }
+WC_DEVICE int row_dx(int r) {
+    return r < 4 ? r : r < 12 ? r - 4 : r < 20 ? r - 8 : r < 28 ? r - 12 : r - 16;
+}
+
+// PRO: 0 = raw segment 0, 1 = GN affine, 2 = GN affine + SiLU.  RES: segment 1 present.
+template <int TH, int BN, int PRO, bool RES>
+__global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
+    using T = X6Tile<TH, BN>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / T::WAVES_N;
+    const int wn = wave % T::WAVES_N;
+
+    // XCD-aware bijective tile order (as wc_conv.hip): consecutive logical tiles, which share
+    // halo rows and weights, land on one XCD's L2.
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int tile_n = bid % p.ntiles_n;
+    int tt = bid / p.ntiles_n;
+    const int txi = tt % p.tiles_x;
+    tt /= p.tiles_x;
+    const int tyi = tt % p.tiles_y;
+    const int b = tt / p.tiles_y;
+    const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
+    const int S = 9 * p.nck0 + (RES ? p.nck1 : 0);
+
+    // ---- halo staging coordinates: item i = tid + NT*j is halo pixel i>>2, channels 4*(i&3).. ----
+    const int q = tid & 3;
+    int hoff0[T::H_PER_T], hoff1[T::H_PER_T], hlds[T::H_PER_T];
+    unsigned hin = 0, hval = 0;
+#pragma unroll
+    for (int j = 0; j < T::H_PER_T; ++j) {
+        const int i = tid + NT * j;
+        const int P = i >> 2;
+        const int hy = P / HWD;
+        const int hx = P - hy * HWD;
+        const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+        const bool valid = i < T::H_ITEMS;
+        const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        hval |= (valid ? 1u : 0u) << j;
+        hin |= (inb ? 1u : 0u) << j;
+        const int pix = (b * p.H + iy) * p.W + ix;
+        hoff0[j] = inb ? pix * p.ldc0 + 4 * q : 0;
+        hoff1[j] = inb ? pix * p.ldc1 + 4 * q : 0;
+        hlds[j] = (q >> 1) * T::HPLANE + P * 16 + (q & 1) * 8;
+    }
+
+    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
+    const __amdgpu_buffer_rsrc_t srd1 = make_srd(RES ? p.src1 : p.src0);
+    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w6);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
+
+    f32x4 rh[T::H_PER_T];
+    f32x4 rsc = {1.f, 1.f, 1.f, 1.f}, rsh = {0.f, 0.f, 0.f, 0.f};
+    u32x4 rb[T::B_PER_T];
+
+    auto load_halo0 = [&](int c) {
+#pragma unroll
+        for (int j = 0; j < T::H_PER_T; ++j)
+            rh[j] = bload_f4(srd0, ((hin >> j) & 1u) ? (unsigned)(hoff0[j] + c * 16) * 4u : OOB);
+        if constexpr (PRO != 0) {
+            const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
+            rsc = bload_f4(srdsc, o);
+            rsh = bload_f4(srdsh, o);
+        }
+    };
+    auto load_halo1 = [&](int c) {
+#pragma unroll
+        for (int j = 0; j < T::H_PER_T; ++j)
+            rh[j] = bload_f4(srd1, ((hin >> j) & 1u) ? (unsigned)(hoff1[j] + c * 16) * 4u : OOB);
+    };
+    auto write_halo = [&](int hs, bool pro) {
+        unsigned char* base = smem + hs * T::HSTAGE;
+#pragma unroll
+        for (int j = 0; j < T::H_PER_T; ++j) {
+            if (!((hval >> j) & 1u)) continue;
+            f32x4 v = rh[j];
+            if constexpr (PRO != 0) {
+                if (pro) {
+                    v = v * rsc + rsh;
+                    if constexpr (PRO == 2) {
+                        v.x = silu_fast(v.x); v.y = silu_fast(v.y);
+                        v.z = silu_fast(v.z); v.w = silu_fast(v.w);
+                    }
+                }
+            }
+            if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+            u32x2 a0, a1, a2;
+            split3(v, a0, a1, a2);
+            *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
+            *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds[j]) = a1;
+            *reinterpret_cast<u32x2*>(base + 4 * T::HPLANE + hlds[j]) = a2;
+        }
+    };
+    auto load_b = [&](int s) {
+        const unsigned base = (unsigned)((tile_n * S + s) * T::BSTAGE);
+#pragma unroll
+        for (int j = 0; j < T::B_PER_T; ++j) {
+            const int i = tid + NT * j;
+            rb[j] = bload_u4(srdw, i < T::B_ITEMS ? base + (unsigned)i * 16u : OOB);
+        }
+    };
+    auto write_b = [&](int bs) {
+        unsigned char* base = smem + 2 * T::HSTAGE + bs * T::BSTAGE;
+#pragma unroll
+        for (int j = 0; j < T::B_PER_T; ++j) {
+            const int i = tid + NT * j;
+            if (i < T::B_ITEMS) *reinterpret_cast<u32x4*>(base + i * 16) = rb[j];
+        }
+    };
+
+    // ---- fragment addressing ----
+    const int l32 = lane & 31;
+    const int half = lane >> 5;
+    int abase[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+        abase[mb] = half * T::HPLANE + ((4 * wm + 2 * mb + row_dy(l32)) * HWD + row_dx(l32)) * 16;
+    const int bbase = 2 * T::HSTAGE + half * T::BPLANE + (wn * 64 + l32) * 16;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto compute = [&](int hs, int toff, int bs) {
+        const unsigned char* ha = smem + hs * T::HSTAGE + toff * 16;
+        const unsigned char* hb = smem + bs * T::BSTAGE;
+        u32x4 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+                fa[mb][pc] = *reinterpret_cast<const u32x4*>(ha + abase[mb] + pc * 2 * T::HPLANE);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                fb[nb][pc] = *reinterpret_cast<const u32x4*>(hb + bbase + nb * 32 * 16 + pc * 2 * T::BPLANE);
+        }
+        // piece-order sums 0, 1, 2: the first MFMAs need only the piece-0 fragments
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+            }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][2], acc[mb][nb]);
+                acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
+            }
+    };
+
+    // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
+    load_halo0(0);
+    load_b(0);
+    write_halo(0, true);
+    write_b(0);
+    __syncthreads();
+    int s = 0;
+    for (int c = 0; c < p.nck0; ++c) {
+        const int hs = c & 1;
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+            const bool more = s + 1 < S;
+            if (more) load_b(s + 1);
+            if (tp == 0) {
+                if (c + 1 < p.nck0) load_halo0(c + 1);
+                else if (RES) load_halo1(0);
+            }
+            compute(hs, (tp / 3) * HWD + tp % 3, s & 1);
+            if (more) write_b((s + 1) & 1);
+            if (tp == 8) {
+                if (c + 1 < p.nck0) write_halo(hs ^ 1, true);
+                else if (RES) write_halo(hs ^ 1, false);
+            }
+            __syncthreads();
+            ++s;
+        }
+    }
+    if constexpr (RES) {
+        for (int c = 0; c < p.nck1; ++c) {
+            const int hs = (p.nck0 + c) & 1;
+            const bool more = s + 1 < S;
+            if (more) {
+                load_b(s + 1);
+                load_halo1(c + 1);
+            }
+            compute(hs, HWD + 1, s & 1);  // the halo centre = the output pixel
+            if (more) {
+                write_b((s + 1) & 1);
+                write_halo(hs ^ 1, false);
+            }
+            __syncthreads();
+            ++s;
+        }
+    }
+
+    // ---- epilogue: + bias + temb, activation, + residual, NHWC store ----
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int n = n0 + wn * 64 + nb * 32 + l32;
+            if (n >= p.N) continue;
+            float add = p.bias ? p.bias[n] : 0.f;
+            if (p.temb) add += p.temb[b * p.temb_ld + n];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int oy = y0 + 4 * wm + 2 * mb + row_dy(row);
+                const int ox = x0 + row_dx(row);
+                const long m = (long)(b * p.H + oy) * p.W + ox;
+                float v = acc[mb][nb][r] + add;
+                if (p.act == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+                else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
+                if (p.res) v += p.res[m * p.ldres + n];
+                p.out[m * p.ldo + n] = v;
+            }
+        }
+    }
+}
+
+template <int TH, int BN, int PRO, bool RES>
+int launch6(const X6Dev& d, hipStream_t stream) {
+    using T = X6Tile<TH, BN>;
+    static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    X6Dev p = d;
+    p.tiles_x = p.W / 16;
+    p.tiles_y = p.H / TH;
+    p.ntiles_n = (p.N + BN - 1) / BN;
+    dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES>), grid, dim3(NT), T::LDS, stream, p);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+template <int TH, int BN>
+int dispatch6(const X6Dev& d, int pro, bool res, hipStream_t s) {
+    switch (pro * 2 + (res ? 1 : 0)) {
+        case 0: return launch6<TH, BN, 0, false>(d, s);
+        case 1: return launch6<TH, BN, 0, true>(d, s);
+        case 2: return launch6<TH, BN, 1, false>(d, s);
+        case 3: return launch6<TH, BN, 1, true>(d, s);
+        case 4: return launch6<TH, BN, 2, false>(d, s);
+        default: return launch6<TH, BN, 2, true>(d, s);
+    }
+}
+
+bool is_3x3(const wc_conv_seg& s) {
+    if (s.ntaps != 9) return false;
+    for (int t = 0; t < 9; ++t)
+        if (s.dy[t] != t / 3 - 1 || s.dx[t] != t % 3 - 1) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int wc_conv3x3_x6_tile_n(int N) { return N <= 64 ? 64 : 128; }
+
+extern "C" int wc_conv3x3_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
+    if (!a || !w6 || !a->out) return WC_E_ARG;
+    if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src) return WC_E_ARG;
+    if ((s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
+    if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    const int TH = BN == 64 ? 16 : 8;
+    if (!is_3x3(s0) || s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
+    if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
+    if (s0.H != a->Hm || s0.W != a->Wm || a->Hm % TH || a->Wm % 16) return WC_E_SHAPE;
+    if (a->B <= 0 || a->N <= 0) return WC_E_SHAPE;
+    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;  // 2 GiB SRD range
+    X6Dev d{};
+    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.scale = s0.scale; d.shift = s0.shift;
+    d.nck0 = s0.C / 16;
+    int steps = 9 * d.nck0;
+    if (a->nseg == 2) {
+        const wc_conv_seg& s1 = a->seg[1];
+        if (!s1.src || s1.scale) return WC_E_ARG;
+        if (s1.ntaps != 1 || s1.dy[0] != 0 || s1.dx[0] != 0 || s1.sy != 1 || s1.sx != 1) return WC_E_SHAPE;
+        if (s1.H != s0.H || s1.W != s0.W || s1.kbase != 9 * s0.C) return WC_E_SHAPE;
+        if (s1.C <= 0 || s1.C % 16 || s1.ldc % 4 || (reinterpret_cast<uintptr_t>(s1.src) & 15)) return WC_E_SHAPE;
+        if ((long)a->B * s1.H * s1.W * s1.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+        d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc; d.nck1 = s1.C / 16;
+        steps += d.nck1;
+    }
+    if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox)
+        return WC_E_SHAPE;
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w6_bytes != ntn * steps * (long)BN * 96 || w6_bytes >= (1L << 31)) return WC_E_SHAPE;
+    if (reinterpret_cast<uintptr_t>(w6) & 15) return WC_E_SHAPE;
+    d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
+    d.w6 = w6; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
+    d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo; d.act = a->act;
+    const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return dispatch6<16, 64>(d, pro, a->nseg == 2, s);
+    return dispatch6<8, 128>(d, pro, a->nseg == 2, s);
+}

@@ -70,6 +70,8 @@ class ResPack:
     w2: torch.Tensor  # conv2 (9*co) ++ residual 1x1 (ci)
     b2: torch.Tensor
     temb_off: int
+    w1x6: Optional[K.X6Weight] = None  # bf16x6 re-packs (precision 'bf16x6')
+    w2x6: Optional[K.X6Weight] = None
 
 
 @dataclass
@@ -94,6 +96,7 @@ class UnetEngine:
         K._native.load()
         self.model = model
         self.device = params[0].device
+        self.precision = getattr(model, 'conv_precision', None) or K.default_conv_precision()
         self._sig = self._signature()
         self._pack()
 
@@ -139,6 +142,9 @@ class UnetEngine:
                     w1=pack_conv(f[2].weight), b1=f[2].bias.detach().float().contiguous(),
                     g2=s[0].weight.detach().float(), be2=s[0].bias.detach().float(), w2=w2,
                     b2=(s[2].bias.detach().float() + r.bias.detach().float()).contiguous(), temb_off=self._temb_P)
+        if self.precision == 'bf16x6' and ci % 16 == 0 and co % 16 == 0:
+            p.w1x6 = K.pack_x6(p.w1, ci)
+            p.w2x6 = K.pack_x6(p.w2, co, ci)
         self.temb_rows_w.append(tl.weight.detach().float())
         self.temb_rows_b.append(tl.bias.detach().float())
         self._temb_P += co
@@ -164,15 +170,23 @@ class UnetEngine:
     def _new(self, B, H, W, C) -> torch.Tensor:
         return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
 
+    @staticmethod
+    def conv3(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: View, H: int, W: int, **kw):
+        """A 3x3 stride-1 conv: bf16x6 MFMA kernel when packed for it and the shape tiles, else fp32 MFMA."""
+        if w6 is not None and K.x6_eligible(segs, w6.N, H, W):
+            K.conv3x3_x6(segs, w6, bias, out, Hm=H, Wm=W, **kw)
+        else:
+            K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
+
     def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int):
         B, H, W = X.B, X.H, X.W
         sc1, sh1 = K.gn_affine(X, p.g1, p.be1)
         h = View.full(self._new(B, H, W, p.co))
-        K.conv_igemm([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.b1, h, Hm=H, Wm=W,
-                     temb=temb[:, p.temb_off:], temb_ld=temb_ld)
+        self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.b1, h, H, W,
+                   temb=temb[:, p.temb_off:], temb_ld=temb_ld)
         sc2, sh2 = K.gn_affine(h, p.g2, p.be2)
-        K.conv_igemm([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
-                      Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.b2, Y, Hm=H, Wm=W)
+        self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
+                    Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.b2, Y, H, W)
 
     def attention(self, Y: View, p: AttnPack):
         B, H, W, C = Y.B, Y.H, Y.W, Y.C

@@ -148,6 +148,7 @@ class Unet(nn.Module):
         self.norm_out = nn.GroupNorm(8, self.down_channels[0])
         self.conv_out = nn.Conv2d(self.down_channels[0], mc.im_channels, kernel_size=3, padding=1)
         self._engine = None
+        self.conv_precision = None  # None = kernels.default_conv_precision()
 
     def level_has_attn(self, i: int) -> bool:
         """Attention placement rule of ``unet_base.py:404-405,434-435``."""
@@ -159,6 +160,15 @@ class Unet(nn.Module):
         if self._engine is None:
             self._engine = UnetEngine(self)
         return self._engine
+
+    def set_conv_precision(self, precision: str) -> 'Unet':
+        """'bf16x6' (default) or 'fp32' arithmetic for the 3x3 convs (see kernels.conv3x3_x6)."""
+        from ... import kernels
+        if precision not in kernels.CONV_PRECISIONS:
+            raise ValueError(f'conv precision must be one of {kernels.CONV_PRECISIONS}')
+        self.conv_precision = precision
+        self._engine = None
+        return self
 
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
         if self.training and torch.is_grad_enabled():

@@ -6,6 +6,8 @@ ever reaches a kernel; the C layer re-validates and returns a status that is tur
 RuntimeError.
 """
 import ctypes
+import functools
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -90,14 +92,14 @@ class Seg:
     kbase: int = 0
 
 
-def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
-               temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
-               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0):
-    """Implicit-GEMM conv: out[b, my*osy+ooy, mx*osx+oox, n] = sum_k A[m, k] W[n, k] (+bias, temb, res)."""
+TAPS3 = [(dy, dx) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
+
+
+def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: Optional[View], Hm: int, Wm: int,
+               temb: Optional[torch.Tensor], temb_ld: int, res: Optional[View], out_map,
+               out_nchw: Optional[torch.Tensor], act: int) -> ConvArgs:
     a = ConvArgs()
-    _req(1 <= len(segs) <= 2, 'conv_igemm takes 1 or 2 K segments')
-    _req(w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2, 'packed weight')
-    N, ldw = w.shape
+    _req(1 <= len(segs) <= 2, 'conv takes 1 or 2 K segments')
     B = segs[0].view.B
     for i, s in enumerate(segs):
         v = s.view
@@ -123,7 +125,6 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
         cs.kbase = s.kbase
     a.nseg = len(segs)
     a.B, a.Hm, a.Wm, a.N = B, Hm, Wm, N
-    a.w, a.ldw = w.data_ptr(), ldw
     a.bias = _ptr(bias)
     a.temb, a.temb_ld = _ptr(temb), temb_ld
     if res is not None:
@@ -141,21 +142,132 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
         out.check()
         _req(out.C == N and out.B == B, 'output view shape')
         a.out, a.ldo, a.Ho, a.Wo = out.ptr, out.ldc, out.H, out.W
+    return a
+
+
+def _timed(name: str, fn_name: str, flops: float, *args):
     if PROFILE is None:
-        _native.call('wc_conv_igemm', ctypes.byref(a), _stream())
+        _native.call(fn_name, *args)
         return
-    ktot = sum(len(sg.taps) * sg.view.C for sg in segs)
-    flops = 2.0 * B * Hm * Wm * N * ktot
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    _native.call('wc_conv_igemm', ctypes.byref(a), _stream())
+    _native.call(fn_name, *args)
     e1.record()
+    PROFILE.append((name, flops, e0, e1))
+
+
+def _flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int) -> float:
+    return 2.0 * segs[0].view.B * Hm * Wm * N * sum(len(sg.taps) * sg.view.C for sg in segs)
+
+
+def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
+               temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
+               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0):
+    """Implicit-GEMM conv on fp32 MFMA:
+    out[b, my*osy+ooy, mx*osx+oox, n] = sum_k A[m, k] W[n, k] (+bias, temb, res)."""
+    _req(w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2, 'packed weight')
+    N, ldw = w.shape
+    a = _conv_args(segs, N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act)
+    a.w, a.ldw = w.data_ptr(), ldw
     # the kernel symbol wc_conv_igemm dispatches to (mirrors dispatch() in csrc/wc_conv.hip)
     bm, bn = (256, 64) if N <= 64 else (128, 128)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
-    PROFILE.append((f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}>', flops, e0, e1))
+    _timed(f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}>', 'wc_conv_igemm',
+           _flops(segs, Hm, Wm, N) if PROFILE is not None else 0.0, ctypes.byref(a), _stream())
+
+
+# ---- bf16x6 split-precision 3x3 conv (csrc/wc_conv6.hip) ----
+
+CONV_PRECISIONS = ('bf16x6', 'fp32')
+
+
+def default_conv_precision() -> str:
+    """Conv arithmetic for 3x3 stride-1 convs: 'bf16x6' (exact 3-piece bf16 split on bf16 MFMA,
+    fp32-level error) or 'fp32' (fp32 MFMA).  Overridable with WC_CONV_PRECISION."""
+    p = os.environ.get('WC_CONV_PRECISION', 'bf16x6')
+    _req(p in CONV_PRECISIONS, f'WC_CONV_PRECISION must be one of {CONV_PRECISIONS}, got {p!r}')
+    return p
+
+
+@dataclass
+class X6Weight:
+    """A conv weight re-packed for wc_conv3x3_x6: its three exact bf16 pieces, laid out as
+    [N tile][step][piece][k-half][BN][8] (bit patterns in an int16 tensor)."""
+    data: torch.Tensor
+    N: int
+    BN: int
+    C0: int
+    C1: int
+
+
+@functools.lru_cache(maxsize=None)
+def x6_tile(N: int) -> Tuple[int, int]:
+    """(TH, BN) of wc_conv3x3_x6 for N output channels (mirrors wc_conv3x3_x6_tile_n)."""
+    bn = _native.load().wc_conv3x3_x6_tile_n(N)
+    return (16 if bn == 64 else 8), bn
+
+
+def split3_bits(x: torch.Tensor) -> torch.Tensor:
+    """Exact 3-piece bf16 split by truncation (csrc/wc_conv6.hip split3): x == p0 + p1 + p2, each
+    piece a bf16 bit pattern.  Returns int16 (3, *x.shape)."""
+    _req(x.dtype == torch.float32, 'split3 takes fp32')
+    mask = torch.tensor(-65536, dtype=torch.int32, device=x.device)  # 0xffff0000
+    u0 = x.view(torch.int32)
+    r1 = x - (u0 & mask).view(torch.float32)
+    u1 = r1.view(torch.int32)
+    r2 = r1 - (u1 & mask).view(torch.float32)
+    u2 = r2.view(torch.int32)
+    return (torch.stack([u0, u1, u2]) >> 16).to(torch.int16)
+
+
+def pack_x6(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
+    """Re-pack a [N][9*C0 + C1] conv weight (K = (tap, c) then the 1x1 residual columns, as
+    engine.pack_conv) for wc_conv3x3_x6: steps are (16-channel chunk, tap) then the residual chunks."""
+    N, K = w.shape
+    _req(K == 9 * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
+    _, BN = x6_tile(N)
+    Np = -(-N // BN) * BN
+    wp = torch.zeros((Np, K), dtype=torch.float32, device=w.device)
+    wp[:N] = w
+    s0 = wp[:, :9 * C0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, 9 * (C0 // 16), 2, 8)
+    s1 = wp[:, 9 * C0:].reshape(Np, C1 // 16, 2, 8)
+    allw = torch.cat([s0, s1], 1)
+    S = allw.shape[1]
+    pieces = split3_bits(allw)  # (3, Np, S, 2, 8)
+    data = pieces.view(3, Np // BN, BN, S, 2, 8).permute(1, 3, 0, 4, 2, 5).contiguous()
+    return X6Weight(data, N, BN, C0, C1)
+
+
+def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
+    """True when wc_conv3x3_x6 accepts this conv (mirrors its host checks; output must be a plain
+    NHWC view on the same grid)."""
+    TH, _ = x6_tile(N)
+    s0 = segs[0]
+    v = s0.view
+    ok = (list(s0.taps) == TAPS3 and s0.stride == 1 and v.C % 16 == 0 and v.H == Hm and v.W == Wm
+          and Hm % TH == 0 and Wm % 16 == 0 and v.B * v.H * v.W * v.ldc * 4 < 2**31)
+    if len(segs) == 2:
+        s1 = segs[1]
+        ok = ok and (list(s1.taps) == [(0, 0)] and s1.stride == 1 and s1.scale is None and s1.view.C % 16 == 0
+                     and s1.view.H == Hm and s1.view.W == Wm and s1.view.B * Hm * Wm * s1.view.ldc * 4 < 2**31)
+    return ok
+
+
+def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
+               temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None, act: int = 0):
+    """3x3 stride-1 conv (+ fused 1x1 residual segment) on bf16x6 split-precision MFMA."""
+    _req(w6.data.is_cuda and w6.data.is_contiguous(), 'x6 weight')
+    _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
+    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act)
+    TH, BN = x6_tile(w6.N)
+    s0 = segs[0]
+    pro = 0 if s0.scale is None else (2 if s0.silu else 1)
+    res_seg = 'true' if len(segs) == 2 else 'false'
+    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}>', 'wc_conv3x3_x6',
+           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
+           w6.data.numel() * 2, _stream())
 
 
 def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float = 1e-5,

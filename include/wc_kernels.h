@@ -72,7 +72,8 @@ typedef struct wc_conv_args {
     int osy, osx, ooy, oox; /* output position = (my*osy + ooy, mx*osx + oox) */
     int out_nchw;       /* 1: write out[(b*N + n)*Ho*Wo + oy*Wo + ox] (ldo ignored) */
     int act;            /* epilogue activation after bias/temb, before the residual add:
-                           WC_ACT_NONE / WC_ACT_GELU (exact erf) / WC_ACT_SILU */
+                           WC_ACT_NONE / WC_ACT_GELU (exact erf) / WC_ACT_SILU; wc_conv_igemm
+                           accepts an activation only with a raw segment 0 (no scale/shift) */
 } wc_conv_args;
 
 #define WC_ACT_NONE 0

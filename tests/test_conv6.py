@@ -75,7 +75,7 @@ CASES = [
     (1, 32, 32, 128, 64, 0, 'silu', 0),
     (2, 8, 16, 96, 256, 64, 'affine', 0),
     (1, 16, 16, 32, 96, 0, 'raw', 0),
-    (1, 16, 48, 64, 80, 0, 'silu', 1),
+    (1, 16, 48, 64, 80, 0, 'raw', 1),  # activations: raw segment 0 (as wc_conv_igemm requires)
     (2, 32, 16, 256, 128, 128, 'silu', 0),
 ]
 

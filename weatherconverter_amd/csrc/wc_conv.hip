@@ -58,7 +58,6 @@ struct ConvDev {
     int ldo;
     int Ho, Wo, osy, osx, ooy, oox, out_nchw;
     int ident;    // output position == GEMM row (plain NHWC store)
-    int act;      // epilogue activation (WC_ACT_*)
     int steps0;   // K-steps of segment 0
     int steps;    // total K-steps
     int ntiles_n; // N tiles
@@ -89,7 +88,10 @@ WC_DEVICE __amdgpu_buffer_rsrc_t make_srd(const float* p) {
 
 // PRO: 0 = raw segment 0, 1 = GN affine, 2 = GN affine + SiLU.
 // UNIB: every tile lies inside one image (Hm*Wm % BM == 0) -> one (scale, shift) per step.
-template <int BM, int BN, int PRO, bool UNIB>
+// ACT: epilogue activation (WC_ACT_*), a template parameter: a runtime branch to an inlined erff
+// makes the 64-element epilogue too large to unroll, which moves the accumulators to scratch and
+// slows every instantiation ~1.8x.
+template <int BM, int BN, int PRO, bool UNIB, int ACT>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
     using T = Tile<BM, BN>;
     __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE];
@@ -341,8 +343,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
                 int b = (HWm >= 32) ? b0 + (m >= bnd ? 1 : 0) : m / HWm;
                 float v = acc[mb][nb][r] + bn;
                 if (p.temb) v += p.temb[b * p.temb_ld + n];
-                if (p.act == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-                else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
+                if constexpr (ACT == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+                else if constexpr (ACT == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
                 if (p.ident) {
                     if (p.res) v += p.res[(long)m * p.ldres + n];
                     p.out[(long)m * p.ldo + n] = v;
@@ -364,20 +366,26 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
     }
 }
 
-template <int BM, int BN, int PRO, bool UNIB>
+template <int BM, int BN, int PRO, bool UNIB, int ACT = WC_ACT_NONE>
 int launch(const ConvDev& d, hipStream_t stream) {
     ConvDev p = d;
     int tiles_m = (p.M + BM - 1) / BM;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(tiles_m * p.ntiles_n);
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, PRO, UNIB>), grid, dim3(NTHREADS), 0, stream, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, PRO, UNIB, ACT>), grid, dim3(NTHREADS), 0, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 template <int BM, int BN>
-int dispatch(const ConvDev& d, int pro, hipStream_t s) {
+int dispatch(const ConvDev& d, int pro, int act, hipStream_t s) {
     const bool unib = (d.Hm * d.Wm) % BM == 0;
+    if (act != WC_ACT_NONE) {  // activations are instantiated for a raw segment 0 only
+        if (pro != 0) return WC_E_ARG;
+        if (act == WC_ACT_GELU)
+            return unib ? launch<BM, BN, 0, true, WC_ACT_GELU>(d, s) : launch<BM, BN, 0, false, WC_ACT_GELU>(d, s);
+        return unib ? launch<BM, BN, 0, true, WC_ACT_SILU>(d, s) : launch<BM, BN, 0, false, WC_ACT_SILU>(d, s);
+    }
     switch (pro * 2 + (unib ? 1 : 0)) {
         case 0: return launch<BM, BN, 0, false>(d, s);
         case 1: return launch<BM, BN, 0, true>(d, s);
@@ -440,7 +448,6 @@ extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     d.Ho = a->Ho; d.Wo = a->Wo; d.osy = a->osy; d.osx = a->osx; d.ooy = a->ooy; d.oox = a->oox;
     d.out_nchw = a->out_nchw;
     if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
-    d.act = a->act;
     d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
               a->Ho == a->Hm && a->Wo == a->Wm;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
@@ -448,6 +455,6 @@ extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // 64-column outputs (C_out = 64 stages, the 3-channel head) use a 256x64 tile.
-    if (a->N <= 64) return dispatch<256, 64>(d, pro, s);
-    return dispatch<128, 128>(d, pro, s);
+    if (a->N <= 64) return dispatch<256, 64>(d, pro, a->act, s);
+    return dispatch<128, 128>(d, pro, a->act, s);
 }

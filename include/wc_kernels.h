@@ -103,8 +103,17 @@ int wc_conv_igemm(const wc_conv_args* args, void* stream);
  * steps = 9*(C0/16) (channel-chunk major, tap minor) + C1/16, w6_bytes its size in bytes.
  * Replaces the same reference layers as wc_conv_igemm's 3x3 case (unet_base.py:92,106). */
 int wc_conv3x3_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, void* stream);
-/* The output-channel tile (BN) wc_conv3x3_x6 uses for N output channels. */
+/* The output-channel tile (BN) wc_conv3x3_x6 and wc_conv_igemm_x6 use for N output channels. */
 int wc_conv3x3_x6_tile_n(int N);
+
+/* General implicit-GEMM conv at the same bf16x6 arithmetic: exactly wc_conv_igemm's contract
+ * (tap grids, input strides, the 1x1 residual segment, output maps, NCHW store; an activation
+ * only with a raw segment 0) with channel counts C % 16 == 0.  args->w / ldw are ignored; w6 is
+ * the weight pre-split as [ceil(N/BN)][K/16][piece 3][k-half 2][BN][8] bf16 bit patterns with K
+ * in wc_conv_igemm's natural order (tap-major, then the residual columns).
+ * Replaces the same reference layers as wc_conv_igemm (unet_base.py:115,129,159,334 and the
+ * old UNet's Linear layers, old_modules.py:87-95). */
+int wc_conv_igemm_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */

@@ -145,3 +145,157 @@ def test_conv3x3_x6_rejects_untiled_shape():
     out = torch.empty((1, 12, 16, 128), device='cuda')
     with pytest.raises(RuntimeError):
         K.conv3x3_x6(segs, w6, None, K.View.full(out), Hm=12, Wm=16)
+
+
+# ---------------------------------------------------------------- general implicit GEMM (wc_conv_igemm_x6)
+
+TAPS4S2 = [(ky - 1, kx - 1) for ky in range(4) for kx in range(4)]
+
+
+def _run_both(K, segs, wp, C0, C1, ntaps, bias, out_fn, **kw):
+    """Run wc_conv_igemm (fp32) and wc_conv_igemm_x6 on identical args; return both outputs (CPU)."""
+    outs = {}
+    for mode in ('x6', 'fp32'):
+        out_view, out_nchw, read = out_fn()
+        if mode == 'x6':
+            K.conv_igemm_x6(segs, K.pack_x6(wp, C0, C1, ntaps=ntaps, order='natural'), bias, out_view,
+                            out_nchw=out_nchw, **kw)
+        else:
+            K.conv_igemm(segs, wp, bias, out_view, out_nchw=out_nchw, **kw)
+        torch.cuda.synchronize()
+        outs[mode] = read()
+    return outs
+
+
+def _check(outs, ref):
+    e6 = rel_l2(outs['x6'].double(), ref)
+    e32 = rel_l2(outs['fp32'].double(), ref)
+    assert e6 < 1e-5 and e6 <= 4 * e32 + 1e-7, (e6, e32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,C,N', [(2, 16, 16, 128, 384), (1, 32, 32, 64, 64), (3, 8, 12, 96, 160)])
+def test_igemm_x6_linear_gn_prologue_residual(B, H, W, C, N):
+    """Attention in_proj / out_proj shapes: (GN-affine(x)) W^T + b (+ residual view)."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((B, H, W, C), generator=g) * 3 + 1
+    sc = 1 + 0.3 * torch.randn((B, C), generator=g)
+    sh = 0.3 * torch.randn((B, C), generator=g)
+    w = torch.randn((N, C), generator=g) / C**0.5
+    b = torch.randn(N, generator=g) * 0.1
+    res = torch.randn((B, H, W, N), generator=g)
+    a = x.double() * sc.double()[:, None, None, :] + sh.double()[:, None, None, :]
+    ref = a @ w.double().t() + b.double() + res.double()
+    segs = [K.Seg(K.View.full(x.cuda()), [(0, 0)], scale=sc.cuda(), shift=sh.cuda())]
+    resv = K.View.full(res.cuda())
+
+    def out_fn():
+        o = torch.empty((B, H, W, N), device='cuda')
+        return K.View.full(o), None, lambda: o.cpu()
+    _check(_run_both(K, segs, w.cuda(), C, 0, 1, b.cuda(), out_fn, Hm=H, Wm=W, res=resv), ref)
+
+
+@pytest.mark.gpu
+def test_igemm_x6_down_conv_4x4_s2():
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(12)
+    B, H, Ci, Co = 2, 16, 64, 128
+    x = torch.randn((B, Ci, H, H), generator=g)
+    w = torch.randn((Co, Ci, 4, 4), generator=g) / (16 * Ci)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1)
+    segs = [K.Seg(K.View.full(_nhwc(x).cuda()), TAPS4S2, stride=2)]
+
+    def out_fn():
+        o = torch.empty((B, H // 2, H // 2, Co), device='cuda')
+        return K.View.full(o), None, lambda: _nchw(o.cpu())
+    _check(_run_both(K, segs, _pack(w).cuda(), Ci, 0, 16, b.cuda(), out_fn, Hm=H // 2, Wm=H // 2), ref)
+
+
+@pytest.mark.gpu
+def test_igemm_x6_conv_transpose_into_concat_slice():
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.models.engine import pack_convT
+    g = torch.Generator().manual_seed(13)
+    B, H, Ci, Co = 2, 8, 128, 64
+    x = torch.randn((B, Ci, H, H), generator=g)
+    wt = torch.randn((Ci, Co, 4, 4), generator=g) / (4 * Ci)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv_transpose2d(x.double(), wt.double(), b.double(), stride=2, padding=1)
+    xv = K.View.full(_nhwc(x).cuda())
+    outs = {'x6': None, 'fp32': None}
+    for mode in outs:
+        buf = torch.full((B, 2 * H, 2 * H, 2 * Co), 5.0, device='cuda')
+        dst = K.View(buf, 0, Co)
+        for py in (0, 1):
+            for px in (0, 1):
+                taps, w = pack_convT(wt, py, px)
+                if mode == 'x6':
+                    K.conv_igemm_x6([K.Seg(xv, taps)], K.pack_x6(w.cuda(), Ci, 0, ntaps=4, order='natural'),
+                                    b.cuda(), dst, Hm=H, Wm=H, out_map=(2, 2, py, px))
+                else:
+                    K.conv_igemm([K.Seg(xv, taps)], w.cuda(), b.cuda(), dst, Hm=H, Wm=H, out_map=(2, 2, py, px))
+        torch.cuda.synchronize()
+        bc = buf.cpu()
+        assert bool((bc[..., Co:] == 5.0).all())
+        outs[mode] = _nchw(bc[..., :Co])
+    _check(outs, ref)
+
+
+@pytest.mark.gpu
+def test_igemm_x6_nchw_head_and_gelu():
+    """The N=3 head (GN+SiLU prologue, NCHW store) and a raw 1x1 with GELU epilogue."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(14)
+    B, H, C = 2, 12, 64
+    h = torch.randn((B, C, H, H), generator=g)
+    sc = 1 + 0.2 * torch.randn((B, C), generator=g)
+    sh = 0.2 * torch.randn((B, C), generator=g)
+    w = torch.randn((3, C, 3, 3), generator=g) / (9 * C)**0.5
+    b = torch.randn(3, generator=g) * 0.1
+    a = F.silu(h.double() * sc.double()[:, :, None, None] + sh.double()[:, :, None, None])
+    ref = F.conv2d(a, w.double(), b.double(), padding=1)
+    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=True)]
+
+    def out_fn():
+        o = torch.empty((B, 3, H, H), device='cuda')
+        return None, o, lambda: o.cpu()
+    _check(_run_both(K, segs, _pack(w).cuda(), C, 0, 9, b.cuda(), out_fn, Hm=H, Wm=H), ref)
+
+    x = torch.randn((B, H, H, C), generator=g)
+    w2 = torch.randn((96, C), generator=g) / C**0.5
+    ref2 = F.gelu(x.double() @ w2.double().t())
+
+    def out_fn2():
+        o = torch.empty((B, H, H, 96), device='cuda')
+        return K.View.full(o), None, lambda: o.cpu()
+    _check(_run_both(K, [K.Seg(K.View.full(x.cuda()), [(0, 0)])], w2.cuda(), C, 0, 1, None, out_fn2, Hm=H, Wm=H,
+                     act=1), ref2)
+
+
+@pytest.mark.gpu
+def test_igemm_x6_3x3_with_residual_segment_odd_grid():
+    """ResBlock conv2 on a grid the halo kernel does not tile (9 x 20): the implicit-GEMM fallback."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(15)
+    B, H, W, Ci, Co, Cr = 2, 9, 20, 64, 128, 32
+    h = torch.randn((B, Ci, H, W), generator=g)
+    x2 = torch.randn((B, Cr, H, W), generator=g)
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (9 * Ci)**0.5
+    wr = torch.randn((Co, Cr, 1, 1), generator=g) / Cr**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    temb = torch.randn((B, Co), generator=g)
+    sc = 1 + 0.2 * torch.randn((B, Ci), generator=g)
+    sh = 0.2 * torch.randn((B, Ci), generator=g)
+    a = F.silu(h.double() * sc.double()[:, :, None, None] + sh.double()[:, :, None, None])
+    ref = F.conv2d(a, w.double(), b.double(), padding=1) + temb.double()[:, :, None, None] + F.conv2d(
+        x2.double(), wr.double())
+    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=True),
+            K.Seg(K.View.full(_nhwc(x2).cuda()), [(0, 0)], kbase=9 * Ci)]
+    wp = torch.cat([_pack(w), wr.reshape(Co, Cr)], 1).contiguous().cuda()
+
+    def out_fn():
+        o = torch.empty((B, H, W, Co), device='cuda')
+        return K.View.full(o), None, lambda: _nchw(o.cpu())
+    _check(_run_both(K, segs, wp, Ci, Cr, 9, b.cuda(), out_fn, Hm=H, Wm=W, temb=temb.cuda(), temb_ld=Co), ref)

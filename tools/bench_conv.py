@@ -25,35 +25,45 @@ def timeit(fn, iters=10):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
-def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32'):
+def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps=None):
+    taps = TAPS3 if taps is None else taps
+    nt = len(taps)
     g = torch.Generator(device='cuda').manual_seed(0)
     x = torch.randn((B, H, H, Ci), device='cuda', generator=g)
-    w = torch.randn((Co, 9 * Ci + res), device='cuda', generator=g) / (9 * Ci)**0.5
+    w = torch.randn((Co, nt * Ci + res), device='cuda', generator=g) / (nt * Ci)**0.5
     b = torch.randn(Co, device='cuda', generator=g)
     sc = torch.rand((B, Ci), device='cuda', generator=g) + 0.5
     sh = torch.randn((B, Ci), device='cuda', generator=g) * 0.1
     out = torch.empty((B, H, H, Co), device='cuda')
-    segs = [K.Seg(K.View.full(x), TAPS3, scale=sc if prologue else None, shift=sh if prologue else None,
-                  silu=prologue)]
+    segs = [K.Seg(K.View.full(x), taps, scale=sc if prologue else None, shift=sh if prologue else None,
+                  silu=prologue and nt > 1)]
     if res:
         xr = torch.randn((B, H, H, res), device='cuda', generator=g)
-        segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=9 * Ci))
-    if mode == 'x6':
+        segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=nt * Ci))
+    if mode == 'x6' and nt != 9:
+        return None, None, None
+    if mode == 'igx6':
+        w6 = K.pack_x6(w, Ci, res, ntaps=nt, order='natural')
+        fn = lambda: K.conv_igemm_x6(segs, w6, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
+    elif mode == 'x6':
         w6 = K.pack_x6(w, Ci, res)
         fn = lambda: K.conv3x3_x6(segs, w6, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
     else:
         fn = lambda: K.conv_igemm(segs, w, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
     t = timeit(fn)
-    fl = 2.0 * B * H * H * Co * (9 * Ci + res)
+    fl = 2.0 * B * H * H * Co * (nt * Ci + res)
     err = None
     if check:
         xx = x.permute(0, 3, 1, 2)
-        a = F.silu(xx * sc[:, :, None, None] + sh[:, :, None, None]) if prologue else xx
-        wt = w[:, :9 * Ci].reshape(Co, 3, 3, Ci).permute(0, 3, 1, 2)
+        a = xx * sc[:, :, None, None] + sh[:, :, None, None] if prologue else xx
+        if prologue and nt > 1:
+            a = F.silu(a)
+        k = 3 if nt == 9 else 1
+        wt = w[:, :nt * Ci].reshape(Co, k, k, Ci).permute(0, 3, 1, 2)
         torch.backends.cudnn.allow_tf32 = False
-        ref = F.conv2d(a, wt, b, padding=1)
+        ref = F.conv2d(a, wt, b, padding=k // 2)
         if res:
-            ref = ref + F.conv2d(xr.permute(0, 3, 1, 2), w[:, 9 * Ci:].reshape(Co, res, 1, 1))
+            ref = ref + F.conv2d(xr.permute(0, 3, 1, 2), w[:, nt * Ci:].reshape(Co, res, 1, 1))
         fn()
         torch.cuda.synchronize()
         got = out.permute(0, 3, 1, 2)
@@ -73,22 +83,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--check', action='store_true')
     ap.add_argument('--only', type=int, default=-1, help='run a single conv case (for PMC profiling)')
-    ap.add_argument('--modes', default='fp32,x6', help='conv arithmetic(s) to time: fp32, x6')
+    ap.add_argument('--modes', default='fp32,x6,igx6', help='conv kernels to time: fp32, x6 (halo 3x3), igx6')
     a = ap.parse_args()
     K._native.load()
     cases = [(16, 256, 128, 128, True, 0), (16, 256, 128, 128, True, 64), (16, 256, 64, 64, True, 0),
              (16, 128, 256, 256, True, 0), (16, 64, 512, 512, True, 0), (16, 32, 768, 768, True, 0),
-             (16, 32, 1024, 256, True, 0), (16, 256, 64, 128, False, 0)]
+             (16, 32, 1024, 256, True, 0), (16, 256, 64, 128, False, 0),
+             (16, 64, 512, 1536, True, 0, [(0, 0)]), (16, 32, 768, 768, False, 0, [(0, 0)])]
     tot_t = tot_f = 0
     if a.only >= 0:
         cases = [cases[a.only]]
     for mode in a.modes.split(','):
         tot_t = tot_f = 0
         for c in cases:
-            t, tf, err = conv_case(*c, check=a.check, mode=mode)
+            t, tf, err = conv_case(*c[:6], check=a.check, mode=mode, taps=c[6] if len(c) > 6 else None)
+            if t is None:
+                continue
             tot_t += t
             tot_f += tf * t
-            print(f'{mode:4s} conv B={c[0]} S={c[1]} {c[2]}->{c[3]} prologue={c[4]} res={c[5]}: {t*1e3:8.3f} ms  '
+            print(f'{mode:4s} conv{"1x1" if len(c) > 6 else "3x3"} B={c[0]} S={c[1]} {c[2]}->{c[3]} prologue={c[4]} res={c[5]}: {t*1e3:8.3f} ms  '
                   f'{tf:6.1f} TF/s' + (f'  relL2={err:.2e}' if err is not None else ''), flush=True)
         print(f'{mode} conv aggregate {tot_f / tot_t:.1f} TF/s')
     if a.only >= 0:

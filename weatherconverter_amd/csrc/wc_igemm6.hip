@@ -1,0 +1,408 @@
+// General implicit-GEMM convolution on bf16x6 split-precision MFMA for gfx950: any tap grid,
+// input stride, 1x1 residual segment and output map (NHWC view / parity-strided / NCHW) — the
+// same contract as wc_conv_igemm (wc_conv.hip), at the bf16x6 arithmetic of wc_conv6.hip.
+//
+// Used for the convs the halo-tiled 3x3 kernel does not take: the attention in/out projections
+// (1x1, GN-affine prologue / residual epilogue), the 4x4 stride-2 down convs, the four parity
+// sub-convs of each ConvTranspose2d, and 3x3 convs whose grid does not tile (head, small levels).
+//
+// Structure (as wc_conv.hip, with 16-channel K-steps):
+//   * GEMM view M = B*Hm*Wm output positions, N = output channels, K-step = 16 channels of one
+//     tap (segment 0, tap-major) or of the 1x1 residual segment.  The weight is pre-split by the
+//     host into [N tile][K-step][piece 3][k-half 2][BN][8] bf16 (K in natural order).
+//   * 4 waves, each a 64x64 sub-tile of 2x2 32x32 accumulators; per K-step 24 MFMAs
+//     (piece-order sums 0, 1, 2 of both operands).
+//   * The global loads of step k+1 are issued before the MFMAs of step k; after them the A
+//     values get the GN(+SiLU) prologue, zero padding, the exact 3-piece split, and are written
+//     into the other LDS buffer with the step's weight pieces; one barrier per step.
+//   * LDS images are [piece][k-half][row][8 bf16] (16-byte row slots): the ds_read_b128 lane
+//     groups {0-3,12-15,20-27} / {4-11,16-19,28-31} read 16 rows distinct mod 16 ->
+//     conflict-free with no swizzle.
+#include "wc_x6.hpp"
+
+namespace {
+
+using namespace wcx6;
+
+constexpr int NT = 256;
+constexpr int BK = 16;  // channels per K-step
+
+struct IgDev {
+    const float* src0;
+    int C0, ldc0, H0, W0, sy, sx;
+    int kh, kw, ty0, tdy, tx0, tdx;  // tap (ky, kx) reads input (y*sy + ty0 + ky*tdy, x*sx + tx0 + kx*tdx)
+    const float* scale;
+    const float* shift;
+    const float* src1;
+    int C1, ldc1;
+    int B, Hm, Wm, N, M;
+    const void* w6;
+    const float* bias;
+    const float* temb;
+    int temb_ld;
+    const float* res;
+    int ldres;
+    float* out;
+    int ldo;
+    int Ho, Wo, osy, osx, ooy, oox, out_nchw;
+    int ident;
+    int steps0, steps;
+    int ntiles_n;
+};
+
+template <int BM, int BN>
+struct IgTile {
+    static constexpr int WAVES_M = BM / 64;
+    static constexpr int WAVES_N = BN / 64;
+    static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
+    static constexpr int A_PER_T = BM * (BK / 4) / NT;  // float4 per thread per step
+    static constexpr int APLANE = BM * 16;              // bytes of one (piece, k-half) plane
+    static constexpr int BPLANE = BN * 16;
+    static constexpr int ASTAGE = 6 * APLANE;
+    static constexpr int BSTAGE = 6 * BPLANE;
+    static constexpr int STAGE = ASTAGE + BSTAGE;
+    static constexpr int B_ITEMS = BSTAGE / 16;
+    static constexpr int B_PER_T = (B_ITEMS + NT - 1) / NT;
+};
+
+// PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU.  UNIB: tiles never straddle images.  ACT: epilogue
+// activation (template, see wc_conv.hip).
+template <int BM, int BN, int PRO, bool UNIB, int ACT>
+__global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
+    using T = IgTile<BM, BN>;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / T::WAVES_N;
+    const int wn = wave % T::WAVES_N;
+
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int tile_m = bid / p.ntiles_n;
+    const int tile_n = bid % p.ntiles_n;
+    const int m0 = tile_m * BM;
+    const int n0 = tile_n * BN;
+    const int HWm = p.Hm * p.Wm;
+
+    // ---- staging coordinates: thread = (row prow + 64 j, channel quad q4) ----
+    const int q4 = tid & 3;
+    const int prow = tid >> 2;  // 0..63
+    int pb[T::A_PER_T], ys[T::A_PER_T], xs[T::A_PER_T], org0[T::A_PER_T], org1[T::A_PER_T];
+#pragma unroll
+    for (int j = 0; j < T::A_PER_T; ++j) {
+        const int m = m0 + prow + 64 * j;
+        if (m < p.M) {
+            const int b = m / HWm;
+            const int r = m - b * HWm;
+            const int y = r / p.Wm;
+            const int x = r - y * p.Wm;
+            pb[j] = b;
+            ys[j] = y * p.sy;
+            xs[j] = x * p.sx;
+            org0[j] = ((b * p.H0 + ys[j]) * p.W0 + xs[j]) * p.ldc0 + q4 * 4;
+            org1[j] = ((b * p.H0 + ys[j]) * p.W0 + xs[j]) * p.ldc1 + q4 * 4;
+        } else {
+            pb[j] = -1; ys[j] = -(1 << 24); xs[j] = 0; org0[j] = 0; org1[j] = 0;
+        }
+    }
+    const int b_tile = m0 / HWm;
+    // LDS byte offset of this thread's 8-byte A write within a piece plane set
+    const int a_wr = (q4 >> 1) * T::APLANE + prow * 16 + (q4 & 1) * 8;
+
+    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
+    const __amdgpu_buffer_rsrc_t srd1 = make_srd(p.src1 ? p.src1 : p.src0);
+    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w6);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
+
+    f32x4 ra[T::A_PER_T];
+    u32x4 rb[T::B_PER_T];
+    f32x4 rsc[UNIB ? 1 : T::A_PER_T], rsh[UNIB ? 1 : T::A_PER_T];
+    unsigned aval = 0;
+    int ky = 0, kx = 0, c0 = 0, c1 = 0, bstep = 0;
+
+    auto load_w = [&]() {
+        const unsigned base = (unsigned)((tile_n * p.steps + bstep) * T::BSTAGE);
+#pragma unroll
+        for (int j = 0; j < T::B_PER_T; ++j) {
+            const int i = tid + NT * j;
+            rb[j] = bload_u4(srdw, i < T::B_ITEMS ? base + (unsigned)i * 16u : OOB);
+        }
+        ++bstep;
+    };
+    auto load0 = [&]() {
+        const int dy = p.ty0 + ky * p.tdy, dx = p.tx0 + kx * p.tdx;
+        const int tap_off = (dy * p.W0 + dx) * p.ldc0 + c0;
+        aval = 0;
+#pragma unroll
+        for (int j = 0; j < T::A_PER_T; ++j) {
+            const int iy = ys[j] + dy, ix = xs[j] + dx;
+            const bool ok = (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
+            aval |= (ok ? 1u : 0u) << j;
+            ra[j] = bload_f4(srd0, ok ? (unsigned)(org0[j] + tap_off) * 4u : OOB);
+        }
+        if constexpr (PRO != 0) {
+            const int c = c0 + q4 * 4;
+            if constexpr (UNIB) {
+                rsc[0] = bload_f4(srdsc, (unsigned)(b_tile * p.C0 + c) * 4u);
+                rsh[0] = bload_f4(srdsh, (unsigned)(b_tile * p.C0 + c) * 4u);
+            } else {
+#pragma unroll
+                for (int j = 0; j < T::A_PER_T; ++j) {
+                    const unsigned o = pb[j] >= 0 ? (unsigned)(pb[j] * p.C0 + c) * 4u : OOB;
+                    rsc[j] = bload_f4(srdsc, o);
+                    rsh[j] = bload_f4(srdsh, o);
+                }
+            }
+        }
+        load_w();
+        c0 += BK;
+        const bool wc = c0 == p.C0;
+        c0 = wc ? 0 : c0;
+        kx += wc ? 1 : 0;
+        const bool wx = kx == p.kw;
+        kx = wx ? 0 : kx;
+        ky += wx ? 1 : 0;
+    };
+    auto load1 = [&]() {
+        aval = 0;
+#pragma unroll
+        for (int j = 0; j < T::A_PER_T; ++j) {
+            aval |= (pb[j] >= 0 ? 1u : 0u) << j;
+            ra[j] = bload_f4(srd1, pb[j] >= 0 ? (unsigned)(org1[j] + c1) * 4u : OOB);
+        }
+        load_w();
+        c1 += BK;
+    };
+
+    auto store = [&](unsigned char* buf, bool pro) {
+#pragma unroll
+        for (int j = 0; j < T::A_PER_T; ++j) {
+            f32x4 v = ra[j];
+            if constexpr (PRO != 0) {
+                if (pro) {
+                    v = v * rsc[UNIB ? 0 : j] + rsh[UNIB ? 0 : j];
+                    if constexpr (PRO == 2) {
+                        v.x = silu_fast(v.x); v.y = silu_fast(v.y);
+                        v.z = silu_fast(v.z); v.w = silu_fast(v.w);
+                    }
+                }
+            }
+            if (!((aval >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+            u32x2 a0, a1, a2;
+            split3(v, a0, a1, a2);
+            unsigned char* d = buf + a_wr + j * 64 * 16;
+            *reinterpret_cast<u32x2*>(d) = a0;
+            *reinterpret_cast<u32x2*>(d + 2 * T::APLANE) = a1;
+            *reinterpret_cast<u32x2*>(d + 4 * T::APLANE) = a2;
+        }
+        unsigned char* bb = buf + T::ASTAGE;
+#pragma unroll
+        for (int j = 0; j < T::B_PER_T; ++j) {
+            const int i = tid + NT * j;
+            if (i < T::B_ITEMS) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[j];
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int l32 = lane & 31;
+    const int half = lane >> 5;
+    const int a_rd = half * T::APLANE + (wm * 64 + l32) * 16;
+    const int b_rd = T::ASTAGE + half * T::BPLANE + (wn * 64 + l32) * 16;
+
+    auto compute = [&](const unsigned char* buf) {
+        u32x4 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+                fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * T::APLANE);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * T::BPLANE);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+            }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][2], acc[mb][nb]);
+                acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
+            }
+    };
+
+    // ---- K loop: one barrier per step ----
+    if (p.steps0 > 0) { load0(); store(smem, true); } else { load1(); store(smem, false); }
+    __syncthreads();
+    int step = 0;
+    for (; step < p.steps0 - 1; ++step) {
+        unsigned char* cur = smem + (step & 1) * T::STAGE;
+        unsigned char* nxt = smem + ((step & 1) ^ 1) * T::STAGE;
+        load0();
+        compute(cur);
+        store(nxt, true);
+        __syncthreads();
+    }
+    for (; step < p.steps - 1; ++step) {
+        unsigned char* cur = smem + (step & 1) * T::STAGE;
+        unsigned char* nxt = smem + ((step & 1) ^ 1) * T::STAGE;
+        load1();
+        compute(cur);
+        store(nxt, false);
+        __syncthreads();
+    }
+    compute(smem + (step & 1) * T::STAGE);
+
+    // ---- epilogue (as wc_conv.hip) ----
+    const int HWo = p.Ho * p.Wo;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int mbase = m0 + wm * 64 + mb * 32;
+        const int b0 = mbase / HWm;
+        const int bnd = (b0 + 1) * HWm;
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int n = n0 + wn * 64 + nb * 32 + l32;
+            if (n >= p.N) continue;
+            const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int m = mbase + row;
+                if (m >= p.M) continue;
+                int b = (HWm >= 32) ? b0 + (m >= bnd ? 1 : 0) : m / HWm;
+                float v = acc[mb][nb][r] + bn;
+                if (p.temb) v += p.temb[b * p.temb_ld + n];
+                if constexpr (ACT == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+                else if constexpr (ACT == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
+                if (p.ident) {
+                    if (p.res) v += p.res[(long)m * p.ldres + n];
+                    p.out[(long)m * p.ldo + n] = v;
+                } else {
+                    const int rr = m - b * HWm;
+                    const int my = rr / p.Wm;
+                    const int mx = rr - my * p.Wm;
+                    const int oy = my * p.osy + p.ooy;
+                    const int ox = mx * p.osx + p.oox;
+                    const long pix = (long)(b * p.Ho + oy) * p.Wo + ox;
+                    if (p.res) v += p.res[pix * p.ldres + n];
+                    if (p.out_nchw)
+                        p.out[((long)b * p.N + n) * HWo + (long)oy * p.Wo + ox] = v;
+                    else
+                        p.out[pix * p.ldo + n] = v;
+                }
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int PRO, bool UNIB, int ACT = WC_ACT_NONE>
+int launch(const IgDev& d, hipStream_t stream) {
+    IgDev p = d;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    p.ntiles_n = (p.N + BN - 1) / BN;
+    dim3 grid(tiles_m * p.ntiles_n);
+    hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT>), grid, dim3(NT), 0, stream, p);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+template <int BM, int BN>
+int dispatch(const IgDev& d, int pro, int act, hipStream_t s) {
+    const bool unib = (d.Hm * d.Wm) % BM == 0;
+    if (act != WC_ACT_NONE) {  // activations are instantiated for a raw segment 0 only
+        if (pro != 0) return WC_E_ARG;
+        if (act == WC_ACT_GELU)
+            return unib ? launch<BM, BN, 0, true, WC_ACT_GELU>(d, s) : launch<BM, BN, 0, false, WC_ACT_GELU>(d, s);
+        return unib ? launch<BM, BN, 0, true, WC_ACT_SILU>(d, s) : launch<BM, BN, 0, false, WC_ACT_SILU>(d, s);
+    }
+    switch (pro * 2 + (unib ? 1 : 0)) {
+        case 0: return launch<BM, BN, 0, false>(d, s);
+        case 1: return launch<BM, BN, 0, true>(d, s);
+        case 2: return launch<BM, BN, 1, false>(d, s);
+        case 3: return launch<BM, BN, 1, true>(d, s);
+        case 4: return launch<BM, BN, 2, false>(d, s);
+        default: return launch<BM, BN, 2, true>(d, s);
+    }
+}
+
+}  // namespace
+
+extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
+    if (!a || !w6 || !a->out) return WC_E_ARG;
+    if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
+    if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src) return WC_E_ARG;
+    if ((s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
+    if (s0.C <= 0 || s0.C % BK || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
+    if (s0.ntaps < 1 || s0.ntaps > WC_MAX_TAPS || s0.kbase != 0) return WC_E_SHAPE;
+    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;  // 2 GiB SRD range
+    int kw = 1;
+    while (kw < s0.ntaps && s0.dy[kw] == s0.dy[0]) ++kw;
+    if (s0.ntaps % kw != 0) return WC_E_SHAPE;
+    const int kh = s0.ntaps / kw;
+    const int tdx = kw > 1 ? s0.dx[1] - s0.dx[0] : 0;
+    const int tdy = kh > 1 ? s0.dy[kw] - s0.dy[0] : 0;
+    for (int t = 0; t < s0.ntaps; ++t)
+        if (s0.dy[t] != s0.dy[0] + (t / kw) * tdy || s0.dx[t] != s0.dx[0] + (t % kw) * tdx) return WC_E_SHAPE;
+    IgDev d{};
+    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.H0 = s0.H; d.W0 = s0.W; d.sy = s0.sy; d.sx = s0.sx;
+    d.kh = kh; d.kw = kw; d.ty0 = s0.dy[0]; d.tdy = tdy; d.tx0 = s0.dx[0]; d.tdx = tdx;
+    d.scale = s0.scale; d.shift = s0.shift;
+    long k = (long)s0.ntaps * s0.C;
+    if (a->nseg == 2) {
+        const wc_conv_seg& s1 = a->seg[1];
+        if (!s1.src || s1.scale) return WC_E_ARG;
+        if (s1.C <= 0 || s1.C % BK || s1.ldc % 4 || (reinterpret_cast<uintptr_t>(s1.src) & 15)) return WC_E_SHAPE;
+        if (s1.ntaps != 1 || s1.dy[0] != 0 || s1.dx[0] != 0) return WC_E_SHAPE;
+        if (s1.H != s0.H || s1.W != s0.W || s1.sy != s0.sy || s1.sx != s0.sx) return WC_E_SHAPE;
+        if (s1.kbase != k) return WC_E_SHAPE;
+        if ((long)a->B * s1.H * s1.W * s1.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+        d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc;
+        k += s1.C;
+    }
+    const long M = (long)a->B * a->Hm * a->Wm;
+    if (M <= 0 || M > (1L << 30) || a->N <= 0) return WC_E_SHAPE;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w6_bytes != ntn * (k / BK) * (long)BN * 96 || w6_bytes >= (1L << 31)) return WC_E_SHAPE;
+    if (reinterpret_cast<uintptr_t>(w6) & 15) return WC_E_SHAPE;
+    d.B = a->B; d.Hm = a->Hm; d.Wm = a->Wm; d.N = a->N; d.M = (int)M;
+    d.w6 = w6; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
+    d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo;
+    d.Ho = a->Ho; d.Wo = a->Wo; d.osy = a->osy; d.osx = a->osx; d.ooy = a->ooy; d.oox = a->oox;
+    d.out_nchw = a->out_nchw;
+    d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
+              a->Ho == a->Hm && a->Wo == a->Wm;
+    d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
+    d.steps = (int)(k / BK);
+    const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return dispatch<256, 64>(d, pro, a->act, s);
+    return dispatch<128, 128>(d, pro, a->act, s);
+}

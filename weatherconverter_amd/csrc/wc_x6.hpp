@@ -1,0 +1,58 @@
+// Shared helpers of the bf16x6 split-precision kernels (wc_conv6.hip, wc_igemm6.hip).
+#pragma once
+#include "wc_common.hpp"
+
+namespace wcx6 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr unsigned OOB = 0x80000000u;  // byte offset past the SRD range -> load returns 0
+constexpr int SRD_BYTES = 0x7FFFFFFF;
+constexpr int SRD_FLAGS = 0x00020000;
+
+WC_DEVICE __amdgpu_buffer_rsrc_t make_srd(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, SRD_BYTES, SRD_FLAGS);
+}
+WC_DEVICE f32x4 bload_f4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+WC_DEVICE u32x4 bload_u4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+WC_DEVICE f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+WC_DEVICE float silu_fast(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+
+// High halves of two fp32 bit patterns packed into one dword: (hi16(hi) << 16) | hi16(lo).
+WC_DEVICE unsigned hi_pair(unsigned hi, unsigned lo) { return __builtin_amdgcn_perm(hi, lo, 0x07060302u); }
+
+// Exact three-piece bf16 split of 4 floats by truncation: v = p0 + p1 + p2 exactly, each piece
+// 8 significant bits (wc_conv6.hip header comment).
+// NOTE: bit-cast a scalar copy, never the subscript v[e] directly: hipcc (ROCm 7.2 clang) lowers
+// __builtin_bit_cast(unsigned, v[e]) of an ext_vector element to element 0 for every e
+// (tools/probes/bitcast_vector_element.hip reproduces it).
+WC_DEVICE void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+    unsigned u0[4], u1[4], u2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e];
+        const unsigned a = __float_as_uint(x);
+        const float r1 = x - __uint_as_float(a & 0xffff0000u);
+        const unsigned c = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(c & 0xffff0000u);
+        u0[e] = a;
+        u1[e] = c;
+        u2[e] = __float_as_uint(r2);
+    }
+    p0 = u32x2{hi_pair(u0[1], u0[0]), hi_pair(u0[3], u0[2])};
+    p1 = u32x2{hi_pair(u1[1], u1[0]), hi_pair(u1[3], u1[2])};
+    p2 = u32x2{hi_pair(u2[1], u2[0]), hi_pair(u2[3], u2[2])};
+}
+
+}  // namespace wcx6

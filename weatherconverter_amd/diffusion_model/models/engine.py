@@ -70,8 +70,8 @@ class ResPack:
     w2: torch.Tensor  # conv2 (9*co) ++ residual 1x1 (ci)
     b2: torch.Tensor
     temb_off: int
-    w1x6: Optional[K.X6Weight] = None  # bf16x6 re-packs (precision 'bf16x6')
-    w2x6: Optional[K.X6Weight] = None
+    w1x6: Optional[Tuple[K.X6Weight, K.X6Weight]] = None  # bf16x6 re-packs (halo, natural order)
+    w2x6: Optional[Tuple[K.X6Weight, K.X6Weight]] = None
 
 
 @dataclass
@@ -84,6 +84,8 @@ class AttnPack:
     b_in: torch.Tensor
     w_out: torch.Tensor
     b_out: torch.Tensor
+    w_in_x6: Optional[K.X6Weight] = None
+    w_out_x6: Optional[K.X6Weight] = None
 
 
 class UnetEngine:
@@ -111,14 +113,22 @@ class UnetEngine:
         self._temb_P = 0
         with torch.no_grad():
             self.downs = [self._pack_stage(blk, n_res=blk.num_layers, attn=blk.use_attn) for blk in m.downs]
-            self.down_convs = [(pack_conv(blk.down_sample_conv.weight), blk.down_sample_conv.bias.detach().float())
-                               if blk.down_sample else None for blk in m.downs]
+            self.down_convs = []
+            for blk in m.downs:
+                if blk.down_sample:
+                    w = pack_conv(blk.down_sample_conv.weight)
+                    self.down_convs.append((w, blk.down_sample_conv.bias.detach().float(),
+                                            self._x6(w, blk.down_sample_conv.in_channels, len(TAPS4S2))))
+                else:
+                    self.down_convs.append(None)
             self.mids = [self._pack_stage(blk, n_res=blk.num_layers + 1, attn=True) for blk in m.mids]
             self.ups = [self._pack_stage(blk, n_res=blk.num_layers, attn=blk.use_attn) for blk in m.ups]
             self.up_convs = []
             for blk in m.ups:
                 if blk.up_sample:
+                    ci = blk.up_sample_conv.in_channels
                     parts = [pack_convT(blk.up_sample_conv.weight, py, px) for py in (0, 1) for px in (0, 1)]
+                    parts = [(taps, w, self._x6(w, ci, len(taps))) for taps, w in parts]
                     self.up_convs.append((parts, blk.up_sample_conv.bias.detach().float()))
                 else:
                     self.up_convs.append(None)
@@ -126,6 +136,7 @@ class UnetEngine:
             self.conv_in_b = m.conv_in.bias.detach().float().contiguous()
             self.norm_out = (m.norm_out.weight.detach().float(), m.norm_out.bias.detach().float())
             self.conv_out_w = pack_conv(m.conv_out.weight)
+            self.conv_out_x6 = self._x6(self.conv_out_w, m.conv_out.in_channels, 9)
             self.conv_out_b = m.conv_out.bias.detach().float().contiguous()
             tp = m.t_proj
             self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
@@ -143,22 +154,31 @@ class UnetEngine:
                     g2=s[0].weight.detach().float(), be2=s[0].bias.detach().float(), w2=w2,
                     b2=(s[2].bias.detach().float() + r.bias.detach().float()).contiguous(), temb_off=self._temb_P)
         if self.precision == 'bf16x6' and ci % 16 == 0 and co % 16 == 0:
-            p.w1x6 = K.pack_x6(p.w1, ci)
-            p.w2x6 = K.pack_x6(p.w2, co, ci)
+            # (halo-order pack for the 3x3 kernel, natural-order pack for the implicit-GEMM fallback)
+            p.w1x6 = (K.pack_x6(p.w1, ci), self._x6(p.w1, ci, 9))
+            p.w2x6 = (K.pack_x6(p.w2, co, ci), self._x6(p.w2, co, 9, ci))
         self.temb_rows_w.append(tl.weight.detach().float())
         self.temb_rows_b.append(tl.bias.detach().float())
         self._temb_P += co
         return p
 
-    @staticmethod
-    def _pack_attn(blk, i: int) -> AttnPack:
+    def _x6(self, w: torch.Tensor, c0: int, ntaps: int, c1: int = 0) -> Optional[K.X6Weight]:
+        """bf16x6 (natural K order) re-pack for wc_conv_igemm_x6, or None in fp32 mode."""
+        if self.precision != 'bf16x6' or c0 % 16 or c1 % 16:
+            return None
+        return K.pack_x6(w, c0, c1, ntaps=ntaps, order='natural')
+
+    def _pack_attn(self, blk, i: int) -> AttnPack:
         mha, gn = blk.attentions[i], blk.attention_norms[i]
         c = mha.embed_dim
-        return AttnPack(c=c, heads=mha.num_heads, g=gn.weight.detach().float(), be=gn.bias.detach().float(),
-                        w_in=mha.in_proj_weight.detach().float().contiguous(),
-                        b_in=mha.in_proj_bias.detach().float().contiguous(),
-                        w_out=mha.out_proj.weight.detach().float().contiguous(),
-                        b_out=mha.out_proj.bias.detach().float().contiguous())
+        p = AttnPack(c=c, heads=mha.num_heads, g=gn.weight.detach().float(), be=gn.bias.detach().float(),
+                     w_in=mha.in_proj_weight.detach().float().contiguous(),
+                     b_in=mha.in_proj_bias.detach().float().contiguous(),
+                     w_out=mha.out_proj.weight.detach().float().contiguous(),
+                     b_out=mha.out_proj.bias.detach().float().contiguous())
+        p.w_in_x6 = self._x6(p.w_in, c, 1)
+        p.w_out_x6 = self._x6(p.w_out, c, 1)
+        return p
 
     def _pack_stage(self, blk, n_res: int, attn: bool):
         res = [self._pack_res(blk, i) for i in range(n_res)]
@@ -171,12 +191,21 @@ class UnetEngine:
         return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
 
     @staticmethod
-    def conv3(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: View, H: int, W: int, **kw):
-        """A 3x3 stride-1 conv: bf16x6 MFMA kernel when packed for it and the shape tiles, else fp32 MFMA."""
-        if w6 is not None and K.x6_eligible(segs, w6.N, H, W):
-            K.conv3x3_x6(segs, w6, bias, out, Hm=H, Wm=W, **kw)
+    def conv(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: Optional[View], H: int, W: int, **kw):
+        """Any conv: bf16x6 implicit GEMM when packed for it, else fp32 MFMA."""
+        if w6 is not None:
+            K.conv_igemm_x6(segs, w6, bias, out, Hm=H, Wm=W, **kw)
         else:
             K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
+
+    @staticmethod
+    def conv3(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: View, H: int, W: int, **kw):
+        """A ResBlock 3x3 stride-1 conv: the halo-tiled bf16x6 kernel when the grid tiles, else the
+        bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode)."""
+        if w6 is not None and K.x6_eligible(segs, w6[0].N, H, W):
+            K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, **kw)
+        else:
+            UnetEngine.conv(segs, w, None if w6 is None else w6[1], bias, out, H, W, **kw)
 
     def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int):
         B, H, W = X.B, X.H, X.W
@@ -193,10 +222,10 @@ class UnetEngine:
         N = H * W
         sc, sh = K.gn_affine(Y, p.g, p.be)
         qkv = self._new(B, H, W, 3 * C)
-        K.conv_igemm([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.b_in, View.full(qkv), Hm=H, Wm=W)
+        self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         o = self._new(B, H, W, C)
         K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads)
-        K.conv_igemm([Seg(View.full(o), TAPS1)], p.w_out, p.b_out, Y, Hm=H, Wm=W, res=Y)
+        self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
@@ -241,8 +270,8 @@ class UnetEngine:
                     self.attention(tgt, att[li])
                 cur = tgt
             if self.down_convs[i] is not None:
-                w, b = self.down_convs[i]
-                K.conv_igemm([Seg(cur, TAPS4S2, stride=2)], w, b, final, Hm=sizes[i + 1][0], Wm=sizes[i + 1][1])
+                w, b, w6 = self.down_convs[i]
+                self.conv([Seg(cur, TAPS4S2, stride=2)], w, w6, b, final, sizes[i + 1][0], sizes[i + 1][1])
                 cur = final
 
         # ---------------- mid path
@@ -266,8 +295,8 @@ class UnetEngine:
             if self.up_convs[k] is not None:
                 parts, b = self.up_convs[k]
                 dst = View(U[i], 0, dc[i])
-                for (py, px), (taps, w) in zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts):
-                    K.conv_igemm([Seg(cur, taps)], w, b, dst, Hm=cur.H, Wm=cur.W, out_map=(2, 2, py, px))
+                for (py, px), (taps, w, w6) in zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts):
+                    self.conv([Seg(cur, taps)], w, w6, b, dst, cur.H, cur.W, out_map=(2, 2, py, px))
             else:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
             cur = View.full(U[i])
@@ -284,6 +313,6 @@ class UnetEngine:
         # ---------------- head: GN -> SiLU -> conv_out, NCHW output
         sc, sh = K.gn_affine(cur, *self.norm_out)
         out = torch.empty((B, m.model_config.im_channels, S, S2), dtype=torch.float32, device=self.device)
-        K.conv_igemm([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.conv_out_w, self.conv_out_b, None,
-                     Hm=S, Wm=S2, out_nchw=out)
+        self.conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.conv_out_w, self.conv_out_x6, self.conv_out_b,
+                  None, S, S2, out_nchw=out)
         return out

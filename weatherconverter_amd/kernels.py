@@ -174,7 +174,7 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
-    _timed(f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}>', 'wc_conv_igemm',
+    _timed(f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}, {act}>', 'wc_conv_igemm',
            _flops(segs, Hm, Wm, N) if PROFILE is not None else 0.0, ctypes.byref(a), _stream())
 
 
@@ -193,13 +193,16 @@ def default_conv_precision() -> str:
 
 @dataclass
 class X6Weight:
-    """A conv weight re-packed for wc_conv3x3_x6: its three exact bf16 pieces, laid out as
-    [N tile][step][piece][k-half][BN][8] (bit patterns in an int16 tensor)."""
+    """A conv weight re-packed for the bf16x6 kernels: its three exact bf16 pieces, laid out as
+    [N tile][step][piece][k-half][BN][8] (bit patterns in an int16 tensor).  order 'halo':
+    steps are (16-channel chunk, tap) for wc_conv3x3_x6; 'natural': K/16 in K order for
+    wc_conv_igemm_x6."""
     data: torch.Tensor
     N: int
     BN: int
     C0: int
     C1: int
+    order: str = 'halo'
 
 
 @functools.lru_cache(maxsize=None)
@@ -222,22 +225,28 @@ def split3_bits(x: torch.Tensor) -> torch.Tensor:
     return (torch.stack([u0, u1, u2]) >> 16).to(torch.int16)
 
 
-def pack_x6(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
-    """Re-pack a [N][9*C0 + C1] conv weight (K = (tap, c) then the 1x1 residual columns, as
-    engine.pack_conv) for wc_conv3x3_x6: steps are (16-channel chunk, tap) then the residual chunks."""
+def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo') -> X6Weight:
+    """Re-pack a [N][ntaps*C0 + C1] conv weight (K = (tap, c) then the 1x1 residual columns, as
+    engine.pack_conv) for the bf16x6 kernels.  order 'halo' (wc_conv3x3_x6, ntaps 9): steps are
+    (16-channel chunk, tap) then the residual chunks; 'natural' (wc_conv_igemm_x6): K/16 in order."""
     N, K = w.shape
-    _req(K == 9 * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
+    _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
+    _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
     _, BN = x6_tile(N)
     Np = -(-N // BN) * BN
     wp = torch.zeros((Np, K), dtype=torch.float32, device=w.device)
-    wp[:N] = w
-    s0 = wp[:, :9 * C0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, 9 * (C0 // 16), 2, 8)
-    s1 = wp[:, 9 * C0:].reshape(Np, C1 // 16, 2, 8)
-    allw = torch.cat([s0, s1], 1)
+    wp[:N] = w.float()
+    if order == 'halo':
+        s0 = wp[:, :9 * C0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, 9 * (C0 // 16), 2, 8)
+        s1 = wp[:, 9 * C0:].reshape(Np, C1 // 16, 2, 8)
+        allw = torch.cat([s0, s1], 1)
+    else:
+        _req(order == 'natural', f'unknown x6 order {order!r}')
+        allw = wp.reshape(Np, K // 16, 2, 8)
     S = allw.shape[1]
     pieces = split3_bits(allw)  # (3, Np, S, 2, 8)
     data = pieces.view(3, Np // BN, BN, S, 2, 8).permute(1, 3, 0, 4, 2, 5).contiguous()
-    return X6Weight(data, N, BN, C0, C1)
+    return X6Weight(data, N, BN, C0, C1, order)
 
 
 def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
@@ -258,7 +267,7 @@ def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
 def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None, act: int = 0):
     """3x3 stride-1 conv (+ fused 1x1 residual segment) on bf16x6 split-precision MFMA."""
-    _req(w6.data.is_cuda and w6.data.is_contiguous(), 'x6 weight')
+    _req(w6.data.is_cuda and w6.data.is_contiguous() and w6.order == 'halo', 'x6 weight (halo order)')
     _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
     a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act)
     TH, BN = x6_tile(w6.N)
@@ -266,6 +275,22 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     res_seg = 'true' if len(segs) == 2 else 'false'
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}>', 'wc_conv3x3_x6',
+           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
+           w6.data.numel() * 2, _stream())
+
+
+def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *, Hm: int,
+                  Wm: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
+                  out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0):
+    """conv_igemm's contract (any taps, strides, output map) on bf16x6 split-precision MFMA."""
+    _req(w6.data.is_cuda and w6.data.is_contiguous() and w6.order == 'natural', 'x6 weight (natural order)')
+    _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
+    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act)
+    bm, bn = (256, 64) if w6.N <= 64 else (128, 128)
+    s0 = segs[0]
+    pro = 0 if s0.scale is None else (2 if s0.silu else 1)
+    unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
+    _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, {act}>', 'wc_conv_igemm_x6',
            _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 

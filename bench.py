@@ -68,16 +68,19 @@ def roofline_leg(model, x, t_dev):
         d[0] += 1
         d[1] += flops
         d[2] += e0.elapsed_time(e1) * 1e-3
-    # dominant kernel = the conv_igemm instantiation with the most event time in one UNet forward
+    # dominant kernel = the conv / attention instantiation with the most event time in one UNet forward
     name = max(per, key=lambda k: per[k][2])
     n, fl, sec = per[name]
     mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
     total_conv = sum(v[2] for v in per.values())
-    if name.startswith('conv3x3_x6'):
-        desc, peak = ' (bf16x6 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue)', BF16X6_PEAK_TFLOPS
-    else:
-        desc, peak = ' (fp32 MFMA implicit-GEMM conv, GN+SiLU prologue)', FP32_PEAK_TFLOPS
+    desc = {'conv3x3_x6': ' (bf16x6 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue)',
+            'conv_igemm_x6': ' (bf16x6 split-precision MFMA implicit-GEMM conv)',
+            'attention_x6': ' (bf16x6 split-precision MFMA flash attention)',
+            'conv_igemm_kernel': ' (fp32 MFMA implicit-GEMM conv)',
+            'attention_kernel': ' (fp32 MFMA flash attention)'}[name.split('<')[0].replace('_kernel', '')
+                                                                   if '_x6' in name else name.split('<')[0]]
+    peak = BF16X6_PEAK_TFLOPS if '_x6' in name else FP32_PEAK_TFLOPS
     return {
         'kernel': name + desc,
         'bound': 'mfma',
@@ -89,8 +92,8 @@ def roofline_leg(model, x, t_dev):
         'launches_per_step': n,
         'mean_launch_ms': round(mean_dur * 1e3, 4),
         'gflop_per_launch': round(fl / n / 1e9, 3),
-        'share_of_conv_event_time': round(sec / max(total_conv, 1e-12), 3),
-        'conv_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1)}
+        'share_of_mfma_event_time': round(sec / max(total_conv, 1e-12), 3),
+        'mfma_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1)}
                          for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])},
     }
 

@@ -136,6 +136,10 @@ int wc_gn_finalize(const float* partials, int B, int HW, int C, int groups, cons
 /* qkv: [B*N][ld_qkv] rows holding q | k | v (C each, head h at columns h*d); out: [B*N][ld_out]. */
 int wc_attention_fwd(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
                      int heads, float scale, void* stream);
+/* Same contract on bf16x6 split-precision MFMA (exact 3-piece bf16 split of Q, K, V and of the
+ * softmax probabilities, six products per block, fp32 accumulation); head dim C/heads % 32 == 0. */
+int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
+                        int heads, float scale, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Time embedding: sinusoid + t_proj MLP + every ResBlock's SiLU→Linear projection in one launch */

@@ -1,4 +1,5 @@
-"""bf16x6 split-precision 3x3 conv (csrc/wc_conv6.hip).
+"""bf16x6 split-precision kernels: the 3x3 halo conv (csrc/wc_conv6.hip), the implicit-GEMM conv
+(csrc/wc_igemm6.hip) and flash attention (csrc/wc_attention6.hip).
 
 CPU: the 3-piece bf16 split is exact, and the weight re-pack has the layout the kernel reads.
 GPU: the conv against a float64 PyTorch reference of the same op.  Stated tolerance: relative L2
@@ -299,3 +300,45 @@ def test_igemm_x6_3x3_with_residual_segment_odd_grid():
         o = torch.empty((B, H, W, Co), device='cuda')
         return K.View.full(o), None, lambda: _nchw(o.cpu())
     _check(_run_both(K, segs, wp, Ci, Cr, 9, b.cuda(), out_fn, Hm=H, Wm=W, temb=temb.cuda(), temb_ld=Co), ref)
+
+
+# ---------------------------------------------------------------- attention (wc_attention_fwd_x6)
+
+
+def _attn_ref(qkv, B, N, C, heads):
+    d = C // heads
+    q, k, v = qkv.double().split(C, -1)
+    q = q.reshape(B, N, heads, d).transpose(1, 2)
+    k = k.reshape(B, N, heads, d).transpose(1, 2)
+    v = v.reshape(B, N, heads, d).transpose(1, 2)
+    return (torch.softmax((q * d**-0.5) @ k.transpose(-1, -2), -1) @ v).transpose(1, 2).reshape(B, N, C)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,N,C,heads', [(2, 100, 128, 4), (1, 1024, 256, 4), (2, 300, 512, 4), (1, 257, 768, 4),
+                                         (1, 64, 384, 4), (1, 96, 640, 4)])
+def test_attention_x6_vs_float64(B, N, C, heads):
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(21)
+    qkv = torch.randn((B, N, 3 * C), generator=g) * 1.5
+    ref = _attn_ref(qkv, B, N, C, heads)
+    errs = {}
+    for prec in ('bf16x6', 'fp32'):
+        out = torch.full((B * N, C), 9.0, device='cuda')
+        K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads, prec)
+        errs[prec] = rel_l2(out.cpu().double().reshape(B, N, C), ref)
+    assert errs['bf16x6'] < 1e-5 and errs['bf16x6'] <= 4 * errs['fp32'] + 1e-7, errs
+
+
+@pytest.mark.gpu
+def test_attention_x6_spiky_scores():
+    """A dominant key forces the running max to jump mid-sequence (online-softmax rescale path)."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(22)
+    B, N, C, heads = 1, 512, 256, 4
+    qkv = torch.randn((B, N, 3 * C), generator=g)
+    qkv[0, 400, C:2 * C] *= 25.0
+    ref = _attn_ref(qkv, B, N, C, heads)
+    out = torch.empty((B * N, C), device='cuda')
+    K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads, 'bf16x6')
+    assert rel_l2(out.cpu().double().reshape(B, N, C), ref) < 1e-5

@@ -1,0 +1,312 @@
+// Flash attention on bf16x6 split-precision MFMA for gfx950 (head dims D % 32 == 0).  Same
+// contract as wc_attention_fwd (wc_attention.hip): softmax(Q K^T * scale) V per (batch, head),
+// replacing the core of nn.MultiheadAttention(C, 4, batch_first=True) (unet_base.py:115,159).
+//
+// Arithmetic: every fp32 operand is split exactly into three bf16 pieces (wc_x6.hpp split3) and
+// the six products with piece-order sum <= 2 are accumulated in fp32 by
+// v_mfma_f32_32x32x16_bf16 (wc_conv6.hip header) — fp32-class error at 2.67x the fp32 MFMA rate.
+//
+// Structure (as wc_attention.hip, with 16-wide K-steps):
+//   * workgroup = 4 waves x 32 queries of one (batch, head); Q is split once into registers.
+//   * K/V tiles of 32 keys, double-buffered in LDS: the next tile's global loads are issued before
+//     the MFMAs of the current tile and split into the other buffer after them; one barrier/tile.
+//   * S^T = K Q^T: 6 MFMAs per 16 head dims.  The accumulator holds keys x queries, so each lane
+//     owns one query and the online softmax is in-lane (+ one lane^32 exchange).
+//   * O^T += V^T P^T: the S^T registers of a 16-key chunk ARE the lane's B operand (P^T), split in
+//     registers; V is staged transposed ([piece][dim][32 keys]) in the matching key permutation
+//     (pos(key) below), its 16-byte slots XOR-swizzled by (dim >> 2) & 3 so each ds_read_b128 lane
+//     group reads 16 distinct slots.
+#include "wc_x6.hpp"
+
+namespace {
+
+using namespace wcx6;
+
+constexpr int NT = 256;
+constexpr int KT = 32;  // keys per tile
+
+template <int D>
+struct Ax6 {
+    static_assert(D % 32 == 0, "bf16x6 attention needs D % 32 == 0");
+    static constexpr int NCH = D / 16;                  // QK^T K-steps
+    static constexpr int NDB = D / 32;                  // O^T 32-dim blocks
+    static constexpr int KPLANE = KT * 16;              // bytes of one (piece, chunk, k-half) K plane
+    static constexpr int KBYTES = 3 * NCH * 2 * KPLANE; // K pieces of one tile
+    static constexpr int VBYTES = 3 * D * KT * 2;       // V^T pieces of one tile
+    static constexpr int STAGE = KBYTES + VBYTES;
+    static constexpr int LDS = 2 * STAGE;
+    static constexpr int KPT = KT * D / 4 / NT;         // K float4 items per thread
+    static constexpr int VITEMS = (KT / 2) * (D / 4);   // V (key pair, dim quad) items
+    static constexpr int VPT = (VITEMS + NT - 1) / NT;
+};
+
+// position of key kk (0..31) in the permuted K16 order of the PV MFMA (see header)
+WC_DEVICE int key_pos(int k) {
+    const int c = k >> 4, kk = k & 15;
+    return 16 * c + 8 * ((kk >> 2) & 1) + (kk & 3) + 4 * (kk >> 3);
+}
+
+// The three piece bit patterns (hi16 = the bf16 piece) of 4 floats, per element.
+WC_DEVICE void split3_elems(f32x4 v, unsigned (&u)[3][4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e];
+        const unsigned a = __float_as_uint(x);
+        const float r1 = x - __uint_as_float(a & 0xffff0000u);
+        const unsigned c = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(c & 0xffff0000u);
+        u[0][e] = a;
+        u[1][e] = c;
+        u[2][e] = __float_as_uint(r2);
+    }
+}
+
+WC_DEVICE void mfma6(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {
+    acc = mfma_bf16(a[0], b[0], acc);
+    acc = mfma_bf16(a[0], b[1], acc);
+    acc = mfma_bf16(a[1], b[0], acc);
+    acc = mfma_bf16(a[0], b[2], acc);
+    acc = mfma_bf16(a[1], b[1], acc);
+    acc = mfma_bf16(a[2], b[0], acc);
+}
+
+template <int D>
+__global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
+                                                             float* __restrict__ out, int ldo, int N,
+                                                             int C, float scale_log2) {
+    using A = Ax6<D>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int l32 = lane & 31;
+    const int half = lane >> 5;
+    const int head = blockIdx.y;
+    const int b = blockIdx.z;
+    const int q0 = blockIdx.x * 128 + wave * 32;
+    const float* base = qkv + (long)b * N * ldq;
+    const int qcol = head * D;
+    const int kcol = C + head * D;
+    const int vcol = 2 * C + head * D;
+    const __amdgpu_buffer_rsrc_t srd = make_srd(base);
+
+    // ---- Q pieces: lane (query l32, half) holds Q[q][16 ch + 8 half + j] ----
+    const int qrow = q0 + l32;
+    u32x4 qp[A::NCH][3];
+#pragma unroll
+    for (int ch = 0; ch < A::NCH; ++ch) {
+        const unsigned o = (unsigned)(qrow * ldq + qcol + 16 * ch + 8 * half) * 4u;
+        const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB);
+        const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB);
+        u32x2 a0, a1, a2, b0, b1, b2;
+        split3(v0, a0, a1, a2);
+        split3(v1, b0, b1, b2);
+        qp[ch][0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+        qp[ch][1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+        qp[ch][2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+    }
+
+    // ---- staging coordinates ----
+    // K: item i -> key i / (D/4), dims 4*(i % (D/4)) .. +3
+    int k_goff[A::KPT], k_key[A::KPT], k_lds[A::KPT];
+#pragma unroll
+    for (int j = 0; j < A::KPT; ++j) {
+        const int i = tid + NT * j;
+        const int key = i / (D / 4), d4 = i % (D / 4);
+        k_key[j] = key;
+        k_goff[j] = key * ldq + kcol + 4 * d4;
+        k_lds[j] = (((d4 >> 2) * 2 + ((d4 >> 1) & 1)) * KT + key) * 16 + (d4 & 1) * 8;
+    }
+    // V: item i -> keys 2kp, 2kp+1 and dims 4*d4 .. +3
+    int v_goff[A::VPT], v_key[A::VPT], v_pos[A::VPT], v_d[A::VPT];
+#pragma unroll
+    for (int j = 0; j < A::VPT; ++j) {
+        const int i = tid + NT * j;
+        const int kp = i / (D / 4), d4 = i % (D / 4);
+        v_key[j] = i < A::VITEMS ? 2 * kp : 1 << 20;  // invalid items never load nor store
+        v_goff[j] = 2 * kp * ldq + vcol + 4 * d4;
+        v_pos[j] = key_pos(2 * kp);
+        v_d[j] = 4 * d4;
+    }
+
+    f32x4 rk[A::KPT], rv[A::VPT][2];
+    auto load_tile = [&](int t) {
+        const int kv0 = t * KT;
+#pragma unroll
+        for (int j = 0; j < A::KPT; ++j)
+            rk[j] = bload_f4(srd, kv0 + k_key[j] < N ? (unsigned)(kv0 * ldq + k_goff[j]) * 4u : OOB);
+#pragma unroll
+        for (int j = 0; j < A::VPT; ++j) {
+            const unsigned o = (unsigned)(kv0 * ldq + v_goff[j]) * 4u;
+            rv[j][0] = bload_f4(srd, kv0 + v_key[j] < N ? o : OOB);
+            rv[j][1] = bload_f4(srd, kv0 + v_key[j] + 1 < N ? o + (unsigned)ldq * 4u : OOB);
+        }
+    };
+    auto write_tile = [&](unsigned char* buf) {
+#pragma unroll
+        for (int j = 0; j < A::KPT; ++j) {
+            u32x2 p0, p1, p2;
+            split3(rk[j], p0, p1, p2);
+            *reinterpret_cast<u32x2*>(buf + k_lds[j]) = p0;
+            *reinterpret_cast<u32x2*>(buf + A::NCH * 2 * A::KPLANE + k_lds[j]) = p1;
+            *reinterpret_cast<u32x2*>(buf + 2 * A::NCH * 2 * A::KPLANE + k_lds[j]) = p2;
+        }
+        unsigned char* vb = buf + A::KBYTES;
+#pragma unroll
+        for (int j = 0; j < A::VPT; ++j) {
+            if (v_key[j] >= KT) continue;
+            unsigned ua[3][4], ub[3][4];
+            split3_elems(rv[j][0], ua);
+            split3_elems(rv[j][1], ub);
+            const int pos = v_pos[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int d = v_d[j] + e;
+                const int off = d * (KT * 2) + (((pos >> 3) ^ ((d >> 2) & 3)) << 4) + (pos & 7) * 2;
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+                    *reinterpret_cast<unsigned*>(vb + pc * D * KT * 2 + off) = hi_pair(ub[pc][e], ua[pc][e]);
+            }
+        }
+    };
+
+    f32x16 o[A::NDB];
+#pragma unroll
+    for (int d = 0; d < A::NDB; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    const int ntiles = (N + KT - 1) / KT;
+    load_tile(0);
+    write_tile(smem);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const unsigned char* cur = smem + (t & 1) * A::STAGE;
+        const int kv0 = t * KT;
+        if (t + 1 < ntiles) load_tile(t + 1);
+
+        // ---- S^T = K Q^T ----
+        f32x16 s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+        for (int ch = 0; ch < A::NCH; ++ch) {
+            u32x4 kf[3];
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                kf[pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE + l32 * 16);
+            mfma6(s, kf, qp[ch]);
+        }
+
+        // ---- online softmax over keys, per query (lane) ----
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float v = (key < N) ? s[r] * scale_log2 : -INFINITY;
+            s[r] = v;
+            mloc = fmaxf(mloc, v);
+        }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = exp2f(m_run - m_new);
+        float lsum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float pv = exp2f(s[r] - m_new);
+            s[r] = pv;
+            lsum += pv;
+        }
+        lsum += __shfl_xor(lsum, 32, 64);
+        l_run = l_run * alpha + lsum;
+        m_run = m_new;
+#pragma unroll
+        for (int d = 0; d < A::NDB; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+
+        // ---- O^T += V^T P^T: two 16-key chunks ----
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            u32x4 pp[3];
+            {
+                u32x2 a0, a1, a2, b0, b1, b2;
+                split3(f32x4{s[8 * c + 0], s[8 * c + 1], s[8 * c + 2], s[8 * c + 3]}, a0, a1, a2);
+                split3(f32x4{s[8 * c + 4], s[8 * c + 5], s[8 * c + 6], s[8 * c + 7]}, b0, b1, b2);
+                pp[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+                pp[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+                pp[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+            }
+#pragma unroll
+            for (int db = 0; db < A::NDB; ++db) {
+                const int d = db * 32 + l32;
+                const int off = A::KBYTES + d * (KT * 2) + (((2 * c + half) ^ ((d >> 2) & 3)) << 4);
+                u32x4 vf[3];
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+                    vf[pc] = *reinterpret_cast<const u32x4*>(cur + off + pc * D * KT * 2);
+                mfma6(o[db], vf, pp);
+            }
+        }
+
+        if (t + 1 < ntiles) write_tile(smem + ((t + 1) & 1) * A::STAGE);
+        __syncthreads();
+    }
+
+    // ---- epilogue: O[q][dv] = O^T[dv][q] / l ----
+    if (qrow < N) {
+        const float inv = 1.0f / l_run;
+        float* orow = out + ((long)b * N + qrow) * ldo + head * D;
+#pragma unroll
+        for (int d = 0; d < A::NDB; ++d) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 4) {
+                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                *reinterpret_cast<f32x4*>(orow + dv) =
+                    f32x4{o[d][r] * inv, o[d][r + 1] * inv, o[d][r + 2] * inv, o[d][r + 3] * inv};
+            }
+        }
+    }
+}
+
+template <int D>
+int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
+                float scale, hipStream_t stream) {
+    using A = Ax6<D>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, A::LDS);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    dim3 grid((N + 127) / 128, heads, B);
+    hipLaunchKernelGGL(attention_x6_kernel<D>, grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N,
+                       C, scale * 1.4426950408889634f);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+}  // namespace
+
+extern "C" int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N,
+                                   int C, int heads, float scale, void* stream) {
+    if (!qkv || !out) return WC_E_ARG;
+    if (heads <= 0 || C % heads != 0 || ld_qkv % 4 != 0 || ld_out % 4 != 0) return WC_E_SHAPE;
+    if (ld_qkv < 3 * C || ld_out < C || N <= 0 || B <= 0) return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(qkv) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return WC_E_SHAPE;
+    if ((long)N * ld_qkv * 4 >= (1L << 31)) return WC_E_SHAPE;  // per-image SRD range
+    const int D = C / heads;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    switch (D) {
+        case 32: return launch_att6<32>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 64: return launch_att6<64>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 96: return launch_att6<96>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 128: return launch_att6<128>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 160: return launch_att6<160>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 192: return launch_att6<192>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        default: return WC_E_SHAPE;
+    }
+}

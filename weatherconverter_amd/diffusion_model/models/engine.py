@@ -224,7 +224,7 @@ class UnetEngine:
         qkv = self._new(B, H, W, 3 * C)
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         o = self._new(B, H, W, C)
-        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads)
+        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
         self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y)
 
     # ------------------------------------------------------------------ forward

@@ -312,12 +312,17 @@ def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tenso
     return scale, shift
 
 
-def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int):
+def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int, precision: str = 'fp32'):
+    """softmax(Q K^T / sqrt(d)) V per (batch, head) over qkv rows [q | k | v]; 'bf16x6' runs the
+    split-precision kernel when the head dim is a multiple of 32 (else the fp32-MFMA kernel)."""
     _req(qkv.shape == (B * N, 3 * C) and qkv.is_contiguous(), 'qkv shape')
     _req(out.shape == (B * N, C) and out.is_contiguous(), 'attention output shape')
+    _req(precision in CONV_PRECISIONS, f'attention precision {precision!r}')
     d = C // heads
-    _native.call('wc_attention_fwd', qkv.data_ptr(), 3 * C, out.data_ptr(), C, B, N, C, heads, float(d)**-0.5,
-                 _stream())
+    x6 = precision == 'bf16x6' and d % 32 == 0
+    _timed(f'attention_x6_kernel<{d}>' if x6 else f'attention_kernel<{d}>',
+           'wc_attention_fwd_x6' if x6 else 'wc_attention_fwd', 4.0 * B * N * N * C,
+           qkv.data_ptr(), 3 * C, out.data_ptr(), C, B, N, C, heads, float(d)**-0.5, _stream())
 
 
 def temb(t: torch.Tensor, w1, b1, w2, b2, proj_w, proj_b) -> torch.Tensor:

@@ -17,7 +17,8 @@ Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
                 is the conv instantiation with the most time (the GN+SiLU-prologue 3x3 convs) —
                 achieved = its algorithmic (fp32-equivalent) FLOPs per launch / its mean launch
                 duration, against its own ceiling: 157.3 TF for the fp32-MFMA conv, 2516.6/6 =
-                419.4 TF for the bf16x6 conv (6 bf16 MFMAs per fp32 product; MI355X_MICROARCH.md).
+                419.4 TF for bf16x6 kernels (6 bf16 MFMAs per fp32 product), 2516.6/3 = 838.9 TF
+                for the f16x3 conv (3 f16 MFMAs per product; MI355X_MICROARCH.md).
   cpu_baseline  the oracle's PyTorch-CPU restatement of the reference UNet step (N=1 only), on a
                 bounded sample (a few 256-px UNet steps), extrapolated x T.
 """
@@ -33,6 +34,8 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.m
 # bf16x6 conv: every fp32-equivalent 32x32x16 block costs 6 bf16 MFMAs, so its ceiling is the dense
 # bf16 MFMA peak (256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz = 2516.6 TF/s) / 6.
 BF16X6_PEAK_TFLOPS = round(2516.6 / 6, 1)
+# f16x3 conv: 3 f16 MFMAs (same rate as bf16) per fp32-equivalent block.
+F16X3_PEAK_TFLOPS = round(2516.6 / 3, 1)
 HBM_PEAK_GBS = 8000.0
 GFLOP_PER_IMAGE_STEP_256 = 590.61  # SURVEY.md §8(d) algorithmic FLOPs (probe hook count)
 
@@ -74,6 +77,7 @@ def roofline_leg(model, x, t_dev):
     mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
     total_conv = sum(v[2] for v in per.values())
+    f16x3 = name.startswith('conv3x3_x6') and name.endswith(', true>')
     desc = {'conv3x3_x6': ' (bf16x6 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue)',
             'conv_igemm_x6': ' (bf16x6 split-precision MFMA implicit-GEMM conv)',
             'attention_x6': ' (bf16x6 split-precision MFMA flash attention)',
@@ -81,6 +85,9 @@ def roofline_leg(model, x, t_dev):
             'attention_kernel': ' (fp32 MFMA flash attention)'}[name.split('<')[0].replace('_kernel', '')
                                                                    if '_x6' in name else name.split('<')[0]]
     peak = BF16X6_PEAK_TFLOPS if '_x6' in name else FP32_PEAK_TFLOPS
+    if f16x3:
+        desc, peak = (' (f16x3 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue; 1x1 residual '
+                      'segment in bf16x6)'), F16X3_PEAK_TFLOPS
     return {
         'kernel': name + desc,
         'bound': 'mfma',

@@ -45,7 +45,7 @@ def test_unet_tiny_shared_and_per_sample_t():
     assert rel_l2(y2.cpu(), g['y_batch_t']) < 1e-5
 
 
-@pytest.mark.parametrize('precision', ['bf16x6', 'fp32'])
+@pytest.mark.parametrize('precision', ['f16x3', 'bf16x6', 'fp32'])
 def test_unet_64_config1_model(precision):
     mc, net = _model('default_64', precision=precision)
     g = np.load(os.path.join(GOLDEN, 'unet_64.npz'))
@@ -54,7 +54,7 @@ def test_unet_64_config1_model(precision):
     assert rel_l2(y.cpu(), g['y']) < 1e-5
 
 
-@pytest.mark.parametrize('precision', ['bf16x6', 'fp32'])
+@pytest.mark.parametrize('precision', ['f16x3', 'bf16x6', 'fp32'])
 def test_unet_256_baseline_architecture(precision):
     mc, net = _model('default_256', precision=precision)
     g = np.load(os.path.join(GOLDEN, 'unet_256.npz'))

@@ -342,3 +342,102 @@ def test_attention_x6_spiky_scores():
     out = torch.empty((B * N, C), device='cuda')
     K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads, 'bf16x6')
     assert rel_l2(out.cpu().double().reshape(B, N, C), ref) < 1e-5
+
+
+# ---------------------------------------------------------------- f16x3 (wc_conv3x3_f16x3)
+
+
+@pytest.mark.parametrize('N,C0,C1', [(128, 64, 32), (64, 32, 0), (96, 48, 16)])
+def test_pack_f16x3_layout_and_scale(N, C0, C1):
+    """Unpack the f16x3 weight: fp16 pieces (h + l) * 2^-sW reproduce the 3x3 part to 2^-22 relative,
+    the bf16 residual pieces exactly; every scaled 3x3 weight is <= 2^14."""
+    from weatherconverter_amd.kernels import pack_f16x3
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn((N, 9 * C0 + C1), generator=g) * 0.05
+    w3 = pack_f16x3(w, C0, C1)
+    BN, T = w3.BN, w3.data.shape[0]
+    S0, S1 = 9 * (C0 // 16), C1 // 16
+    raw = w3.data.view(T, -1)
+    main = raw[:, :S0 * 2 * 2 * BN * 8].reshape(T, S0, 2, 2, BN, 8)
+    hl = main.view(torch.float16).double()
+    assert hl[:, :, 0].abs().max() <= 2.0**14
+    v = hl.sum(2).permute(0, 3, 1, 2, 4).reshape(T * BN, S0, 16)[:N]
+    inv = w3.wsinv[:N].double()[:, None]
+    s0 = v.reshape(N, C0 // 16, 9, 16).permute(0, 2, 1, 3).reshape(N, 9 * C0) * inv
+    ref = w[:, :9 * C0].double()
+    assert ((s0 - ref).abs() <= ref.abs() * 2.0**-21 + 2.0**-40).all()
+    if C1:
+        res = raw[:, S0 * 2 * 2 * BN * 8:].reshape(T, S1, 3, 2, BN, 8)
+        r = _bits_to_f32(res).double().sum(2).permute(0, 3, 1, 2, 4).reshape(T * BN, S1 * 16)[:N] * inv
+        assert torch.equal(r, w[:, 9 * C0:].double())
+
+
+def test_f16x3_a_exp_bound():
+    from weatherconverter_amd.kernels import f16x3_a_exp
+    for gmax, bmax, n in [(1.0, 0.0, 524288), (3.7, 1.2, 4096), (1e-3, 0.0, 64), (200.0, 5.0, 1 << 20)]:
+        e = f16x3_a_exp(gmax, bmax, n)
+        bound = (n - 1)**0.5 * gmax + bmax
+        assert bound * 2.0**e <= 2.0**14 < bound * 2.0**(e + 1) or e in (-60, 60)
+
+
+def _gn_affine(x, gamma, beta, G=8, eps=1e-5):
+    """Per-(b, c) scale/shift of GroupNorm(G) on NCHW x (float64)."""
+    B, C = x.shape[:2]
+    xg = x.double().reshape(B, G, -1)
+    rstd = 1.0 / torch.sqrt(xg.var(-1, unbiased=False) + eps)
+    mean = xg.mean(-1)
+    sc = rstd.repeat_interleave(C // G, 1) * gamma.double()
+    sh = beta.double() - mean.repeat_interleave(C // G, 1) * sc
+    return sc, sh
+
+
+F3_CASES = [
+    # B, H, W, Ci, Co, Cr, silu, gamma scale, outlier
+    (2, 16, 32, 64, 128, 32, True, 1.0, False),
+    (1, 32, 32, 128, 64, 0, True, 1.0, False),
+    (2, 8, 16, 96, 256, 64, False, 1.0, False),
+    (1, 16, 16, 64, 128, 64, True, 20.0, True),  # Samuelson-extreme outlier + large gamma
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr,silu,gs,outlier', F3_CASES)
+def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier):
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(31)
+    h = torch.randn((B, Ci, H, W), generator=g) * 3 + 0.7
+    if outlier:  # one huge value per group: its normalized value approaches sqrt(n - 1)
+        h.zero_()
+        h[:, ::Ci // 8, 0, 0] = 1e4
+    gamma = gs * (1 + 0.3 * torch.randn(Ci, generator=g))
+    beta = 0.5 * torch.randn(Ci, generator=g)
+    sc, sh = _gn_affine(h, gamma, beta)
+    x2 = torch.randn((B, max(Cr, 16), H, W), generator=g) * 5
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    wr = torch.randn((Co, max(Cr, 16), 1, 1), generator=g) / max(Cr, 16)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    a = h.double() * sc[:, :, None, None] + sh[:, :, None, None]
+    if silu:
+        a = F.silu(a)
+    ref = F.conv2d(a, w.double(), b.double(), padding=1)
+    if Cr:
+        ref = ref + F.conv2d(x2.double(), wr.double())
+    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.float().cuda(), shift=sh.float().cuda(), silu=silu)]
+    wp = _pack(w)
+    if Cr:
+        segs.append(K.Seg(K.View.full(_nhwc(x2).cuda()), [(0, 0)], kbase=9 * Ci))
+        wp = torch.cat([wp, wr.reshape(Co, Cr)], 1)
+    wp = wp.contiguous().cuda()
+    e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * W * Ci // 8)
+    outs = {}
+    for mode in ('f16x3', 'fp32'):
+        out = torch.empty((B, H, W, Co), device='cuda')
+        if mode == 'f16x3':
+            K.conv3x3_f16x3(segs, K.pack_f16x3(wp, Ci, Cr), b.cuda(), K.View.full(out), Hm=H, Wm=W, a_exp=e)
+        else:
+            K.conv_igemm(segs, wp, b.cuda(), K.View.full(out), Hm=H, Wm=W)
+        torch.cuda.synchronize()
+        outs[mode] = _nchw(out.cpu()).double()
+    assert torch.isfinite(outs['f16x3']).all()
+    e3, e32 = rel_l2(outs['f16x3'], ref), rel_l2(outs['fp32'], ref)
+    assert e3 < 1e-5 and e3 <= 4 * e32 + 2e-7, (e3, e32)

@@ -25,11 +25,16 @@ def timeit(fn, iters=10):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
+ZEROS = False
+
+
 def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps=None):
     taps = TAPS3 if taps is None else taps
     nt = len(taps)
     g = torch.Generator(device='cuda').manual_seed(0)
     x = torch.randn((B, H, H, Ci), device='cuda', generator=g)
+    if ZEROS:
+        x.zero_()
     w = torch.randn((Co, nt * Ci + res), device='cuda', generator=g) / (nt * Ci)**0.5
     b = torch.randn(Co, device='cuda', generator=g)
     sc = torch.rand((B, Ci), device='cuda', generator=g) + 0.5
@@ -40,9 +45,12 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps
     if res:
         xr = torch.randn((B, H, H, res), device='cuda', generator=g)
         segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=nt * Ci))
-    if mode == 'x6' and nt != 9:
+    if mode in ('x6', 'f3') and nt != 9 or mode == 'f3' and not prologue:
         return None, None, None
-    if mode == 'igx6':
+    if mode == 'f3':  # a_exp 4 keeps |x*sc + sh| * 16 far inside fp16 for these synthetic inputs
+        w3 = K.pack_f16x3(w, Ci, res)
+        fn = lambda: K.conv3x3_f16x3(segs, w3, b, K.View.full(out), Hm=H, Wm=H, a_exp=4)  # noqa: E731
+    elif mode == 'igx6':
         w6 = K.pack_x6(w, Ci, res, ntaps=nt, order='natural')
         fn = lambda: K.conv_igemm_x6(segs, w6, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731
     elif mode == 'x6':
@@ -83,8 +91,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--check', action='store_true')
     ap.add_argument('--only', type=int, default=-1, help='run a single conv case (for PMC profiling)')
-    ap.add_argument('--modes', default='fp32,x6,igx6', help='conv kernels to time: fp32, x6 (halo 3x3), igx6')
+    ap.add_argument('--modes', default='fp32,x6,f3,igx6',
+                    help='conv kernels to time: fp32, x6 (halo 3x3 bf16x6), f3 (halo 3x3 f16x3), igx6')
+    ap.add_argument('--zeros', action='store_true', help='all-zero activations (clock/power experiment)')
     a = ap.parse_args()
+    global ZEROS
+    ZEROS = a.zeros
     K._native.load()
     cases = [(16, 256, 128, 128, True, 0), (16, 256, 128, 128, True, 64), (16, 256, 64, 64, True, 0),
              (16, 128, 256, 256, True, 0), (16, 64, 512, 512, True, 0), (16, 32, 768, 768, True, 0),

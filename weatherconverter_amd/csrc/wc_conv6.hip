@@ -1,29 +1,40 @@
-// 3x3 stride-1 convolution on bf16x6 split-precision MFMA for gfx950.
+// 3x3 stride-1 convolution on split-precision MFMA for gfx950: bf16x6 and f16x3.
 //
-// Precision.  Every fp32 operand v is split EXACTLY into three bf16 pieces by truncation:
+// bf16x6.  Every fp32 operand v is split EXACTLY into three bf16 pieces by truncation:
 // v0 = v with the low 16 bits cleared, v1 = (v - v0) likewise, v2 = v - v0 - v1 (at most 8
 // significant bits, so it is exact in bf16).  The product a*w is accumulated as the six terms
 // a_i*w_j with i + j <= 2, each an exact bf16 x bf16 product summed in fp32 by
 // v_mfma_f32_32x32x16_bf16.  The dropped terms a1w2 + a2w1 + a2w2 are < 3*2^-24 |a w|, the size
 // of one fp32 rounding, so the result stays inside the fp32 tolerance of the reference conv.  A
-// 32x32x16 block costs 6 bf16 MFMAs (192 cycles) instead of 8 fp32 MFMAs (512 cycles): 2.67x the
-// fp32 MFMA rate (emulated-fp32 peak 2516.6 / 6 = 419.4 TF/s).
+// 32x32x16 block costs 6 bf16 MFMAs (192 cycles) instead of 8 fp32 MFMAs (512 cycles).
+//
+// f16x3 (only for a GroupNorm-applied segment 0, whose magnitude has a static bound).  a' =
+// a * 2^sA and w' = w * 2^sW[n] (exact power-of-two scales) are split into two fp16 pieces by
+// round-to-nearest (h = fp16(v), l = fp16(v - h): v = h + l to ~2^-22 relative, l may be
+// subnormal — the f16 MFMA honours subnormal inputs, tools/probes/mfma_f16_subnormal.hip), and
+// a'w' = h_a h_w + h_a l_w + l_a h_w on v_mfma_f32_32x32x16_f16: 3 MFMAs per block, half the
+// bf16x6 work.  No overflow is possible: a GN output z = (x - mean)/sqrt(var + eps) obeys
+// |z| <= sqrt(n - 1) (Samuelson), so |gamma z + beta| <= sqrt(n-1) max|gamma| + max|beta| =: bound,
+// and the host picks sA with bound * 2^sA <= 2^14 (fp16 max 65504).  The 1x1 residual segment
+// (raw input, no static bound) stays bf16x6 with the same scales, so every product carries the
+// factor 2^(sA + sW[n]), removed exactly in the epilogue.
 //
 // Tiling (implicit GEMM, M = output pixels, N = output channels, K = (16-channel chunk, tap)).
 // A workgroup owns a TH x 16 pixel tile of one image and BN output channels; each of its 4 waves
 // owns 4 image rows x 16 columns (64 pixels) x 64 channels as 2 x 2 32x32 accumulators.
 //   * Per 16-channel chunk the (TH+2) x 18 input HALO is loaded once, GroupNorm-applied (+SiLU),
-//     zero-padded, split into its three bf16 pieces and written to LDS.  All 9 taps then read
-//     their A fragments from that one halo image at a constant per-tap offset, so the prologue
-//     VALU is paid (TH+2)*18/(TH*16) times per input element instead of 9 times.
+//     zero-padded, split into its pieces and written to LDS.  All 9 taps then read their A
+//     fragments from that one halo image at a constant per-tap offset, so the prologue VALU is
+//     paid (TH+2)*18/(TH*16) times per input element instead of 9 times.  The halo loads are
+//     issued at tap 7 and consumed at tap 8 (see the K loop for why not earlier).
 //   * A K-step is one (chunk, tap): the tap's 16 x BN weight pieces (pre-split and pre-laid-out
 //     by the host in the exact LDS order) are staged through registers one step ahead; one
-//     barrier per step.  The next chunk's halo is loaded at the chunk's first tap and written
-//     at its last, into the other halo buffer.
+//     barrier per step.  The next chunk's halo is written at the chunk's last tap, into the
+//     other halo buffer.
 //   * The fused 1x1 residual_input_conv (raw input, same pixel) runs as extra chunks with one
 //     tap (the halo centre).
-// LDS images.  Halo: [piece 3][k-half 2][pixel (TH+2)*18][8 bf16]; weights: [piece][k-half][BN]
-// [8 bf16].  The MFMA row -> pixel map is chosen so that each ds_read_b128 lane group
+// LDS images.  Halo: [piece][k-half 2][pixel (TH+2)*18][8 x 16-bit]; weights: [piece][k-half]
+// [BN][8 x 16-bit].  The MFMA row -> pixel map is chosen so that each ds_read_b128 lane group
 // ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) reads 16 consecutive pixels of one image row:
 // 16 distinct 16-byte slots, bank-conflict-free for every tap offset.
 //
@@ -37,7 +48,7 @@ namespace {
 using namespace wcx6;
 
 constexpr int NT = 256;
-constexpr int HWD = 18;                // halo row width: 16 output columns + 2
+constexpr int HWD = 18;  // halo row width: 16 output columns + 2
 
 struct X6Dev {
     const float* src0;
@@ -56,26 +67,35 @@ struct X6Dev {
     float* out;
     int ldo;
     int act;
-    int nck0, nck1;  // 16-channel chunks of segment 0 (3x3) and segment 1 (1x1 residual)
+    int nck0, nck1;       // 16-channel chunks of segment 0 (3x3) and segment 1 (1x1 residual)
+    float ascale;         // f16x3: 2^sA applied to the A values before splitting (else 1)
+    float ainv;           // 2^-sA
+    const float* wsinv;   // f16x3: 2^-sW[n] per output channel (else NULL)
     int tiles_x, tiles_y, ntiles_n;
 };
 
-template <int TH, int BN>
+// F3: segment 0 in f16x3 (2 pieces), else bf16x6 (3 pieces).  Segment 1 is always bf16x6.
+template <int TH, int BN, bool RES, bool F3>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
     static constexpr int WAVES_M = 4 / WAVES_N;
     static_assert(WAVES_M * 64 == BM, "each wave owns 4 image rows x 16 columns");
-    static constexpr int HPIX = (TH + 2) * HWD;   // halo pixels
-    static constexpr int HPLANE = HPIX * 16;      // bytes of one (piece, k-half) halo plane
-    static constexpr int HSTAGE = 6 * HPLANE;     // one halo buffer
-    static constexpr int BPLANE = BN * 16;        // bytes of one (piece, k-half) weight plane
-    static constexpr int BSTAGE = 6 * BPLANE;     // one weight step
+    static constexpr int NP0 = F3 ? 2 : 3;              // pieces of segment 0
+    static constexpr int NPH = RES ? 3 : NP0;           // halo planes per k-half
+    static constexpr int HPIX = (TH + 2) * HWD;          // halo pixels
+    static constexpr int HPLANE = HPIX * 16;             // bytes of one (piece, k-half) halo plane
+    static constexpr int HSTAGE = 2 * NPH * HPLANE;      // one halo buffer
+    static constexpr int BPLANE = BN * 16;               // bytes of one (piece, k-half) weight plane
+    static constexpr int BSTEP0 = 2 * NP0 * BPLANE;      // one segment-0 weight step
+    static constexpr int BSTEP1 = 6 * BPLANE;            // one segment-1 weight step
+    static constexpr int BSTAGE = RES ? BSTEP1 : BSTEP0;  // LDS weight buffer
     static constexpr int LDS = 2 * HSTAGE + 2 * BSTAGE;
-    static constexpr int H_ITEMS = HPIX * 4;      // float4 items of one halo chunk
+    static constexpr int H_ITEMS = HPIX * 4;             // float4 items of one halo chunk
     static constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
-    static constexpr int B_ITEMS = BSTAGE / 16;   // 16-byte items of one weight step
-    static constexpr int B_PER_T = (B_ITEMS + NT - 1) / NT;
+    static constexpr int B_PER_T = (BSTAGE / 16 + NT - 1) / NT;
+    // weight items j < B_FULL of every thread are valid in every step (both segments)
+    static constexpr int B_FULL = (RES ? (BSTEP0 < BSTEP1 ? BSTEP0 : BSTEP1) : BSTEP0) / 16 / NT;
 };
 
 // MFMA row r (0..31) -> pixel (dy, dx) of a 2 x 16 strip: the ds_read_b128 lane group
@@ -86,9 +106,9 @@ WC_DEVICE int row_dx(int r) {
 }
 
 // PRO: 0 = raw segment 0, 1 = GN affine, 2 = GN affine + SiLU.  RES: segment 1 present.
-template <int TH, int BN, int PRO, bool RES>
+template <int TH, int BN, int PRO, bool RES, bool F3>
 __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
-    using T = X6Tile<TH, BN>;
+    using T = X6Tile<TH, BN, RES, F3>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -112,7 +132,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     const int tyi = tt % p.tiles_y;
     const int b = tt / p.tiles_y;
     const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
-    const int S = 9 * p.nck0 + (RES ? p.nck1 : 0);
+    const int S0 = 9 * p.nck0;
+    const int S = S0 + (RES ? p.nck1 : 0);
+    const unsigned wtile = (unsigned)tile_n * (unsigned)(S0 * T::BSTEP0 + (RES ? p.nck1 : 0) * T::BSTEP1);
 
     // ---- halo staging coordinates: item i = tid + NT*j is halo pixel i>>2, channels 4*(i&3).. ----
     const int q = tid & 3;
@@ -160,14 +182,15 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
         for (int j = 0; j < T::H_PER_T; ++j)
             rh[j] = bload_f4(srd1, ((hin >> j) & 1u) ? (unsigned)(hoff1[j] + c * 16) * 4u : OOB);
     };
-    auto write_halo = [&](int hs, bool pro) {
+    // seg0: prologue + (F3: scale, 2 fp16 pieces | 3 bf16 pieces); seg1: (F3: scale) 3 bf16 pieces
+    auto write_halo = [&](int hs, bool seg0) {
         unsigned char* base = smem + hs * T::HSTAGE;
 #pragma unroll
         for (int j = 0; j < T::H_PER_T; ++j) {
-            if (!((hval >> j) & 1u)) continue;
+            if (j >= T::H_ITEMS / NT && !((hval >> j) & 1u)) continue;  // only the last item can be partial
             f32x4 v = rh[j];
             if constexpr (PRO != 0) {
-                if (pro) {
+                if (seg0) {
                     v = v * rsc + rsh;
                     if constexpr (PRO == 2) {
                         v.x = silu_fast(v.x); v.y = silu_fast(v.y);
@@ -176,27 +199,41 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 }
             }
             if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
-            u32x2 a0, a1, a2;
-            split3(v, a0, a1, a2);
-            *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
-            *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds[j]) = a1;
-            *reinterpret_cast<u32x2*>(base + 4 * T::HPLANE + hlds[j]) = a2;
+            if constexpr (F3) v = v * p.ascale;
+            if (F3 && seg0) {
+                u32x2 a0, a1;
+                split2_f16(v, a0, a1);
+                *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
+                *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds[j]) = a1;
+            } else {
+                u32x2 a0, a1, a2;
+                split3(v, a0, a1, a2);
+                *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
+                *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds[j]) = a1;
+                *reinterpret_cast<u32x2*>(base + 4 * T::HPLANE + hlds[j]) = a2;
+            }
         }
     };
+    // weight step s (segment-0 steps are BSTEP0 bytes, segment-1 steps BSTEP1)
     auto load_b = [&](int s) {
-        const unsigned base = (unsigned)((tile_n * S + s) * T::BSTAGE);
+        const bool s1 = RES && s >= S0;
+        const unsigned base = wtile + (s1 ? (unsigned)(S0 * T::BSTEP0 + (s - S0) * T::BSTEP1)
+                                          : (unsigned)(s * T::BSTEP0));
+        const int items = s1 ? T::BSTEP1 / 16 : T::BSTEP0 / 16;
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            rb[j] = bload_u4(srdw, i < T::B_ITEMS ? base + (unsigned)i * 16u : OOB);
+            const bool ok = j < T::B_FULL || i < items;
+            rb[j] = bload_u4(srdw, ok ? base + (unsigned)i * 16u : OOB);
         }
     };
-    auto write_b = [&](int bs) {
+    auto write_b = [&](int bs, int s) {
         unsigned char* base = smem + 2 * T::HSTAGE + bs * T::BSTAGE;
+        const int items = (RES && s >= S0) ? T::BSTEP1 / 16 : T::BSTEP0 / 16;
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            if (i < T::B_ITEMS) *reinterpret_cast<u32x4*>(base + i * 16) = rb[j];
+            if (j < T::B_FULL || i < items) *reinterpret_cast<u32x4*>(base + i * 16) = rb[j];
         }
     };
 
@@ -217,7 +254,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto compute = [&](int hs, int toff, int bs) {
+    // bf16x6 step (segment 0 without F3, and segment 1)
+    auto compute6 = [&](int hs, int toff, int bs) {
         const unsigned char* ha = smem + hs * T::HSTAGE + toff * 16;
         const unsigned char* hb = smem + bs * T::BSTAGE;
         u32x4 fa[2][3], fb[2][3];
@@ -251,12 +289,42 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 acc[mb][nb] = mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
             }
     };
+    // f16x3 step (segment 0 with F3)
+    auto compute3 = [&](int hs, int toff, int bs) {
+        const unsigned char* ha = smem + hs * T::HSTAGE + toff * 16;
+        const unsigned char* hb = smem + bs * T::BSTAGE;
+        u32x4 fa[2][2], fb[2][2];
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+                fa[mb][pc] = *reinterpret_cast<const u32x4*>(ha + abase[mb] + pc * 2 * T::HPLANE);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                fb[nb][pc] = *reinterpret_cast<const u32x4*>(hb + bbase + nb * 32 * 16 + pc * 2 * T::BPLANE);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+            }
+    };
+    auto compute0 = [&](int hs, int toff, int bs) {
+        if constexpr (F3) compute3(hs, toff, bs);
+        else compute6(hs, toff, bs);
+    };
 
     // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
     load_halo0(0);
     load_b(0);
     write_halo(0, true);
-    write_b(0);
+    write_b(0, 0);
     __syncthreads();
     int s = 0;
     for (int c = 0; c < p.nck0; ++c) {
@@ -265,12 +333,15 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
         for (int tp = 0; tp < 9; ++tp) {
             const bool more = s + 1 < S;
             if (more) load_b(s + 1);
-            if (tp == 0) {
+            // The next chunk's halo loads go out at tap 7, after that step's weight loads: vmcnt
+            // drains in issue order, so a halo load issued earlier would be waited for by every
+            // later step's weight-tile wait (an HBM-latency stall per chunk).
+            if (tp == 7) {
                 if (c + 1 < p.nck0) load_halo0(c + 1);
                 else if (RES) load_halo1(0);
             }
-            compute(hs, (tp / 3) * HWD + tp % 3, s & 1);
-            if (more) write_b((s + 1) & 1);
+            compute0(hs, (tp / 3) * HWD + tp % 3, s & 1);
+            if (more) write_b((s + 1) & 1, s + 1);
             if (tp == 8) {
                 if (c + 1 < p.nck0) write_halo(hs ^ 1, true);
                 else if (RES) write_halo(hs ^ 1, false);
@@ -287,9 +358,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 load_b(s + 1);
                 load_halo1(c + 1);
             }
-            compute(hs, HWD + 1, s & 1);  // the halo centre = the output pixel
+            compute6(hs, HWD + 1, s & 1);  // the halo centre = the output pixel
             if (more) {
-                write_b((s + 1) & 1);
+                write_b((s + 1) & 1, s + 1);
                 write_halo(hs ^ 1, false);
             }
             __syncthreads();
@@ -297,7 +368,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
         }
     }
 
-    // ---- epilogue: + bias + temb, activation, + residual, NHWC store ----
+    // ---- epilogue: (F3: x 2^-(sA + sW[n])) + bias + temb, activation, + residual, NHWC store ----
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
@@ -306,13 +377,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             if (n >= p.N) continue;
             float add = p.bias ? p.bias[n] : 0.f;
             if (p.temb) add += p.temb[b * p.temb_ld + n];
+            const float mul = F3 ? p.wsinv[n] * p.ainv : 1.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
                 const int oy = y0 + 4 * wm + 2 * mb + row_dy(row);
                 const int ox = x0 + row_dx(row);
                 const long m = (long)(b * p.H + oy) * p.W + ox;
-                float v = acc[mb][nb][r] + add;
+                float v = (F3 ? acc[mb][nb][r] * mul : acc[mb][nb][r]) + add;
                 if (p.act == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
                 else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
                 if (p.res) v += p.res[m * p.ldres + n];
@@ -322,12 +394,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     }
 }
 
-template <int TH, int BN, int PRO, bool RES>
+template <int TH, int BN, int PRO, bool RES, bool F3>
 int launch6(const X6Dev& d, hipStream_t stream) {
-    using T = X6Tile<TH, BN>;
+    using T = X6Tile<TH, BN, RES, F3>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -337,20 +409,28 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES>), grid, dim3(NT), T::LDS, stream, p);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 template <int TH, int BN>
-int dispatch6(const X6Dev& d, int pro, bool res, hipStream_t s) {
+int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
+    if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here
+        switch ((pro - 1) * 2 + (res ? 1 : 0)) {
+            case 0: return launch6<TH, BN, 1, false, true>(d, s);
+            case 1: return launch6<TH, BN, 1, true, true>(d, s);
+            case 2: return launch6<TH, BN, 2, false, true>(d, s);
+            default: return launch6<TH, BN, 2, true, true>(d, s);
+        }
+    }
     switch (pro * 2 + (res ? 1 : 0)) {
-        case 0: return launch6<TH, BN, 0, false>(d, s);
-        case 1: return launch6<TH, BN, 0, true>(d, s);
-        case 2: return launch6<TH, BN, 1, false>(d, s);
-        case 3: return launch6<TH, BN, 1, true>(d, s);
-        case 4: return launch6<TH, BN, 2, false>(d, s);
-        default: return launch6<TH, BN, 2, true>(d, s);
+        case 0: return launch6<TH, BN, 0, false, false>(d, s);
+        case 1: return launch6<TH, BN, 0, true, false>(d, s);
+        case 2: return launch6<TH, BN, 1, false, false>(d, s);
+        case 3: return launch6<TH, BN, 1, true, false>(d, s);
+        case 4: return launch6<TH, BN, 2, false, false>(d, s);
+        default: return launch6<TH, BN, 2, true, false>(d, s);
     }
 }
 
@@ -361,28 +441,25 @@ bool is_3x3(const wc_conv_seg& s) {
     return true;
 }
 
-}  // namespace
-
-extern "C" int wc_conv3x3_x6_tile_n(int N) { return N <= 64 ? 64 : 128; }
-
-extern "C" int wc_conv3x3_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
-    if (!a || !w6 || !a->out) return WC_E_ARG;
+// Shared host validation; fills d and returns the number of K-steps (or a negative status).
+int prepare(const wc_conv_args* a, const void* w, X6Dev& d, int& BN, int& TH) {
+    if (!a || !w || !a->out) return WC_E_ARG;
     if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
     const wc_conv_seg& s0 = a->seg[0];
     if (!s0.src) return WC_E_ARG;
     if ((s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
     if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
-    const int BN = wc_conv3x3_x6_tile_n(a->N);
-    const int TH = BN == 64 ? 16 : 8;
+    BN = wc_conv3x3_x6_tile_n(a->N);
+    TH = BN == 64 ? 16 : 8;
     if (!is_3x3(s0) || s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
     if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
     if (s0.H != a->Hm || s0.W != a->Wm || a->Hm % TH || a->Wm % 16) return WC_E_SHAPE;
     if (a->B <= 0 || a->N <= 0) return WC_E_SHAPE;
     if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;  // 2 GiB SRD range
-    X6Dev d{};
+    if (reinterpret_cast<uintptr_t>(w) & 15) return WC_E_SHAPE;
+    d = X6Dev{};
     d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.scale = s0.scale; d.shift = s0.shift;
     d.nck0 = s0.C / 16;
-    int steps = 9 * d.nck0;
     if (a->nseg == 2) {
         const wc_conv_seg& s1 = a->seg[1];
         if (!s1.src || s1.scale) return WC_E_ARG;
@@ -391,18 +468,50 @@ extern "C" int wc_conv3x3_x6(const wc_conv_args* a, const void* w6, int64_t w6_b
         if (s1.C <= 0 || s1.C % 16 || s1.ldc % 4 || (reinterpret_cast<uintptr_t>(s1.src) & 15)) return WC_E_SHAPE;
         if ((long)a->B * s1.H * s1.W * s1.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
         d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc; d.nck1 = s1.C / 16;
-        steps += d.nck1;
     }
     if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox)
         return WC_E_SHAPE;
-    const long ntn = (a->N + BN - 1) / BN;
-    if (w6_bytes != ntn * steps * (long)BN * 96 || w6_bytes >= (1L << 31)) return WC_E_SHAPE;
-    if (reinterpret_cast<uintptr_t>(w6) & 15) return WC_E_SHAPE;
     d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
-    d.w6 = w6; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
+    d.w6 = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo; d.act = a->act;
-    const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
+    d.ascale = 1.f; d.ainv = 1.f; d.wsinv = nullptr;
+    return WC_OK;
+}
+
+}  // namespace
+
+extern "C" int wc_conv3x3_x6_tile_n(int N) { return N <= 64 ? 64 : 128; }
+
+extern "C" int wc_conv3x3_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
+    X6Dev d;
+    int BN, TH;
+    const int st = prepare(a, w6, d, BN, TH);
+    if (st != WC_OK) return st;
+    const long ntn = (a->N + BN - 1) / BN;
+    const long steps = 9L * d.nck0 + d.nck1;
+    if (w6_bytes != ntn * steps * (long)BN * 96 || w6_bytes >= (1L << 31)) return WC_E_SHAPE;
+    const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (BN == 64) return dispatch6<16, 64>(d, pro, a->nseg == 2, s);
-    return dispatch6<8, 128>(d, pro, a->nseg == 2, s);
+    if (BN == 64) return dispatch6<16, 64>(d, pro, a->nseg == 2, false, s);
+    return dispatch6<8, 128>(d, pro, a->nseg == 2, false, s);
+}
+
+extern "C" int wc_conv3x3_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, int a_exp,
+                                const float* w_inv_scale, void* stream) {
+    X6Dev d;
+    int BN, TH;
+    const int st = prepare(a, w3, d, BN, TH);
+    if (st != WC_OK) return st;
+    if (!a->seg[0].scale || !w_inv_scale) return WC_E_ARG;  // the static bound needs the GN prologue
+    if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w3_bytes != ntn * (9L * d.nck0 * BN * 64 + (long)d.nck1 * BN * 96) || w3_bytes >= (1L << 31))
+        return WC_E_SHAPE;
+    d.ascale = ldexpf(1.0f, a_exp);
+    d.ainv = ldexpf(1.0f, -a_exp);
+    d.wsinv = w_inv_scale;
+    const int pro = a->seg[0].silu ? 2 : 1;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return dispatch6<16, 64>(d, pro, a->nseg == 2, true, s);
+    return dispatch6<8, 128>(d, pro, a->nseg == 2, true, s);
 }

@@ -132,7 +132,8 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            rb[j] = bload_u4(srdw, i < T::B_ITEMS ? base + (unsigned)i * 16u : OOB);
+            const bool ok = T::B_ITEMS % NT == 0 || i < T::B_ITEMS;
+            rb[j] = bload_u4(srdw, ok ? base + (unsigned)i * 16u : OOB);
         }
         ++bstep;
     };
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            if (i < T::B_ITEMS) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[j];
+            if (T::B_ITEMS % NT == 0 || i < T::B_ITEMS) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[j];
         }
     };
 

@@ -5,6 +5,7 @@
 namespace wcx6 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
@@ -25,6 +26,11 @@ WC_DEVICE u32x4 bload_u4(__amdgpu_buffer_rsrc_t r, unsigned off) {
 WC_DEVICE f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+WC_DEVICE f32x16 mfma_f16(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
 }
 
 WC_DEVICE float silu_fast(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
@@ -53,6 +59,22 @@ WC_DEVICE void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
     p0 = u32x2{hi_pair(u0[1], u0[0]), hi_pair(u0[3], u0[2])};
     p1 = u32x2{hi_pair(u1[1], u1[0]), hi_pair(u1[3], u1[2])};
     p2 = u32x2{hi_pair(u2[1], u2[0]), hi_pair(u2[3], u2[2])};
+}
+
+// Two-piece fp16 split by round-to-nearest: h = fp16(v), l = fp16(v - h) (v - h is exact in fp32),
+// so v = h + l to 2^-22 |v| (or 2^-25 absolute when l is subnormal).  Callers bound |v| < 2^15.
+WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
+    unsigned h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e];
+        const _Float16 hh = (_Float16)x;
+        const _Float16 ll = (_Float16)(x - (float)hh);
+        h[e] = __builtin_bit_cast(unsigned short, hh);
+        l[e] = __builtin_bit_cast(unsigned short, ll);
+    }
+    ph = u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+    pl = u32x2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
 }
 
 }  // namespace wcx6

@@ -70,8 +70,12 @@ class ResPack:
     w2: torch.Tensor  # conv2 (9*co) ++ residual 1x1 (ci)
     b2: torch.Tensor
     temb_off: int
-    w1x6: Optional[Tuple[K.X6Weight, K.X6Weight]] = None  # bf16x6 re-packs (halo, natural order)
-    w2x6: Optional[Tuple[K.X6Weight, K.X6Weight]] = None
+    w1x6: Optional[Tuple[Optional[K.X6Weight], K.X6Weight]] = None  # bf16x6 re-packs (halo, natural order)
+    w2x6: Optional[Tuple[Optional[K.X6Weight], K.X6Weight]] = None
+    w1f3: Optional[K.X6Weight] = None  # f16x3 re-packs (precision 'f16x3')
+    w2f3: Optional[K.X6Weight] = None
+    gb1: Tuple[float, float] = (0.0, 0.0)  # (max|gamma|, max|beta|) of the GroupNorms (f16x3 bound)
+    gb2: Tuple[float, float] = (0.0, 0.0)
 
 
 @dataclass
@@ -153,10 +157,17 @@ class UnetEngine:
                     w1=pack_conv(f[2].weight), b1=f[2].bias.detach().float().contiguous(),
                     g2=s[0].weight.detach().float(), be2=s[0].bias.detach().float(), w2=w2,
                     b2=(s[2].bias.detach().float() + r.bias.detach().float()).contiguous(), temb_off=self._temb_P)
-        if self.precision == 'bf16x6' and ci % 16 == 0 and co % 16 == 0:
-            # (halo-order pack for the 3x3 kernel, natural-order pack for the implicit-GEMM fallback)
-            p.w1x6 = (K.pack_x6(p.w1, ci), self._x6(p.w1, ci, 9))
-            p.w2x6 = (K.pack_x6(p.w2, co, ci), self._x6(p.w2, co, 9, ci))
+        if self.precision in ('bf16x6', 'f16x3') and ci % 16 == 0 and co % 16 == 0:
+            # halo-order pack for the 3x3 kernel (bf16x6 mode), natural-order pack for the
+            # implicit-GEMM fallback (grids the halo kernel does not tile), f16x3 pack
+            f3 = self.precision == 'f16x3'
+            p.w1x6 = (None if f3 else K.pack_x6(p.w1, ci), self._x6(p.w1, ci, 9))
+            p.w2x6 = (None if f3 else K.pack_x6(p.w2, co, ci), self._x6(p.w2, co, 9, ci))
+            if f3:
+                p.w1f3 = K.pack_f16x3(p.w1, ci)
+                p.w2f3 = K.pack_f16x3(p.w2, co, ci)
+                p.gb1 = (float(p.g1.abs().max()), float(p.be1.abs().max()))
+                p.gb2 = (float(p.g2.abs().max()), float(p.be2.abs().max()))
         self.temb_rows_w.append(tl.weight.detach().float())
         self.temb_rows_b.append(tl.bias.detach().float())
         self._temb_P += co
@@ -164,7 +175,7 @@ class UnetEngine:
 
     def _x6(self, w: torch.Tensor, c0: int, ntaps: int, c1: int = 0) -> Optional[K.X6Weight]:
         """bf16x6 (natural K order) re-pack for wc_conv_igemm_x6, or None in fp32 mode."""
-        if self.precision != 'bf16x6' or c0 % 16 or c1 % 16:
+        if self.precision == 'fp32' or c0 % 16 or c1 % 16:
             return None
         return K.pack_x6(w, c0, c1, ntaps=ntaps, order='natural')
 
@@ -199,10 +210,15 @@ class UnetEngine:
             K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
 
     @staticmethod
-    def conv3(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: View, H: int, W: int, **kw):
-        """A ResBlock 3x3 stride-1 conv: the halo-tiled bf16x6 kernel when the grid tiles, else the
+    def conv3(segs, w: torch.Tensor, w6, w3: Optional[K.X6Weight], gb: Tuple[float, float], bias, out: View, H: int,
+              W: int, **kw):
+        """A ResBlock 3x3 stride-1 conv (GN+SiLU prologue): the halo-tiled kernel in f16x3 (bound
+        from the GroupNorm affine gb and the group size) or bf16x6 when the grid tiles, else the
         bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode)."""
-        if w6 is not None and K.x6_eligible(segs, w6[0].N, H, W):
+        if w3 is not None and K.x6_eligible(segs, w3.N, H, W):
+            n_group = H * W * segs[0].view.C // 8
+            K.conv3x3_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(gb[0], gb[1], n_group), **kw)
+        elif w6 is not None and w6[0] is not None and K.x6_eligible(segs, w6[0].N, H, W):
             K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, **kw)
         else:
             UnetEngine.conv(segs, w, None if w6 is None else w6[1], bias, out, H, W, **kw)
@@ -211,11 +227,11 @@ class UnetEngine:
         B, H, W = X.B, X.H, X.W
         sc1, sh1 = K.gn_affine(X, p.g1, p.be1)
         h = View.full(self._new(B, H, W, p.co))
-        self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.b1, h, H, W,
+        self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.w1f3, p.gb1, p.b1, h, H, W,
                    temb=temb[:, p.temb_off:], temb_ld=temb_ld)
         sc2, sh2 = K.gn_affine(h, p.g2, p.be2)
         self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
-                    Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.b2, Y, H, W)
+                    Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W)
 
     def attention(self, Y: View, p: AttnPack):
         B, H, W, C = Y.B, Y.H, Y.W, Y.C
@@ -224,7 +240,8 @@ class UnetEngine:
         qkv = self._new(B, H, W, 3 * C)
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         o = self._new(B, H, W, C)
-        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
+        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads,
+                    'fp32' if self.precision == 'fp32' else 'bf16x6')
         self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y)
 
     # ------------------------------------------------------------------ forward

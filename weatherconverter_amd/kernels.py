@@ -180,13 +180,15 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
 
 # ---- bf16x6 split-precision 3x3 conv (csrc/wc_conv6.hip) ----
 
-CONV_PRECISIONS = ('bf16x6', 'fp32')
+CONV_PRECISIONS = ('f16x3', 'bf16x6', 'fp32')
 
 
 def default_conv_precision() -> str:
-    """Conv arithmetic for 3x3 stride-1 convs: 'bf16x6' (exact 3-piece bf16 split on bf16 MFMA,
-    fp32-level error) or 'fp32' (fp32 MFMA).  Overridable with WC_CONV_PRECISION."""
-    p = os.environ.get('WC_CONV_PRECISION', 'bf16x6')
+    """Conv / attention arithmetic: 'f16x3' (the GN-prologue 3x3 convs on two-piece fp16 with a
+    provable range bound, everything else bf16x6), 'bf16x6' (exact 3-piece bf16 split on bf16 MFMA
+    everywhere) or 'fp32' (fp32 MFMA).  All three are fp32-class.  Overridable with
+    WC_CONV_PRECISION."""
+    p = os.environ.get('WC_CONV_PRECISION', 'f16x3')
     _req(p in CONV_PRECISIONS, f'WC_CONV_PRECISION must be one of {CONV_PRECISIONS}, got {p!r}')
     return p
 
@@ -203,6 +205,7 @@ class X6Weight:
     C0: int
     C1: int
     order: str = 'halo'
+    wsinv: Optional[torch.Tensor] = None  # order 'f16x3': 2^-sW[n]
 
 
 @functools.lru_cache(maxsize=None)
@@ -249,6 +252,65 @@ def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str
     return X6Weight(data, N, BN, C0, C1, order)
 
 
+def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
+    """Re-pack a [N][9*C0 + C1] 3x3 (+ 1x1 residual) weight for wc_conv3x3_f16x3: per output
+    channel n a power-of-two scale 2^sW[n] with max_k |w[n, :9*C0]| * 2^sW[n] <= 2^14; the 3x3 part
+    as two round-to-nearest fp16 pieces in (chunk, tap) step order, the residual part as three
+    bf16 pieces (same scale)."""
+    N, K = w.shape
+    _req(K == 9 * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'f16x3 weight shape')
+    _, BN = x6_tile(N)
+    Np = -(-N // BN) * BN
+    T = Np // BN
+    wp = torch.zeros((Np, K), dtype=torch.float32, device=w.device)
+    wp[:N] = w.float()
+    amax = wp[:, :9 * C0].abs().amax(1).double()
+    sw = torch.where(amax > 0, torch.floor(torch.log2(2.0**14 / amax.clamp_min(1e-300))), torch.zeros_like(amax))
+    sw = sw.clamp(-60, 60).to(torch.int32)
+    ws = wp * torch.ldexp(torch.ones_like(wp[:, :1]), sw[:, None].float())  # exact power-of-two scaling
+    S0, S1 = 9 * (C0 // 16), C1 // 16
+    main = ws[:, :9 * C0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, S0, 2, 8)
+    h = main.half()
+    lo = (main - h.float()).half()
+    pm = torch.stack([h, lo]).view(torch.int16).view(2, T, BN, S0, 2, 8).permute(1, 3, 0, 4, 2, 5)
+    parts = [pm.reshape(T, -1)]
+    if C1:
+        pr = split3_bits(ws[:, 9 * C0:].reshape(Np, S1, 2, 8)).view(3, T, BN, S1, 2, 8).permute(1, 3, 0, 4, 2, 5)
+        parts.append(pr.reshape(T, -1))
+    data = torch.cat(parts, 1).contiguous()
+    wsinv = torch.ldexp(torch.ones(Np, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
+    return X6Weight(data, N, BN, C0, C1, 'f16x3', wsinv)
+
+
+def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
+    """sA for wc_conv3x3_f16x3: (sqrt(n - 1) max|gamma| + max|beta|) * 2^sA <= 2^14 (Samuelson's
+    bound on a GroupNorm output, times a 4x margin under the fp16 maximum 65504)."""
+    import math
+    bound = math.sqrt(max(n_group - 1, 1)) * gamma_absmax + beta_absmax
+    if not math.isfinite(bound):
+        raise RuntimeError('weatherconverter_amd: non-finite GroupNorm affine in an f16x3 conv')
+    if bound <= 0:
+        return 0
+    return max(-60, min(60, math.floor(math.log2(2.0**14 / bound))))
+
+
+def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
+                  a_exp: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
+                  act: int = 0):
+    """3x3 stride-1 conv with a GN(+SiLU) prologue on f16x3 (see wc_conv3x3_f16x3); a_exp from
+    f16x3_a_exp of that GroupNorm."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3', 'f16x3 weight')
+    _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
+    _req(segs[0].scale is not None, 'f16x3 needs the GroupNorm prologue')
+    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act)
+    TH, BN = x6_tile(w3.N)
+    pro = 2 if segs[0].silu else 1
+    res_seg = 'true' if len(segs) == 2 else 'false'
+    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, true>', 'wc_conv3x3_f16x3',
+           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
+
+
 def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
     """True when wc_conv3x3_x6 accepts this conv (mirrors its host checks; output must be a plain
     NHWC view on the same grid)."""
@@ -274,7 +336,7 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     res_seg = 'true' if len(segs) == 2 else 'false'
-    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}>', 'wc_conv3x3_x6',
+    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, false>', 'wc_conv3x3_x6',
            _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 

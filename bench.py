@@ -54,6 +54,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=2)
     ap.add_argument('--cpu-steps', type=int, default=2)
+    ap.add_argument('--precision', default=None, choices=['f16x3', 'bf16x6', 'fp32'],
+                    help='conv/attention arithmetic (default: kernels.default_conv_precision(), i.e. f16x3)')
     return ap.parse_args()
 
 
@@ -155,6 +157,8 @@ def main():
     mc = model_config(args.size)
     model = Unet(mc)
     init_synthetic_(model, seed=0)
+    precision = args.precision or kernels.default_conv_precision()
+    model.set_conv_precision(precision)
     model = model.to(dev).eval()
     sched = LinearNoiseScheduler(args.timesteps, 0.0001, 0.02, device=dev)
     B = args.batch
@@ -230,6 +234,13 @@ def main():
                     'timesteps': T,
                     'parallelism': f'batch-sharded x{world}, 1 RCCL all-gather of x0' if world > 1 else 'single GPU',
                     'hip_graph': bool(args.graph),
+                    'arithmetic': {
+                        'f16x3': 'fp32-class: GN-prologue 3x3 convs on f16x3 (2-piece fp16 split, Samuelson-bounded '
+                                 'scale), all other convs and attention on bf16x6 (exact 3-piece bf16 split); fp32 '
+                                 'accumulation; fp32 activations in HBM',
+                        'bf16x6': 'fp32-class: every conv and attention on bf16x6 (exact 3-piece bf16 split), fp32 '
+                                  'accumulation; fp32 activations in HBM',
+                        'fp32': 'fp32 MFMA (v_mfma_f32_32x32x2_f32) everywhere'}[precision],
                     'x_finite': finite,
                 },
                 'ms_per_unet_step': round(ms_step, 3),

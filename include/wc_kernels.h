@@ -149,6 +149,12 @@ int wc_attention_fwd(const float* qkv, int ld_qkv, float* out, int ld_out, int B
  * softmax probabilities, six products per block, fp32 accumulation); head dim C/heads % 32 == 0. */
 int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
                         int heads, float scale, void* stream);
+/* Same contract on f16x3: Q, K, V are scaled by 2^q_exp, 2^k_exp, 2^v_exp (the caller guarantees
+ * |x| * 2^exp <= 2^14, e.g. from the in-projection row norms and the GroupNorm bound) and the
+ * probabilities by 2^14, each split into two round-to-nearest fp16 pieces, three f16 MFMAs per block;
+ * the scales are removed in the softmax multiplier and the final 1/l. */
+int wc_attention_fwd_f16x3(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
+                           int heads, float scale, int q_exp, int k_exp, int v_exp, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Time embedding: sinusoid + t_proj MLP + every ResBlock's SiLU→Linear projection in one launch */

@@ -441,3 +441,27 @@ def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier):
     assert torch.isfinite(outs['f16x3']).all()
     e3, e32 = rel_l2(outs['f16x3'], ref), rel_l2(outs['fp32'], ref)
     assert e3 < 1e-5 and e3 <= 4 * e32 + 2e-7, (e3, e32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,N,C,heads,gs', [(2, 300, 128, 4, 1.0), (1, 1024, 256, 4, 1.0), (2, 257, 512, 4, 3.0),
+                                            (1, 200, 768, 4, 1.0), (1, 96, 384, 4, 1.0), (1, 64, 640, 4, 0.5)])
+def test_attention_f16x3_vs_float64(B, N, C, heads, gs):
+    """qkv = GN(Y) W_in^T + b_in as in the UNet, exponents from the static bound; vs float64."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(41)
+    y = torch.randn((B, C, N), generator=g) * 2 + 1
+    gamma = gs * (1 + 0.3 * torch.randn(C, generator=g))
+    beta = 0.3 * torch.randn(C, generator=g)
+    yn = F.group_norm(y.double(), 8, gamma.double(), beta.double(), 1e-5).transpose(1, 2)  # (B, N, C)
+    w_in = torch.randn((3 * C, C), generator=g) / C**0.5
+    b_in = 0.1 * torch.randn(3 * C, generator=g)
+    qkv = (yn @ w_in.double().t() + b_in.double()).float()
+    ref = _attn_ref(qkv, B, N, C, heads)
+    exps = K.attention_f16x3_exps(w_in, b_in, float(gamma.abs().max()), float(beta.abs().max()), N * C // 8)
+    errs = {}
+    for prec in ('f16x3', 'fp32'):
+        out = torch.full((B * N, C), 9.0, device='cuda')
+        K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads, prec, exps)
+        errs[prec] = rel_l2(out.cpu().double().reshape(B, N, C), ref)
+    assert errs['f16x3'] < 1e-5 and errs['f16x3'] <= 4 * errs['fp32'] + 2e-7, (errs, exps)

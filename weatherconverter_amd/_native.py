@@ -17,7 +17,7 @@ NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 EXPORTS = [
     'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
     'wc_gn_num_splits',
-    'wc_gn_stats', 'wc_gn_finalize', 'wc_attention_fwd', 'wc_attention_fwd_x6',
+    'wc_gn_stats', 'wc_gn_finalize', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed', 'wc_version'
 ]
@@ -63,6 +63,7 @@ _SIGS = {
     'wc_gn_finalize': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P],
     'wc_attention_fwd': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_x6': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
+    'wc_attention_fwd_f16x3': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],
     'wc_temb': [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     'wc_conv_in': [_P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
     'wc_ddpm_step': [_P, _P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _I, _U, _L, _L, _P],

@@ -1,20 +1,25 @@
-// Flash attention on bf16x6 split-precision MFMA for gfx950 (head dims D % 32 == 0).  Same
-// contract as wc_attention_fwd (wc_attention.hip): softmax(Q K^T * scale) V per (batch, head),
-// replacing the core of nn.MultiheadAttention(C, 4, batch_first=True) (unet_base.py:115,159).
+// Flash attention on split-precision MFMA for gfx950 (head dims D % 32 == 0).  Same contract as
+// wc_attention_fwd (wc_attention.hip): softmax(Q K^T * scale) V per (batch, head), replacing the
+// core of nn.MultiheadAttention(C, 4, batch_first=True) (unet_base.py:115,159).
 //
-// Arithmetic: every fp32 operand is split exactly into three bf16 pieces (wc_x6.hpp split3) and
-// the six products with piece-order sum <= 2 are accumulated in fp32 by
-// v_mfma_f32_32x32x16_bf16 (wc_conv6.hip header) — fp32-class error at 2.67x the fp32 MFMA rate.
+// Arithmetic (fp32-class, fp32 accumulation):
+//   bf16x6  every fp32 operand (Q, K, V and the probabilities P) split exactly into three bf16
+//           pieces (wc_x6.hpp split3); six products per block on v_mfma_f32_32x32x16_bf16.
+//   f16x3   Q, K, V scaled by caller-chosen powers of two 2^eq, 2^ek, 2^ev with |x| 2^e < 2^15
+//           (static bounds from the in-projection and its GroupNorm, see kernels.py), P by 2^14,
+//           each split into two round-to-nearest fp16 pieces; three products per block on
+//           v_mfma_f32_32x32x16_f16.  The scales fold into the softmax multiplier and the final
+//           1/l, so no extra arithmetic is spent on them.
 //
-// Structure (as wc_attention.hip, with 16-wide K-steps):
+// Structure:
 //   * workgroup = 4 waves x 32 queries of one (batch, head); Q is split once into registers.
 //   * K/V tiles of 32 keys, double-buffered in LDS: the next tile's global loads are issued before
 //     the MFMAs of the current tile and split into the other buffer after them; one barrier/tile.
-//   * S^T = K Q^T: 6 MFMAs per 16 head dims.  The accumulator holds keys x queries, so each lane
-//     owns one query and the online softmax is in-lane (+ one lane^32 exchange).
+//   * S^T = K Q^T per 16 head dims.  The accumulator holds keys x queries, so each lane owns one
+//     query and the online softmax is in-lane (+ one lane^32 exchange).
 //   * O^T += V^T P^T: the S^T registers of a 16-key chunk ARE the lane's B operand (P^T), split in
 //     registers; V is staged transposed ([piece][dim][32 keys]) in the matching key permutation
-//     (pos(key) below), its 16-byte slots XOR-swizzled by (dim >> 2) & 3 so each ds_read_b128 lane
+//     (key_pos below), its 16-byte slots XOR-swizzled by (dim >> 2) & 3 so each ds_read_b128 lane
 //     group reads 16 distinct slots.
 #include "wc_x6.hpp"
 
@@ -25,14 +30,16 @@ using namespace wcx6;
 constexpr int NT = 256;
 constexpr int KT = 32;  // keys per tile
 
-template <int D>
+template <int D, bool F3>
 struct Ax6 {
-    static_assert(D % 32 == 0, "bf16x6 attention needs D % 32 == 0");
+    static_assert(D % 32 == 0, "split-precision attention needs D % 32 == 0");
+    static constexpr int NP = F3 ? 2 : 3;               // pieces per operand
     static constexpr int NCH = D / 16;                  // QK^T K-steps
     static constexpr int NDB = D / 32;                  // O^T 32-dim blocks
     static constexpr int KPLANE = KT * 16;              // bytes of one (piece, chunk, k-half) K plane
-    static constexpr int KBYTES = 3 * NCH * 2 * KPLANE; // K pieces of one tile
-    static constexpr int VBYTES = 3 * D * KT * 2;       // V^T pieces of one tile
+    static constexpr int KBYTES = NP * NCH * 2 * KPLANE; // K pieces of one tile
+    static constexpr int VPLANE = D * KT * 2;           // bytes of one V^T piece
+    static constexpr int VBYTES = NP * VPLANE;
     static constexpr int STAGE = KBYTES + VBYTES;
     static constexpr int LDS = 2 * STAGE;
     static constexpr int KPT = KT * D / 4 / NT;         // K float4 items per thread
@@ -40,13 +47,13 @@ struct Ax6 {
     static constexpr int VPT = (VITEMS + NT - 1) / NT;
 };
 
-// position of key kk (0..31) in the permuted K16 order of the PV MFMA (see header)
+// position of key k (0..31) in the permuted K16 order of the PV MFMA (see header)
 WC_DEVICE int key_pos(int k) {
     const int c = k >> 4, kk = k & 15;
     return 16 * c + 8 * ((kk >> 2) & 1) + (kk & 3) + 4 * (kk >> 3);
 }
 
-// The three piece bit patterns (hi16 = the bf16 piece) of 4 floats, per element.
+// The three bf16 piece bit patterns (hi16 = the piece) of 4 floats, per element.
 WC_DEVICE void split3_elems(f32x4 v, unsigned (&u)[3][4]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -61,20 +68,50 @@ WC_DEVICE void split3_elems(f32x4 v, unsigned (&u)[3][4]) {
     }
 }
 
-WC_DEVICE void mfma6(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {
-    acc = mfma_bf16(a[0], b[0], acc);
-    acc = mfma_bf16(a[0], b[1], acc);
-    acc = mfma_bf16(a[1], b[0], acc);
-    acc = mfma_bf16(a[0], b[2], acc);
-    acc = mfma_bf16(a[1], b[1], acc);
-    acc = mfma_bf16(a[2], b[0], acc);
+// 16-bit pieces of 8 consecutive values as MFMA operands: NP x u32x4
+template <bool F3>
+WC_DEVICE void pieces8(f32x4 v0, f32x4 v1, u32x4 (&out)[F3 ? 2 : 3]) {
+    if constexpr (F3) {
+        u32x2 a0, a1, b0, b1;
+        split2_f16(v0, a0, a1);
+        split2_f16(v1, b0, b1);
+        out[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+        out[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+    } else {
+        u32x2 a0, a1, a2, b0, b1, b2;
+        split3(v0, a0, a1, a2);
+        split3(v1, b0, b1, b2);
+        out[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+        out[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+        out[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+    }
 }
 
-template <int D>
+template <bool F3>
+WC_DEVICE void mfma_split(f32x16& acc, const u32x4 (&a)[F3 ? 2 : 3], const u32x4 (&b)[F3 ? 2 : 3]) {
+    if constexpr (F3) {
+        acc = mfma_f16(a[0], b[0], acc);
+        acc = mfma_f16(a[0], b[1], acc);
+        acc = mfma_f16(a[1], b[0], acc);
+    } else {
+        acc = mfma_bf16(a[0], b[0], acc);
+        acc = mfma_bf16(a[0], b[1], acc);
+        acc = mfma_bf16(a[1], b[0], acc);
+        acc = mfma_bf16(a[0], b[2], acc);
+        acc = mfma_bf16(a[1], b[1], acc);
+        acc = mfma_bf16(a[2], b[0], acc);
+    }
+}
+
+// qs, ks, vs: scales applied to Q, K, V before splitting (1 for bf16x6); score_mul multiplies the
+// raw S^T accumulator into the exp2 domain; out_mul multiplies O / l at the end.
+template <int D, bool F3>
 __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
                                                              float* __restrict__ out, int ldo, int N,
-                                                             int C, float scale_log2) {
-    using A = Ax6<D>;
+                                                             int C, float score_mul, float qs, float ks,
+                                                             float vs, float ps, float out_mul) {
+    using A = Ax6<D, F3>;
+    constexpr int NP = A::NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -93,18 +130,13 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
 
     // ---- Q pieces: lane (query l32, half) holds Q[q][16 ch + 8 half + j] ----
     const int qrow = q0 + l32;
-    u32x4 qp[A::NCH][3];
+    u32x4 qp[A::NCH][NP];
 #pragma unroll
     for (int ch = 0; ch < A::NCH; ++ch) {
         const unsigned o = (unsigned)(qrow * ldq + qcol + 16 * ch + 8 * half) * 4u;
-        const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB);
-        const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB);
-        u32x2 a0, a1, a2, b0, b1, b2;
-        split3(v0, a0, a1, a2);
-        split3(v1, b0, b1, b2);
-        qp[ch][0] = u32x4{a0.x, a0.y, b0.x, b0.y};
-        qp[ch][1] = u32x4{a1.x, a1.y, b1.x, b1.y};
-        qp[ch][2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+        const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB) * qs;
+        const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB) * qs;
+        pieces8<F3>(v0, v1, qp[ch]);
     }
 
     // ---- staging coordinates ----
@@ -146,27 +178,47 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
     auto write_tile = [&](unsigned char* buf) {
 #pragma unroll
         for (int j = 0; j < A::KPT; ++j) {
-            u32x2 p0, p1, p2;
-            split3(rk[j], p0, p1, p2);
-            *reinterpret_cast<u32x2*>(buf + k_lds[j]) = p0;
-            *reinterpret_cast<u32x2*>(buf + A::NCH * 2 * A::KPLANE + k_lds[j]) = p1;
-            *reinterpret_cast<u32x2*>(buf + 2 * A::NCH * 2 * A::KPLANE + k_lds[j]) = p2;
+            if constexpr (F3) {
+                u32x2 p0, p1;
+                split2_f16(rk[j] * ks, p0, p1);
+                *reinterpret_cast<u32x2*>(buf + k_lds[j]) = p0;
+                *reinterpret_cast<u32x2*>(buf + A::NCH * 2 * A::KPLANE + k_lds[j]) = p1;
+            } else {
+                u32x2 p0, p1, p2;
+                split3(rk[j], p0, p1, p2);
+                *reinterpret_cast<u32x2*>(buf + k_lds[j]) = p0;
+                *reinterpret_cast<u32x2*>(buf + A::NCH * 2 * A::KPLANE + k_lds[j]) = p1;
+                *reinterpret_cast<u32x2*>(buf + 2 * A::NCH * 2 * A::KPLANE + k_lds[j]) = p2;
+            }
         }
         unsigned char* vb = buf + A::KBYTES;
 #pragma unroll
         for (int j = 0; j < A::VPT; ++j) {
             if (v_key[j] >= KT) continue;
-            unsigned ua[3][4], ub[3][4];
-            split3_elems(rv[j][0], ua);
-            split3_elems(rv[j][1], ub);
             const int pos = v_pos[j];
+            if constexpr (F3) {
+                unsigned ha[4], la[4], hb[4], lb[4];
+                split2_f16_elems(rv[j][0] * vs, ha, la);
+                split2_f16_elems(rv[j][1] * vs, hb, lb);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int d = v_d[j] + e;
-                const int off = d * (KT * 2) + (((pos >> 3) ^ ((d >> 2) & 3)) << 4) + (pos & 7) * 2;
+                for (int e = 0; e < 4; ++e) {
+                    const int d = v_d[j] + e;
+                    const int off = d * (KT * 2) + (((pos >> 3) ^ ((d >> 2) & 3)) << 4) + (pos & 7) * 2;
+                    *reinterpret_cast<unsigned*>(vb + off) = ha[e] | (hb[e] << 16);
+                    *reinterpret_cast<unsigned*>(vb + A::VPLANE + off) = la[e] | (lb[e] << 16);
+                }
+            } else {
+                unsigned ua[3][4], ub[3][4];
+                split3_elems(rv[j][0], ua);
+                split3_elems(rv[j][1], ub);
 #pragma unroll
-                for (int pc = 0; pc < 3; ++pc)
-                    *reinterpret_cast<unsigned*>(vb + pc * D * KT * 2 + off) = hi_pair(ub[pc][e], ua[pc][e]);
+                for (int e = 0; e < 4; ++e) {
+                    const int d = v_d[j] + e;
+                    const int off = d * (KT * 2) + (((pos >> 3) ^ ((d >> 2) & 3)) << 4) + (pos & 7) * 2;
+#pragma unroll
+                    for (int pc = 0; pc < 3; ++pc)
+                        *reinterpret_cast<unsigned*>(vb + pc * A::VPLANE + off) = hi_pair(ub[pc][e], ua[pc][e]);
+                }
             }
         }
     };
@@ -193,11 +245,11 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
         for (int r = 0; r < 16; ++r) s[r] = 0.f;
 #pragma unroll
         for (int ch = 0; ch < A::NCH; ++ch) {
-            u32x4 kf[3];
+            u32x4 kf[NP];
 #pragma unroll
-            for (int pc = 0; pc < 3; ++pc)
+            for (int pc = 0; pc < NP; ++pc)
                 kf[pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE + l32 * 16);
-            mfma6(s, kf, qp[ch]);
+            mfma_split<F3>(s, kf, qp[ch]);
         }
 
         // ---- online softmax over keys, per query (lane) ----
@@ -205,7 +257,7 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            const float v = (key < N) ? s[r] * scale_log2 : -INFINITY;
+            const float v = (key < N) ? s[r] * score_mul : -INFINITY;
             s[r] = v;
             mloc = fmaxf(mloc, v);
         }
@@ -230,24 +282,18 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
         // ---- O^T += V^T P^T: two 16-key chunks ----
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            u32x4 pp[3];
-            {
-                u32x2 a0, a1, a2, b0, b1, b2;
-                split3(f32x4{s[8 * c + 0], s[8 * c + 1], s[8 * c + 2], s[8 * c + 3]}, a0, a1, a2);
-                split3(f32x4{s[8 * c + 4], s[8 * c + 5], s[8 * c + 6], s[8 * c + 7]}, b0, b1, b2);
-                pp[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
-                pp[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
-                pp[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
-            }
+            u32x4 pp[NP];
+            pieces8<F3>(f32x4{s[8 * c + 0], s[8 * c + 1], s[8 * c + 2], s[8 * c + 3]} * ps,
+                        f32x4{s[8 * c + 4], s[8 * c + 5], s[8 * c + 6], s[8 * c + 7]} * ps, pp);
 #pragma unroll
             for (int db = 0; db < A::NDB; ++db) {
                 const int d = db * 32 + l32;
                 const int off = A::KBYTES + d * (KT * 2) + (((2 * c + half) ^ ((d >> 2) & 3)) << 4);
-                u32x4 vf[3];
+                u32x4 vf[NP];
 #pragma unroll
-                for (int pc = 0; pc < 3; ++pc)
-                    vf[pc] = *reinterpret_cast<const u32x4*>(cur + off + pc * D * KT * 2);
-                mfma6(o[db], vf, pp);
+                for (int pc = 0; pc < NP; ++pc)
+                    vf[pc] = *reinterpret_cast<const u32x4*>(cur + off + pc * A::VPLANE);
+                mfma_split<F3>(o[db], vf, pp);
             }
         }
 
@@ -257,7 +303,7 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
 
     // ---- epilogue: O[q][dv] = O^T[dv][q] / l ----
     if (qrow < N) {
-        const float inv = 1.0f / l_run;
+        const float inv = out_mul / l_run;
         float* orow = out + ((long)b * N + qrow) * ldo + head * D;
 #pragma unroll
         for (int d = 0; d < A::NDB; ++d) {
@@ -271,42 +317,58 @@ __global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __rest
     }
 }
 
-template <int D>
+template <int D, bool F3>
 int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
-                float scale, hipStream_t stream) {
-    using A = Ax6<D>;
+                float scale, int eq, int ek, int ev, hipStream_t stream) {
+    using A = Ax6<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, A::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
+    constexpr int EP = F3 ? 14 : 0;  // P scale: keeps small probabilities in the fp16 normal range
+    const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
     dim3 grid((N + 127) / 128, heads, B);
-    hipLaunchKernelGGL(attention_x6_kernel<D>, grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N,
-                       C, scale * 1.4426950408889634f);
+    hipLaunchKernelGGL((attention_x6_kernel<D, F3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
+                       score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), ldexpf(1.f, EP),
+                       ldexpf(1.f, -(ev + EP)));
     WC_CHECK_LAUNCH();
     return WC_OK;
+}
+
+template <bool F3>
+int dispatch_att6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C, int heads,
+                  float scale, int eq, int ek, int ev, hipStream_t s) {
+    if (!qkv || !out) return WC_E_ARG;
+    if (heads <= 0 || C % heads != 0 || ld_qkv % 4 != 0 || ld_out % 4 != 0) return WC_E_SHAPE;
+    if (ld_qkv < 3 * C || ld_out < C || N <= 0 || B <= 0) return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(qkv) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return WC_E_SHAPE;
+    if ((long)N * ld_qkv * 4 >= (1L << 31)) return WC_E_SHAPE;  // per-image SRD range
+    if (eq < -60 || eq > 60 || ek < -60 || ek > 60 || ev < -60 || ev > 60) return WC_E_ARG;
+    switch (C / heads) {
+        case 32: return launch_att6<32, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 64: return launch_att6<64, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 96: return launch_att6<96, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 128: return launch_att6<128, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 160: return launch_att6<160, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 192: return launch_att6<192, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        default: return WC_E_SHAPE;
+    }
 }
 
 }  // namespace
 
 extern "C" int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N,
                                    int C, int heads, float scale, void* stream) {
-    if (!qkv || !out) return WC_E_ARG;
-    if (heads <= 0 || C % heads != 0 || ld_qkv % 4 != 0 || ld_out % 4 != 0) return WC_E_SHAPE;
-    if (ld_qkv < 3 * C || ld_out < C || N <= 0 || B <= 0) return WC_E_SHAPE;
-    if ((reinterpret_cast<uintptr_t>(qkv) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return WC_E_SHAPE;
-    if ((long)N * ld_qkv * 4 >= (1L << 31)) return WC_E_SHAPE;  // per-image SRD range
-    const int D = C / heads;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    switch (D) {
-        case 32: return launch_att6<32>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 64: return launch_att6<64>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 96: return launch_att6<96>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 128: return launch_att6<128>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 160: return launch_att6<160>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 192: return launch_att6<192>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        default: return WC_E_SHAPE;
-    }
+    return dispatch_att6<false>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, 0, 0, 0,
+                                reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int wc_attention_fwd_f16x3(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N,
+                                      int C, int heads, float scale, int q_exp, int k_exp, int v_exp,
+                                      void* stream) {
+    return dispatch_att6<true>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, q_exp, k_exp, v_exp,
+                               reinterpret_cast<hipStream_t>(stream));
 }

@@ -77,4 +77,16 @@ WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
     pl = u32x2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
 }
 
+// Per-element form of split2_f16: the fp16 bit patterns (low 16 bits) of h and l for 4 floats.
+WC_DEVICE void split2_f16_elems(f32x4 v, unsigned (&h)[4], unsigned (&l)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e];
+        const _Float16 hh = (_Float16)x;
+        const _Float16 ll = (_Float16)(x - (float)hh);
+        h[e] = __builtin_bit_cast(unsigned short, hh);
+        l[e] = __builtin_bit_cast(unsigned short, ll);
+    }
+}
+
 }  // namespace wcx6

@@ -90,6 +90,9 @@ class AttnPack:
     b_out: torch.Tensor
     w_in_x6: Optional[K.X6Weight] = None
     w_out_x6: Optional[K.X6Weight] = None
+    qkv_l1: Optional[torch.Tensor] = None  # f16x3: host row-L1 norms of W_in and |b_in| (bounds)
+    qkv_babs: Optional[torch.Tensor] = None
+    gb: Tuple[float, float] = (0.0, 0.0)
 
 
 class UnetEngine:
@@ -189,6 +192,10 @@ class UnetEngine:
                      b_out=mha.out_proj.bias.detach().float().contiguous())
         p.w_in_x6 = self._x6(p.w_in, c, 1)
         p.w_out_x6 = self._x6(p.w_out, c, 1)
+        if self.precision == 'f16x3':
+            p.qkv_l1 = p.w_in.double().abs().sum(1).cpu()
+            p.qkv_babs = p.b_in.double().abs().cpu()
+            p.gb = (float(p.g.abs().max()), float(p.be.abs().max()))
         return p
 
     def _pack_stage(self, blk, n_res: int, attn: bool):
@@ -240,8 +247,10 @@ class UnetEngine:
         qkv = self._new(B, H, W, 3 * C)
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         o = self._new(B, H, W, C)
-        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads,
-                    'fp32' if self.precision == 'fp32' else 'bf16x6')
+        exps = None
+        if self.precision == 'f16x3':
+            exps = K.attention_exps_from_norms(p.qkv_l1, p.qkv_babs, p.gb[0], p.gb[1], N * C // 8)
+        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision, exps)
         self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y)
 
     # ------------------------------------------------------------------ forward

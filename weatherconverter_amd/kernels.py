@@ -374,17 +374,53 @@ def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tenso
     return scale, shift
 
 
-def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int, precision: str = 'fp32'):
-    """softmax(Q K^T / sqrt(d)) V per (batch, head) over qkv rows [q | k | v]; 'bf16x6' runs the
-    split-precision kernel when the head dim is a multiple of 32 (else the fp32-MFMA kernel)."""
+def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int, precision: str = 'fp32',
+              exps: Optional[Tuple[int, int, int]] = None):
+    """softmax(Q K^T / sqrt(d)) V per (batch, head) over qkv rows [q | k | v].  'bf16x6' / 'f16x3'
+    run the split-precision kernel when the head dim is a multiple of 32 (else the fp32-MFMA
+    kernel); 'f16x3' needs exps = (q, k, v) power-of-two exponents from attention_f16x3_exps."""
     _req(qkv.shape == (B * N, 3 * C) and qkv.is_contiguous(), 'qkv shape')
     _req(out.shape == (B * N, C) and out.is_contiguous(), 'attention output shape')
     _req(precision in CONV_PRECISIONS, f'attention precision {precision!r}')
     d = C // heads
-    x6 = precision == 'bf16x6' and d % 32 == 0
-    _timed(f'attention_x6_kernel<{d}>' if x6 else f'attention_kernel<{d}>',
-           'wc_attention_fwd_x6' if x6 else 'wc_attention_fwd', 4.0 * B * N * N * C,
-           qkv.data_ptr(), 3 * C, out.data_ptr(), C, B, N, C, heads, float(d)**-0.5, _stream())
+    split = precision != 'fp32' and d % 32 == 0
+    flops = 4.0 * B * N * N * C
+    args = (qkv.data_ptr(), 3 * C, out.data_ptr(), C, B, N, C, heads, float(d)**-0.5)
+    if split and precision == 'f16x3':
+        _req(exps is not None, 'f16x3 attention needs (q, k, v) exponents')
+        _timed(f'attention_x6_kernel<{d}, true>', 'wc_attention_fwd_f16x3', flops, *args, *[int(e) for e in exps],
+               _stream())
+    elif split:
+        _timed(f'attention_x6_kernel<{d}, false>', 'wc_attention_fwd_x6', flops, *args, _stream())
+    else:
+        _timed(f'attention_kernel<{d}>', 'wc_attention_fwd', flops, *args, _stream())
+
+
+def attention_f16x3_exps(w_in: torch.Tensor, b_in: torch.Tensor, gamma_absmax: float, beta_absmax: float,
+                         n_group: int) -> Tuple[int, int, int]:
+    """Exponents (q, k, v) for wc_attention_fwd_f16x3 when qkv = GN(Y) W_in^T + b_in (see
+    attention_exps_from_norms)."""
+    l1 = w_in.detach().double().abs().sum(1).cpu()
+    babs = b_in.detach().double().abs().cpu()
+    return attention_exps_from_norms(l1, babs, gamma_absmax, beta_absmax, n_group)
+
+
+def attention_exps_from_norms(l1: torch.Tensor, babs: torch.Tensor, gamma_absmax: float, beta_absmax: float,
+                              n_group: int) -> Tuple[int, int, int]:
+    """The GroupNorm output is bounded by sqrt(n - 1) max|gamma| + max|beta| (Samuelson), so row i of
+    the projection by l1[i] times that plus babs[i] (l1 = row L1 norms of W_in, babs = |b_in|, host
+    tensors); each exponent puts the max bound of its q / k / v block at <= 2^14."""
+    import math
+    C = l1.shape[0] // 3
+    bound_y = math.sqrt(max(n_group - 1, 1)) * gamma_absmax + beta_absmax
+    exps = []
+    for part in range(3):
+        sl = slice(part * C, (part + 1) * C)
+        bound = float((l1[sl] * bound_y + babs[sl]).max())
+        if not math.isfinite(bound):
+            raise RuntimeError('weatherconverter_amd: non-finite attention projection bound')
+        exps.append(0 if bound <= 0 else max(-60, min(60, math.floor(math.log2(2.0**14 / bound)))))
+    return tuple(exps)
 
 
 def temb(t: torch.Tensor, w1, b1, w2, b2, proj_w, proj_b) -> torch.Tensor:

@@ -123,6 +123,13 @@ int wc_conv3x3_x6_tile_n(int N);
  * Replaces the same reference layers as wc_conv_igemm (unet_base.py:115,129,159,334 and the
  * old UNet's Linear layers, old_modules.py:87-95). */
 int wc_conv_igemm_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, void* stream);
+/* wc_conv_igemm_x6 with segment 0 on f16x3 (as wc_conv3x3_f16x3; no epilogue activation).  The
+ * caller guarantees |a| * 2^a_exp <= 2^14 for every segment-0 value after the prologue.  w3 layout
+ * per N tile: [ntaps*C0/16 steps][piece 2][k-half 2][BN][8] fp16 bits, then
+ * [C1/16][piece 3][k-half 2][BN][8] bf16 bits, all scaled by 2^sW[n]; w_inv_scale[n] = 2^-sW[n].
+ * Replaces the attention in/out projections (unet_base.py:115,159) and the head conv (:483-485). */
+int wc_conv_igemm_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
+                        const float* w_inv_scale, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */

@@ -465,3 +465,60 @@ def test_attention_f16x3_vs_float64(B, N, C, heads, gs):
         K.attention(qkv.reshape(B * N, 3 * C).cuda(), out, B, N, C, heads, prec, exps)
         errs[prec] = rel_l2(out.cpu().double().reshape(B, N, C), ref)
     assert errs['f16x3'] < 1e-5 and errs['f16x3'] <= 4 * errs['fp32'] + 2e-7, (errs, exps)
+
+
+def test_pack_f16x3_natural_order():
+    from weatherconverter_amd.kernels import pack_f16x3
+    g = torch.Generator().manual_seed(4)
+    N, C0, nt = 96, 32, 16
+    w = torch.randn((N, nt * C0), generator=g) * 0.05
+    w3 = pack_f16x3(w, C0, ntaps=nt, order='natural')
+    T, BN = w3.data.shape[0], w3.BN
+    S0 = nt * C0 // 16
+    hl = w3.data.view(T, S0, 2, 2, BN, 8).view(torch.float16).double().sum(2)
+    v = hl.permute(0, 3, 1, 2, 4).reshape(T * BN, S0 * 16)[:N] * w3.wsinv[:N].double()[:, None]
+    assert ((v - w.double()).abs() <= w.double().abs() * 2.0**-21 + 2.0**-40).all()
+
+
+@pytest.mark.gpu
+def test_igemm_f16x3_projections_and_head():
+    """in_proj (GN-affine prologue, Samuelson bound), out_proj-style raw input with an explicit bound
+    and residual, and the N=3 head (GN+SiLU, NCHW store) vs float64."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(51)
+    B, H, C, N = 2, 16, 128, 384
+    x = torch.randn((B, C, H, H), generator=g) * 2 + 1
+    gamma = 1 + 0.3 * torch.randn(C, generator=g)
+    beta = 0.3 * torch.randn(C, generator=g)
+    sc, sh = _gn_affine(x, gamma, beta)
+    w = torch.randn((N, C), generator=g) / C**0.5
+    b = 0.1 * torch.randn(N, generator=g)
+    a = x.double() * sc[:, :, None, None] + sh[:, :, None, None]
+    ref = torch.einsum('bchw,nc->bhwn', a, w.double()) + b.double()
+    e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * H * C // 8)
+    out = torch.empty((B, H, H, N), device='cuda')
+    seg = [K.Seg(K.View.full(_nhwc(x).cuda()), [(0, 0)], scale=sc.float().cuda(), shift=sh.float().cuda())]
+    K.conv_igemm_f16x3(seg, K.pack_f16x3(w.cuda(), C, ntaps=1, order='natural'), b.cuda(), K.View.full(out),
+                       Hm=H, Wm=H, a_exp=e)
+    assert rel_l2(out.cpu().double(), ref) < 2e-6
+
+    # raw input bounded by 7 (as |O| <= max|V|) + residual view
+    o = (torch.rand((B, H, H, C), generator=g) * 14 - 7)
+    res = torch.randn((B, H, H, C), generator=g)
+    w2 = torch.randn((C, C), generator=g) / C**0.5
+    ref2 = o.double() @ w2.double().t() + res.double()
+    out2 = torch.empty((B, H, H, C), device='cuda')
+    K.conv_igemm_f16x3([K.Seg(K.View.full(o.cuda()), [(0, 0)])], K.pack_f16x3(w2.cuda(), C, ntaps=1, order='natural'),
+                       None, K.View.full(out2), Hm=H, Wm=H, a_exp=K.f16x3_a_exp(0.0, 7.0, 2),
+                       res=K.View.full(res.cuda()))
+    assert rel_l2(out2.cpu().double(), ref2) < 2e-6
+
+    # head: GN + SiLU, 3 outputs, NCHW
+    wh = torch.randn((3, C, 3, 3), generator=g) / (9 * C)**0.5
+    bh = 0.1 * torch.randn(3, generator=g)
+    ref3 = F.conv2d(F.silu(a), wh.double(), bh.double(), padding=1)
+    out3 = torch.empty((B, 3, H, H), device='cuda')
+    seg3 = [K.Seg(K.View.full(_nhwc(x).cuda()), TAPS3, scale=sc.float().cuda(), shift=sh.float().cuda(), silu=True)]
+    K.conv_igemm_f16x3(seg3, K.pack_f16x3(_pack(wh).cuda(), C, order='natural'), bh.cuda(), None, Hm=H, Wm=H,
+                       a_exp=e, out_nchw=out3)
+    assert rel_l2(out3.cpu().double(), ref3) < 2e-6

@@ -48,9 +48,13 @@ struct IgDev {
     int ident;
     int steps0, steps;
     int ntiles_n;
+    float ascale;        // f16x3: 2^a_exp applied to the A values before splitting (else 1)
+    float ainv;          // 2^-a_exp
+    const float* wsinv;  // f16x3: 2^-sW[n] (else NULL)
 };
 
-template <int BM, int BN>
+// F3: segment 0 in f16x3 (2 fp16 pieces), else bf16x6; segment 1 is always bf16x6.
+template <int BM, int BN, bool F3>
 struct IgTile {
     static constexpr int WAVES_M = BM / 64;
     static constexpr int WAVES_N = BN / 64;
@@ -61,15 +65,17 @@ struct IgTile {
     static constexpr int ASTAGE = 6 * APLANE;
     static constexpr int BSTAGE = 6 * BPLANE;
     static constexpr int STAGE = ASTAGE + BSTAGE;
-    static constexpr int B_ITEMS = BSTAGE / 16;
-    static constexpr int B_PER_T = (B_ITEMS + NT - 1) / NT;
+    static constexpr int BSTEP0 = (F3 ? 4 : 6) * BPLANE;  // weight bytes of a segment-0 step
+    static constexpr int BSTEP1 = 6 * BPLANE;             // ... of a segment-1 step
+    static constexpr int B_PER_T = (BSTAGE / 16 + NT - 1) / NT;
+    static constexpr int B_FULL = BSTEP0 / 16 / NT;       // items j < B_FULL valid in every step
 };
 
 // PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU.  UNIB: tiles never straddle images.  ACT: epilogue
-// activation (template, see wc_conv.hip).
-template <int BM, int BN, int PRO, bool UNIB, int ACT>
+// activation (template, see wc_conv.hip).  F3: segment 0 on f16x3 (caller bounds |a| 2^a_exp).
+template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
-    using T = IgTile<BM, BN>;
+    using T = IgTile<BM, BN, F3>;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
 
     const int tid = threadIdx.x;
@@ -127,13 +133,17 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     unsigned aval = 0;
     int ky = 0, kx = 0, c0 = 0, c1 = 0, bstep = 0;
 
+    const unsigned wtile =
+        (unsigned)tile_n * (unsigned)(p.steps0 * T::BSTEP0 + (p.steps - p.steps0) * T::BSTEP1);
     auto load_w = [&]() {
-        const unsigned base = (unsigned)((tile_n * p.steps + bstep) * T::BSTAGE);
+        const bool s1 = bstep >= p.steps0;
+        const unsigned base = wtile + (s1 ? (unsigned)(p.steps0 * T::BSTEP0 + (bstep - p.steps0) * T::BSTEP1)
+                                          : (unsigned)(bstep * T::BSTEP0));
+        const int items = (s1 ? T::BSTEP1 : T::BSTEP0) / 16;
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            const bool ok = T::B_ITEMS % NT == 0 || i < T::B_ITEMS;
-            rb[j] = bload_u4(srdw, ok ? base + (unsigned)i * 16u : OOB);
+            rb[j] = bload_u4(srdw, (j < T::B_FULL || i < items) ? base + (unsigned)i * 16u : OOB);
         }
         ++bstep;
     };
@@ -196,18 +206,27 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                 }
             }
             if (!((aval >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
-            u32x2 a0, a1, a2;
-            split3(v, a0, a1, a2);
             unsigned char* d = buf + a_wr + j * 64 * 16;
-            *reinterpret_cast<u32x2*>(d) = a0;
-            *reinterpret_cast<u32x2*>(d + 2 * T::APLANE) = a1;
-            *reinterpret_cast<u32x2*>(d + 4 * T::APLANE) = a2;
+            if constexpr (F3) v = v * p.ascale;
+            if (F3 && pro) {
+                u32x2 a0, a1;
+                split2_f16(v, a0, a1);
+                *reinterpret_cast<u32x2*>(d) = a0;
+                *reinterpret_cast<u32x2*>(d + 2 * T::APLANE) = a1;
+            } else {
+                u32x2 a0, a1, a2;
+                split3(v, a0, a1, a2);
+                *reinterpret_cast<u32x2*>(d) = a0;
+                *reinterpret_cast<u32x2*>(d + 2 * T::APLANE) = a1;
+                *reinterpret_cast<u32x2*>(d + 4 * T::APLANE) = a2;
+            }
         }
         unsigned char* bb = buf + T::ASTAGE;
+        const int items = ((bstep - 1 >= p.steps0) ? T::BSTEP1 : T::BSTEP0) / 16;  // the step just loaded
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            if (T::B_ITEMS % NT == 0 || i < T::B_ITEMS) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[j];
+            if (j < T::B_FULL || i < items) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[j];
         }
     };
 
@@ -224,7 +243,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     const int a_rd = half * T::APLANE + (wm * 64 + l32) * 16;
     const int b_rd = T::ASTAGE + half * T::BPLANE + (wn * 64 + l32) * 16;
 
-    auto compute = [&](const unsigned char* buf) {
+    auto compute6 = [&](const unsigned char* buf) {
         u32x4 fa[2][3], fb[2][3];
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc) {
@@ -255,6 +274,34 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                 acc[mb][nb] = mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
             }
     };
+    auto compute3 = [&](const unsigned char* buf) {
+        u32x4 fa[2][2], fb[2][2];
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+                fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * T::APLANE);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * T::BPLANE);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+            }
+    };
+    // the data of K-step `step` is segment 0 iff step < steps0
+    auto compute = [&](const unsigned char* buf, bool seg0) {
+        if (F3 && seg0) compute3(buf);
+        else compute6(buf);
+    };
 
     // ---- K loop: one barrier per step ----
     if (p.steps0 > 0) { load0(); store(smem, true); } else { load1(); store(smem, false); }
@@ -264,7 +311,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
         unsigned char* cur = smem + (step & 1) * T::STAGE;
         unsigned char* nxt = smem + ((step & 1) ^ 1) * T::STAGE;
         load0();
-        compute(cur);
+        compute(cur, true);
         store(nxt, true);
         __syncthreads();
     }
@@ -272,11 +319,11 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
         unsigned char* cur = smem + (step & 1) * T::STAGE;
         unsigned char* nxt = smem + ((step & 1) ^ 1) * T::STAGE;
         load1();
-        compute(cur);
+        compute(cur, step < p.steps0);
         store(nxt, false);
         __syncthreads();
     }
-    compute(smem + (step & 1) * T::STAGE);
+    compute(smem + (step & 1) * T::STAGE, step < p.steps0);
 
     // ---- epilogue (as wc_conv.hip) ----
     const int HWo = p.Ho * p.Wo;
@@ -290,13 +337,14 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
             const int n = n0 + wn * 64 + nb * 32 + l32;
             if (n >= p.N) continue;
             const float bn = p.bias ? p.bias[n] : 0.f;
+            const float mul = F3 ? p.wsinv[n] * p.ainv : 1.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
                 const int m = mbase + row;
                 if (m >= p.M) continue;
                 int b = (HWm >= 32) ? b0 + (m >= bnd ? 1 : 0) : m / HWm;
-                float v = acc[mb][nb][r] + bn;
+                float v = (F3 ? acc[mb][nb][r] * mul : acc[mb][nb][r]) + bn;
                 if (p.temb) v += p.temb[b * p.temb_ld + n];
                 if constexpr (ACT == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
                 else if constexpr (ACT == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
@@ -321,20 +369,31 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     }
 }
 
-template <int BM, int BN, int PRO, bool UNIB, int ACT = WC_ACT_NONE>
+template <int BM, int BN, int PRO, bool UNIB, int ACT = WC_ACT_NONE, bool F3 = false>
 int launch(const IgDev& d, hipStream_t stream) {
     IgDev p = d;
     const int tiles_m = (p.M + BM - 1) / BM;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(tiles_m * p.ntiles_n);
-    hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT>), grid, dim3(NT), 0, stream, p);
+    hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3>), grid, dim3(NT), 0, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 template <int BM, int BN>
-int dispatch(const IgDev& d, int pro, int act, hipStream_t s) {
+int dispatch(const IgDev& d, int pro, int act, bool f3, hipStream_t s) {
     const bool unib = (d.Hm * d.Wm) % BM == 0;
+    if (f3) {  // f16x3: no epilogue activation instantiated
+        if (act != WC_ACT_NONE) return WC_E_ARG;
+        switch (pro * 2 + (unib ? 1 : 0)) {
+            case 0: return launch<BM, BN, 0, false, WC_ACT_NONE, true>(d, s);
+            case 1: return launch<BM, BN, 0, true, WC_ACT_NONE, true>(d, s);
+            case 2: return launch<BM, BN, 1, false, WC_ACT_NONE, true>(d, s);
+            case 3: return launch<BM, BN, 1, true, WC_ACT_NONE, true>(d, s);
+            case 4: return launch<BM, BN, 2, false, WC_ACT_NONE, true>(d, s);
+            default: return launch<BM, BN, 2, true, WC_ACT_NONE, true>(d, s);
+        }
+    }
     if (act != WC_ACT_NONE) {  // activations are instantiated for a raw segment 0 only
         if (pro != 0) return WC_E_ARG;
         if (act == WC_ACT_GELU)
@@ -353,7 +412,10 @@ int dispatch(const IgDev& d, int pro, int act, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
+namespace {
+
+// Shared host validation (wc_conv_igemm's contract with C % 16); fills d.
+int prepare(const wc_conv_args* a, const void* w6, IgDev& d, long& k) {
     if (!a || !w6 || !a->out) return WC_E_ARG;
     if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
     if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
@@ -371,11 +433,11 @@ extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w
     const int tdy = kh > 1 ? s0.dy[kw] - s0.dy[0] : 0;
     for (int t = 0; t < s0.ntaps; ++t)
         if (s0.dy[t] != s0.dy[0] + (t / kw) * tdy || s0.dx[t] != s0.dx[0] + (t % kw) * tdx) return WC_E_SHAPE;
-    IgDev d{};
+    d = IgDev{};
     d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.H0 = s0.H; d.W0 = s0.W; d.sy = s0.sy; d.sx = s0.sx;
     d.kh = kh; d.kw = kw; d.ty0 = s0.dy[0]; d.tdy = tdy; d.tx0 = s0.dx[0]; d.tdx = tdx;
     d.scale = s0.scale; d.shift = s0.shift;
-    long k = (long)s0.ntaps * s0.C;
+    k = (long)s0.ntaps * s0.C;
     if (a->nseg == 2) {
         const wc_conv_seg& s1 = a->seg[1];
         if (!s1.src || s1.scale) return WC_E_ARG;
@@ -389,9 +451,6 @@ extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w
     }
     const long M = (long)a->B * a->Hm * a->Wm;
     if (M <= 0 || M > (1L << 30) || a->N <= 0) return WC_E_SHAPE;
-    const int BN = wc_conv3x3_x6_tile_n(a->N);
-    const long ntn = (a->N + BN - 1) / BN;
-    if (w6_bytes != ntn * (k / BK) * (long)BN * 96 || w6_bytes >= (1L << 31)) return WC_E_SHAPE;
     if (reinterpret_cast<uintptr_t>(w6) & 15) return WC_E_SHAPE;
     d.B = a->B; d.Hm = a->Hm; d.Wm = a->Wm; d.N = a->N; d.M = (int)M;
     d.w6 = w6; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
@@ -402,8 +461,42 @@ extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w
               a->Ho == a->Hm && a->Wo == a->Wm;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
     d.steps = (int)(k / BK);
-    const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
+    d.ascale = 1.f; d.ainv = 1.f; d.wsinv = nullptr;
+    return WC_OK;
+}
+
+}  // namespace
+
+extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
+    IgDev d;
+    long k;
+    const int st = prepare(a, w6, d, k);
+    if (st != WC_OK) return st;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w6_bytes != ntn * (k / BK) * (long)BN * 96 || w6_bytes >= (1L << 31)) return WC_E_SHAPE;
+    const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (BN == 64) return dispatch<256, 64>(d, pro, a->act, s);
-    return dispatch<128, 128>(d, pro, a->act, s);
+    if (BN == 64) return dispatch<256, 64>(d, pro, a->act, false, s);
+    return dispatch<128, 128>(d, pro, a->act, false, s);
+}
+
+extern "C" int wc_conv_igemm_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, int a_exp,
+                                   const float* w_inv_scale, void* stream) {
+    IgDev d;
+    long k;
+    const int st = prepare(a, w3, d, k);
+    if (st != WC_OK) return st;
+    if (!w_inv_scale || a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    const long ntn = (a->N + BN - 1) / BN;
+    const long s1 = d.steps - d.steps0;
+    if (w3_bytes != ntn * ((long)d.steps0 * BN * 64 + s1 * BN * 96) || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    d.ascale = ldexpf(1.0f, a_exp);
+    d.ainv = ldexpf(1.0f, -a_exp);
+    d.wsinv = w_inv_scale;
+    const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return dispatch<256, 64>(d, pro, a->act, true, s);
+    return dispatch<128, 128>(d, pro, a->act, true, s);
 }

@@ -90,6 +90,8 @@ class AttnPack:
     b_out: torch.Tensor
     w_in_x6: Optional[K.X6Weight] = None
     w_out_x6: Optional[K.X6Weight] = None
+    w_in_f3: Optional[K.X6Weight] = None  # f16x3 re-packs (in_proj: GN bound, out_proj: V bound)
+    w_out_f3: Optional[K.X6Weight] = None
     qkv_l1: Optional[torch.Tensor] = None  # f16x3: host row-L1 norms of W_in and |b_in| (bounds)
     qkv_babs: Optional[torch.Tensor] = None
     gb: Tuple[float, float] = (0.0, 0.0)
@@ -144,6 +146,10 @@ class UnetEngine:
             self.norm_out = (m.norm_out.weight.detach().float(), m.norm_out.bias.detach().float())
             self.conv_out_w = pack_conv(m.conv_out.weight)
             self.conv_out_x6 = self._x6(self.conv_out_w, m.conv_out.in_channels, 9)
+            self.conv_out_f3 = None
+            if self.precision == 'f16x3' and m.conv_out.in_channels % 16 == 0:
+                self.conv_out_f3 = K.pack_f16x3(self.conv_out_w, m.conv_out.in_channels, order='natural')
+                self.norm_out_gb = (float(m.norm_out.weight.abs().max()), float(m.norm_out.bias.abs().max()))
             self.conv_out_b = m.conv_out.bias.detach().float().contiguous()
             tp = m.t_proj
             self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
@@ -193,6 +199,8 @@ class UnetEngine:
         p.w_in_x6 = self._x6(p.w_in, c, 1)
         p.w_out_x6 = self._x6(p.w_out, c, 1)
         if self.precision == 'f16x3':
+            p.w_in_f3 = K.pack_f16x3(p.w_in, c, ntaps=1, order='natural')
+            p.w_out_f3 = K.pack_f16x3(p.w_out, c, ntaps=1, order='natural')
             p.qkv_l1 = p.w_in.double().abs().sum(1).cpu()
             p.qkv_babs = p.b_in.double().abs().cpu()
             p.gb = (float(p.g.abs().max()), float(p.be.abs().max()))
@@ -245,12 +253,18 @@ class UnetEngine:
         N = H * W
         sc, sh = K.gn_affine(Y, p.g, p.be)
         qkv = self._new(B, H, W, 3 * C)
-        self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         o = self._new(B, H, W, C)
-        exps = None
-        if self.precision == 'f16x3':
+        if p.w_in_f3 is not None:
+            # in_proj: GN output bound; attention: q/k/v bounds; out_proj: |O| <= max|V| (convex
+            # combination of V rows), so the V exponent bounds it
+            K.conv_igemm_f16x3([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in_f3, p.b_in, View.full(qkv),
+                               Hm=H, Wm=W, a_exp=K.f16x3_a_exp(p.gb[0], p.gb[1], N * C // 8))
             exps = K.attention_exps_from_norms(p.qkv_l1, p.qkv_babs, p.gb[0], p.gb[1], N * C // 8)
-        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision, exps)
+            K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
+            K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y)
+            return
+        self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
+        K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
         self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y)
 
     # ------------------------------------------------------------------ forward
@@ -339,6 +353,10 @@ class UnetEngine:
         # ---------------- head: GN -> SiLU -> conv_out, NCHW output
         sc, sh = K.gn_affine(cur, *self.norm_out)
         out = torch.empty((B, m.model_config.im_channels, S, S2), dtype=torch.float32, device=self.device)
-        self.conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.conv_out_w, self.conv_out_x6, self.conv_out_b,
-                  None, S, S2, out_nchw=out)
+        head = [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)]
+        if self.conv_out_f3 is not None:
+            K.conv_igemm_f16x3(head, self.conv_out_f3, self.conv_out_b, None, Hm=S, Wm=S2, out_nchw=out,
+                               a_exp=K.f16x3_a_exp(*self.norm_out_gb, S * S2 * cur.C // 8))
+        else:
+            self.conv(head, self.conv_out_w, self.conv_out_x6, self.conv_out_b, None, S, S2, out_nchw=out)
         return out

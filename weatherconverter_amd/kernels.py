@@ -252,34 +252,41 @@ def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str
     return X6Weight(data, N, BN, C0, C1, order)
 
 
-def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
-    """Re-pack a [N][9*C0 + C1] 3x3 (+ 1x1 residual) weight for wc_conv3x3_f16x3: per output
-    channel n a power-of-two scale 2^sW[n] with max_k |w[n, :9*C0]| * 2^sW[n] <= 2^14; the 3x3 part
-    as two round-to-nearest fp16 pieces in (chunk, tap) step order, the residual part as three
+def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo') -> X6Weight:
+    """Re-pack a [N][ntaps*C0 + C1] conv (+ 1x1 residual) weight for the f16x3 kernels: per output
+    channel n a power-of-two scale 2^sW[n] with max_k |w[n, :ntaps*C0]| * 2^sW[n] <= 2^14; segment 0
+    as two round-to-nearest fp16 pieces, in (chunk, tap) step order for wc_conv3x3_f16x3 ('halo',
+    ntaps 9) or natural K order for wc_conv_igemm_f16x3 ('natural'); the residual part as three
     bf16 pieces (same scale)."""
     N, K = w.shape
-    _req(K == 9 * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'f16x3 weight shape')
+    _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'f16x3 weight shape')
+    _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
     _, BN = x6_tile(N)
     Np = -(-N // BN) * BN
     T = Np // BN
     wp = torch.zeros((Np, K), dtype=torch.float32, device=w.device)
     wp[:N] = w.float()
-    amax = wp[:, :9 * C0].abs().amax(1).double()
+    K0 = ntaps * C0
+    amax = wp[:, :K0].abs().amax(1).double()
     sw = torch.where(amax > 0, torch.floor(torch.log2(2.0**14 / amax.clamp_min(1e-300))), torch.zeros_like(amax))
     sw = sw.clamp(-60, 60).to(torch.int32)
     ws = wp * torch.ldexp(torch.ones_like(wp[:, :1]), sw[:, None].float())  # exact power-of-two scaling
-    S0, S1 = 9 * (C0 // 16), C1 // 16
-    main = ws[:, :9 * C0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, S0, 2, 8)
+    S0, S1 = K0 // 16, C1 // 16
+    if order == 'halo':
+        main = ws[:, :K0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, S0, 2, 8)
+    else:
+        _req(order == 'natural', f'unknown f16x3 order {order!r}')
+        main = ws[:, :K0].reshape(Np, S0, 2, 8)
     h = main.half()
     lo = (main - h.float()).half()
     pm = torch.stack([h, lo]).view(torch.int16).view(2, T, BN, S0, 2, 8).permute(1, 3, 0, 4, 2, 5)
     parts = [pm.reshape(T, -1)]
     if C1:
-        pr = split3_bits(ws[:, 9 * C0:].reshape(Np, S1, 2, 8)).view(3, T, BN, S1, 2, 8).permute(1, 3, 0, 4, 2, 5)
+        pr = split3_bits(ws[:, K0:].reshape(Np, S1, 2, 8)).view(3, T, BN, S1, 2, 8).permute(1, 3, 0, 4, 2, 5)
         parts.append(pr.reshape(T, -1))
     data = torch.cat(parts, 1).contiguous()
     wsinv = torch.ldexp(torch.ones(Np, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
-    return X6Weight(data, N, BN, C0, C1, 'f16x3', wsinv)
+    return X6Weight(data, N, BN, C0, C1, 'f16x3' if order == 'halo' else 'f16x3n', wsinv)
 
 
 def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
@@ -307,6 +314,24 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
     pro = 2 if segs[0].silu else 1
     res_seg = 'true' if len(segs) == 2 else 'false'
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, true>', 'wc_conv3x3_f16x3',
+           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
+
+
+def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,
+                     Hm: int, Wm: int, a_exp: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0,
+                     res: Optional[View] = None, out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None):
+    """conv_igemm's contract with segment 0 on f16x3; the caller guarantees |a| * 2^a_exp <= 2^14 for
+    every segment-0 value after the prologue (a GroupNorm bound, f16x3_a_exp, or a bound the
+    producer implies, e.g. an attention output by its V bound)."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3n', 'f16x3 weight (natural order)')
+    _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
+    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, 0)
+    bm, bn = (256, 64) if w3.N <= 64 else (128, 128)
+    s0 = segs[0]
+    pro = 0 if s0.scale is None else (2 if s0.silu else 1)
+    unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
+    _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, 0, true>', 'wc_conv_igemm_f16x3',
            _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
 
@@ -352,7 +377,7 @@ def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
-    _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, {act}>', 'wc_conv_igemm_x6',
+    _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, {act}, false>', 'wc_conv_igemm_x6',
            _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 

@@ -61,8 +61,13 @@ def parse():
 
 def roofline_leg(model, x, t_dev):
     from weatherconverter_amd import kernels
+    with torch.no_grad():
+        model(x, t_dev)  # packs / allocations outside the measured forward
     torch.cuda.synchronize()
     prof = kernels.profile_conv(True)
+    # Park the GPU first so the host enqueues the whole forward ahead of it: the kernels then run
+    # back to back and each event pair brackets one kernel, not a host launch gap.
+    torch.cuda._sleep(1 << 28)
     with torch.no_grad():
         model(x, t_dev)
     torch.cuda.synchronize()

@@ -82,7 +82,8 @@ _lib = None
 
 
 def lib_path() -> str:
-    return _build.LIB_PATH
+    """The in-tree library; WC_KERNEL_LIB points at another build (developer experiments only)."""
+    return os.environ.get('WC_KERNEL_LIB', _build.LIB_PATH)
 
 
 def load(build_if_missing: bool = True):

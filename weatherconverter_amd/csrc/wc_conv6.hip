@@ -26,11 +26,11 @@
 //     zero-padded, split into its pieces and written to LDS.  All 9 taps then read their A
 //     fragments from that one halo image at a constant per-tap offset, so the prologue VALU is
 //     paid (TH+2)*18/(TH*16) times per input element instead of 9 times.  The halo loads are
-//     issued at tap 7 and consumed at tap 8 (see the K loop for why not earlier).
-//   * A K-step is one (chunk, tap): the tap's 16 x BN weight pieces (pre-split and pre-laid-out
-//     by the host in the exact LDS order) are staged through registers one step ahead; one
-//     barrier per step.  The next chunk's halo is written at the chunk's last tap, into the
-//     other halo buffer.
+//     issued one K-step before the chunk's last and consumed in it (see the K loop for why).
+//   * A K-step is one tap of a chunk (bf16x6) or two (f16x3, 24 MFMAs per wave either way): the
+//     taps' 16 x BN weight pieces (pre-split and pre-laid-out by the host in the exact LDS order)
+//     are staged through registers one step ahead; one barrier per step.  The next chunk's halo
+//     is written at the chunk's last K-step, into the other halo buffer.
 //   * The fused 1x1 residual_input_conv (raw input, same pixel) runs as extra chunks with one
 //     tap (the halo centre).
 // LDS images.  Halo: [piece][k-half 2][pixel (TH+2)*18][8 x 16-bit]; weights: [piece][k-half]
@@ -89,12 +89,17 @@ struct X6Tile {
     static constexpr int BPLANE = BN * 16;               // bytes of one (piece, k-half) weight plane
     static constexpr int BSTEP0 = 2 * NP0 * BPLANE;      // one segment-0 weight step
     static constexpr int BSTEP1 = 6 * BPLANE;            // one segment-1 weight step
-    static constexpr int BSTAGE = RES ? BSTEP1 : BSTEP0;  // LDS weight buffer
+    // taps per K-step (2 for f16x3 measured slower: 302 vs 322 TF/s, larger LDS weight stage)
+    static constexpr int TPS = 1;
+    static constexpr int NMT = (9 + TPS - 1) / TPS;       // K-steps per 16-channel chunk
+    static constexpr int BSTEPM = TPS * BSTEP0;           // weight bytes of a full segment-0 K-step
+    static constexpr int BSTAGE = (RES && BSTEP1 > BSTEPM) ? BSTEP1 : BSTEPM;  // LDS weight buffer
     static constexpr int LDS = 2 * HSTAGE + 2 * BSTAGE;
     static constexpr int H_ITEMS = HPIX * 4;             // float4 items of one halo chunk
     static constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
     static constexpr int B_PER_T = (BSTAGE / 16 + NT - 1) / NT;
-    // weight items j < B_FULL of every thread are valid in every step (both segments)
+    // weight items j < B_FULL of every thread are valid in every step (both segments; the last
+    // K-step of a chunk may carry a single tap)
     static constexpr int B_FULL = (RES ? (BSTEP0 < BSTEP1 ? BSTEP0 : BSTEP1) : BSTEP0) / 16 / NT;
 };
 
@@ -132,9 +137,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     const int tyi = tt % p.tiles_y;
     const int b = tt / p.tiles_y;
     const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
-    const int S0 = 9 * p.nck0;
+    const int S0 = T::NMT * p.nck0;  // segment-0 K-steps
     const int S = S0 + (RES ? p.nck1 : 0);
-    const unsigned wtile = (unsigned)tile_n * (unsigned)(S0 * T::BSTEP0 + (RES ? p.nck1 : 0) * T::BSTEP1);
+    const unsigned seg0_bytes = (unsigned)(9 * p.nck0 * T::BSTEP0);
+    const unsigned wtile = (unsigned)tile_n * (seg0_bytes + (unsigned)((RES ? p.nck1 : 0) * T::BSTEP1));
 
     // ---- halo staging coordinates: item i = tid + NT*j is halo pixel i>>2, channels 4*(i&3).. ----
     const int q = tid & 3;
@@ -215,11 +221,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
         }
     };
     // weight step s (segment-0 steps are BSTEP0 bytes, segment-1 steps BSTEP1)
+    // K-step s -> (byte offset of its weights, 16-byte items): segment-0 step s is taps
+    // TPS*(s % NMT) .. of chunk s / NMT (the host packs taps of a chunk contiguously)
+    auto step_w = [&](int s, unsigned& off, int& items) {
+        if (RES && s >= S0) {
+            off = wtile + seg0_bytes + (unsigned)((s - S0) * T::BSTEP1);
+            items = T::BSTEP1 / 16;
+        } else {
+            const int c = s / T::NMT, t0 = (s - c * T::NMT) * T::TPS;
+            const int nt = 9 - t0 < T::TPS ? 9 - t0 : T::TPS;
+            off = wtile + (unsigned)((c * 9 + t0) * T::BSTEP0);
+            items = nt * T::BSTEP0 / 16;
+        }
+    };
     auto load_b = [&](int s) {
-        const bool s1 = RES && s >= S0;
-        const unsigned base = wtile + (s1 ? (unsigned)(S0 * T::BSTEP0 + (s - S0) * T::BSTEP1)
-                                          : (unsigned)(s * T::BSTEP0));
-        const int items = s1 ? T::BSTEP1 / 16 : T::BSTEP0 / 16;
+        unsigned base;
+        int items;
+        step_w(s, base, items);
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
@@ -229,7 +247,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     };
     auto write_b = [&](int bs, int s) {
         unsigned char* base = smem + 2 * T::HSTAGE + bs * T::BSTAGE;
-        const int items = (RES && s >= S0) ? T::BSTEP1 / 16 : T::BSTEP0 / 16;
+        unsigned off_unused;
+        int items;
+        step_w(s, off_unused, items);
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
@@ -290,9 +310,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             }
     };
     // f16x3 step (segment 0 with F3)
-    auto compute3 = [&](int hs, int toff, int bs) {
+    auto compute3 = [&](int hs, int toff, int bs, int tt) {
         const unsigned char* ha = smem + hs * T::HSTAGE + toff * 16;
-        const unsigned char* hb = smem + bs * T::BSTAGE;
+        const unsigned char* hb = smem + bs * T::BSTAGE + tt * T::BSTEP0;
         u32x4 fa[2][2], fb[2][2];
 #pragma unroll
         for (int pc = 0; pc < 2; ++pc) {
@@ -315,8 +335,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 acc[mb][nb] = mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
             }
     };
-    auto compute0 = [&](int hs, int toff, int bs) {
-        if constexpr (F3) compute3(hs, toff, bs);
+    auto compute0 = [&](int hs, int toff, int bs, int tt) {
+        if constexpr (F3) compute3(hs, toff, bs, tt);
         else compute6(hs, toff, bs);
     };
 
@@ -330,19 +350,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     for (int c = 0; c < p.nck0; ++c) {
         const int hs = c & 1;
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) {
+        for (int mt = 0; mt < T::NMT; ++mt) {
             const bool more = s + 1 < S;
             if (more) load_b(s + 1);
-            // The next chunk's halo loads go out at tap 7, after that step's weight loads: vmcnt
-            // drains in issue order, so a halo load issued earlier would be waited for by every
-            // later step's weight-tile wait (an HBM-latency stall per chunk).
-            if (tp == 7) {
+            // The next chunk's halo loads go out one K-step before the last, after that step's
+            // weight loads: vmcnt drains in issue order, so a halo load issued earlier would be
+            // waited for by every later step's weight-tile wait (an HBM-latency stall per chunk).
+            if (mt == T::NMT - 2) {
                 if (c + 1 < p.nck0) load_halo0(c + 1);
                 else if (RES) load_halo1(0);
             }
-            compute0(hs, (tp / 3) * HWD + tp % 3, s & 1);
+#pragma unroll
+            for (int tt = 0; tt < T::TPS; ++tt) {
+                const int tp = mt * T::TPS + tt;
+                if (tp < 9) compute0(hs, (tp / 3) * HWD + tp % 3, s & 1, tt);
+            }
             if (more) write_b((s + 1) & 1, s + 1);
-            if (tp == 8) {
+            if (mt == T::NMT - 1) {
                 if (c + 1 < p.nck0) write_halo(hs ^ 1, true);
                 else if (RES) write_halo(hs ^ 1, false);
             }

@@ -82,7 +82,8 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps
 def attn_case(B, N, C, prec='fp32'):
     qkv = torch.randn((B * N, 3 * C), device='cuda')
     o = torch.empty((B * N, C), device='cuda')
-    t = timeit(lambda: K.attention(qkv, o, B, N, C, 4, prec))
+    exps = (10, 10, 10) if prec == 'f16x3' else None  # |randn| * 2^10 stays far inside fp16
+    t = timeit(lambda: K.attention(qkv, o, B, N, C, 4, prec, exps))
     fl = 4.0 * B * N * N * C
     return t, fl / t / 1e12
 
@@ -118,7 +119,7 @@ def main():
         print(f'{mode} conv aggregate {tot_f / tot_t:.1f} TF/s')
     if a.only >= 0:
         return
-    for prec in ('fp32', 'bf16x6'):
+    for prec in ('fp32', 'bf16x6', 'f16x3'):
         for c in [(16, 4096, 512), (16, 1024, 768), (16, 1024, 512), (16, 4096, 128), (16, 1024, 256)]:
             t, tf = attn_case(*c, prec=prec)
             print(f'attn {prec:6s} B={c[0]} N={c[1]} C={c[2]}: {t*1e3:8.3f} ms  {tf:6.1f} TF/s', flush=True)

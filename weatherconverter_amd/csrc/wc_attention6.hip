@@ -105,8 +105,10 @@ WC_DEVICE void mfma_split(f32x16& acc, const u32x4 (&a)[F3 ? 2 : 3], const u32x4
 
 // qs, ks, vs: scales applied to Q, K, V before splitting (1 for bf16x6); score_mul multiplies the
 // raw S^T accumulator into the exp2 domain; out_mul multiplies O / l at the end.
+// f16x3 up to D = 128 fits 256 registers (two waves per SIMD: one wave's softmax / staging VALU
+// runs under the other's MFMAs); the larger forms keep Q and O in 512 registers at one wave.
 template <int D, bool F3>
-__global__ __launch_bounds__(NT, 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
+__global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
                                                              float* __restrict__ out, int ldo, int N,
                                                              int C, float score_mul, float qs, float ks,
                                                              float vs, float ps, float out_mul) {

@@ -103,15 +103,18 @@ int wc_conv_igemm(const wc_conv_args* args, void* stream);
  * steps = 9*(C0/16) (channel-chunk major, tap minor) + C1/16, w6_bytes its size in bytes.
  * Replaces the same reference layers as wc_conv_igemm's 3x3 case (unet_base.py:92,106). */
 int wc_conv3x3_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, void* stream);
-/* The same conv with segment 0 on f16x3 (two round-to-nearest fp16 pieces of a*2^a_exp and of
- * w*2^sW[n], three f16 MFMAs per block; segment 1 stays bf16x6 at the same scales).  Requires
- * the GN prologue on segment 0: the caller picks a_exp with
- * (sqrt(n_group - 1) * max|gamma| + max|beta|) * 2^a_exp <= 2^14, which bounds every scaled A
- * value below the fp16 range (Samuelson's inequality on the normalized group).
+/* The same conv with segment 0 on f16x3 (two round-to-nearest fp16 pieces of a*2^s and of
+ * w*2^sW[n], three f16 MFMAs per block).  Requires the GN prologue on segment 0: the caller picks
+ * a_exp with (sqrt(n_group - 1) * max|gamma| + max|beta|) * 2^a_exp <= 2^14, which bounds every
+ * scaled A value below the fp16 range (Samuelson's inequality on the normalized group).
+ * a_bound (optional, per image, e.g. wc_gn_finalize_bound of segment 1's input): image b uses
+ * s = min(a_exp, 13 - floor(log2 a_bound[b])), which also bounds segment 1's raw values, and
+ * segment 1 runs on f16x3 as well; without it s = a_exp and segment 1 stays bf16x6.
  * w3 layout per N tile: [9*C0/16 steps][piece 2][k-half 2][BN][8] fp16 bits (scaled by 2^sW[n]),
- * then [C1/16 steps][piece 3][k-half 2][BN][8] bf16 bits (same scale); w_inv_scale[n] = 2^-sW[n]. */
+ * then [C1/16 steps][piece 2 (fp16, a_bound given) or 3 (bf16)][k-half 2][BN][8] (same scale);
+ * w_inv_scale[n] = 2^-sW[n]. */
 int wc_conv3x3_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
-                     const float* w_inv_scale, void* stream);
+                     const float* w_inv_scale, const float* a_bound, void* stream);
 /* The output-channel tile (BN) wc_conv3x3_x6 and wc_conv_igemm_x6 use for N output channels. */
 int wc_conv3x3_x6_tile_n(int N);
 
@@ -143,6 +146,11 @@ int wc_gn_stats(const float* x, int B, int HW, int C, int ldc, int groups, float
 /* Combine partials → per-(b, c) affine: scale = rstd*gamma, shift = beta - mean*rstd*gamma. */
 int wc_gn_finalize(const float* partials, int B, int HW, int C, int groups, const float* gamma,
                    const float* beta, float eps, float* scale, float* shift, void* stream);
+/* The same, plus bound[b] = max over groups of |mean| + sqrt(n - 1) * std (x 1.001): every element
+ * of image b of the INPUT x is at most this in magnitude (Samuelson's inequality; n = HW*C/groups). */
+int wc_gn_finalize_bound(const float* partials, int B, int HW, int C, int groups, const float* gamma,
+                         const float* beta, float eps, float* scale, float* shift, float* bound,
+                         void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Flash attention, fp32 MFMA (replaces nn.MultiheadAttention's softmax(QK^T/sqrt(d))V,        */

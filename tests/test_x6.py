@@ -401,8 +401,27 @@ F3_CASES = [
 
 
 @pytest.mark.gpu
+def test_gn_finalize_bound_covers_every_element():
+    """wc_gn_finalize_bound: bound[b] >= max |x[b]| (Samuelson), also for a group with one extreme outlier."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(61)
+    x = torch.randn((3, 16, 16, 64), generator=g) * 4 + 2
+    x[1] = 0.5
+    x[1, 3, 5, ::8] = 3e3  # one huge value per group of image 1
+    x[2] *= 1e-3
+    _, _, bnd = K.gn_affine(K.View.full(x.cuda()), None, None, bound=True)
+    bnd = bnd.cpu()
+    amax = x.abs().amax((1, 2, 3))
+    assert bool((bnd >= amax).all()), (bnd, amax)
+    assert bool((bnd <= amax * (16 * 16 * 8)**0.5 * 1.01).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bounded', [False, True])
 @pytest.mark.parametrize('B,H,W,Ci,Co,Cr,silu,gs,outlier', F3_CASES)
-def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier):
+def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier, bounded):
+    if bounded and not Cr:
+        pytest.skip('the per-image bound only matters with a residual segment')
     from weatherconverter_amd import kernels as K
     g = torch.Generator().manual_seed(31)
     h = torch.randn((B, Ci, H, W), generator=g) * 3 + 0.7
@@ -429,11 +448,21 @@ def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier):
         wp = torch.cat([wp, wr.reshape(Co, Cr)], 1)
     wp = wp.contiguous().cuda()
     e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * W * Ci // 8)
+    xb = None
+    if bounded:  # the residual input's per-image bound from its own GroupNorm statistics
+        if outlier:
+            x2v = segs[1].view.t
+            x2v[:, 0, 0, :] = 5e3  # a large raw residual value lowers the image's scale
+            x2[:, :, 0, 0] = 5e3
+            ref = F.conv2d(a if not silu else F.silu(h.double() * sc[:, :, None, None] + sh[:, :, None, None]),
+                           w.double(), b.double(), padding=1) + F.conv2d(x2.double(), wr.double())
+        _, _, xb = K.gn_affine(segs[1].view, None, None, bound=True)
     outs = {}
     for mode in ('f16x3', 'fp32'):
         out = torch.empty((B, H, W, Co), device='cuda')
         if mode == 'f16x3':
-            K.conv3x3_f16x3(segs, K.pack_f16x3(wp, Ci, Cr), b.cuda(), K.View.full(out), Hm=H, Wm=W, a_exp=e)
+            K.conv3x3_f16x3(segs, K.pack_f16x3(wp, Ci, Cr, res_f16=bounded), b.cuda(), K.View.full(out), Hm=H, Wm=W,
+                            a_exp=e, a_bound=xb)
         else:
             K.conv_igemm(segs, wp, b.cuda(), K.View.full(out), Hm=H, Wm=W)
         torch.cuda.synchronize()

@@ -48,8 +48,9 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps
     if mode in ('x6', 'f3') and nt != 9 or mode == 'f3' and not prologue:
         return None, None, None
     if mode == 'f3':  # a_exp 4 keeps |x*sc + sh| * 16 far inside fp16 for these synthetic inputs
-        w3 = K.pack_f16x3(w, Ci, res)
-        fn = lambda: K.conv3x3_f16x3(segs, w3, b, K.View.full(out), Hm=H, Wm=H, a_exp=4)  # noqa: E731
+        w3 = K.pack_f16x3(w, Ci, res, res_f16=bool(res))
+        xb = torch.full((B, ), 8.0, device='cuda') if res else None  # |randn| residual input < 8
+        fn = lambda: K.conv3x3_f16x3(segs, w3, b, K.View.full(out), Hm=H, Wm=H, a_exp=4, a_bound=xb)  # noqa: E731
     elif mode == 'igx6':
         w6 = K.pack_x6(w, Ci, res, ntaps=nt, order='natural')
         fn = lambda: K.conv_igemm_x6(segs, w6, b, K.View.full(out), Hm=H, Wm=H)  # noqa: E731

@@ -18,7 +18,7 @@ EXPORTS = [
     'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
     'wc_conv_igemm_f16x3',
     'wc_gn_num_splits',
-    'wc_gn_stats', 'wc_gn_finalize', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
+    'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed', 'wc_version'
 ]
@@ -57,12 +57,13 @@ _SIGS = {
     'wc_conv_igemm': [ctypes.POINTER(ConvArgs), _P],
     'wc_conv3x3_x6': [ctypes.POINTER(ConvArgs), _P, _L, _P],
     'wc_conv3x3_x6_tile_n': [_I],
-    'wc_conv3x3_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P],
+    'wc_conv3x3_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
     'wc_conv_igemm_x6': [ctypes.POINTER(ConvArgs), _P, _L, _P],
     'wc_conv_igemm_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P],
     'wc_gn_num_splits': [_I, _I, _I],
     'wc_gn_stats': [_P, _I, _I, _I, _I, _I, _P, _P],
     'wc_gn_finalize': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P],
+    'wc_gn_finalize_bound': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P],
     'wc_attention_fwd': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_x6': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_f16x3': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],

@@ -68,27 +68,29 @@ struct X6Dev {
     int ldo;
     int act;
     int nck0, nck1;       // 16-channel chunks of segment 0 (3x3) and segment 1 (1x1 residual)
-    float ascale;         // f16x3: 2^sA applied to the A values before splitting (else 1)
-    float ainv;           // 2^-sA
+    int a_exp;            // f16x3: static exponent sA of the segment-0 bound (else 0)
+    const float* abound;  // f16x3: per-image bound of every A value (segment 1 in fp16), or NULL
     const float* wsinv;   // f16x3: 2^-sW[n] per output channel (else NULL)
     int tiles_x, tiles_y, ntiles_n;
 };
 
-// F3: segment 0 in f16x3 (2 pieces), else bf16x6 (3 pieces).  Segment 1 is always bf16x6.
-template <int TH, int BN, bool RES, bool F3>
+// F3: segment 0 in f16x3 (2 pieces), else bf16x6 (3 pieces).  R16: segment 1 in f16x3 too (needs
+// the per-image bound), else bf16x6.
+template <int TH, int BN, bool RES, bool F3, bool R16>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
     static constexpr int WAVES_M = 4 / WAVES_N;
     static_assert(WAVES_M * 64 == BM, "each wave owns 4 image rows x 16 columns");
     static constexpr int NP0 = F3 ? 2 : 3;              // pieces of segment 0
-    static constexpr int NPH = RES ? 3 : NP0;           // halo planes per k-half
+    static constexpr int NP1 = R16 ? 2 : 3;             // pieces of segment 1
+    static constexpr int NPH = RES && NP1 > NP0 ? NP1 : NP0;  // halo planes per k-half
     static constexpr int HPIX = (TH + 2) * HWD;          // halo pixels
     static constexpr int HPLANE = HPIX * 16;             // bytes of one (piece, k-half) halo plane
     static constexpr int HSTAGE = 2 * NPH * HPLANE;      // one halo buffer
     static constexpr int BPLANE = BN * 16;               // bytes of one (piece, k-half) weight plane
     static constexpr int BSTEP0 = 2 * NP0 * BPLANE;      // one segment-0 weight step
-    static constexpr int BSTEP1 = 6 * BPLANE;            // one segment-1 weight step
+    static constexpr int BSTEP1 = 2 * NP1 * BPLANE;      // one segment-1 weight step
     // taps per K-step (2 for f16x3 measured slower: 302 vs 322 TF/s, larger LDS weight stage)
     static constexpr int TPS = 1;
     static constexpr int NMT = (9 + TPS - 1) / TPS;       // K-steps per 16-channel chunk
@@ -111,9 +113,9 @@ WC_DEVICE int row_dx(int r) {
 }
 
 // PRO: 0 = raw segment 0, 1 = GN affine, 2 = GN affine + SiLU.  RES: segment 1 present.
-template <int TH, int BN, int PRO, bool RES, bool F3>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16>
 __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
-    using T = X6Tile<TH, BN, RES, F3>;
+    using T = X6Tile<TH, BN, RES, F3, R16>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -137,6 +139,16 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     const int tyi = tt % p.tiles_y;
     const int b = tt / p.tiles_y;
     const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
+    // f16x3 scale of this image: the static exponent, lowered so that the per-image bound (which
+    // covers segment 1's raw input) also fits: bound * 2^s < 2^14 with s = 13 - floor(log2 bound)
+    int s_exp = p.a_exp;
+    if (F3 && p.abound) {
+        const float bnd = p.abound[b];
+        const int e = (int)((__float_as_uint(bnd) >> 23) & 0xffu) - 127;
+        if (bnd > 0.f) s_exp = min(s_exp, 13 - e);
+        s_exp = max(s_exp, -100);
+    }
+    const float ascale = ldexpf(1.0f, s_exp), ainv = ldexpf(1.0f, -s_exp);
     const int S0 = T::NMT * p.nck0;  // segment-0 K-steps
     const int S = S0 + (RES ? p.nck1 : 0);
     const unsigned seg0_bytes = (unsigned)(9 * p.nck0 * T::BSTEP0);
@@ -205,8 +217,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 }
             }
             if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
-            if constexpr (F3) v = v * p.ascale;
-            if (F3 && seg0) {
+            if constexpr (F3) v = v * ascale;
+            if ((F3 && seg0) || (R16 && !seg0)) {
                 u32x2 a0, a1;
                 split2_f16(v, a0, a1);
                 *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
@@ -382,7 +394,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 load_b(s + 1);
                 load_halo1(c + 1);
             }
-            compute6(hs, HWD + 1, s & 1);  // the halo centre = the output pixel
+            if constexpr (R16) compute3(hs, HWD + 1, s & 1, 0);  // the halo centre = the output pixel
+            else compute6(hs, HWD + 1, s & 1);
             if (more) {
                 write_b((s + 1) & 1, s + 1);
                 write_halo(hs ^ 1, false);
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             if (n >= p.N) continue;
             float add = p.bias ? p.bias[n] : 0.f;
             if (p.temb) add += p.temb[b * p.temb_ld + n];
-            const float mul = F3 ? p.wsinv[n] * p.ainv : 1.0f;
+            const float mul = F3 ? p.wsinv[n] * ainv : 1.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -418,12 +431,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, bool F3>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false>
 int launch6(const X6Dev& d, hipStream_t stream) {
-    using T = X6Tile<TH, BN, RES, F3>;
+    using T = X6Tile<TH, BN, RES, F3, R16>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -433,7 +446,7 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3>), grid, dim3(NT), T::LDS, stream, p);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -441,11 +454,14 @@ int launch6(const X6Dev& d, hipStream_t stream) {
 template <int TH, int BN>
 int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
     if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here
-        switch ((pro - 1) * 2 + (res ? 1 : 0)) {
+        const bool r16 = res && d.abound != nullptr;
+        switch ((pro - 1) * 3 + (res ? (r16 ? 2 : 1) : 0)) {
             case 0: return launch6<TH, BN, 1, false, true>(d, s);
             case 1: return launch6<TH, BN, 1, true, true>(d, s);
-            case 2: return launch6<TH, BN, 2, false, true>(d, s);
-            default: return launch6<TH, BN, 2, true, true>(d, s);
+            case 2: return launch6<TH, BN, 1, true, true, true>(d, s);
+            case 3: return launch6<TH, BN, 2, false, true>(d, s);
+            case 4: return launch6<TH, BN, 2, true, true>(d, s);
+            default: return launch6<TH, BN, 2, true, true, true>(d, s);
         }
     }
     switch (pro * 2 + (res ? 1 : 0)) {
@@ -498,7 +514,7 @@ int prepare(const wc_conv_args* a, const void* w, X6Dev& d, int& BN, int& TH) {
     d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
     d.w6 = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo; d.act = a->act;
-    d.ascale = 1.f; d.ainv = 1.f; d.wsinv = nullptr;
+    d.a_exp = 0; d.abound = nullptr; d.wsinv = nullptr;
     return WC_OK;
 }
 
@@ -521,7 +537,7 @@ extern "C" int wc_conv3x3_x6(const wc_conv_args* a, const void* w6, int64_t w6_b
 }
 
 extern "C" int wc_conv3x3_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, int a_exp,
-                                const float* w_inv_scale, void* stream) {
+                                const float* w_inv_scale, const float* a_bound, void* stream) {
     X6Dev d;
     int BN, TH;
     const int st = prepare(a, w3, d, BN, TH);
@@ -529,10 +545,11 @@ extern "C" int wc_conv3x3_f16x3(const wc_conv_args* a, const void* w3, int64_t w
     if (!a->seg[0].scale || !w_inv_scale) return WC_E_ARG;  // the static bound needs the GN prologue
     if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
     const long ntn = (a->N + BN - 1) / BN;
-    if (w3_bytes != ntn * (9L * d.nck0 * BN * 64 + (long)d.nck1 * BN * 96) || w3_bytes >= (1L << 31))
+    const long res_step = a_bound ? 64 : 96;  // segment 1 in fp16 (2 pieces) when bounded, else bf16x6
+    if (w3_bytes != ntn * (9L * d.nck0 * BN * 64 + (long)d.nck1 * BN * res_step) || w3_bytes >= (1L << 31))
         return WC_E_SHAPE;
-    d.ascale = ldexpf(1.0f, a_exp);
-    d.ainv = ldexpf(1.0f, -a_exp);
+    d.a_exp = a_exp;
+    d.abound = a_bound;
     d.wsinv = w_inv_scale;
     const int pro = a->seg[0].silu ? 2 : 1;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -82,11 +82,11 @@ __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const float* __res
 __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(
     const float* __restrict__ partials, int HW, int C, int G, int splits,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-    float* __restrict__ scale, float* __restrict__ shift) {
+    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ bound) {
     const int b = blockIdx.x;
     const int cpg = C / G;
     const int pps = (HW + splits - 1) / splits;
-    __shared__ float s_mean[32], s_rstd[32];
+    __shared__ float s_mean[32], s_rstd[32], s_bound[32];
     // 32 lanes per group: lane j merges splits j, j+32, ... then a 32-lane butterfly.
     const int g = threadIdx.x / 32;
     const int j = threadIdx.x % 32;
@@ -108,9 +108,17 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(
             float var = n > 0.f ? m2 / n : 0.f;  // biased, as torch
             s_mean[g] = mean;
             s_rstd[g] = 1.0f / sqrtf(fmaxf(var, 0.f) + eps);
+            // Samuelson: every element of the group lies within sqrt(n - 1) population standard
+            // deviations of the mean; 1e-3 relative slack covers the fp32 moments' rounding.
+            s_bound[g] = (fabsf(mean) + sqrtf(fmaxf(n - 1.f, 0.f)) * sqrtf(fmaxf(var, 0.f))) * 1.001f;
         }
     }
     __syncthreads();
+    if (bound && threadIdx.x == 0) {
+        float m = 0.f;
+        for (int gg = 0; gg < G; ++gg) m = fmaxf(m, s_bound[gg]);
+        bound[b] = m;
+    }
     for (int c = threadIdx.x; c < C; c += GN_THREADS) {
         int gg = c / cpg;
         float r = s_rstd[gg];
@@ -149,7 +157,20 @@ extern "C" int wc_gn_finalize(const float* partials, int B, int HW, int C, int g
     int splits = splits_for(B, HW, C);
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(GN_THREADS), 0,
                        reinterpret_cast<hipStream_t>(stream), partials, HW, C, groups, splits,
-                       gamma, beta, eps, scale, shift);
+                       gamma, beta, eps, scale, shift, nullptr);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_gn_finalize_bound(const float* partials, int B, int HW, int C, int groups,
+                                    const float* gamma, const float* beta, float eps, float* scale,
+                                    float* shift, float* bound, void* stream) {
+    if (!partials || !scale || !shift || !bound) return WC_E_ARG;
+    if (groups < 1 || groups > 8 || C % groups != 0) return WC_E_SHAPE;
+    int splits = splits_for(B, HW, C);
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(B), dim3(GN_THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), partials, HW, C, groups, splits,
+                       gamma, beta, eps, scale, shift, bound);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -174,7 +174,7 @@ class UnetEngine:
             p.w2x6 = (None if f3 else K.pack_x6(p.w2, co, ci), self._x6(p.w2, co, 9, ci))
             if f3:
                 p.w1f3 = K.pack_f16x3(p.w1, ci)
-                p.w2f3 = K.pack_f16x3(p.w2, co, ci)
+                p.w2f3 = K.pack_f16x3(p.w2, co, ci, res_f16=True)  # residual bounded by GN1's stats of X
                 p.gb1 = (float(p.g1.abs().max()), float(p.be1.abs().max()))
                 p.gb2 = (float(p.g2.abs().max()), float(p.be2.abs().max()))
         self.temb_rows_w.append(tl.weight.detach().float())
@@ -226,13 +226,14 @@ class UnetEngine:
 
     @staticmethod
     def conv3(segs, w: torch.Tensor, w6, w3: Optional[K.X6Weight], gb: Tuple[float, float], bias, out: View, H: int,
-              W: int, **kw):
+              W: int, a_bound: Optional[torch.Tensor] = None, **kw):
         """A ResBlock 3x3 stride-1 conv (GN+SiLU prologue): the halo-tiled kernel in f16x3 (bound
         from the GroupNorm affine gb and the group size) or bf16x6 when the grid tiles, else the
         bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode)."""
         if w3 is not None and K.x6_eligible(segs, w3.N, H, W):
             n_group = H * W * segs[0].view.C // 8
-            K.conv3x3_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(gb[0], gb[1], n_group), **kw)
+            K.conv3x3_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(gb[0], gb[1], n_group),
+                            a_bound=a_bound if w3.res_f16 else None, **kw)
         elif w6 is not None and w6[0] is not None and K.x6_eligible(segs, w6[0].N, H, W):
             K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, **kw)
         else:
@@ -240,13 +241,17 @@ class UnetEngine:
 
     def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int):
         B, H, W = X.B, X.H, X.W
-        sc1, sh1 = K.gn_affine(X, p.g1, p.be1)
+        xb = None
+        if p.w2f3 is not None and p.w2f3.res_f16:
+            sc1, sh1, xb = K.gn_affine(X, p.g1, p.be1, bound=True)  # xb bounds |X| (conv2's residual input)
+        else:
+            sc1, sh1 = K.gn_affine(X, p.g1, p.be1)
         h = View.full(self._new(B, H, W, p.co))
         self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.w1f3, p.gb1, p.b1, h, H, W,
                    temb=temb[:, p.temb_off:], temb_ld=temb_ld)
         sc2, sh2 = K.gn_affine(h, p.g2, p.be2)
         self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
-                    Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W)
+                    Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W, a_bound=xb)
 
     def attention(self, Y: View, p: AttnPack):
         B, H, W, C = Y.B, Y.H, Y.W, Y.C

@@ -206,6 +206,7 @@ class X6Weight:
     C1: int
     order: str = 'halo'
     wsinv: Optional[torch.Tensor] = None  # order 'f16x3': 2^-sW[n]
+    res_f16: bool = False  # f16x3: the residual segment packed as fp16 pieces (needs an A bound)
 
 
 @functools.lru_cache(maxsize=None)
@@ -252,12 +253,15 @@ def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str
     return X6Weight(data, N, BN, C0, C1, order)
 
 
-def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo') -> X6Weight:
+def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo',
+               res_f16: bool = False) -> X6Weight:
     """Re-pack a [N][ntaps*C0 + C1] conv (+ 1x1 residual) weight for the f16x3 kernels: per output
-    channel n a power-of-two scale 2^sW[n] with max_k |w[n, :ntaps*C0]| * 2^sW[n] <= 2^14; segment 0
+    channel n a power-of-two scale 2^sW[n] with max_k |w[n, k]| * 2^sW[n] <= 2^14 over the fp16-packed
+    columns (segment 0, and the residual with res_f16); segment 0
     as two round-to-nearest fp16 pieces, in (chunk, tap) step order for wc_conv3x3_f16x3 ('halo',
     ntaps 9) or natural K order for wc_conv_igemm_f16x3 ('natural'); the residual part as three
-    bf16 pieces (same scale)."""
+    bf16 pieces (same scale), or as two fp16 pieces with res_f16 (for a conv given a per-image A
+    bound, wc_conv3x3_f16x3)."""
     N, K = w.shape
     _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'f16x3 weight shape')
     _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
@@ -267,7 +271,8 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     wp = torch.zeros((Np, K), dtype=torch.float32, device=w.device)
     wp[:N] = w.float()
     K0 = ntaps * C0
-    amax = wp[:, :K0].abs().amax(1).double()
+    # the scale must keep every fp16-packed column <= 2^14: segment 0, plus the residual with res_f16
+    amax = (wp if res_f16 else wp[:, :K0]).abs().amax(1).double()
     sw = torch.where(amax > 0, torch.floor(torch.log2(2.0**14 / amax.clamp_min(1e-300))), torch.zeros_like(amax))
     sw = sw.clamp(-60, 60).to(torch.int32)
     ws = wp * torch.ldexp(torch.ones_like(wp[:, :1]), sw[:, None].float())  # exact power-of-two scaling
@@ -282,11 +287,16 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     pm = torch.stack([h, lo]).view(torch.int16).view(2, T, BN, S0, 2, 8).permute(1, 3, 0, 4, 2, 5)
     parts = [pm.reshape(T, -1)]
     if C1:
-        pr = split3_bits(ws[:, K0:].reshape(Np, S1, 2, 8)).view(3, T, BN, S1, 2, 8).permute(1, 3, 0, 4, 2, 5)
-        parts.append(pr.reshape(T, -1))
+        rw = ws[:, K0:].reshape(Np, S1, 2, 8)
+        if res_f16:
+            rh = rw.half()
+            pr = torch.stack([rh, (rw - rh.float()).half()]).view(torch.int16).view(2, T, BN, S1, 2, 8)
+        else:
+            pr = split3_bits(rw).view(3, T, BN, S1, 2, 8)
+        parts.append(pr.permute(1, 3, 0, 4, 2, 5).reshape(T, -1))
     data = torch.cat(parts, 1).contiguous()
     wsinv = torch.ldexp(torch.ones(Np, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
-    return X6Weight(data, N, BN, C0, C1, 'f16x3' if order == 'halo' else 'f16x3n', wsinv)
+    return X6Weight(data, N, BN, C0, C1, 'f16x3' if order == 'halo' else 'f16x3n', wsinv, res_f16)
 
 
 def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
@@ -302,20 +312,26 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
 
 
 def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
-                  a_exp: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
-                  act: int = 0):
+                  a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
+                  temb_ld: int = 0, res: Optional[View] = None, act: int = 0):
     """3x3 stride-1 conv with a GN(+SiLU) prologue on f16x3 (see wc_conv3x3_f16x3); a_exp from
-    f16x3_a_exp of that GroupNorm."""
+    f16x3_a_exp of that GroupNorm; a_bound = per-image bound of the residual segment's input
+    (gn_affine(..., bound=True)), required iff w3 packs the residual in fp16."""
     _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3', 'f16x3 weight')
+    _req((a_bound is not None) == (w3.res_f16 and w3.C1 > 0) or w3.C1 == 0 and not w3.res_f16,
+         'a residual packed in fp16 needs an A bound (and only then)')
+    if a_bound is not None:
+        _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
     _req(segs[0].scale is not None, 'f16x3 needs the GroupNorm prologue')
     a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act)
     TH, BN = x6_tile(w3.N)
     pro = 2 if segs[0].silu else 1
     res_seg = 'true' if len(segs) == 2 else 'false'
-    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, true>', 'wc_conv3x3_f16x3',
+    r16 = 'true' if a_bound is not None and len(segs) == 2 else 'false'
+    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, true, {r16}>', 'wc_conv3x3_f16x3',
            _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
-           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
+           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
 
 
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,
@@ -361,7 +377,7 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     res_seg = 'true' if len(segs) == 2 else 'false'
-    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, false>', 'wc_conv3x3_x6',
+    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, false, false>', 'wc_conv3x3_x6',
            _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 
@@ -383,8 +399,9 @@ def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor
 
 
 def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float = 1e-5,
-              groups: int = 8) -> Tuple[torch.Tensor, torch.Tensor]:
-    """GroupNorm statistics of a view -> per-(b, c) (scale, shift) so that GN(x) = x*scale + shift."""
+              groups: int = 8, bound: bool = False):
+    """GroupNorm statistics of a view -> per-(b, c) (scale, shift) so that GN(x) = x*scale + shift;
+    with bound=True also the per-image bound of |x| (wc_gn_finalize_bound) as a third result."""
     v.check()
     B, HW, C = v.B, v.H * v.W, v.C
     lib = _native.load()
@@ -394,6 +411,11 @@ def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tenso
     shift = torch.empty_like(scale)
     s = _stream()
     _native.call('wc_gn_stats', v.ptr, B, HW, C, v.ldc, groups, part.data_ptr(), s)
+    if bound:
+        bnd = torch.empty((B, ), dtype=torch.float32, device=v.t.device)
+        _native.call('wc_gn_finalize_bound', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps,
+                     scale.data_ptr(), shift.data_ptr(), bnd.data_ptr(), s)
+        return scale, shift, bnd
     _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps,
                  scale.data_ptr(), shift.data_ptr(), s)
     return scale, shift

@@ -80,6 +80,15 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps
     return t, fl / t / 1e12, err
 
 
+def gn_case(B, H, C, ldc=None):
+    ldc = ldc or C
+    x = torch.randn((B, H, H, ldc), device='cuda')
+    g = torch.ones(C, device='cuda')
+    v = K.View(x, 0, C)
+    t = timeit(lambda: K.gn_affine(v, g, g))
+    return t, B * H * H * C * 4 / t / 1e9
+
+
 def attn_case(B, N, C, prec='fp32'):
     qkv = torch.randn((B * N, 3 * C), device='cuda')
     o = torch.empty((B * N, C), device='cuda')
@@ -120,6 +129,10 @@ def main():
         print(f'{mode} conv aggregate {tot_f / tot_t:.1f} TF/s')
     if a.only >= 0:
         return
+    for c in [(16, 256, 128), (16, 256, 64), (16, 128, 256), (16, 64, 512), (16, 32, 768), (16, 256, 128, 256)]:
+        t, gbs = gn_case(*c)
+        print(f'gn B={c[0]} S={c[1]} C={c[2]} ldc={c[3] if len(c) > 3 else c[2]}: {t*1e3:8.3f} ms  {gbs:7.1f} GB/s',
+              flush=True)
     for prec in ('fp32', 'bf16x6', 'f16x3'):
         for c in [(16, 4096, 512), (16, 1024, 768), (16, 1024, 512), (16, 4096, 128), (16, 1024, 256)]:
             t, tf = attn_case(*c, prec=prec)

@@ -1,9 +1,11 @@
 // GroupNorm statistics for NHWC fp32 views (reference: nn.GroupNorm(8, C), unet_base.py:90 etc.).
 //
-// Pass 1 (wc_gn_stats): grid = B * splits * G workgroups, group index fastest so the G blocks that
-// read the same pixel rows run together and share L2 lines.  Each thread accumulates shifted
-// sums around its own first element (pivot), which keeps the moments free of E[x^2]-E[x]^2
-// cancellation; the workgroup merges (n, mean, M2) with Chan's formula.  HBM-bound: 4 B/element.
+// Pass 1 (wc_gn_stats): grid = B * splits workgroups, each streaming whole pixel rows (all C
+// channels, float4 loads: full cache lines, ~HBM rate) of one pixel range of one image.  Thread t
+// keeps one fixed 4-channel slice (so one group) and accumulates shifted sums around its own first
+// element (pivot), which keeps the moments free of E[x^2]-E[x]^2 cancellation; the workgroup then
+// merges the (n, mean, M2) of each group's threads with Chan's formula in a fixed order.
+// HBM-bound: 4 B/element.  (Channel counts with C/4 > 256 use a per-group fallback kernel.)
 // Pass 2 (wc_gn_finalize): one workgroup per batch element merges the split partials (again
 // Chan, fixed order => deterministic) and emits the per-(b, c) affine
 //   scale = gamma * rstd,   shift = beta - mean * rstd * gamma,
@@ -15,15 +17,67 @@ namespace {
 constexpr int GN_THREADS = 256;
 
 int splits_for(int B, int HW, int C) {
-    (void)C;
-    const int G = 8;
-    int target = 2048 / (B * G);
-    if (target < 1) target = 1;
-    int max_by_hw = HW / 64;
-    if (max_by_hw < 1) max_by_hw = 1;
-    if (target > max_by_hw) target = max_by_hw;
-    if (target > 256) target = 256;
-    return target;
+    if (C / 4 > GN_THREADS) {  // fallback kernel: B * splits * G workgroups
+        int target = 2048 / (B * 8);
+        target = target < 1 ? 1 : target;
+        const int max_by_hw = HW / 64 < 1 ? 1 : HW / 64;
+        target = target > max_by_hw ? max_by_hw : target;
+        return target > 256 ? 256 : target;
+    }
+    int target = 2048 / B;  // ~2048 workgroups of whole pixel rows
+    target = target < 1 ? 1 : target;
+    const int max_by_hw = HW / 16 < 1 ? 1 : HW / 16;
+    target = target > max_by_hw ? max_by_hw : target;
+    return target > 256 ? 256 : target;
+}
+
+// Whole-row kernel: thread t handles channel quad q = t % Q of pixels p_begin + t / Q + k * R.
+__global__ __launch_bounds__(GN_THREADS) void gn_stats_rows_kernel(const float* __restrict__ x, int HW,
+                                                                   int C, int ldc, int G, int splits,
+                                                                   float* __restrict__ partials) {
+    const int split = blockIdx.x % splits;
+    const int b = blockIdx.x / splits;
+    const int Q = C / 4;
+    const int R = GN_THREADS / Q;  // pixel rows per iteration (threads >= R*Q idle)
+    const int cpg = C / G;
+    const int q = threadIdx.x % Q;
+    const int r = threadIdx.x / Q;
+    const int pps = (HW + splits - 1) / splits;
+    const int p_begin = split * pps;
+    const int p_end = min(HW, p_begin + pps);
+    float n = 0.f, s = 0.f, ss = 0.f, pivot = 0.f;
+    if (r < R) {
+        const float* base = x + (long)b * HW * ldc + q * 4;
+        bool have = false;
+        for (int p = p_begin + r; p < p_end; p += R) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(base + (long)p * ldc);
+            if (!have) { pivot = v.x; have = true; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float d = v[i] - pivot;
+                s += d;
+                ss = fmaf(d, d, ss);
+            }
+            n += 4.f;
+        }
+    }
+    __shared__ float sn[GN_THREADS], sm[GN_THREADS], sq[GN_THREADS];
+    sn[threadIdx.x] = n;
+    sm[threadIdx.x] = n > 0.f ? pivot + s / n : 0.f;
+    sq[threadIdx.x] = n > 0.f ? fmaxf(ss - s * (s / n), 0.f) : 0.f;
+    __syncthreads();
+    if (threadIdx.x < G) {  // group g: quads [g*cpg/4, (g+1)*cpg/4) of every row, fixed order
+        const int g = threadIdx.x;
+        float N0 = 0.f, M0 = 0.f, Q0 = 0.f;
+        for (int rr = 0; rr < R; ++rr)
+            for (int qq = g * (cpg / 4); qq < (g + 1) * (cpg / 4); ++qq) {
+                const int t = rr * Q + qq;
+                chan_merge(N0, M0, Q0, sn[t], sm[t], sq[t]);
+            }
+        float* o = partials + (((long)b * splits + split) * G + g) * 2;
+        o[0] = M0;
+        o[1] = Q0;
+    }
 }
 
 __global__ __launch_bounds__(GN_THREADS) void gn_stats_kernel(const float* __restrict__ x, int HW,
@@ -141,10 +195,14 @@ extern "C" int wc_gn_stats(const float* x, int B, int HW, int C, int ldc, int gr
         return WC_E_SHAPE;
     if ((reinterpret_cast<uintptr_t>(x) & 15) != 0) return WC_E_SHAPE;
     int splits = splits_for(B, HW, C);
-    dim3 grid(B * splits * groups);
-    hipLaunchKernelGGL(gn_stats_kernel, grid, dim3(GN_THREADS), 0,
-                       reinterpret_cast<hipStream_t>(stream), x, HW, C, ldc, groups, splits,
-                       partials);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (C / 4 <= GN_THREADS) {
+        hipLaunchKernelGGL(gn_stats_rows_kernel, dim3(B * splits), dim3(GN_THREADS), 0, st, x, HW, C, ldc,
+                           groups, splits, partials);
+    } else {
+        hipLaunchKernelGGL(gn_stats_kernel, dim3(B * splits * groups), dim3(GN_THREADS), 0, st, x, HW, C,
+                           ldc, groups, splits, partials);
+    }
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -23,6 +23,7 @@ Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
                 bounded sample (a few 256-px UNet steps), extrapolated x T.
 """
 import argparse
+import glob
 import json
 import os
 import time
@@ -84,7 +85,20 @@ def roofline_leg(model, x, t_dev):
     mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
     total_conv = sum(v[2] for v in per.values())
-    f16x3 = name.startswith('conv3x3_x6') and name.endswith(', true>')
+    # HBM bytes per launch of this kernel from the committed two-pass PMC measurement
+    # (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), if present
+    traffic, traffic_src = None, None
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
+                                              '*_hbm_traffic.json')))[-1:]:
+        rec = json.load(open(path)).get(name)
+        if rec:
+            traffic = round(rec['total_bytes'] / 1e9, 4)
+            traffic_src = (f'{os.path.relpath(path, os.path.dirname(os.path.abspath(__file__)))}: GB per launch '
+                           f'(read {rec["read_bytes"] / 1e9:.3f} + write {rec["write_bytes"] / 1e9:.3f}), '
+                           f'mean over {rec["launches"]} launches')
+    targs = name[name.index('<') + 1:name.rindex('>')].split(', ')
+    f16x3 = ((name.startswith('conv3x3_x6') and len(targs) >= 5 and targs[4] == 'true')
+             or (name.startswith(('conv_igemm_x6', 'attention_x6')) and targs[-1] == 'true'))
     desc = {'conv3x3_x6': ' (bf16x6 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue)',
             'conv_igemm_x6': ' (bf16x6 split-precision MFMA implicit-GEMM conv)',
             'attention_x6': ' (bf16x6 split-precision MFMA flash attention)',
@@ -93,8 +107,11 @@ def roofline_leg(model, x, t_dev):
                                                                    if '_x6' in name else name.split('<')[0]]
     peak = BF16X6_PEAK_TFLOPS if '_x6' in name else FP32_PEAK_TFLOPS
     if f16x3:
-        desc, peak = (' (f16x3 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue; 1x1 residual '
-                      'segment in bf16x6)'), F16X3_PEAK_TFLOPS
+        desc = desc.replace('bf16x6', 'f16x3')
+        if name.startswith('conv3x3_x6'):
+            desc = (' (f16x3 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue, fused 1x1 residual in '
+                    + ('f16x3 under the per-image GN bound)' if targs[5:] == ['true'] else 'bf16x6)'))
+        peak = F16X3_PEAK_TFLOPS
     return {
         'kernel': name + desc,
         'bound': 'mfma',
@@ -102,7 +119,8 @@ def roofline_leg(model, x, t_dev):
         'peak': peak,
         'unit': 'TFLOP/s',
         'frac': round(achieved / peak, 4),
-        'traffic': None,
+        'traffic': traffic,
+        'traffic_source': traffic_src,
         'launches_per_step': n,
         'mean_launch_ms': round(mean_dur * 1e3, 4),
         'gflop_per_launch': round(fl / n / 1e9, 3),

@@ -121,9 +121,20 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     const int wave = tid >> 6;
     const int l32 = lane & 31;
     const int half = lane >> 5;
-    const int head = blockIdx.y;
-    const int b = blockIdx.z;
-    const int q0 = blockIdx.x * 128 + wave * 32;
+    // XCD-aware bijective order: the workgroups of one (batch, head) — which all stream the same
+    // K/V — are consecutive logical blocks and land on one XCD, so its L2 holds that K/V once
+    // (round-robin placement would pull it into all eight L2s).
+    const int nqb = (N + 127) / 128;
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int heads = C / D;
+    const int head = (bid / nqb) % heads;
+    const int b = bid / (nqb * heads);
+    const int q0 = (bid % nqb) * 128 + wave * 32;
     const float* base = qkv + (long)b * N * ldq;
     const int qcol = head * D;
     const int kcol = C + head * D;
@@ -332,7 +343,7 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
     }
     constexpr int EP = F3 ? 14 : 0;  // P scale: keeps small probabilities in the fp16 normal range
     const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
-    dim3 grid((N + 127) / 128, heads, B);
+    dim3 grid(((N + 127) / 128) * heads * B);
     hipLaunchKernelGGL((attention_x6_kernel<D, F3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
                        score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), ldexpf(1.f, EP),
                        ldexpf(1.f, -(ev + EP)));

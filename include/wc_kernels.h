@@ -74,6 +74,9 @@ typedef struct wc_conv_args {
     int act;            /* epilogue activation after bias/temb, before the residual add:
                            WC_ACT_NONE / WC_ACT_GELU (exact erf) / WC_ACT_SILU; wc_conv_igemm
                            accepts an activation only with a raw segment 0 (no scale/shift) */
+    float* absmax_out;  /* optional, per image [B] (caller-zeroed): atomically raised to max |out| of
+                           the image's written values (a bound for a later f16x3 consumer);
+                           split-precision kernels only (the fp32 kernel returns WC_E_ARG) */
 } wc_conv_args;
 
 #define WC_ACT_NONE 0
@@ -127,12 +130,16 @@ int wc_conv3x3_x6_tile_n(int N);
  * old UNet's Linear layers, old_modules.py:87-95). */
 int wc_conv_igemm_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, void* stream);
 /* wc_conv_igemm_x6 with segment 0 on f16x3 (as wc_conv3x3_f16x3; no epilogue activation).  The
- * caller guarantees |a| * 2^a_exp <= 2^14 for every segment-0 value after the prologue.  w3 layout
+ * caller guarantees |a| * 2^a_exp <= 2^14 for every segment-0 value after the prologue, or passes
+ * a_bound (per image, >= max |a| of the image's segment-0 values after the prologue, e.g. the
+ * producer's absmax_out): image b then uses s = min(a_exp, 13 - floor(log2 a_bound[b])), which
+ * needs tiles within one image ((Hm*Wm) % BM == 0, BM = 256 for N <= 64 else 128).  w3 layout
  * per N tile: [ntaps*C0/16 steps][piece 2][k-half 2][BN][8] fp16 bits, then
  * [C1/16][piece 3][k-half 2][BN][8] bf16 bits, all scaled by 2^sW[n]; w_inv_scale[n] = 2^-sW[n].
- * Replaces the attention in/out projections (unet_base.py:115,159) and the head conv (:483-485). */
+ * Replaces the attention in/out projections (unet_base.py:115,159), the head conv (:483-485), the
+ * down-sampling convs (:231) and the up-sampling transposed convs (:300). */
 int wc_conv_igemm_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
-                        const float* w_inv_scale, void* stream);
+                        const float* w_inv_scale, const float* a_bound, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */

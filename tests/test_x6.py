@@ -6,6 +6,8 @@ GPU: the conv against a float64 PyTorch reference of the same op.  Stated tolera
 <= 1e-5 (the fp32 tolerance of SURVEY.md §8c) and, tighter, within 4x (+1e-7) of the error of the
 fp32-MFMA conv on the same inputs, i.e. fp32-class accuracy.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -551,3 +553,140 @@ def test_igemm_f16x3_projections_and_head():
     K.conv_igemm_f16x3(seg3, K.pack_f16x3(_pack(wh).cuda(), C, order='natural'), bh.cuda(), None, Hm=H, Wm=H,
                        a_exp=e, out_nchw=out3)
     assert rel_l2(out3.cpu().double(), ref3) < 2e-6
+
+
+# ---------------------------------------------------------------- producer absmax -> per-image f16x3 scale
+
+def _img_amax(o_bhwc):
+    return o_bhwc.reshape(o_bhwc.shape[0], -1).abs().amax(1)
+
+
+@pytest.mark.gpu
+def test_absmax_output_of_split_precision_kernels():
+    """absmax_out = exact per-image max |out| of the written values (halo x6 / f16x3, igemm with
+    tiles inside one image, straddling tiles, and a transposed-conv parity into a concat slice)."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.models.engine import pack_convT
+    g = torch.Generator().manual_seed(61)
+    B, H, C, N = 3, 16, 64, 128
+    x = torch.randn((B, C, H, H), generator=g) * torch.tensor([1.0, 30.0, 0.01])[:, None, None, None]
+    sc = (1 + 0.3 * torch.randn((B, C), generator=g)).cuda()
+    sh = (0.3 * torch.randn((B, C), generator=g)).cuda()
+    w = (torch.randn((N, 9 * C), generator=g) / (9 * C)**0.5).cuda()
+    xv = K.View.full(_nhwc(x).cuda())
+    seg = [K.Seg(xv, TAPS3, scale=sc, shift=sh, silu=True)]
+    for mode in ('x6', 'f3'):
+        out = torch.empty((B, H, H, N), device='cuda')
+        am = torch.zeros(B, device='cuda')
+        if mode == 'x6':
+            K.conv3x3_x6(seg, K.pack_x6(w, C), None, K.View.full(out), Hm=H, Wm=H, absmax=am)
+        else:
+            K.conv3x3_f16x3(seg, K.pack_f16x3(w, C), None, K.View.full(out), Hm=H, Wm=H, a_exp=6, absmax=am)
+        torch.cuda.synchronize()
+        assert torch.equal(am.cpu(), _img_amax(out.cpu())), mode
+    # igemm x6: 8x8 grids straddle images (BM = 128), 16x16 grids do not
+    for Hm in (8, 16):
+        xr = torch.randn((B, Hm, Hm, C), generator=g) * torch.tensor([2.0, 0.1, 50.0])[:, None, None, None]
+        wr = (torch.randn((N, C), generator=g) / C**0.5).cuda()
+        out = torch.empty((B, Hm, Hm, N), device='cuda')
+        am = torch.zeros(B, device='cuda')
+        K.conv_igemm_x6([K.Seg(K.View.full(xr.cuda()), [(0, 0)])], K.pack_x6(wr, C, ntaps=1, order='natural'), None,
+                        K.View.full(out), Hm=Hm, Wm=Hm, absmax=am)
+        torch.cuda.synchronize()
+        assert torch.equal(am.cpu(), _img_amax(out.cpu())), Hm
+    # transposed conv parity into the first half of a concat buffer whose other half holds 1e6
+    Ci, Co = 128, 64
+    wt = torch.randn((Ci, Co, 4, 4), generator=g) / (4 * Ci)**0.5
+    xt = K.View.full(torch.randn((B, 8, 8, Ci), generator=g).cuda())
+    buf = torch.full((B, 16, 16, 2 * Co), 1e6, device='cuda')
+    am = torch.zeros(B, device='cuda')
+    for py in (0, 1):
+        for px in (0, 1):
+            taps, wp = pack_convT(wt, py, px)
+            K.conv_igemm_x6([K.Seg(xt, taps)], K.pack_x6(wp.cuda(), Ci, 0, ntaps=4, order='natural'), None,
+                            K.View(buf, 0, Co), Hm=8, Wm=8, out_map=(2, 2, py, px), absmax=am)
+    torch.cuda.synchronize()
+    assert torch.equal(am.cpu(), _img_amax(buf.cpu()[..., :Co]))
+
+
+@pytest.mark.gpu
+def test_fp32_conv_rejects_absmax():
+    from weatherconverter_amd import kernels as K, _native
+    x = torch.randn((1, 8, 8, 16), device='cuda')
+    w = torch.randn((16, 16), device='cuda')
+    out = torch.empty((1, 8, 8, 16), device='cuda')
+    am = torch.zeros(1, device='cuda')
+    a = K._conv_args([K.Seg(K.View.full(x), [(0, 0)])], 16, None, K.View.full(out), 8, 8, None, 0, None,
+                     (1, 1, 0, 0), None, 0, am)
+    a.w, a.ldw = w.data_ptr(), 16
+    rc = _native.load().wc_conv_igemm(ctypes.byref(a), None)
+    assert rc != 0
+
+
+@pytest.mark.gpu
+def test_igemm_f16x3_resampling_with_producer_bound():
+    """Down-sampling 4x4/s2 conv and the transposed conv's four parities on f16x3, scaled per image
+    by a bound: images of very different magnitude and one outlier, vs float64; the bound comes
+    from the producer's absmax.  A straddling grid with a bound is rejected."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.models.engine import pack_convT
+    g = torch.Generator().manual_seed(62)
+    B, H, Ci, Co = 3, 32, 64, 128
+    x = torch.randn((B, Ci, H, H), generator=g) * torch.tensor([1.0, 1e3, 1e-3])[:, None, None, None]
+    x[0, 5, 7, 9] = 4e4  # one outlier in image 0: far past the fp16 range unscaled
+    # producer: an identity 1x1 conv on bf16x6 whose epilogue emits the absmax
+    xin = _nhwc(x).cuda()
+    xp = torch.empty_like(xin)
+    am = torch.zeros(B, device='cuda')
+    K.conv_igemm_x6([K.Seg(K.View.full(xin), [(0, 0)])], K.pack_x6(torch.eye(Ci).cuda(), Ci, ntaps=1,
+                    order='natural'), None, K.View.full(xp), Hm=H, Wm=H, absmax=am)
+    torch.cuda.synchronize()
+    assert torch.equal(xp.cpu(), xin.cpu()) and torch.equal(am.cpu(), _img_amax(xin.cpu()))
+    w = torch.randn((Co, Ci, 4, 4), generator=g) / (16 * Ci)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1)
+    seg = [K.Seg(K.View.full(xp), TAPS4S2, stride=2)]
+    outs = {}
+    for mode in ('f16x3', 'fp32'):
+        o = torch.empty((B, H // 2, H // 2, Co), device='cuda')
+        if mode == 'f16x3':
+            K.conv_igemm_f16x3(seg, K.pack_f16x3(_pack(w).cuda(), Ci, ntaps=16, order='natural'), b.cuda(),
+                               K.View.full(o), Hm=H // 2, Wm=H // 2, a_exp=60, a_bound=am)
+        else:
+            K.conv_igemm(seg, _pack(w).cuda(), b.cuda(), K.View.full(o), Hm=H // 2, Wm=H // 2)
+        torch.cuda.synchronize()
+        outs[mode] = _nchw(o.cpu()).double()
+    for i in range(B):  # per image: each one's own scale
+        e3, e32 = rel_l2(outs['f16x3'][i], ref[i]), rel_l2(outs['fp32'][i], ref[i])
+        assert e3 < 1e-5 and e3 <= 4 * e32 + 2e-7, (i, e3, e32)
+
+    # transposed conv (ConvTranspose2d(Ci, Co2, 4, 2, 1)) from the same producer output
+    Co2 = 64
+    wt = torch.randn((Ci, Co2, 4, 4), generator=g) / (4 * Ci)**0.5
+    bt = torch.randn(Co2, generator=g) * 0.1
+    reft = F.conv_transpose2d(x.double(), wt.double(), bt.double(), stride=2, padding=1)
+    xv = K.View.full(xp)
+    for mode in ('f16x3', 'fp32'):
+        buf = torch.full((B, 2 * H, 2 * H, 2 * Co2), 5.0, device='cuda')
+        dst = K.View(buf, 0, Co2)
+        for py in (0, 1):
+            for px in (0, 1):
+                taps, wp = pack_convT(wt, py, px)
+                if mode == 'f16x3':
+                    K.conv_igemm_f16x3([K.Seg(xv, taps)], K.pack_f16x3(wp.cuda(), Ci, ntaps=4, order='natural'),
+                                       bt.cuda(), dst, Hm=H, Wm=H, a_exp=60, a_bound=am, out_map=(2, 2, py, px))
+                else:
+                    K.conv_igemm([K.Seg(xv, taps)], wp.cuda(), bt.cuda(), dst, Hm=H, Wm=H, out_map=(2, 2, py, px))
+        torch.cuda.synchronize()
+        bc = buf.cpu()
+        assert bool((bc[..., Co2:] == 5.0).all())
+        outs[mode] = _nchw(bc[..., :Co2]).double()
+    for i in range(B):
+        e3, e32 = rel_l2(outs['f16x3'][i], reft[i]), rel_l2(outs['fp32'][i], reft[i])
+        assert e3 < 1e-5 and e3 <= 4 * e32 + 2e-7, (i, e3, e32)
+
+    with pytest.raises(RuntimeError):  # 12x12 grid: BM = 128 tiles straddle images
+        xs = K.View.full(torch.randn((B, 12, 12, Ci), device='cuda'))
+        K.conv_igemm_f16x3([K.Seg(xs, [(0, 0)])], K.pack_f16x3(torch.randn(Co, Ci).cuda(), Ci, ntaps=1,
+                           order='natural'), None, K.View.full(torch.empty((B, 12, 12, Co), device='cuda')),
+                           Hm=12, Wm=12, a_exp=60, a_bound=am)

@@ -42,7 +42,7 @@ class ConvArgs(ctypes.Structure):
         ('res', ctypes.c_void_p), ('ldres', ctypes.c_int), ('out', ctypes.c_void_p),
         ('ldo', ctypes.c_int), ('Ho', ctypes.c_int), ('Wo', ctypes.c_int), ('osy', ctypes.c_int),
         ('osx', ctypes.c_int), ('ooy', ctypes.c_int), ('oox', ctypes.c_int),
-        ('out_nchw', ctypes.c_int), ('act', ctypes.c_int)
+        ('out_nchw', ctypes.c_int), ('act', ctypes.c_int), ('absmax_out', ctypes.c_void_p)
     ]
 
 
@@ -59,7 +59,7 @@ _SIGS = {
     'wc_conv3x3_x6_tile_n': [_I],
     'wc_conv3x3_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
     'wc_conv_igemm_x6': [ctypes.POINTER(ConvArgs), _P, _L, _P],
-    'wc_conv_igemm_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P],
+    'wc_conv_igemm_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
     'wc_gn_num_splits': [_I, _I, _I],
     'wc_gn_stats': [_P, _I, _I, _I, _I, _I, _P, _P],
     'wc_gn_finalize': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P],

@@ -71,6 +71,7 @@ struct X6Dev {
     int a_exp;            // f16x3: static exponent sA of the segment-0 bound (else 0)
     const float* abound;  // f16x3: per-image bound of every A value (segment 1 in fp16), or NULL
     const float* wsinv;   // f16x3: 2^-sW[n] per output channel (else NULL)
+    float* absmax;        // optional per-image max |out| (atomic)
     int tiles_x, tiles_y, ntiles_n;
 };
 
@@ -406,6 +407,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     }
 
     // ---- epilogue: (F3: x 2^-(sA + sW[n])) + bias + temb, activation, + residual, NHWC store ----
+    float vmax = 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
@@ -426,9 +428,11 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
                 if (p.res) v += p.res[m * p.ldres + n];
                 p.out[m * p.ldo + n] = v;
+                vmax = fmaxf(vmax, fabsf(v));
             }
         }
     }
+    if (p.absmax) wave_absmax_atomic(p.absmax, b, vmax);  // the whole tile is image b
 }
 
 template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false>
@@ -515,6 +519,7 @@ int prepare(const wc_conv_args* a, const void* w, X6Dev& d, int& BN, int& TH) {
     d.w6 = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo; d.act = a->act;
     d.a_exp = 0; d.abound = nullptr; d.wsinv = nullptr;
+    d.absmax = a->absmax_out;
     return WC_OK;
 }
 

@@ -51,6 +51,9 @@ struct IgDev {
     float ascale;        // f16x3: 2^a_exp applied to the A values before splitting (else 1)
     float ainv;          // 2^-a_exp
     const float* wsinv;  // f16x3: 2^-sW[n] (else NULL)
+    const float* abound; // f16x3: per-image bound of the segment-0 values (UNIB only), or NULL
+    int a_exp;           // f16x3: static exponent (the per-image bound may lower it)
+    float* absmax;       // optional per-image max |out| (atomic)
 };
 
 // F3: segment 0 in f16x3 (2 fp16 pieces), else bf16x6; segment 1 is always bf16x6.
@@ -118,6 +121,19 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
         }
     }
     const int b_tile = m0 / HWm;
+    // f16x3 scale: the static exponent, lowered per image by the producer's bound (tile = 1 image)
+    float ascale = 1.f, ainv = 1.f;
+    if constexpr (F3) {
+        int s_exp = p.a_exp;
+        if (UNIB && p.abound) {
+            const float bnd = p.abound[b_tile];
+            const int e = (int)((__float_as_uint(bnd) >> 23) & 0xffu) - 127;
+            if (bnd > 0.f) s_exp = min(s_exp, 13 - e);
+            s_exp = max(s_exp, -100);
+        }
+        ascale = ldexpf(1.0f, s_exp);
+        ainv = ldexpf(1.0f, -s_exp);
+    }
     // LDS byte offset of this thread's 8-byte A write within a piece plane set
     const int a_wr = (q4 >> 1) * T::APLANE + prow * 16 + (q4 & 1) * 8;
 
@@ -207,7 +223,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
             }
             if (!((aval >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
             unsigned char* d = buf + a_wr + j * 64 * 16;
-            if constexpr (F3) v = v * p.ascale;
+            if constexpr (F3) v = v * ascale;
             if (F3 && pro) {
                 u32x2 a0, a1;
                 split2_f16(v, a0, a1);
@@ -327,6 +343,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
 
     // ---- epilogue (as wc_conv.hip) ----
     const int HWo = p.Ho * p.Wo;
+    float vmax = 0.f;  // absmax: per image; tiles straddling images take the per-value atomic below
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
         const int mbase = m0 + wm * 64 + mb * 32;
@@ -337,7 +354,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
             const int n = n0 + wn * 64 + nb * 32 + l32;
             if (n >= p.N) continue;
             const float bn = p.bias ? p.bias[n] : 0.f;
-            const float mul = F3 ? p.wsinv[n] * p.ainv : 1.0f;
+            const float mul = F3 ? p.wsinv[n] * ainv : 1.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -351,6 +368,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                 if (p.ident) {
                     if (p.res) v += p.res[(long)m * p.ldres + n];
                     p.out[(long)m * p.ldo + n] = v;
+                    if (p.absmax) {
+                        if constexpr (UNIB) vmax = fmaxf(vmax, fabsf(v));
+                        else atomicMax(reinterpret_cast<unsigned*>(p.absmax) + b, __float_as_uint(fabsf(v)));
+                    }
                 } else {
                     const int rr = m - b * HWm;
                     const int my = rr / p.Wm;
@@ -363,9 +384,16 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                         p.out[((long)b * p.N + n) * HWo + (long)oy * p.Wo + ox] = v;
                     else
                         p.out[pix * p.ldo + n] = v;
+                    if (p.absmax) {
+                        if constexpr (UNIB) vmax = fmaxf(vmax, fabsf(v));
+                        else atomicMax(reinterpret_cast<unsigned*>(p.absmax) + b, __float_as_uint(fabsf(v)));
+                    }
                 }
             }
         }
+    }
+    if constexpr (UNIB) {
+        if (p.absmax) wave_absmax_atomic(p.absmax, b_tile, vmax);
     }
 }
 
@@ -461,7 +489,8 @@ int prepare(const wc_conv_args* a, const void* w6, IgDev& d, long& k) {
               a->Ho == a->Hm && a->Wo == a->Wm;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
     d.steps = (int)(k / BK);
-    d.ascale = 1.f; d.ainv = 1.f; d.wsinv = nullptr;
+    d.wsinv = nullptr; d.abound = nullptr; d.a_exp = 0;
+    d.absmax = a->absmax_out;
     return WC_OK;
 }
 
@@ -482,7 +511,7 @@ extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w
 }
 
 extern "C" int wc_conv_igemm_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, int a_exp,
-                                   const float* w_inv_scale, void* stream) {
+                                   const float* w_inv_scale, const float* a_bound, void* stream) {
     IgDev d;
     long k;
     const int st = prepare(a, w3, d, k);
@@ -492,9 +521,11 @@ extern "C" int wc_conv_igemm_f16x3(const wc_conv_args* a, const void* w3, int64_
     const long ntn = (a->N + BN - 1) / BN;
     const long s1 = d.steps - d.steps0;
     if (w3_bytes != ntn * ((long)d.steps0 * BN * 64 + s1 * BN * 96) || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
-    d.ascale = ldexpf(1.0f, a_exp);
-    d.ainv = ldexpf(1.0f, -a_exp);
+    d.a_exp = a_exp;
     d.wsinv = w_inv_scale;
+    d.abound = a_bound;
+    const int BM = BN == 64 ? 256 : 128;
+    if (a_bound && (d.Hm * d.Wm) % BM != 0) return WC_E_SHAPE;  // per-image scale needs 1-image tiles
     const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (BN == 64) return dispatch<256, 64>(d, pro, a->act, true, s);

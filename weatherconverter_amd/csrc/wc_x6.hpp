@@ -89,4 +89,11 @@ WC_DEVICE void split2_f16_elems(f32x4 v, unsigned (&h)[4], unsigned (&l)[4]) {
     }
 }
 
+// Raise absmax[b] to the wave's max of m (|values| >= 0: their float bits order like unsigned ints).
+WC_DEVICE void wave_absmax_atomic(float* absmax, int b, float m) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(absmax) + b, __float_as_uint(m));
+}
+
 }  // namespace wcx6

@@ -126,8 +126,9 @@ class UnetEngine:
             for blk in m.downs:
                 if blk.down_sample:
                     w = pack_conv(blk.down_sample_conv.weight)
+                    ci = blk.down_sample_conv.in_channels
                     self.down_convs.append((w, blk.down_sample_conv.bias.detach().float(),
-                                            self._x6(w, blk.down_sample_conv.in_channels, len(TAPS4S2))))
+                                            self._x6(w, ci, len(TAPS4S2)), self._f3n(w, ci, len(TAPS4S2))))
                 else:
                     self.down_convs.append(None)
             self.mids = [self._pack_stage(blk, n_res=blk.num_layers + 1, attn=True) for blk in m.mids]
@@ -137,7 +138,7 @@ class UnetEngine:
                 if blk.up_sample:
                     ci = blk.up_sample_conv.in_channels
                     parts = [pack_convT(blk.up_sample_conv.weight, py, px) for py in (0, 1) for px in (0, 1)]
-                    parts = [(taps, w, self._x6(w, ci, len(taps))) for taps, w in parts]
+                    parts = [(taps, w, self._x6(w, ci, len(taps)), self._f3n(w, ci, len(taps))) for taps, w in parts]
                     self.up_convs.append((parts, blk.up_sample_conv.bias.detach().float()))
                 else:
                     self.up_convs.append(None)
@@ -188,6 +189,13 @@ class UnetEngine:
             return None
         return K.pack_x6(w, c0, c1, ntaps=ntaps, order='natural')
 
+    def _f3n(self, w: torch.Tensor, c0: int, ntaps: int) -> Optional[K.X6Weight]:
+        """f16x3 (natural K order) pack for a resampling conv whose input range comes from its
+        producer's per-image absmax, or None outside f16x3 mode."""
+        if self.precision != 'f16x3' or c0 % 16:
+            return None
+        return K.pack_f16x3(w, c0, ntaps=ntaps, order='natural')
+
     def _pack_attn(self, blk, i: int) -> AttnPack:
         mha, gn = blk.attentions[i], blk.attention_norms[i]
         c = mha.embed_dim
@@ -217,29 +225,44 @@ class UnetEngine:
         return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
 
     @staticmethod
-    def conv(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: Optional[View], H: int, W: int, **kw):
-        """Any conv: bf16x6 implicit GEMM when packed for it, else fp32 MFMA."""
+    def conv(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: Optional[View], H: int, W: int,
+             absmax: Optional[torch.Tensor] = None, **kw) -> bool:
+        """Any conv: bf16x6 implicit GEMM when packed for it, else fp32 MFMA.  Returns True when
+        the per-image output absmax was emitted into `absmax` (split-precision kernels only)."""
         if w6 is not None:
-            K.conv_igemm_x6(segs, w6, bias, out, Hm=H, Wm=W, **kw)
+            K.conv_igemm_x6(segs, w6, bias, out, Hm=H, Wm=W, absmax=absmax, **kw)
+            return absmax is not None
+        K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
+        return False
+
+    @staticmethod
+    def resample(segs, pack, bias, out: View, H: int, W: int, bound: Optional[torch.Tensor], **kw):
+        """Down-sampling conv / one transposed-conv parity: f16x3 implicit GEMM scaled per image by
+        the producer's absmax when there is one (and the tiles stay within an image), else bf16x6."""
+        w, w6, w3 = pack
+        if w3 is not None and bound is not None and (H * W) % (256 if w3.N <= 64 else 128) == 0:
+            K.conv_igemm_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=60, a_bound=bound, **kw)
         else:
-            K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
+            UnetEngine.conv(segs, w, w6, bias, out, H, W, **kw)
 
     @staticmethod
     def conv3(segs, w: torch.Tensor, w6, w3: Optional[K.X6Weight], gb: Tuple[float, float], bias, out: View, H: int,
-              W: int, a_bound: Optional[torch.Tensor] = None, **kw):
+              W: int, a_bound: Optional[torch.Tensor] = None, absmax: Optional[torch.Tensor] = None, **kw) -> bool:
         """A ResBlock 3x3 stride-1 conv (GN+SiLU prologue): the halo-tiled kernel in f16x3 (bound
         from the GroupNorm affine gb and the group size) or bf16x6 when the grid tiles, else the
         bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode)."""
         if w3 is not None and K.x6_eligible(segs, w3.N, H, W):
             n_group = H * W * segs[0].view.C // 8
             K.conv3x3_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(gb[0], gb[1], n_group),
-                            a_bound=a_bound if w3.res_f16 else None, **kw)
-        elif w6 is not None and w6[0] is not None and K.x6_eligible(segs, w6[0].N, H, W):
-            K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, **kw)
-        else:
-            UnetEngine.conv(segs, w, None if w6 is None else w6[1], bias, out, H, W, **kw)
+                            a_bound=a_bound if w3.res_f16 else None, absmax=absmax, **kw)
+            return absmax is not None
+        if w6 is not None and w6[0] is not None and K.x6_eligible(segs, w6[0].N, H, W):
+            K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, absmax=absmax, **kw)
+            return absmax is not None
+        return UnetEngine.conv(segs, w, None if w6 is None else w6[1], bias, out, H, W, absmax=absmax, **kw)
 
-    def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int):
+    def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int,
+                 absmax: Optional[torch.Tensor] = None) -> bool:
         B, H, W = X.B, X.H, X.W
         xb = None
         if p.w2f3 is not None and p.w2f3.res_f16:
@@ -250,10 +273,11 @@ class UnetEngine:
         self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.w1f3, p.gb1, p.b1, h, H, W,
                    temb=temb[:, p.temb_off:], temb_ld=temb_ld)
         sc2, sh2 = K.gn_affine(h, p.g2, p.be2)
-        self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
-                    Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W, a_bound=xb)
+        return self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
+                           Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W, a_bound=xb,
+                          absmax=absmax)
 
-    def attention(self, Y: View, p: AttnPack):
+    def attention(self, Y: View, p: AttnPack, absmax: Optional[torch.Tensor] = None) -> bool:
         B, H, W, C = Y.B, Y.H, Y.W, Y.C
         N = H * W
         sc, sh = K.gn_affine(Y, p.g, p.be)
@@ -266,11 +290,12 @@ class UnetEngine:
                                Hm=H, Wm=W, a_exp=K.f16x3_a_exp(p.gb[0], p.gb[1], N * C // 8))
             exps = K.attention_exps_from_norms(p.qkv_l1, p.qkv_babs, p.gb[0], p.gb[1], N * C // 8)
             K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
-            K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y)
-            return
+            K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y,
+                               absmax=absmax)
+            return absmax is not None
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
-        self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y)
+        return self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y, absmax=absmax)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
@@ -300,6 +325,16 @@ class UnetEngine:
         cur = View(U[0], dc[0], dc[0])
         K.conv_in(x, self.conv_in_w, self.conv_in_b, cur)
 
+        # per-image max |x| of each resampling conv's input, emitted by its producer's epilogue
+        # (the f16x3 down / transposed convs scale by it; one row per resampling conv)
+        amax = None
+        if self.precision == 'f16x3':
+            amax = torch.zeros((2 * L + 1, B), dtype=torch.float32, device=self.device)
+        slots = iter(range(2 * L + 1))
+
+        def bound_slot(needed: bool):
+            return amax[next(slots)] if (needed and amax is not None) else None
+
         # ---------------- down path
         for i in range(L):
             res, att = self.downs[i]
@@ -307,19 +342,23 @@ class UnetEngine:
             H, W = sizes[i]
             final = View(U[i + 1], dc[i + 1], dc[i + 1]) if i < L - 1 else View.full(
                 self._new(B, sizes[i + 1][0], sizes[i + 1][1], co))
+            bnd = None
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
                 tgt = final if (last and self.down_convs[i] is None) else View.full(self._new(B, H, W, co))
-                self.resblock(cur, tgt, rp, temb, temb_ld)
+                slot = bound_slot(last and self.down_convs[i] is not None)
+                bnd = slot if self.resblock(cur, tgt, rp, temb, temb_ld, absmax=None if att else slot) else None
                 if att:
-                    self.attention(tgt, att[li])
+                    bnd = slot if self.attention(tgt, att[li], absmax=slot) else None
                 cur = tgt
             if self.down_convs[i] is not None:
-                w, b, w6 = self.down_convs[i]
-                self.conv([Seg(cur, TAPS4S2, stride=2)], w, w6, b, final, sizes[i + 1][0], sizes[i + 1][1])
+                w, b, w6, w3 = self.down_convs[i]
+                self.resample([Seg(cur, TAPS4S2, stride=2)], (w, w6, w3), b, final, sizes[i + 1][0], sizes[i + 1][1],
+                              bnd)
                 cur = final
 
         # ---------------- mid path
+        bnd = None
         for j, (res, att) in enumerate(self.mids):
             last_mid = j == len(self.mids) - 1
             H, W = cur.H, cur.W
@@ -328,10 +367,12 @@ class UnetEngine:
                     tgt = View(U[L - 1], 0, dc[L - 1])
                 else:
                     tgt = View.full(self._new(B, H, W, rp.co))
-                self.resblock(cur, tgt, rp, temb, temb_ld)
+                has_att = li < len(att)
+                slot = bound_slot(last_mid and li == len(res) - 1 and self.up_convs[0] is not None)
+                bnd = slot if self.resblock(cur, tgt, rp, temb, temb_ld, absmax=None if has_att else slot) else None
                 cur = tgt
-                if li < len(att):
-                    self.attention(cur, att[li])
+                if has_att:
+                    bnd = slot if self.attention(cur, att[li], absmax=slot) else None
 
         # ---------------- up path
         for k, (res, att) in enumerate(self.ups):
@@ -340,19 +381,22 @@ class UnetEngine:
             if self.up_convs[k] is not None:
                 parts, b = self.up_convs[k]
                 dst = View(U[i], 0, dc[i])
-                for (py, px), (taps, w, w6) in zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts):
-                    self.conv([Seg(cur, taps)], w, w6, b, dst, cur.H, cur.W, out_map=(2, 2, py, px))
+                for (py, px), (taps, w, w6, w3) in zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts):
+                    self.resample([Seg(cur, taps)], (w, w6, w3), b, dst, cur.H, cur.W, bnd, out_map=(2, 2, py, px))
             else:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
             cur = View.full(U[i])
             next_in_place = i > 0 and self.up_convs[k + 1] is None
+            next_up = k + 1 < len(self.ups) and self.up_convs[k + 1] is not None
+            bnd = None
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
                 tgt = View(U[i - 1], 0, dc[i - 1]) if (last and next_in_place) else View.full(
                     self._new(B, H, W, rp.co))
-                self.resblock(cur, tgt, rp, temb, temb_ld)
+                slot = bound_slot(last and next_up)
+                bnd = slot if self.resblock(cur, tgt, rp, temb, temb_ld, absmax=None if att else slot) else None
                 if att:
-                    self.attention(tgt, att[li])
+                    bnd = slot if self.attention(tgt, att[li], absmax=slot) else None
                 cur = tgt
 
         # ---------------- head: GN -> SiLU -> conv_out, NCHW output

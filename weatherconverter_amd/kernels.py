@@ -97,7 +97,7 @@ TAPS3 = [(dy, dx) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
 
 def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: Optional[View], Hm: int, Wm: int,
                temb: Optional[torch.Tensor], temb_ld: int, res: Optional[View], out_map,
-               out_nchw: Optional[torch.Tensor], act: int) -> ConvArgs:
+               out_nchw: Optional[torch.Tensor], act: int, absmax: Optional[torch.Tensor] = None) -> ConvArgs:
     a = ConvArgs()
     _req(1 <= len(segs) <= 2, 'conv takes 1 or 2 K segments')
     B = segs[0].view.B
@@ -132,6 +132,10 @@ def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: O
         a.res, a.ldres = res.ptr, res.ldc
     a.osy, a.osx, a.ooy, a.oox = out_map
     a.act = act
+    if absmax is not None:
+        _req(absmax.is_cuda and absmax.dtype == torch.float32 and absmax.is_contiguous() and absmax.numel() == B,
+             'absmax output: float32[B] on the device')
+        a.absmax_out = absmax.data_ptr()
     if out_nchw is not None:
         _req(out_nchw.is_contiguous() and out_nchw.shape[0] == B and out_nchw.shape[1] == N, 'NCHW output shape')
         a.out = out_nchw.data_ptr()
@@ -313,10 +317,12 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
 
 def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                   a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
-                  temb_ld: int = 0, res: Optional[View] = None, act: int = 0):
+                  temb_ld: int = 0, res: Optional[View] = None, act: int = 0,
+                  absmax: Optional[torch.Tensor] = None):
     """3x3 stride-1 conv with a GN(+SiLU) prologue on f16x3 (see wc_conv3x3_f16x3); a_exp from
     f16x3_a_exp of that GroupNorm; a_bound = per-image bound of the residual segment's input
-    (gn_affine(..., bound=True)), required iff w3 packs the residual in fp16."""
+    (gn_affine(..., bound=True)), required iff w3 packs the residual in fp16.  absmax: optional
+    caller-zeroed float32[B], raised to each image's max |out|."""
     _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3', 'f16x3 weight')
     _req((a_bound is not None) == (w3.res_f16 and w3.C1 > 0) or w3.C1 == 0 and not w3.res_f16,
          'a residual packed in fp16 needs an A bound (and only then)')
@@ -324,7 +330,7 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
     _req(segs[0].scale is not None, 'f16x3 needs the GroupNorm prologue')
-    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act)
+    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax)
     TH, BN = x6_tile(w3.N)
     pro = 2 if segs[0].silu else 1
     res_seg = 'true' if len(segs) == 2 else 'false'
@@ -335,21 +341,28 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
 
 
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,
-                     Hm: int, Wm: int, a_exp: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0,
-                     res: Optional[View] = None, out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None):
+                     Hm: int, Wm: int, a_exp: int, a_bound: Optional[torch.Tensor] = None,
+                     temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
+                     out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None,
+                     absmax: Optional[torch.Tensor] = None):
     """conv_igemm's contract with segment 0 on f16x3; the caller guarantees |a| * 2^a_exp <= 2^14 for
     every segment-0 value after the prologue (a GroupNorm bound, f16x3_a_exp, or a bound the
-    producer implies, e.g. an attention output by its V bound)."""
+    producer implies, e.g. an attention output by its V bound), or passes a_bound, a per-image
+    float32[B] bound of those values (e.g. the producer's absmax), which lowers the exponent per
+    image (tiles must not straddle images).  absmax: optional caller-zeroed float32[B] output."""
     _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3n', 'f16x3 weight (natural order)')
     _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
-    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, 0)
+    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, 0, absmax)
     bm, bn = (256, 64) if w3.N <= 64 else (128, 128)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
+    if a_bound is not None:
+        _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == s0.view.B, 'A bound')
+        _req(unib == 'true', 'a per-image A bound needs (Hm*Wm) % BM == 0')
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, 0, true>', 'wc_conv_igemm_f16x3',
            _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
-           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
+           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
 
 
 def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
@@ -368,11 +381,12 @@ def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
 
 
 def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
-               temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None, act: int = 0):
+               temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None, act: int = 0,
+               absmax: Optional[torch.Tensor] = None):
     """3x3 stride-1 conv (+ fused 1x1 residual segment) on bf16x6 split-precision MFMA."""
     _req(w6.data.is_cuda and w6.data.is_contiguous() and w6.order == 'halo', 'x6 weight (halo order)')
     _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
-    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act)
+    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax)
     TH, BN = x6_tile(w6.N)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
@@ -384,11 +398,12 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
 
 def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *, Hm: int,
                   Wm: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
-                  out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0):
+                  out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0,
+                  absmax: Optional[torch.Tensor] = None):
     """conv_igemm's contract (any taps, strides, output map) on bf16x6 split-precision MFMA."""
     _req(w6.data.is_cuda and w6.data.is_contiguous() and w6.order == 'natural', 'x6 weight (natural order)')
     _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
-    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act)
+    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act, absmax)
     bm, bn = (256, 64) if w6.N <= 64 else (128, 128)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)

@@ -73,9 +73,9 @@ def roofline_leg(model, x, t_dev):
         model(x, t_dev)
     torch.cuda.synchronize()
     kernels.profile_conv(False)
-    per = {}
-    for tile, flops, e0, e1 in prof:
-        d = per.setdefault(tile, [0, 0.0, 0.0])
+    per, hbm = {}, {}
+    for tile, flops, e0, e1 in prof:  # HBM-bound launches (GroupNorm statistics) carry bytes, not FLOPs
+        d = (hbm if tile.startswith('gn_') else per).setdefault(tile, [0, 0.0, 0.0])
         d[0] += 1
         d[1] += flops
         d[2] += e0.elapsed_time(e1) * 1e-3
@@ -127,7 +127,22 @@ def roofline_leg(model, x, t_dev):
         'share_of_mfma_event_time': round(sec / max(total_conv, 1e-12), 3),
         'mfma_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1)}
                          for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])},
+        'hbm_kernels': hbm_leg(hbm),
     }
+
+
+def hbm_leg(hbm):
+    """The HBM-bound half of the fused ResBlock: GroupNorm+SiLU are applied in the convs' prologues,
+    so what stays on HBM is the statistics pass (one read of the activation, 4 B/element); its
+    achieved GB/s over every launch of one forward against the 8 TB/s HBM peak."""
+    if not hbm:
+        return None
+    out = {}
+    for k, (n, by, sec) in hbm.items():
+        out[k] = {'launches': n, 'ms': round(sec * 1e3, 3), 'gbytes': round(by / 1e9, 3),
+                  'achieved': round(by / sec / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                  'frac': round(by / sec / 1e9 / HBM_PEAK_GBS, 4)}
+    return out
 
 
 def cpu_baseline_leg(args):

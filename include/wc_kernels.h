@@ -257,6 +257,18 @@ int wc_layernorm_channels(const float* in, int ldi, const float* gamma, const fl
 int wc_noise_embed(const float* noise, const float* ang, int K, float* out, int ldo, int B,
                    int HW, void* stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Training step (diffusion_model/train_ddpm.py:94-114)                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Size (in doubles) of the workspace wc_mse_loss needs. */
+int wc_mse_workspace_doubles(void);
+/* criterion = torch.nn.MSELoss() (train_ddpm.py:177, :107): loss[0] = mean((a - b)^2) over n
+ * elements, fp64 accumulation in a fixed order (deterministic).  grad (optional, same shape) =
+ * grad_scale * (a - b), i.e. d loss / d a for grad_scale = 2/n.  a, b, grad 16-byte aligned. */
+int wc_mse_loss(const float* a, const float* b, int64_t n, float* grad, float grad_scale,
+                double* workspace, float* loss, void* stream);
+
 /* Library identification (for the CPU load test). */
 const char* wc_version(void);
 

@@ -20,7 +20,8 @@ EXPORTS = [
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
-    'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed', 'wc_version'
+    'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
+    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_version'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
 
@@ -77,6 +78,8 @@ _SIGS = {
     'wc_upsample2x_bilinear': [_P, _I, _P, _I, _I, _I, _I, _I, _P],
     'wc_layernorm_channels': [_P, _I, _P, _P, _F, _P, _I, _L, _I, _P],
     'wc_noise_embed': [_P, _P, _I, _P, _I, _I, _I, _P],
+    'wc_mse_workspace_doubles': [],
+    'wc_mse_loss': [_P, _P, _L, _P, _F, _P, _P, _P],
 }
 
 _lib = None

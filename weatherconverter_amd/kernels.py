@@ -425,7 +425,9 @@ def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tenso
     scale = torch.empty((B, C), dtype=torch.float32, device=v.t.device)
     shift = torch.empty_like(scale)
     s = _stream()
-    _native.call('wc_gn_stats', v.ptr, B, HW, C, v.ldc, groups, part.data_ptr(), s)
+    # HBM-bound: the algorithmic bytes are one read of the view (partials are negligible)
+    _timed('gn_stats_rows_kernel' if C // 4 <= 256 else 'gn_stats_kernel', 'wc_gn_stats', 4.0 * B * HW * C,
+           v.ptr, B, HW, C, v.ldc, groups, part.data_ptr(), s)
     if bound:
         bnd = torch.empty((B, ), dtype=torch.float32, device=v.t.device)
         _native.call('wc_gn_finalize_bound', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps,
@@ -528,6 +530,22 @@ def add_noise(x0: torch.Tensor, noise: torch.Tensor, coef_a: torch.Tensor, coef_
     _native.call('wc_add_noise', x0.data_ptr(), noise.data_ptr(), coef_a.contiguous().data_ptr(),
                  coef_b.contiguous().data_ptr(), out.data_ptr(), B, x0.numel() // B, _stream())
     return out
+
+
+def mse_loss(pred: torch.Tensor, target: torch.Tensor, grad: bool = False):
+    """torch.nn.MSELoss() (mean) on the device (wc_mse_loss); returns the 0-dim loss, and with
+    grad=True also d loss / d pred = 2 (pred - target) / n from the same pass."""
+    _req(pred.shape == target.shape and pred.is_cuda and target.is_cuda and pred.dtype == torch.float32
+         and target.dtype == torch.float32, 'mse_loss operands: equal-shape fp32 device tensors')
+    pred, target = pred.contiguous(), target.contiguous()
+    n = pred.numel()
+    lib = _native.load()
+    ws = torch.empty(lib.wc_mse_workspace_doubles(), dtype=torch.float64, device=pred.device)
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    g = torch.empty_like(pred) if grad else None
+    _native.call('wc_mse_loss', pred.data_ptr(), target.data_ptr(), n, _ptr(g), 2.0 / n, ws.data_ptr(),
+                 loss.data_ptr(), _stream())
+    return (loss, g) if grad else loss
 
 
 def philox_normal(shape, device, seed: int, sample0: int = 0, step: int = 0) -> torch.Tensor:

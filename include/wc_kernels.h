@@ -72,16 +72,20 @@ typedef struct wc_conv_args {
     int osy, osx, ooy, oox; /* output position = (my*osy + ooy, mx*osx + oox) */
     int out_nchw;       /* 1: write out[(b*N + n)*Ho*Wo + oy*Wo + ox] (ldo ignored) */
     int act;            /* epilogue activation after bias/temb, before the residual add:
-                           WC_ACT_NONE / WC_ACT_GELU (exact erf) / WC_ACT_SILU; wc_conv_igemm
-                           accepts an activation only with a raw segment 0 (no scale/shift) */
+                           WC_ACT_NONE / WC_ACT_GELU (exact erf) / WC_ACT_SILU / WC_ACT_PRELU /
+                           WC_ACT_TANH01; wc_conv_igemm accepts an activation only with a raw
+                           segment 0 (no scale/shift) */
     float* absmax_out;  /* optional, per image [B] (caller-zeroed): atomically raised to max |out| of
                            the image's written values (a bound for a later f16x3 consumer);
                            split-precision kernels only (the fp32 kernel returns WC_E_ARG) */
+    const float* act_param; /* WC_ACT_PRELU: per-output-channel slopes [N] (else ignored) */
 } wc_conv_args;
 
 #define WC_ACT_NONE 0
 #define WC_ACT_GELU 1
 #define WC_ACT_SILU 2
+#define WC_ACT_PRELU 3  /* v >= 0 ? v : act_param[n] * v (nn.PReLU(num_parameters=N)); fp32 kernel only */
+#define WC_ACT_TANH01 4 /* (tanh(v) + 1) / 2 (Swift-SRGAN output, srgan_model/models.py:92); fp32 only */
 
 /* Replaces: nn.Conv2d 3x3/1x1/4x4-s2 and nn.ConvTranspose2d (per output parity), the GN+SiLU
  * prologue of nn.Sequential(GroupNorm, SiLU, Conv2d), the temb broadcast add, the 1x1
@@ -268,6 +272,17 @@ int wc_mse_workspace_doubles(void);
  * grad_scale * (a - b), i.e. d loss / d a for grad_scale = 2/n.  a, b, grad 16-byte aligned. */
 int wc_mse_loss(const float* a, const float* b, int64_t n, float* grad, float grad_scale,
                 double* workspace, float* loss, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Swift-SRGAN generator (srgan_model/models.py:6-92)                                         */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Depthwise half of SeperableConv2d (:9-17): nn.Conv2d(C, C, K, stride 1, padding K//2, groups=C)
+ * on NHWC views (row strides ldx / ldo in floats), w = torch weight (C, 1, K, K), bias [C] or NULL.
+ * K in {3, 9}; C % 4 == 0 (pad channels with zero weights).  The pointwise half, folded BatchNorm,
+ * PReLU, PixelShuffle and tanh run in wc_conv_igemm (WC_ACT_PRELU / WC_ACT_TANH01, output maps). */
+int wc_dwconv(const float* x, int ldx, float* out, int ldo, const float* w, const float* bias, int B,
+              int H, int W, int C, int K, void* stream);
 
 /* Library identification (for the CPU load test). */
 const char* wc_version(void);

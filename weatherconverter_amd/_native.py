@@ -21,9 +21,9 @@ EXPORTS = [
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
-    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_version'
+    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version'
 ]
-ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
 
 class ConvSeg(ctypes.Structure):
@@ -43,7 +43,8 @@ class ConvArgs(ctypes.Structure):
         ('res', ctypes.c_void_p), ('ldres', ctypes.c_int), ('out', ctypes.c_void_p),
         ('ldo', ctypes.c_int), ('Ho', ctypes.c_int), ('Wo', ctypes.c_int), ('osy', ctypes.c_int),
         ('osx', ctypes.c_int), ('ooy', ctypes.c_int), ('oox', ctypes.c_int),
-        ('out_nchw', ctypes.c_int), ('act', ctypes.c_int), ('absmax_out', ctypes.c_void_p)
+        ('out_nchw', ctypes.c_int), ('act', ctypes.c_int), ('absmax_out', ctypes.c_void_p),
+        ('act_param', ctypes.c_void_p)
     ]
 
 
@@ -80,6 +81,7 @@ _SIGS = {
     'wc_noise_embed': [_P, _P, _I, _P, _I, _I, _I, _P],
     'wc_mse_workspace_doubles': [],
     'wc_mse_loss': [_P, _P, _L, _P, _F, _P, _P, _P],
+    'wc_dwconv': [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
 }
 
 _lib = None

@@ -61,6 +61,7 @@ struct ConvDev {
     int steps0;   // K-steps of segment 0
     int steps;    // total K-steps
     int ntiles_n; // N tiles
+    const float* act_param;  // PReLU slopes [N]
 };
 
 template <int BM, int BN>
@@ -345,6 +346,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvDev p) {
                 if (p.temb) v += p.temb[b * p.temb_ld + n];
                 if constexpr (ACT == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
                 else if constexpr (ACT == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
+                else if constexpr (ACT == WC_ACT_PRELU) v = v >= 0.f ? v : p.act_param[n] * v;
+                else if constexpr (ACT == WC_ACT_TANH01) v = (tanhf(v) + 1.0f) * 0.5f;
                 if (p.ident) {
                     if (p.res) v += p.res[(long)m * p.ldres + n];
                     p.out[(long)m * p.ldo + n] = v;
@@ -384,6 +387,10 @@ int dispatch(const ConvDev& d, int pro, int act, hipStream_t s) {
         if (pro != 0) return WC_E_ARG;
         if (act == WC_ACT_GELU)
             return unib ? launch<BM, BN, 0, true, WC_ACT_GELU>(d, s) : launch<BM, BN, 0, false, WC_ACT_GELU>(d, s);
+        if (act == WC_ACT_PRELU)
+            return unib ? launch<BM, BN, 0, true, WC_ACT_PRELU>(d, s) : launch<BM, BN, 0, false, WC_ACT_PRELU>(d, s);
+        if (act == WC_ACT_TANH01)
+            return unib ? launch<BM, BN, 0, true, WC_ACT_TANH01>(d, s) : launch<BM, BN, 0, false, WC_ACT_TANH01>(d, s);
         return unib ? launch<BM, BN, 0, true, WC_ACT_SILU>(d, s) : launch<BM, BN, 0, false, WC_ACT_SILU>(d, s);
     }
     switch (pro * 2 + (unib ? 1 : 0)) {
@@ -448,7 +455,9 @@ extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo;
     d.Ho = a->Ho; d.Wo = a->Wo; d.osy = a->osy; d.osx = a->osx; d.ooy = a->ooy; d.oox = a->oox;
     d.out_nchw = a->out_nchw;
-    if (a->act < WC_ACT_NONE || a->act > WC_ACT_SILU) return WC_E_ARG;
+    if (a->act < WC_ACT_NONE || a->act > WC_ACT_TANH01) return WC_E_ARG;
+    if (a->act == WC_ACT_PRELU && !a->act_param) return WC_E_ARG;
+    d.act_param = a->act_param;
     d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
               a->Ho == a->Hm && a->Wo == a->Wm;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);

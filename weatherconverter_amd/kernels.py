@@ -97,7 +97,8 @@ TAPS3 = [(dy, dx) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
 
 def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: Optional[View], Hm: int, Wm: int,
                temb: Optional[torch.Tensor], temb_ld: int, res: Optional[View], out_map,
-               out_nchw: Optional[torch.Tensor], act: int, absmax: Optional[torch.Tensor] = None) -> ConvArgs:
+               out_nchw: Optional[torch.Tensor], act: int, absmax: Optional[torch.Tensor] = None,
+               act_param: Optional[torch.Tensor] = None) -> ConvArgs:
     a = ConvArgs()
     _req(1 <= len(segs) <= 2, 'conv takes 1 or 2 K segments')
     B = segs[0].view.B
@@ -132,6 +133,10 @@ def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: O
         a.res, a.ldres = res.ptr, res.ldc
     a.osy, a.osx, a.ooy, a.oox = out_map
     a.act = act
+    if act == _native.ACT_PRELU:
+        _req(act_param is not None and act_param.is_cuda and act_param.dtype == torch.float32
+             and act_param.numel() >= N, 'PReLU slopes: float32[N] on the device')
+        a.act_param = act_param.data_ptr()
     if absmax is not None:
         _req(absmax.is_cuda and absmax.dtype == torch.float32 and absmax.is_contiguous() and absmax.numel() == B,
              'absmax output: float32[B] on the device')
@@ -166,12 +171,13 @@ def _flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int) -> float:
 
 def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
-               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0):
+               out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0,
+               act_param: Optional[torch.Tensor] = None):
     """Implicit-GEMM conv on fp32 MFMA:
-    out[b, my*osy+ooy, mx*osx+oox, n] = sum_k A[m, k] W[n, k] (+bias, temb, res)."""
+    out[b, my*osy+ooy, mx*osx+oox, n] = act(sum_k A[m, k] W[n, k] + bias (+ temb)) (+ res)."""
     _req(w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2, 'packed weight')
     N, ldw = w.shape
-    a = _conv_args(segs, N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act)
+    a = _conv_args(segs, N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act, act_param=act_param)
     a.w, a.ldw = w.data_ptr(), ldw
     # the kernel symbol wc_conv_igemm dispatches to (mirrors dispatch() in csrc/wc_conv.hip)
     bm, bn = (256, 64) if N <= 64 else (128, 128)
@@ -568,6 +574,16 @@ def sgg_update(grad: torch.Tensor, mu: torch.Tensor, sigma: torch.Tensor, lam: f
     _native.call('wc_sgg_update', grad.data_ptr(), mu.data_ptr(), sigma.data_ptr(), xt.data_ptr(), mag.data_ptr(),
                  nb, S, float(lam), float(std[0]), float(std[1]), float(std[2]), int(batch_axis_sum), _stream())
     return xt, mag
+
+
+def dwconv(x: View, w: torch.Tensor, bias: Optional[torch.Tensor], out: View, K: int):
+    """Depthwise KxK conv, padding K//2 (wc_dwconv); w: (C, 1, K, K) or (C, K*K) fp32, C = x.C."""
+    x.check()
+    out.check()
+    _req(out.B == x.B and out.H == x.H and out.W == x.W and out.C == x.C, 'dwconv shapes')
+    w = w.reshape(x.C, K * K).contiguous()
+    _native.call('wc_dwconv', x.ptr, x.ldc, out.ptr, out.ldc, w.data_ptr(), _ptr(bias), x.B, x.H, x.W, x.C, K,
+                 _stream())
 
 
 def avgpool2x2(x: View, out: View):

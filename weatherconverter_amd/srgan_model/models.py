@@ -98,7 +98,7 @@ class SrganEngine:
         self.dev = next(gen.parameters()).device
         self._sig = self._signature()
         with torch.no_grad():
-            self.initial = self._pack_block(gen.initial, pad_in=16)
+            self.initial = self._pack_block(gen.initial, pad_in=32)  # wc_conv_igemm: C % 32
             self.blocks = [(self._pack_block(rb.block1), self._pack_block(rb.block2)) for rb in gen.residual]
             self.convblock = self._pack_block(gen.convblock)
             self.ups = [self._pack_up(u) for u in gen.upsampler]
@@ -176,10 +176,10 @@ class SrganEngine:
         xin = self._new(B, H, W, 4, zero=True)  # NHWC, channels padded to a float4
         xin[..., :Cin] = x.permute(0, 2, 3, 1)
         (sep0, slope0) = self.initial
-        t16 = V.full(self._new(B, H, W, 16, zero=True))  # zero channels beyond Cin for the pointwise K
+        t32 = V.full(self._new(B, H, W, 32, zero=True))  # zero channels beyond Cin for the pointwise K
         C = sep0[2].shape[0]
         initial = V.full(self._new(B, H, W, C))
-        self._sep(V(xin, 0, 4), sep0, slope0, initial, tmp=t16)
+        self._sep(V(xin, 0, 4), sep0, slope0, initial, tmp=t32)
         tmp = V.full(self._new(B, H, W, C))
         cur = initial
         for (p1, s1), (p2, s2) in self.blocks:

@@ -79,6 +79,11 @@ typedef struct wc_conv_args {
                            the image's written values (a bound for a later f16x3 consumer);
                            split-precision kernels only (the fp32 kernel returns WC_E_ARG) */
     const float* act_param; /* WC_ACT_PRELU: per-output-channel slopes [N] (else ignored) */
+    /* Optional GroupNorm tile partials of the output (split-precision kernels; see wc_gn_partials):
+     * the written channels are [gn_c0, gn_c0 + N) of a tensor with gn_ncb*32 channels; the output
+     * rows are pixel blocks gn_p64 .. of the tensor's gn_np64 blocks of 64 per image. */
+    float* gn_part;
+    int gn_ncb, gn_sw, gn_c0, gn_p64, gn_np64;
 } wc_conv_args;
 
 #define WC_ACT_NONE 0
@@ -162,6 +167,17 @@ int wc_gn_finalize(const float* partials, int B, int HW, int C, int groups, cons
 int wc_gn_finalize_bound(const float* partials, int B, int HW, int C, int groups, const float* gamma,
                          const float* beta, float eps, float* scale, float* shift, float* bound,
                          void* stream);
+/* Tile partials (the format the split-precision conv epilogues emit through wc_conv_args.gn_part):
+ * part = float[B][HW/64][ncb][32/sw][2], (mean, M2) over each 64-pixel block x sw-channel sub-slot
+ * of a tensor with ncb*32 channels.  wc_gn_partials fills the slots of the view x (channels
+ * [c0, c0 + C) of that tensor; C, c0 multiples of 32; HW % 64 == 0) from memory. */
+int wc_gn_partials(const float* x, int ldx, int B, int HW, int C, float* part, int ncb, int sw, int c0,
+                   void* stream);
+/* GroupNorm of the view channels [c0, c0 + C) (groups over that range) from tile partials: the
+ * per-(b, c) affine of wc_gn_finalize (and, if bound != NULL, wc_gn_finalize_bound's bound). */
+int wc_gn_finalize_part(const float* part, int B, int HW, int ncb, int sw, int c0, int C, int groups,
+                        const float* gamma, const float* beta, float eps, float* scale, float* shift,
+                        float* bound, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Flash attention, fp32 MFMA (replaces nn.MultiheadAttention's softmax(QK^T/sqrt(d))V,        */

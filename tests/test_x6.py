@@ -690,3 +690,70 @@ def test_igemm_f16x3_resampling_with_producer_bound():
         K.conv_igemm_f16x3([K.Seg(xs, [(0, 0)])], K.pack_f16x3(torch.randn(Co, Ci).cuda(), Ci, ntaps=1,
                            order='natural'), None, K.View.full(torch.empty((B, 12, 12, Co), device='cuda')),
                            Hm=12, Wm=12, a_exp=60, a_bound=am)
+
+
+# ---------------------------------------------------------------- GroupNorm tile partials (epilogue-fused statistics)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('sw', [4, 8, 16, 32])
+def test_gn_tile_partials_match_stats_pass(sw):
+    """GroupNorm affine from tile partials emitted by (a) the halo conv's epilogue, (b) the implicit
+    GEMM's epilogue for the four ConvT parities (pixel-block offsets) into half of a skip buffer and
+    (c) wc_gn_partials for the other half == the stats-pass affine (wc_gn_stats) within fp32 rounding,
+    for the half views and the whole buffer."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.models.engine import pack_convT
+    g = torch.Generator().manual_seed(71)
+    B, H, C = 2, 16, 8 * sw
+    # (a) 3x3 halo conv writing a (B, H, H, C) tensor with partials
+    x = torch.randn((B, H, H, 64), generator=g).cuda() * 2 + 3
+    sc = (1 + 0.2 * torch.randn((B, 64), generator=g)).cuda()
+    sh = (0.2 * torch.randn((B, 64), generator=g)).cuda()
+    w = (torch.randn((C, 9 * 64), generator=g) / 24).cuda()
+    y = torch.empty((B, H, H, C), device='cuda')
+    gp = K.GnPart.attach(y, sw)
+    K.conv3x3_f16x3([K.Seg(K.View.full(x), TAPS3, scale=sc, shift=sh, silu=True)], K.pack_f16x3(w, 64),
+                    (torch.randn(C, generator=g) + 5).cuda(), K.View.full(y), Hm=H, Wm=H, a_exp=6, gn=gp)
+    gamma, beta = (1 + torch.randn(C, generator=g)).cuda(), torch.randn(C, generator=g).cuda()
+    a1 = K.gn_affine(K.View.full(y), gamma, beta, bound=True, part=gp)
+    a0 = K.gn_affine(K.View.full(y), gamma, beta, bound=True)
+    for u, v in zip(a1, a0):
+        assert torch.allclose(u, v, rtol=2e-6, atol=1e-7), (u - v).abs().max()
+    # (b)+(c) skip buffer (B, 2H, 2H, 2C): ConvT parities into [0, C), a raw tensor copied into [C, 2C)
+    U = torch.full((B, 2 * H, 2 * H, 2 * C), float('nan'), device='cuda')
+    gu = K.GnPart.attach(U, sw)
+    xt = K.View.full(torch.randn((B, H, H, 64), generator=g).cuda())
+    wt = torch.randn((64, C, 4, 4), generator=g) / 16
+    for par, (py, px) in enumerate(((0, 0), (0, 1), (1, 0), (1, 1))):
+        taps, wp = pack_convT(wt, py, px)
+        K.conv_igemm_x6([K.Seg(xt, taps)], K.pack_x6(wp.cuda(), 64, 0, ntaps=4, order='natural'), None,
+                        K.View(U, 0, C), Hm=H, Wm=H, out_map=(2, 2, py, px), gn=gu, gn_p64=par * H * H // 64)
+    U[..., C:] = torch.randn((B, 2 * H, 2 * H, C), generator=g).cuda() * 3 - 1
+    K.gn_partials(K.View(U, C, C), gu)
+    for v in (K.View(U, 0, C), K.View(U, C, C), K.View.full(U)):
+        gm, bt = (1 + torch.randn(v.C, generator=g)).cuda(), torch.randn(v.C, generator=g).cuda()
+        a1 = K.gn_affine(v, gm, bt, part=gu)
+        a0 = K.gn_affine(v, gm, bt)
+        for u_, v_ in zip(a1, a0):
+            assert torch.isfinite(u_).all() and torch.allclose(u_, v_, rtol=2e-6, atol=1e-7), (u_ - v_).abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('precision', ['f16x3', 'bf16x6', 'fp32'])
+def test_unet_gn_partials_equal_stats_pass(precision):
+    """The whole UNet (256-cfg at 64 px, B=2) with epilogue GN partials vs one stats pass per GN."""
+    from weatherconverter_amd.diffusion_model.config import model_config
+    from weatherconverter_amd.diffusion_model.models.unet_base import Unet
+    from weatherconverter_amd.synthetic import init_synthetic_
+    mc = model_config(256)
+    mc.im_size = 64
+    net = Unet(mc)
+    init_synthetic_(net, seed=0)
+    net.set_conv_precision(precision)
+    net = net.cuda().eval()
+    x = torch.randn((2, 3, 64, 64), generator=torch.Generator().manual_seed(3)).cuda()
+    with torch.no_grad():
+        y1 = net(x, torch.tensor([400]).cuda())
+        net.engine().gn_partials = False
+        y0 = net(x, torch.tensor([400]).cuda())
+    assert rel_l2(y1, y0) < 2e-6

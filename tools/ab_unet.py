@@ -22,7 +22,12 @@ def no_f3_resample(eng):
     eng.up_convs = [None if u is None else ([(t, w, w6, None) for t, w, w6, _ in u[0]], u[1]) for u in eng.up_convs]
 
 
-VARIANTS = {'base': lambda eng: None, 'no_f3_resample': no_f3_resample}
+def no_gn_partials(eng):
+    """One GroupNorm stats pass per GN instead of the producers' epilogue tile partials."""
+    eng.gn_partials = False
+
+
+VARIANTS = {'base': lambda eng: None, 'no_f3_resample': no_f3_resample, 'no_gn_partials': no_gn_partials}
 
 
 def main():

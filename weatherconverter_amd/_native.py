@@ -18,7 +18,7 @@ EXPORTS = [
     'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
     'wc_conv_igemm_f16x3',
     'wc_gn_num_splits',
-    'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
+    'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version'
@@ -44,7 +44,8 @@ class ConvArgs(ctypes.Structure):
         ('ldo', ctypes.c_int), ('Ho', ctypes.c_int), ('Wo', ctypes.c_int), ('osy', ctypes.c_int),
         ('osx', ctypes.c_int), ('ooy', ctypes.c_int), ('oox', ctypes.c_int),
         ('out_nchw', ctypes.c_int), ('act', ctypes.c_int), ('absmax_out', ctypes.c_void_p),
-        ('act_param', ctypes.c_void_p)
+        ('act_param', ctypes.c_void_p), ('gn_part', ctypes.c_void_p), ('gn_ncb', ctypes.c_int),
+        ('gn_sw', ctypes.c_int), ('gn_c0', ctypes.c_int), ('gn_p64', ctypes.c_int), ('gn_np64', ctypes.c_int)
     ]
 
 
@@ -66,6 +67,8 @@ _SIGS = {
     'wc_gn_stats': [_P, _I, _I, _I, _I, _I, _P, _P],
     'wc_gn_finalize': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P],
     'wc_gn_finalize_bound': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P],
+    'wc_gn_partials': [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P],
+    'wc_gn_finalize_part': [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P],
     'wc_attention_fwd': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_x6': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_f16x3': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],

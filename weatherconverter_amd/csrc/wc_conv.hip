@@ -408,7 +408,7 @@ int dispatch(const ConvDev& d, int pro, int act, hipStream_t s) {
 extern "C" int wc_conv_igemm(const wc_conv_args* a, void* stream) {
     if (!a || !a->w || !a->out) return WC_E_ARG;
     if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
-    if (a->absmax_out) return WC_E_ARG;  // only the split-precision kernels emit output bounds
+    if (a->absmax_out || a->gn_part) return WC_E_ARG;  // output bounds / GN partials: split-precision kernels
     ConvDev d{};
     const wc_conv_seg& s0 = a->seg[0];
     if (!s0.src) return WC_E_ARG;

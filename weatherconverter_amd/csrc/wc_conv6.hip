@@ -72,6 +72,8 @@ struct X6Dev {
     const float* abound;  // f16x3: per-image bound of every A value (segment 1 in fp16), or NULL
     const float* wsinv;   // f16x3: 2^-sW[n] per output channel (else NULL)
     float* absmax;        // optional per-image max |out| (atomic)
+    float* gn_part;       // optional GroupNorm tile partials of the output (wcx6::gn_tile_partials)
+    int gn_ncb, gn_sw, gn_c0, gn_np64;
     int tiles_x, tiles_y, ntiles_n;
 };
 
@@ -429,10 +431,17 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
                 if (p.res) v += p.res[m * p.ldres + n];
                 p.out[m * p.ldo + n] = v;
                 vmax = fmaxf(vmax, fabsf(v));
+                acc[mb][nb][r] = v;
             }
         }
     }
     if (p.absmax) wave_absmax_atomic(p.absmax, b, vmax);  // the whole tile is image b
+    if (p.gn_part) {
+        // this wave's 64 pixels (4 rows x 16 columns of the tile) are pixel block p64 of image b
+        GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
+                 (long)b * p.gn_np64 + (tyi * p.tiles_x + txi) * T::WAVES_M + wm, (p.gn_c0 + n0 + wn * 64) / 32};
+        gn_tile_partials(acc, g, min(2, max(0, (p.N - n0 - wn * 64) / 32)));
+    }
 }
 
 template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false>
@@ -520,6 +529,14 @@ int prepare(const wc_conv_args* a, const void* w, X6Dev& d, int& BN, int& TH) {
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo; d.act = a->act;
     d.a_exp = 0; d.abound = nullptr; d.wsinv = nullptr;
     d.absmax = a->absmax_out;
+    d.gn_part = a->gn_part;
+    if (a->gn_part) {  // N whole 32-channel blocks at a 32-aligned offset; 64-pixel blocks per image
+        const int sw = a->gn_sw;
+        if ((sw != 4 && sw != 8 && sw != 16 && sw != 32) || a->N % 32 || a->gn_c0 % 32 || a->gn_c0 < 0 ||
+            a->gn_c0 + a->N > a->gn_ncb * 32 || a->gn_p64 != 0 || a->gn_np64 * 64 != a->Hm * a->Wm)
+            return WC_E_SHAPE;
+        d.gn_ncb = a->gn_ncb; d.gn_sw = sw; d.gn_c0 = a->gn_c0; d.gn_np64 = a->gn_np64;
+    }
     return WC_OK;
 }
 

@@ -184,7 +184,135 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_kernel(
     }
 }
 
+// ---- tile partials (the format the split-precision conv epilogues emit, wcx6::gn_tile_partials) ----
+// part[((b * np64 + p) * ncb + cb) * (32 / sw) + sub] = (mean, M2) over pixel block p (64 pixels) x
+// the sw channels of sub-slot sub of 32-channel block cb.  One wave per (b, p, cb): lane = channel
+// quad (0..7) + 8 * pixel row (0..7), 8 pixel rows per pass, two passes over the registers.
+__global__ __launch_bounds__(256) void gn_partials_kernel(const float* __restrict__ x, int ldx, int HW, int ncbv,
+                                                          int np64, float* __restrict__ part, int ncb, int sw,
+                                                          int cb_off, long nwaves) {
+    const long wv = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wv >= nwaves) return;
+    const int lane = threadIdx.x & 63;
+    const int cbl = (int)(wv % ncbv);
+    const long bp = wv / ncbv;  // b * np64 + p
+    const int p = (int)(bp % np64);
+    const long b = bp / np64;
+    const int q = lane & 7, row = lane >> 3;
+    const float* base = x + (b * HW + (long)p * 64 + row) * ldx + cbl * 32 + 4 * q;
+    f32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(base + (long)i * 8 * ldx);
+    const int qw = sw / 4;  // quads per sub-slot
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sum += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    for (int o = 1; o < qw; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    sum += __shfl_xor(sum, 8, 64);
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float mean = sum / (64.0f * (float)sw);
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float d = v[i][e] - mean;
+            m2 = fmaf(d, d, m2);
+        }
+    for (int o = 1; o < qw; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+    m2 += __shfl_xor(m2, 8, 64);
+    m2 += __shfl_xor(m2, 16, 64);
+    m2 += __shfl_xor(m2, 32, 64);
+    if (row == 0 && (q % qw) == 0) {
+        float* o = part + ((bp * ncb + cb_off + cbl) * (32 / sw) + q / qw) * 2;
+        o[0] = mean;
+        o[1] = m2;
+    }
+}
+
+// Per (b, group) merge of the tile partials of the view's channels [c0, c0 + C) (Chan, 32 lanes per
+// group in a fixed order), then the same per-(b, c) affine (and optional bound) as gn_finalize.
+__global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(
+    const float* __restrict__ part, int np64, int ncb, int sw, int c0, int C, int G,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* __restrict__ scale,
+    float* __restrict__ shift, float* __restrict__ bound) {
+    const int b = blockIdx.x;
+    const int cpg = C / G;
+    const int spg = cpg / sw;       // sub-slots per group
+    const int spb = 32 / sw;        // sub-slots per 32-channel block
+    __shared__ float s_mean[32], s_rstd[32], s_bound[32];
+    const int g = threadIdx.x / 32;
+    const int j = threadIdx.x % 32;
+    const float n0 = 64.0f * (float)sw;
+    if (g < G) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        const int slot0 = (c0 + g * cpg) / sw;  // first global sub-slot of the group
+        const long items = (long)np64 * spg;
+        for (long it = j; it < items; it += 32) {
+            const int pp = (int)(it / spg);
+            const int gs = slot0 + (int)(it % spg);
+            const float* pr = part + ((((long)b * np64 + pp) * ncb + gs / spb) * spb + gs % spb) * 2;
+            chan_merge(n, mean, m2, n0, pr[0], pr[1]);
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            float nb = __shfl_xor(n, o, 32), mb = __shfl_xor(mean, o, 32), m2b = __shfl_xor(m2, o, 32);
+            chan_merge(n, mean, m2, nb, mb, m2b);
+        }
+        if (j == 0) {
+            const float var = n > 0.f ? m2 / n : 0.f;
+            s_mean[g] = mean;
+            s_rstd[g] = 1.0f / sqrtf(fmaxf(var, 0.f) + eps);
+            s_bound[g] = (fabsf(mean) + sqrtf(fmaxf(n - 1.f, 0.f)) * sqrtf(fmaxf(var, 0.f))) * 1.001f;
+        }
+    }
+    __syncthreads();
+    if (bound && threadIdx.x == 0) {
+        float m = 0.f;
+        for (int gg = 0; gg < G; ++gg) m = fmaxf(m, s_bound[gg]);
+        bound[b] = m;
+    }
+    for (int c = threadIdx.x; c < C; c += GN_THREADS) {
+        const int gg = c / cpg;
+        const float r = s_rstd[gg];
+        const float ga = gamma ? gamma[c] : 1.f;
+        const float be = beta ? beta[c] : 0.f;
+        const float sc = r * ga;
+        scale[(long)b * C + c] = sc;
+        shift[(long)b * C + c] = be - s_mean[gg] * sc;
+    }
+}
+
 }  // namespace
+
+extern "C" int wc_gn_partials(const float* x, int ldx, int B, int HW, int C, float* part, int ncb, int sw, int c0,
+                              void* stream) {
+    if (!x || !part) return WC_E_ARG;
+    if ((sw != 4 && sw != 8 && sw != 16 && sw != 32) || C % 32 || c0 % 32 || c0 < 0 || c0 + C > ncb * 32 ||
+        HW % 64 || ldx % 4 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
+        return WC_E_SHAPE;
+    const int np64 = HW / 64;
+    const long nwaves = (long)B * np64 * (C / 32);
+    hipLaunchKernelGGL(gn_partials_kernel, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), x, ldx, HW, C / 32, np64, part, ncb, sw, c0 / 32,
+                       nwaves);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_gn_finalize_part(const float* part, int B, int HW, int ncb, int sw, int c0, int C, int groups,
+                                   const float* gamma, const float* beta, float eps, float* scale, float* shift,
+                                   float* bound, void* stream) {
+    if (!part || !scale || !shift) return WC_E_ARG;
+    if (groups < 1 || groups > 8 || C % groups || (C / groups) % sw || c0 % sw || HW % 64 || c0 + C > ncb * 32 ||
+        (sw != 4 && sw != 8 && sw != 16 && sw != 32))
+        return WC_E_SHAPE;
+    hipLaunchKernelGGL(gn_finalize_part_kernel, dim3(B), dim3(GN_THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                       part, HW / 64, ncb, sw, c0, C, groups, gamma, beta, eps, scale, shift, bound);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
 
 extern "C" int wc_gn_num_splits(int B, int HW, int C) { return splits_for(B, HW, C); }
 

@@ -54,6 +54,8 @@ struct IgDev {
     const float* abound; // f16x3: per-image bound of the segment-0 values (UNIB only), or NULL
     int a_exp;           // f16x3: static exponent (the per-image bound may lower it)
     float* absmax;       // optional per-image max |out| (atomic)
+    float* gn_part;      // optional GroupNorm tile partials (UNIB only; wcx6::gn_tile_partials)
+    int gn_ncb, gn_sw, gn_c0, gn_p64, gn_np64;
 };
 
 // F3: segment 0 in f16x3 (2 fp16 pieces), else bf16x6; segment 1 is always bf16x6.
@@ -372,6 +374,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                         if constexpr (UNIB) vmax = fmaxf(vmax, fabsf(v));
                         else atomicMax(reinterpret_cast<unsigned*>(p.absmax) + b, __float_as_uint(fabsf(v)));
                     }
+                    acc[mb][nb][r] = v;
                 } else {
                     const int rr = m - b * HWm;
                     const int my = rr / p.Wm;
@@ -388,12 +391,19 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                         if constexpr (UNIB) vmax = fmaxf(vmax, fabsf(v));
                         else atomicMax(reinterpret_cast<unsigned*>(p.absmax) + b, __float_as_uint(fabsf(v)));
                     }
+                    acc[mb][nb][r] = v;
                 }
             }
         }
     }
     if constexpr (UNIB) {
         if (p.absmax) wave_absmax_atomic(p.absmax, b_tile, vmax);
+        if (p.gn_part) {  // this wave's 64 GEMM rows are one pixel block of image b_tile
+            GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
+                     (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + wm,
+                     (p.gn_c0 + n0 + wn * 64) / 32};
+            gn_tile_partials(acc, g, min(2, max(0, (p.N - n0 - wn * 64) / 32)));
+        }
     }
 }
 
@@ -411,6 +421,7 @@ int launch(const IgDev& d, hipStream_t stream) {
 template <int BM, int BN>
 int dispatch(const IgDev& d, int pro, int act, bool f3, hipStream_t s) {
     const bool unib = (d.Hm * d.Wm) % BM == 0;
+    if (d.gn_part && !unib) return WC_E_SHAPE;  // tile partials need tiles inside one image
     if (f3) {  // f16x3: no epilogue activation instantiated
         if (act != WC_ACT_NONE) return WC_E_ARG;
         switch (pro * 2 + (unib ? 1 : 0)) {
@@ -491,6 +502,15 @@ int prepare(const wc_conv_args* a, const void* w6, IgDev& d, long& k) {
     d.steps = (int)(k / BK);
     d.wsinv = nullptr; d.abound = nullptr; d.a_exp = 0;
     d.absmax = a->absmax_out;
+    d.gn_part = a->gn_part;
+    if (a->gn_part) {  // N whole 32-channel blocks at a 32-aligned offset, NHWC output
+        const int sw = a->gn_sw;
+        if ((sw != 4 && sw != 8 && sw != 16 && sw != 32) || a->N % 32 || a->gn_c0 % 32 || a->gn_c0 < 0 ||
+            a->gn_c0 + a->N > a->gn_ncb * 32 || a->out_nchw || (a->Hm * a->Wm) % 64 || a->gn_p64 < 0 ||
+            a->gn_p64 + a->Hm * a->Wm / 64 > a->gn_np64)
+            return WC_E_SHAPE;
+        d.gn_ncb = a->gn_ncb; d.gn_sw = sw; d.gn_c0 = a->gn_c0; d.gn_p64 = a->gn_p64; d.gn_np64 = a->gn_np64;
+    }
     return WC_OK;
 }
 

@@ -96,4 +96,49 @@ WC_DEVICE void wave_absmax_atomic(float* absmax, int b, float m) {
     if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(absmax) + b, __float_as_uint(m));
 }
 
+// GroupNorm tile partials from a wave's 64 x 64 output block (2 x 2 MFMA 32x32 blocks whose
+// acc[mb][nb][r] already hold the FINAL stored values).  For each valid 32-channel column block nb
+// and each sub-slot of sw channels in it: (mean, M2) over the 64 pixels x sw channels, two passes
+// over the registers (no E[x^2] - E[x]^2 cancellation), lane butterflies in a fixed order
+// (deterministic).  Written to part[((pix64 * ncb + cb) * (32 / sw) + sub) * 2 + {0, 1}].
+struct GnTile {
+    float* part;
+    int ncb, sw;  // channel blocks of 32 in the tensor, sub-slot width (4, 8, 16 or 32)
+    long pix64;   // b * np64 + p64 of this wave's 64 pixels
+    int cb0;      // column block of nb = 0
+};
+WC_DEVICE float gn_seg_sum(float v, int sw) {
+    for (int o = 1; o < sw; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+WC_DEVICE void gn_tile_partials(const f32x16 (&acc)[2][2], const GnTile& g, int nvalid) {
+    const int lane = threadIdx.x & 63;
+    const float inv_n = 1.0f / (64.0f * (float)g.sw);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        if (nb >= nvalid) break;
+        float s = 0.f;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s += acc[mb][nb][r];
+        const float mean = gn_seg_sum(s, g.sw) * inv_n;
+        float q = 0.f;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float d = acc[mb][nb][r] - mean;
+                q = fmaf(d, d, q);
+            }
+        const float m2 = gn_seg_sum(q, g.sw);
+        const int c = lane & 31;
+        if (lane < 32 && (c & (g.sw - 1)) == 0) {
+            const long idx = ((g.pix64 * g.ncb + g.cb0 + nb) * (32 / g.sw) + c / g.sw) * 2;
+            g.part[idx] = mean;
+            g.part[idx + 1] = m2;
+        }
+    }
+}
+
 }  // namespace wcx6

@@ -26,6 +26,7 @@ Per attention layer (``unet_base.py:153-161``), in place on Y::
     sc, sh = GN-stats(Y);  qkv = (Y*sc + sh) W_in^T + b_in      (GN-apply fused in the GEMM)
     O = flash-attention(qkv);  Y = Y + O W_out^T + b_out        (residual fused in the epilogue)
 """
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -108,6 +109,8 @@ class UnetEngine:
         self.model = model
         self.device = params[0].device
         self.precision = getattr(model, 'conv_precision', None) or K.default_conv_precision()
+        # GroupNorm statistics from the producers' epilogue tile partials (False: a stats pass per GN)
+        self.gn_partials = os.environ.get('WC_GN_PARTIALS', '1') != '0'
         self._sig = self._signature()
         self._pack()
 
@@ -221,58 +224,105 @@ class UnetEngine:
         return res, att
 
     # ------------------------------------------------------------------ building blocks
-    def _new(self, B, H, W, C) -> torch.Tensor:
-        return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
+    def _new(self, B, H, W, C, gn_sw: Optional[int] = None) -> torch.Tensor:
+        """Scratch activation.  With gn_sw (and a shape the partials tile) it also carries GroupNorm
+        tile partials (kernels.GnPart) that its producers' epilogues fill, so that its GroupNorm
+        consumers finalize from them instead of re-reading the tensor."""
+        t = torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
+        if gn_sw is not None and self.gn_partials and K.GnPart.eligible(t):
+            K.GnPart.attach(t, gn_sw)
+        return t
 
     @staticmethod
-    def conv(segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: Optional[View], H: int, W: int,
-             absmax: Optional[torch.Tensor] = None, **kw) -> bool:
-        """Any conv: bf16x6 implicit GEMM when packed for it, else fp32 MFMA.  Returns True when
-        the per-image output absmax was emitted into `absmax` (split-precision kernels only)."""
+    def _sw(C: int) -> Optional[int]:
+        """Partials sub-slot width for GroupNorm(8) over C channels (and over 2C for the skip buffers)."""
+        cpg = C // 8
+        for sw in (32, 16, 8, 4):
+            if C % 8 == 0 and cpg % sw == 0:
+                return sw
+        return None
+
+    def _gn(self, v: View, gamma, beta, bound: bool = False):
+        """GroupNorm(8) affine of a view: from its tile partials when it has them, else a stats pass."""
+        gp = K.GnPart.of(v)
+        if gp is not None and (v.C // 8) % gp.sw == 0:
+            return K.gn_affine(v, gamma, beta, bound=bound, part=gp)
+        return K.gn_affine(v, gamma, beta, bound=bound)
+
+    def _gn_fill(self, v: Optional[View], fused: bool = False):
+        """Partials of a view written by a kernel that did not emit them from its epilogue."""
+        gp = K.GnPart.of(v)
+        if gp is not None and not fused:
+            K.gn_partials(v, gp)
+
+    def conv(self, segs, w: torch.Tensor, w6: Optional[K.X6Weight], bias, out: Optional[View], H: int, W: int,
+             absmax: Optional[torch.Tensor] = None, gn_p64: int = 0, gn_defer: bool = False, **kw) -> Tuple[bool, bool]:
+        """Any conv: bf16x6 implicit GEMM when packed for it, else fp32 MFMA.  Returns (the per-image
+        output absmax was emitted into `absmax`, the output's GN partials came from the epilogue);
+        partials not emitted are filled by a stats pass unless gn_defer."""
+        gp = K.GnPart.of(out)
+        fused = False
         if w6 is not None:
-            K.conv_igemm_x6(segs, w6, bias, out, Hm=H, Wm=W, absmax=absmax, **kw)
-            return absmax is not None
-        K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
-        return False
+            fused = K.gn_conv_ok(out, gp, w6.N, H, W, 256 if w6.N <= 64 else 128)
+            K.conv_igemm_x6(segs, w6, bias, out, Hm=H, Wm=W, absmax=absmax, gn=gp if fused else None, gn_p64=gn_p64,
+                            **kw)
+        else:
+            K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
+        if not gn_defer:
+            self._gn_fill(out, fused)
+        return absmax is not None and w6 is not None, fused
 
-    @staticmethod
-    def resample(segs, pack, bias, out: View, H: int, W: int, bound: Optional[torch.Tensor], **kw):
+    def resample(self, segs, pack, bias, out: View, H: int, W: int, bound: Optional[torch.Tensor], gn_p64: int = 0,
+                 gn_defer: bool = False, **kw) -> bool:
         """Down-sampling conv / one transposed-conv parity: f16x3 implicit GEMM scaled per image by
-        the producer's absmax when there is one (and the tiles stay within an image), else bf16x6."""
+        the producer's absmax when there is one (and the tiles stay within an image), else bf16x6.
+        Returns whether the output's GN partials came from the epilogue."""
         w, w6, w3 = pack
         if w3 is not None and bound is not None and (H * W) % (256 if w3.N <= 64 else 128) == 0:
-            K.conv_igemm_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=60, a_bound=bound, **kw)
-        else:
-            UnetEngine.conv(segs, w, w6, bias, out, H, W, **kw)
+            gp = K.GnPart.of(out)
+            fused = K.gn_conv_ok(out, gp, w3.N, H, W, 256 if w3.N <= 64 else 128)
+            K.conv_igemm_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=60, a_bound=bound, gn=gp if fused else None,
+                               gn_p64=gn_p64, **kw)
+            if not gn_defer:
+                self._gn_fill(out, fused)
+            return fused
+        return self.conv(segs, w, w6, bias, out, H, W, gn_p64=gn_p64, gn_defer=gn_defer, **kw)[1]
 
-    @staticmethod
-    def conv3(segs, w: torch.Tensor, w6, w3: Optional[K.X6Weight], gb: Tuple[float, float], bias, out: View, H: int,
-              W: int, a_bound: Optional[torch.Tensor] = None, absmax: Optional[torch.Tensor] = None, **kw) -> bool:
+    def conv3(self, segs, w: torch.Tensor, w6, w3: Optional[K.X6Weight], gb: Tuple[float, float], bias, out: View,
+              H: int, W: int, a_bound: Optional[torch.Tensor] = None, absmax: Optional[torch.Tensor] = None,
+              **kw) -> bool:
         """A ResBlock 3x3 stride-1 conv (GN+SiLU prologue): the halo-tiled kernel in f16x3 (bound
         from the GroupNorm affine gb and the group size) or bf16x6 when the grid tiles, else the
-        bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode)."""
+        bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode).  GN partials of `out` are emitted by the
+        split-precision epilogues where they can be, else filled by a stats pass.  Returns whether
+        the absmax was emitted."""
+        gp = K.GnPart.of(out)
         if w3 is not None and K.x6_eligible(segs, w3.N, H, W):
             n_group = H * W * segs[0].view.C // 8
+            fused = K.gn_conv_ok(out, gp, w3.N, H, W)
             K.conv3x3_f16x3(segs, w3, bias, out, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(gb[0], gb[1], n_group),
-                            a_bound=a_bound if w3.res_f16 else None, absmax=absmax, **kw)
+                            a_bound=a_bound if w3.res_f16 else None, absmax=absmax, gn=gp if fused else None, **kw)
+            self._gn_fill(out, fused)
             return absmax is not None
         if w6 is not None and w6[0] is not None and K.x6_eligible(segs, w6[0].N, H, W):
-            K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, absmax=absmax, **kw)
+            fused = K.gn_conv_ok(out, gp, w6[0].N, H, W)
+            K.conv3x3_x6(segs, w6[0], bias, out, Hm=H, Wm=W, absmax=absmax, gn=gp if fused else None, **kw)
+            self._gn_fill(out, fused)
             return absmax is not None
-        return UnetEngine.conv(segs, w, None if w6 is None else w6[1], bias, out, H, W, absmax=absmax, **kw)
+        return self.conv(segs, w, None if w6 is None else w6[1], bias, out, H, W, absmax=absmax, **kw)[0]
 
     def resblock(self, X: View, Y: View, p: ResPack, temb: torch.Tensor, temb_ld: int,
                  absmax: Optional[torch.Tensor] = None) -> bool:
         B, H, W = X.B, X.H, X.W
         xb = None
         if p.w2f3 is not None and p.w2f3.res_f16:
-            sc1, sh1, xb = K.gn_affine(X, p.g1, p.be1, bound=True)  # xb bounds |X| (conv2's residual input)
+            sc1, sh1, xb = self._gn(X, p.g1, p.be1, bound=True)  # xb bounds |X| (conv2's residual input)
         else:
-            sc1, sh1 = K.gn_affine(X, p.g1, p.be1)
-        h = View.full(self._new(B, H, W, p.co))
+            sc1, sh1 = self._gn(X, p.g1, p.be1)
+        h = View.full(self._new(B, H, W, p.co, gn_sw=self._sw(p.co)))
         self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.w1f3, p.gb1, p.b1, h, H, W,
                    temb=temb[:, p.temb_off:], temb_ld=temb_ld)
-        sc2, sh2 = K.gn_affine(h, p.g2, p.be2)
+        sc2, sh2 = self._gn(h, p.g2, p.be2)
         return self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
                            Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W, a_bound=xb,
                           absmax=absmax)
@@ -280,7 +330,7 @@ class UnetEngine:
     def attention(self, Y: View, p: AttnPack, absmax: Optional[torch.Tensor] = None) -> bool:
         B, H, W, C = Y.B, Y.H, Y.W, Y.C
         N = H * W
-        sc, sh = K.gn_affine(Y, p.g, p.be)
+        sc, sh = self._gn(Y, p.g, p.be)
         qkv = self._new(B, H, W, 3 * C)
         o = self._new(B, H, W, C)
         if p.w_in_f3 is not None:
@@ -290,12 +340,15 @@ class UnetEngine:
                                Hm=H, Wm=W, a_exp=K.f16x3_a_exp(p.gb[0], p.gb[1], N * C // 8))
             exps = K.attention_exps_from_norms(p.qkv_l1, p.qkv_babs, p.gb[0], p.gb[1], N * C // 8)
             K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
+            gp = K.GnPart.of(Y)
+            fused = K.gn_conv_ok(Y, gp, p.w_out_f3.N, H, W, 256 if p.w_out_f3.N <= 64 else 128)
             K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y,
-                               absmax=absmax)
+                               absmax=absmax, gn=gp if fused else None)
+            self._gn_fill(Y, fused)
             return absmax is not None
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
-        return self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y, absmax=absmax)
+        return self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y, absmax=absmax)[0]
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
@@ -320,10 +373,13 @@ class UnetEngine:
         for i in range(L):
             h, w = sizes[-1]
             sizes.append((h // 2, w // 2) if m.down_sample[i] else (h, w))
-        U = [self._new(B, sizes[i][0], sizes[i][1], 2 * dc[i]) for i in range(L)]
+        # skip buffers: partials at the sub-slot width of the half (down-path) view, which also tiles
+        # the whole (up-path, 2C-channel) view's groups
+        U = [self._new(B, sizes[i][0], sizes[i][1], 2 * dc[i], gn_sw=self._sw(dc[i])) for i in range(L)]
 
         cur = View(U[0], dc[0], dc[0])
         K.conv_in(x, self.conv_in_w, self.conv_in_b, cur)
+        self._gn_fill(cur)
 
         # per-image max |x| of each resampling conv's input, emitted by its producer's epilogue
         # (the f16x3 down / transposed convs scale by it; one row per resampling conv)
@@ -341,11 +397,12 @@ class UnetEngine:
             co = dc[i + 1]
             H, W = sizes[i]
             final = View(U[i + 1], dc[i + 1], dc[i + 1]) if i < L - 1 else View.full(
-                self._new(B, sizes[i + 1][0], sizes[i + 1][1], co))
+                self._new(B, sizes[i + 1][0], sizes[i + 1][1], co, gn_sw=self._sw(co)))
             bnd = None
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
-                tgt = final if (last and self.down_convs[i] is None) else View.full(self._new(B, H, W, co))
+                tgt = final if (last and self.down_convs[i] is None) else View.full(
+                    self._new(B, H, W, co, gn_sw=self._sw(co)))
                 slot = bound_slot(last and self.down_convs[i] is not None)
                 bnd = slot if self.resblock(cur, tgt, rp, temb, temb_ld, absmax=None if att else slot) else None
                 if att:
@@ -366,7 +423,7 @@ class UnetEngine:
                 if last_mid and li == len(res) - 1 and self.up_convs[0] is None:
                     tgt = View(U[L - 1], 0, dc[L - 1])
                 else:
-                    tgt = View.full(self._new(B, H, W, rp.co))
+                    tgt = View.full(self._new(B, H, W, rp.co, gn_sw=self._sw(rp.co)))
                 has_att = li < len(att)
                 slot = bound_slot(last_mid and li == len(res) - 1 and self.up_convs[0] is not None)
                 bnd = slot if self.resblock(cur, tgt, rp, temb, temb_ld, absmax=None if has_att else slot) else None
@@ -381,8 +438,13 @@ class UnetEngine:
             if self.up_convs[k] is not None:
                 parts, b = self.up_convs[k]
                 dst = View(U[i], 0, dc[i])
-                for (py, px), (taps, w, w6, w3) in zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts):
-                    self.resample([Seg(cur, taps)], (w, w6, w3), b, dst, cur.H, cur.W, bnd, out_map=(2, 2, py, px))
+                np_in = cur.H * cur.W // 64 if (cur.H * cur.W) % 64 == 0 else 0
+                fused = []
+                for par, ((py, px), (taps, w, w6, w3)) in enumerate(zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts)):
+                    # each parity covers a quarter of the output pixels: its own range of pixel blocks
+                    fused.append(self.resample([Seg(cur, taps)], (w, w6, w3), b, dst, cur.H, cur.W, bnd,
+                                               gn_p64=par * np_in, gn_defer=True, out_map=(2, 2, py, px)))
+                self._gn_fill(dst, all(fused) and np_in > 0)
             else:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
             cur = View.full(U[i])
@@ -392,7 +454,7 @@ class UnetEngine:
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
                 tgt = View(U[i - 1], 0, dc[i - 1]) if (last and next_in_place) else View.full(
-                    self._new(B, H, W, rp.co))
+                    self._new(B, H, W, rp.co, gn_sw=self._sw(rp.co)))
                 slot = bound_slot(last and next_up)
                 bnd = slot if self.resblock(cur, tgt, rp, temb, temb_ld, absmax=None if att else slot) else None
                 if att:
@@ -400,7 +462,7 @@ class UnetEngine:
                 cur = tgt
 
         # ---------------- head: GN -> SiLU -> conv_out, NCHW output
-        sc, sh = K.gn_affine(cur, *self.norm_out)
+        sc, sh = self._gn(cur, *self.norm_out)
         out = torch.empty((B, m.model_config.im_channels, S, S2), dtype=torch.float32, device=self.device)
         head = [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)]
         if self.conv_out_f3 is not None:

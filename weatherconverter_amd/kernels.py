@@ -95,10 +95,44 @@ class Seg:
 TAPS3 = [(dy, dx) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
 
 
+@dataclass
+class GnPart:
+    """GroupNorm tile partials of one NHWC tensor (B, H, W, 32*ncb), attached to it as
+    ``t._wc_gn``: float32 [B][HW/64][ncb][32/sw][2] (mean, M2) per 64-pixel block x sw-channel
+    sub-slot.  Written by the split-precision conv epilogues (wc_conv_args.gn_part) or
+    wc_gn_partials; read by wc_gn_finalize_part for any channel range whose groups are whole
+    sub-slots, instead of another pass over the tensor."""
+    part: torch.Tensor
+    sw: int
+    ncb: int
+    np64: int
+
+    @staticmethod
+    def eligible(t: torch.Tensor) -> bool:
+        return t.dim() == 4 and (t.shape[1] * t.shape[2]) % 64 == 0 and t.shape[-1] % 32 == 0
+
+    @staticmethod
+    def attach(t: torch.Tensor, sw: int) -> 'GnPart':
+        _req(GnPart.eligible(t) and sw in (4, 8, 16, 32), 'GN tile partials: HW % 64 == 0, C % 32 == 0')
+        B, H, W, C = t.shape
+        gp = GnPart(torch.empty((B, H * W // 64, C // 32, 32 // sw, 2), dtype=torch.float32, device=t.device), sw,
+                    C // 32, H * W // 64)
+        t._wc_gn = gp
+        return gp
+
+    @staticmethod
+    def of(v: Optional['View']) -> Optional['GnPart']:
+        gp = getattr(v.t, '_wc_gn', None) if v is not None else None
+        return gp if (gp is not None and gp.covers(v)) else None
+
+    def covers(self, v: 'View') -> bool:
+        return getattr(v.t, '_wc_gn', None) is self and v.c0 % 32 == 0 and v.C % 32 == 0
+
+
 def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: Optional[View], Hm: int, Wm: int,
                temb: Optional[torch.Tensor], temb_ld: int, res: Optional[View], out_map,
                out_nchw: Optional[torch.Tensor], act: int, absmax: Optional[torch.Tensor] = None,
-               act_param: Optional[torch.Tensor] = None) -> ConvArgs:
+               act_param: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None, gn_p64: int = 0) -> ConvArgs:
     a = ConvArgs()
     _req(1 <= len(segs) <= 2, 'conv takes 1 or 2 K segments')
     B = segs[0].view.B
@@ -141,6 +175,10 @@ def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: O
         _req(absmax.is_cuda and absmax.dtype == torch.float32 and absmax.is_contiguous() and absmax.numel() == B,
              'absmax output: float32[B] on the device')
         a.absmax_out = absmax.data_ptr()
+    if gn is not None:
+        _req(out is not None and gn.covers(out) and N == out.C, 'GN partials: output view of the partials tensor')
+        a.gn_part, a.gn_ncb, a.gn_sw = gn.part.data_ptr(), gn.ncb, gn.sw
+        a.gn_c0, a.gn_p64, a.gn_np64 = out.c0, gn_p64, gn.np64
     if out_nchw is not None:
         _req(out_nchw.is_contiguous() and out_nchw.shape[0] == B and out_nchw.shape[1] == N, 'NCHW output shape')
         a.out = out_nchw.data_ptr()
@@ -324,7 +362,7 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
 def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                   a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
                   temb_ld: int = 0, res: Optional[View] = None, act: int = 0,
-                  absmax: Optional[torch.Tensor] = None):
+                  absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None):
     """3x3 stride-1 conv with a GN(+SiLU) prologue on f16x3 (see wc_conv3x3_f16x3); a_exp from
     f16x3_a_exp of that GroupNorm; a_bound = per-image bound of the residual segment's input
     (gn_affine(..., bound=True)), required iff w3 packs the residual in fp16.  absmax: optional
@@ -336,7 +374,7 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
     _req(segs[0].scale is not None, 'f16x3 needs the GroupNorm prologue')
-    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax)
+    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax, gn=gn)
     TH, BN = x6_tile(w3.N)
     pro = 2 if segs[0].silu else 1
     res_seg = 'true' if len(segs) == 2 else 'false'
@@ -350,7 +388,7 @@ def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Ten
                      Hm: int, Wm: int, a_exp: int, a_bound: Optional[torch.Tensor] = None,
                      temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
                      out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None,
-                     absmax: Optional[torch.Tensor] = None):
+                     absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None, gn_p64: int = 0):
     """conv_igemm's contract with segment 0 on f16x3; the caller guarantees |a| * 2^a_exp <= 2^14 for
     every segment-0 value after the prologue (a GroupNorm bound, f16x3_a_exp, or a bound the
     producer implies, e.g. an attention output by its V bound), or passes a_bound, a per-image
@@ -358,7 +396,8 @@ def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Ten
     image (tiles must not straddle images).  absmax: optional caller-zeroed float32[B] output."""
     _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3n', 'f16x3 weight (natural order)')
     _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
-    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, 0, absmax)
+    a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, 0, absmax, gn=gn,
+                   gn_p64=gn_p64)
     bm, bn = (256, 64) if w3.N <= 64 else (128, 128)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
@@ -388,11 +427,11 @@ def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
 
 def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None, act: int = 0,
-               absmax: Optional[torch.Tensor] = None):
+               absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None):
     """3x3 stride-1 conv (+ fused 1x1 residual segment) on bf16x6 split-precision MFMA."""
     _req(w6.data.is_cuda and w6.data.is_contiguous() and w6.order == 'halo', 'x6 weight (halo order)')
     _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
-    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax)
+    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax, gn=gn)
     TH, BN = x6_tile(w6.N)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
@@ -405,11 +444,12 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
 def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *, Hm: int,
                   Wm: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,
                   out_map=(1, 1, 0, 0), out_nchw: Optional[torch.Tensor] = None, act: int = 0,
-                  absmax: Optional[torch.Tensor] = None):
+                  absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None, gn_p64: int = 0):
     """conv_igemm's contract (any taps, strides, output map) on bf16x6 split-precision MFMA."""
     _req(w6.data.is_cuda and w6.data.is_contiguous() and w6.order == 'natural', 'x6 weight (natural order)')
     _req(w6.C0 == segs[0].view.C and w6.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'x6 weight segments')
-    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act, absmax)
+    a = _conv_args(segs, w6.N, bias, out, Hm, Wm, temb, temb_ld, res, out_map, out_nchw, act, absmax, gn=gn,
+                   gn_p64=gn_p64)
     bm, bn = (256, 64) if w6.N <= 64 else (128, 128)
     s0 = segs[0]
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
@@ -419,12 +459,36 @@ def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor
            w6.data.numel() * 2, _stream())
 
 
+def gn_partials(v: View, gp: GnPart):
+    """Fill the tile partials of view v (channels [v.c0, v.c0 + v.C) of gp's tensor) from memory."""
+    v.check()
+    _req(gp.covers(v), 'GN partials: view of the partials tensor, 32-channel aligned')
+    _timed('gn_partials_kernel', 'wc_gn_partials', 4.0 * v.B * v.H * v.W * v.C, v.ptr, v.ldc, v.B, v.H * v.W, v.C,
+           gp.part.data_ptr(), gp.ncb, gp.sw, v.c0, _stream())
+
+
+def gn_conv_ok(out: Optional[View], gn: Optional[GnPart], N: int, Hm: int, Wm: int, bm: Optional[int] = None) -> bool:
+    """True when a split-precision conv writing `out` can emit gn's tile partials from its epilogue
+    (mirrors the host checks of wc_conv3x3_x6 / wc_conv_igemm_x6; bm = the implicit GEMM's M tile)."""
+    return (gn is not None and out is not None and gn.covers(out) and N == out.C and N % 32 == 0
+            and (Hm * Wm) % 64 == 0 and (bm is None or (Hm * Wm) % bm == 0))
+
+
 def gn_affine(v: View, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float = 1e-5,
-              groups: int = 8, bound: bool = False):
+              groups: int = 8, bound: bool = False, part: Optional[GnPart] = None):
     """GroupNorm statistics of a view -> per-(b, c) (scale, shift) so that GN(x) = x*scale + shift;
-    with bound=True also the per-image bound of |x| (wc_gn_finalize_bound) as a third result."""
+    with bound=True also the per-image bound of |x| (wc_gn_finalize_bound) as a third result.
+    With `part` (tile partials of v's tensor, already written by v's producers) no pass over v."""
     v.check()
     B, HW, C = v.B, v.H * v.W, v.C
+    if part is not None:
+        _req(part.covers(v) and (C // groups) % part.sw == 0, 'GN partials do not tile these groups')
+        scale = torch.empty((B, C), dtype=torch.float32, device=v.t.device)
+        shift = torch.empty_like(scale)
+        bnd = torch.empty((B, ), dtype=torch.float32, device=v.t.device) if bound else None
+        _native.call('wc_gn_finalize_part', part.part.data_ptr(), B, HW, part.ncb, part.sw, v.c0, C, groups,
+                     _ptr(gamma), _ptr(beta), eps, scale.data_ptr(), shift.data_ptr(), _ptr(bnd), _stream())
+        return (scale, shift, bnd) if bound else (scale, shift)
     lib = _native.load()
     splits = lib.wc_gn_num_splits(B, HW, C)
     part = torch.empty((B, splits, groups, 2), dtype=torch.float32, device=v.t.device)

@@ -216,6 +216,11 @@ int wc_temb(const int64_t* t, int nt, int D, const float* w1, const float* b1, c
 /* conv_in: NCHW input (B, Cin<=4, H, W) → NHWC view, 3x3 pad 1 (unet_base.py:400,456). */
 int wc_conv_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* b,
                int Cout, float* out, int ldo, void* stream);
+/* Head (unet_base.py:448-449,483-485): out = conv3x3(SiLU(x*scale[b,c] + shift[b,c])) + bias for
+ * NO <= 4 output channels, x an NHWC view (C % 16 == 0), out NCHW (B, NO, H, W), pad 1 after the
+ * prologue.  w packed as [C/16][9 taps (ky-major)][16 channels][4 outputs, zero-padded]. */
+int wc_head_conv(const float* x, int ldx, const float* scale, const float* shift, int B, int H, int W,
+                 int C, const float* w, const float* bias, int NO, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Scheduler (linear_noise_scheduler.py)                                                       */

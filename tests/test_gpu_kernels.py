@@ -349,3 +349,22 @@ def test_old_unet_helper_kernels(K):
     o = torch.empty((2, 16, 12, 64)).cuda()
     K.conv_igemm([K.Seg(xn, [(0, 0)])], w.cuda(), b.cuda(), K.View.full(o), Hm=16, Wm=12, act=1)
     assert rel_l2(o.cpu(), F.gelu(F.linear(_nhwc(x), w, b))) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,C,NO', [(2, 32, 48, 64, 3), (1, 20, 13, 32, 4), (3, 16, 16, 128, 1)])
+def test_head_conv_vs_float64(B, H, W, C, NO):
+    """norm_out -> SiLU -> conv_out on wc_head_conv (ragged tiles, strided view) vs float64."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(B * 100 + C)
+    buf = torch.randn((B, H, W, C + 32), generator=g) * 2 + 0.5
+    x = buf[..., 16:16 + C]
+    sc = 1 + 0.3 * torch.randn((B, C), generator=g)
+    sh = 0.3 * torch.randn((B, C), generator=g)
+    w = torch.randn((NO, C, 3, 3), generator=g) / (9 * C)**0.5
+    b = torch.randn(NO, generator=g)
+    a = torch.nn.functional.silu(x.double() * sc.double()[:, None, None, :] + sh.double()[:, None, None, :])
+    ref = torch.nn.functional.conv2d(a.permute(0, 3, 1, 2), w.double(), b.double(), padding=1)
+    out = torch.empty((B, NO, H, W), device='cuda')
+    K.head_conv(K.View(buf.cuda(), 16, C), sc.cuda(), sh.cuda(), K.pack_head(w.cuda()), b.cuda(), out)
+    assert rel_l2(out.cpu(), ref) < 1e-6

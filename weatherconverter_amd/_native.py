@@ -19,7 +19,7 @@ EXPORTS = [
     'wc_conv_igemm_f16x3',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
-    'wc_temb', 'wc_conv_in', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
+    'wc_temb', 'wc_conv_in', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version'
 ]
@@ -74,6 +74,7 @@ _SIGS = {
     'wc_attention_fwd_f16x3': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],
     'wc_temb': [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     'wc_conv_in': [_P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
+    'wc_head_conv': [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P],
     'wc_ddpm_step': [_P, _P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _I, _U, _L, _L, _P],
     'wc_add_noise': [_P, _P, _P, _P, _P, _L, _L, _P],
     'wc_philox_normal': [_P, _L, _L, _U, _L, _L, _P],

@@ -110,6 +110,76 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const float* __restrict__ 
 }
 
 // --------------------------------------------------------------------------------------------
+// Head: norm_out -> SiLU -> conv_out (unet_base.py:448-449,483-485), 3x3 pad-1 conv from an NHWC
+// view with the GroupNorm affine + SiLU applied on load, to NO <= 4 output channels stored NCHW.
+// With 3 outputs an MFMA tile wastes 20x its work; this kernel is HBM-bound instead: one 16x16
+// pixel tile per workgroup (thread = pixel), 16-channel chunks whose 18x18 halo is transformed
+// once into LDS, weights read as wave-uniform scalars.  fp32 FMAs (the reference's precision).
+// w layout: [C/16][9 taps][16 ch][4] (outputs padded to 4).
+// --------------------------------------------------------------------------------------------
+constexpr int HD_T = 16;
+
+__global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict__ x, int ldx,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int B, int H, int W,
+                                                        int C, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, int NO,
+                                                        float* __restrict__ out, int tiles_x, int tiles_y) {
+    __shared__ f32x4 halo[(HD_T + 2) * (HD_T + 2) * 4];
+    const int tile = blockIdx.x;
+    const int tx = tile % tiles_x, ty = (tile / tiles_x) % tiles_y, b = tile / (tiles_x * tiles_y);
+    const int x0 = tx * HD_T, y0 = ty * HD_T;
+    const int px = threadIdx.x % HD_T, py = threadIdx.x / HD_T;
+    float acc0 = bias[0], acc1 = NO > 1 ? bias[1] : 0.f, acc2 = NO > 2 ? bias[2] : 0.f,
+          acc3 = NO > 3 ? bias[3] : 0.f;
+    for (int c0 = 0; c0 < C; c0 += 16) {
+        __syncthreads();  // previous chunk's reads done
+        for (int i = threadIdx.x; i < (HD_T + 2) * (HD_T + 2) * 4; i += 256) {
+            const int q = i & 3, hp = i >> 2;
+            const int hx = hp % (HD_T + 2), hy = hp / (HD_T + 2);
+            const int gy = y0 + hy - 1, gx = x0 + hx - 1;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+                const int c = c0 + 4 * q;
+                const f32x4 a = *reinterpret_cast<const f32x4*>(x + ((long)(b * H + gy) * W + gx) * ldx + c);
+                const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
+                const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(a[e], sc[e], sh[e]));
+            }
+            halo[i] = v;  // zero padding is applied after the prologue, as the reference's conv pads
+        }
+        __syncthreads();
+        const float* wc = w + (long)(c0 / 16) * 9 * 16 * 4;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int hy = py + tap / 3, hx = px + tap % 3;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 a = halo[(hy * (HD_T + 2) + hx) * 4 + q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const f32x4 wv = *reinterpret_cast<const f32x4*>(wc + ((tap * 16) + 4 * q + e) * 4);
+                    acc0 = fmaf(a[e], wv.x, acc0);
+                    acc1 = fmaf(a[e], wv.y, acc1);
+                    acc2 = fmaf(a[e], wv.z, acc2);
+                    acc3 = fmaf(a[e], wv.w, acc3);
+                }
+            }
+        }
+    }
+    const int gx = x0 + px, gy = y0 + py;
+    if (gx < W && gy < H) {
+        const long o = ((long)b * NO * H + gy) * W + gx;
+        const long ps = (long)H * W;
+        out[o] = acc0;
+        if (NO > 1) out[o + ps] = acc1;
+        if (NO > 2) out[o + 2 * ps] = acc2;
+        if (NO > 3) out[o + 3 * ps] = acc3;
+    }
+}
+
+// --------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. 2011) + Box-Muller.  Counter = (element/4, global sample, step, 0),
 // key = seed.  Independent of batch sharding by construction.
 // --------------------------------------------------------------------------------------------
@@ -311,6 +381,22 @@ extern "C" int wc_conv_in(const float* x, int B, int Cin, int H, int W, const fl
     long total = (long)B * H * W * (Cout / 4);
     hipLaunchKernelGGL(conv_in_kernel, dim3(grid_for(total, 256)), dim3(256), lds,
                        reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, Cout, out, ldo);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_head_conv(const float* x, int ldx, const float* scale, const float* shift, int B, int H,
+                            int W, int C, const float* w, const float* bias, int NO, float* out, void* stream) {
+    if (!x || !scale || !shift || !w || !bias || !out) return WC_E_ARG;
+    if (NO < 1 || NO > 4 || C < 16 || C % 16 || ldx % 4 || ldx < C) return WC_E_SHAPE;
+    if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(scale) |
+          reinterpret_cast<uintptr_t>(shift)) & 15) != 0)
+        return WC_E_SHAPE;
+    const int tiles_x = (W + HD_T - 1) / HD_T, tiles_y = (H + HD_T - 1) / HD_T;
+    const long n = (long)B * tiles_x * tiles_y;
+    if (n >= (1L << 31)) return WC_E_SHAPE;
+    hipLaunchKernelGGL(head_conv_kernel, dim3((unsigned)n), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x,
+                       ldx, scale, shift, B, H, W, C, w, bias, NO, out, tiles_x, tiles_y);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -155,6 +155,10 @@ class UnetEngine:
                 self.conv_out_f3 = K.pack_f16x3(self.conv_out_w, m.conv_out.in_channels, order='natural')
                 self.norm_out_gb = (float(m.norm_out.weight.abs().max()), float(m.norm_out.bias.abs().max()))
             self.conv_out_b = m.conv_out.bias.detach().float().contiguous()
+            # <= 4 output channels: the dedicated HBM-bound head kernel (an MFMA tile would waste 20x)
+            self.conv_out_head = None
+            if m.conv_out.out_channels <= 4 and m.conv_out.in_channels % 16 == 0:
+                self.conv_out_head = K.pack_head(m.conv_out.weight)
             tp = m.t_proj
             self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
                           tp[2].weight.detach().float().contiguous(), tp[2].bias.detach().float().contiguous()]
@@ -465,7 +469,9 @@ class UnetEngine:
         sc, sh = self._gn(cur, *self.norm_out)
         out = torch.empty((B, m.model_config.im_channels, S, S2), dtype=torch.float32, device=self.device)
         head = [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)]
-        if self.conv_out_f3 is not None:
+        if self.conv_out_head is not None:
+            K.head_conv(cur, sc, sh, self.conv_out_head, self.conv_out_b, out)
+        elif self.conv_out_f3 is not None:
             K.conv_igemm_f16x3(head, self.conv_out_f3, self.conv_out_b, None, Hm=S, Wm=S2, out_nchw=out,
                                a_exp=K.f16x3_a_exp(*self.norm_out_gb, S * S2 * cur.C // 8))
         else:

@@ -577,6 +577,28 @@ def conv_in(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: View):
                  _stream())
 
 
+def pack_head(w: torch.Tensor) -> torch.Tensor:
+    """conv_out weight (NO, C, 3, 3) -> wc_head_conv layout [C/16][9][16][4] (outputs zero-padded)."""
+    NO, C = w.shape[0], w.shape[1]
+    _req(NO <= 4 and C % 16 == 0 and tuple(w.shape[2:]) == (3, 3), 'head conv: <= 4 outputs, C % 16 == 0, 3x3')
+    wp = torch.zeros((C // 16, 9, 16, 4), dtype=torch.float32, device=w.device)
+    wt = w.detach().float().reshape(NO, C // 16, 16, 9)  # [n][chunk][c][tap]
+    wp[..., :NO] = wt.permute(1, 3, 2, 0)
+    return wp.contiguous()
+
+
+def head_conv(x: View, scale: torch.Tensor, shift: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor,
+              out: torch.Tensor):
+    """GN-affine + SiLU + 3x3 conv to <= 4 channels, NCHW output (wc_head_conv)."""
+    x.check()
+    B, NO = out.shape[0], out.shape[1]
+    _req(out.is_contiguous() and out.shape == (x.B, NO, x.H, x.W) and bias.numel() >= NO, 'head output shape')
+    _req(w_packed.shape == (x.C // 16, 9, 16, 4), 'head weight layout')
+    _timed('head_conv_kernel', 'wc_head_conv', 2.0 * x.B * x.H * x.W * NO * 9 * x.C if PROFILE is not None else 0.0,
+           x.ptr, x.ldc, scale.data_ptr(), shift.data_ptr(), x.B, x.H, x.W, x.C, w_packed.data_ptr(),
+           bias.data_ptr(), NO, out.data_ptr(), _stream())
+
+
 def ddpm_step(x: torch.Tensor, eps: torch.Tensor, out: torch.Tensor, beta: float, s1m: float, sqrt_alpha: float,
               sigma: float, *, z: Optional[torch.Tensor] = None, mode: int = _native.NOISE_NONE, seed: int = 0,
               sample0: int = 0, step: int = 0, sz_out: Optional[torch.Tensor] = None):

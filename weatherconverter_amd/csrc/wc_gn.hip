@@ -231,40 +231,52 @@ __global__ __launch_bounds__(256) void gn_partials_kernel(const float* __restric
     }
 }
 
-// Per (b, group) merge of the tile partials of the view's channels [c0, c0 + C) (Chan, 32 lanes per
-// group in a fixed order), then the same per-(b, c) affine (and optional bound) as gn_finalize.
-__global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(
+// Per (b, group) merge of the tile partials of the view's channels [c0, c0 + C): one wave per group
+// (workgroup = image).  Every partial covers the same n0 = 64*sw values, so the merge is the exact
+// equal-count identity  mean = avg(m_i),  M2 = sum(M2_i) + n0 * sum((m_i - mean)^2)  in two
+// division-free passes over the partials, lane butterflies in a fixed order (deterministic); then
+// the same per-(b, c) affine (and optional bound) as gn_finalize.
+constexpr int GNF_THREADS = 512;
+
+__global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
     const float* __restrict__ part, int np64, int ncb, int sw, int c0, int C, int G,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* __restrict__ scale,
     float* __restrict__ shift, float* __restrict__ bound) {
     const int b = blockIdx.x;
     const int cpg = C / G;
-    const int spg = cpg / sw;       // sub-slots per group
-    const int spb = 32 / sw;        // sub-slots per 32-channel block
-    __shared__ float s_mean[32], s_rstd[32], s_bound[32];
-    const int g = threadIdx.x / 32;
-    const int j = threadIdx.x % 32;
+    const int spg = cpg / sw;  // sub-slots per group
+    const int spb = 32 / sw;   // sub-slots per 32-channel block
+    __shared__ float s_mean[8], s_rstd[8], s_bound[8];
+    const int g = threadIdx.x >> 6;
+    const int j = threadIdx.x & 63;
     const float n0 = 64.0f * (float)sw;
     if (g < G) {
-        float n = 0.f, mean = 0.f, m2 = 0.f;
         const int slot0 = (c0 + g * cpg) / sw;  // first global sub-slot of the group
-        const long items = (long)np64 * spg;
-        for (long it = j; it < items; it += 32) {
-            const int pp = (int)(it / spg);
-            const int gs = slot0 + (int)(it % spg);
-            const float* pr = part + ((((long)b * np64 + pp) * ncb + gs / spb) * spb + gs % spb) * 2;
-            chan_merge(n, mean, m2, n0, pr[0], pr[1]);
+        const int items = np64 * spg;
+        auto at = [&](int it) -> const float* {
+            const int pp = it / spg;
+            const int gs = slot0 + it % spg;
+            return part + ((((long)b * np64 + pp) * ncb + gs / spb) * spb + gs % spb) * 2;
+        };
+        float sm = 0.f;
+        for (int it = j; it < items; it += 64) sm += at(it)[0];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+        const float mean = sm / (float)items;
+        float q = 0.f;
+        for (int it = j; it < items; it += 64) {
+            const float* pr = at(it);
+            const float d = pr[0] - mean;
+            q += fmaf(n0 * d, d, pr[1]);
         }
 #pragma unroll
-        for (int o = 16; o > 0; o >>= 1) {
-            float nb = __shfl_xor(n, o, 32), mb = __shfl_xor(mean, o, 32), m2b = __shfl_xor(m2, o, 32);
-            chan_merge(n, mean, m2, nb, mb, m2b);
-        }
+        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
         if (j == 0) {
-            const float var = n > 0.f ? m2 / n : 0.f;
+            const float n = n0 * (float)items;
+            const float var = fmaxf(q / n, 0.f);  // biased, as torch
             s_mean[g] = mean;
-            s_rstd[g] = 1.0f / sqrtf(fmaxf(var, 0.f) + eps);
-            s_bound[g] = (fabsf(mean) + sqrtf(fmaxf(n - 1.f, 0.f)) * sqrtf(fmaxf(var, 0.f))) * 1.001f;
+            s_rstd[g] = 1.0f / sqrtf(var + eps);
+            s_bound[g] = (fabsf(mean) + sqrtf(fmaxf(n - 1.f, 0.f)) * sqrtf(var)) * 1.001f;
         }
     }
     __syncthreads();
@@ -273,7 +285,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_finalize_part_kernel(
         for (int gg = 0; gg < G; ++gg) m = fmaxf(m, s_bound[gg]);
         bound[b] = m;
     }
-    for (int c = threadIdx.x; c < C; c += GN_THREADS) {
+    for (int c = threadIdx.x; c < C; c += GNF_THREADS) {
         const int gg = c / cpg;
         const float r = s_rstd[gg];
         const float ga = gamma ? gamma[c] : 1.f;
@@ -308,7 +320,7 @@ extern "C" int wc_gn_finalize_part(const float* part, int B, int HW, int ncb, in
     if (groups < 1 || groups > 8 || C % groups || (C / groups) % sw || c0 % sw || HW % 64 || c0 + C > ncb * 32 ||
         (sw != 4 && sw != 8 && sw != 16 && sw != 32))
         return WC_E_SHAPE;
-    hipLaunchKernelGGL(gn_finalize_part_kernel, dim3(B), dim3(GN_THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(gn_finalize_part_kernel, dim3(B), dim3(GNF_THREADS), 0, reinterpret_cast<hipStream_t>(stream),
                        part, HW / 64, ncb, sw, c0, C, groups, gamma, beta, eps, scale, shift, bound);
     WC_CHECK_LAUNCH();
     return WC_OK;

@@ -41,6 +41,8 @@
 // Fused work (reference unet_base.py ResBlock, :87-109 / :146-150), as in wc_conv.hip:
 // prologue SiLU(v*scale[b,c] + shift[b,c]) with zero padding applied after it; epilogue
 // + bias[n] + temb[b,n], activation, + residual view, NHWC store.
+#include <stdlib.h>
+
 #include "wc_x6.hpp"
 
 namespace {
@@ -79,7 +81,10 @@ struct X6Dev {
 
 // F3: segment 0 in f16x3 (2 pieces), else bf16x6 (3 pieces).  R16: segment 1 in f16x3 too (needs
 // the per-image bound), else bf16x6.
-template <int TH, int BN, bool RES, bool F3, bool R16>
+// GL: weights staged by LDS-DMA (global_load_lds_dwordx4 straight into the LDS image the host
+// pre-laid out) at three taps (one halo row) per K-step: 36 MFMAs per wave between barriers and
+// no weight registers; else register-staged, one tap per K-step.
+template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
@@ -95,7 +100,7 @@ struct X6Tile {
     static constexpr int BSTEP0 = 2 * NP0 * BPLANE;      // one segment-0 weight step
     static constexpr int BSTEP1 = 2 * NP1 * BPLANE;      // one segment-1 weight step
     // taps per K-step (2 for f16x3 measured slower: 302 vs 322 TF/s, larger LDS weight stage)
-    static constexpr int TPS = 1;
+    static constexpr int TPS = GL ? 3 : 1;
     static constexpr int NMT = (9 + TPS - 1) / TPS;       // K-steps per 16-channel chunk
     static constexpr int BSTEPM = TPS * BSTEP0;           // weight bytes of a full segment-0 K-step
     static constexpr int BSTAGE = (RES && BSTEP1 > BSTEPM) ? BSTEP1 : BSTEPM;  // LDS weight buffer
@@ -116,9 +121,9 @@ WC_DEVICE int row_dx(int r) {
 }
 
 // PRO: 0 = raw segment 0, 1 = GN affine, 2 = GN affine + SiLU.  RES: segment 1 present.
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL>
 __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
-    using T = X6Tile<TH, BN, RES, F3, R16>;
+    using T = X6Tile<TH, BN, RES, F3, R16, GL>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
 
     f32x4 rh[T::H_PER_T];
     f32x4 rsc = {1.f, 1.f, 1.f, 1.f}, rsh = {0.f, 0.f, 0.f, 0.f};
-    u32x4 rb[T::B_PER_T];
+    u32x4 rb[GL ? 1 : T::B_PER_T];
 
     auto load_halo0 = [&](int c) {
 #pragma unroll
@@ -249,7 +254,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             items = nt * T::BSTEP0 / 16;
         }
     };
+    // LDS-DMA: each wave-instruction writes 1 KiB lane-linearly at a wave-uniform LDS base; the
+    // host's weight image is already in LDS order, so item i goes to byte 16 i of the stage
+    auto glds_b = [&](int s) {
+        unsigned base;
+        int items;
+        step_w(s, base, items);
+        const unsigned char* src = reinterpret_cast<const unsigned char*>(p.w6) + base + tid * 16;
+        unsigned char* dst = smem + 2 * T::HSTAGE + (s & 1) * T::BSTAGE + wave * 1024;
+#pragma unroll
+        for (int j = 0; j < T::B_PER_T; ++j) {
+            if (j < T::B_FULL || tid + NT * j < items)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + j * NT * 16),
+                                                 (__attribute__((address_space(3))) void*)(dst + j * NT * 16), 16, 0, 0);
+        }
+    };
     auto load_b = [&](int s) {
+        if constexpr (GL) return;
         unsigned base;
         int items;
         step_w(s, base, items);
@@ -261,6 +282,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
         }
     };
     auto write_b = [&](int bs, int s) {
+        if constexpr (GL) return;
         unsigned char* base = smem + 2 * T::HSTAGE + bs * T::BSTAGE;
         unsigned off_unused;
         int items;
@@ -357,6 +379,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
 
     // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
     load_halo0(0);
+    if constexpr (GL) glds_b(0);
     load_b(0);
     write_halo(0, true);
     write_b(0, 0);
@@ -367,6 +390,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
 #pragma unroll
         for (int mt = 0; mt < T::NMT; ++mt) {
             const bool more = s + 1 < S;
+            if constexpr (GL) {
+                if (more) glds_b(s + 1);  // buffer (s+1)&1 was last read in step s-1
+            }
             if (more) load_b(s + 1);
             // The next chunk's halo loads go out one K-step before the last, after that step's
             // weight loads: vmcnt drains in issue order, so a halo load issued earlier would be
@@ -394,6 +420,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             const int hs = (p.nck0 + c) & 1;
             const bool more = s + 1 < S;
             if (more) {
+                if constexpr (GL) glds_b(s + 1);
                 load_b(s + 1);
                 load_halo1(c + 1);
             }
@@ -444,12 +471,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false>
 int launch6(const X6Dev& d, hipStream_t stream) {
-    using T = X6Tile<TH, BN, RES, F3, R16>;
+    using T = X6Tile<TH, BN, RES, F3, R16, GL>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -459,13 +486,34 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16>), grid, dim3(NT), T::LDS, stream, p);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
+// f16x3 weight staging: LDS-DMA at three taps per K-step (default) or registers at one tap
+// (WC_CONV3_GL=0, kept for A/B measurement)
+bool conv3_glds() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_GL");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+}
+
 template <int TH, int BN>
 int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
+    if (f3 && conv3_glds()) {
+        const bool r16 = res && d.abound != nullptr;
+        switch ((pro - 1) * 3 + (res ? (r16 ? 2 : 1) : 0)) {
+            case 0: return launch6<TH, BN, 1, false, true, false, true>(d, s);
+            case 1: return launch6<TH, BN, 1, true, true, false, true>(d, s);
+            case 2: return launch6<TH, BN, 1, true, true, true, true>(d, s);
+            case 3: return launch6<TH, BN, 2, false, true, false, true>(d, s);
+            case 4: return launch6<TH, BN, 2, true, true, false, true>(d, s);
+            default: return launch6<TH, BN, 2, true, true, true, true>(d, s);
+        }
+    }
     if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here
         const bool r16 = res && d.abound != nullptr;
         switch ((pro - 1) * 3 + (res ? (r16 ? 2 : 1) : 0)) {

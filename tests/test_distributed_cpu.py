@@ -41,7 +41,8 @@ def _worker(rank, world, port, total, q):
         full_noise = torch.randn((total, 3, 4, 4))
         x_local = x_local + full_noise[start:start + count]
         out = gather_samples(x_local.contiguous(), total)
-        q.put((rank, out))
+        # by value: a shared-memory tensor handle can outlive this worker's fd sharer
+        q.put((rank, out.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -55,7 +56,7 @@ def test_gloo_world2_gather_equals_single_rank(total):
     procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=120) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

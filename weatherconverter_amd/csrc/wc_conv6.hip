@@ -491,12 +491,12 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     return WC_OK;
 }
 
-// f16x3 weight staging: LDS-DMA at three taps per K-step (default) or registers at one tap
-// (WC_CONV3_GL=0, kept for A/B measurement)
+// f16x3 weight staging: registers at one tap per K-step (default) or LDS-DMA at three taps
+// (WC_CONV3_GL=1, kept for A/B measurement: 292 vs 318 TF/s aggregate, tools/gpu_ab_conv.sh)
 bool conv3_glds() {
     static const int v = [] {
         const char* e = getenv("WC_CONV3_GL");
-        return (e && e[0] == '0') ? 0 : 1;
+        return (e && e[0] == '1') ? 1 : 0;
     }();
     return v != 0;
 }

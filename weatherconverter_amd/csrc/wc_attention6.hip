@@ -153,22 +153,28 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     }
 
     // ---- staging coordinates ----
-    // K: item i -> key i / (D/4), dims 4*(i % (D/4)) .. +3
+    // K: item i -> key i / (D/4), dims 4*(i % (D/4)) .. +3 (a wave reads whole key rows).  In LDS
+    // plane pl = (16-dim chunk, k-half) the key's 16-byte slot is key ^ (pl & 15): the 16 lanes of a
+    // ds_write_b64 group (one key, 8 planes x 2 halves) then hit 16 distinct bank pairs, where the
+    // unswizzled image (planes 512 B apart) put them on one bank pair.
     int k_goff[A::KPT], k_key[A::KPT], k_lds[A::KPT];
 #pragma unroll
     for (int j = 0; j < A::KPT; ++j) {
         const int i = tid + NT * j;
         const int key = i / (D / 4), d4 = i % (D / 4);
+        const int pl = (d4 >> 2) * 2 + ((d4 >> 1) & 1);
         k_key[j] = key;
         k_goff[j] = key * ldq + kcol + 4 * d4;
-        k_lds[j] = (((d4 >> 2) * 2 + ((d4 >> 1) & 1)) * KT + key) * 16 + (d4 & 1) * 8;
+        k_lds[j] = (pl * KT + (key ^ (pl & 15))) * 16 + (d4 & 1) * 8;
     }
-    // V: item i -> keys 2kp, 2kp+1 and dims 4*d4 .. +3
+    // V: item i -> keys 2kp, 2kp+1 (kp = i % 16) and dims 4*d4 .. +3 (d4 = i / 16): a 32-lane
+    // ds_write_b32 group covers 16 key pairs x 2 dim quads, 2-way on the banks (free), where
+    // dim-quad-major items put 32 lanes on 4 banks.
     int v_goff[A::VPT], v_key[A::VPT], v_pos[A::VPT], v_d[A::VPT];
 #pragma unroll
     for (int j = 0; j < A::VPT; ++j) {
         const int i = tid + NT * j;
-        const int kp = i / (D / 4), d4 = i % (D / 4);
+        const int kp = i % (KT / 2), d4 = i / (KT / 2);
         v_key[j] = i < A::VITEMS ? 2 * kp : 1 << 20;  // invalid items never load nor store
         v_goff[j] = 2 * kp * ldq + vcol + 4 * d4;
         v_pos[j] = key_pos(2 * kp);
@@ -261,18 +267,27 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
             u32x4 kf[NP];
 #pragma unroll
             for (int pc = 0; pc < NP; ++pc)
-                kf[pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE + l32 * 16);
+                kf[pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE +
+                                                          (l32 ^ ((ch * 2 + half) & 15)) * 16);
             mfma_split<F3>(s, kf, qp[ch]);
         }
 
         // ---- online softmax over keys, per query (lane) ----
         float mloc = -INFINITY;
+        if (kv0 + KT <= N) {  // full tile (wave-uniform): no key mask
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            const float v = (key < N) ? s[r] * score_mul : -INFINITY;
-            s[r] = v;
-            mloc = fmaxf(mloc, v);
+            for (int r = 0; r < 16; ++r) {
+                s[r] *= score_mul;
+                mloc = fmaxf(mloc, s[r]);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const float v = (key < N) ? s[r] * score_mul : -INFINITY;
+                s[r] = v;
+                mloc = fmaxf(mloc, v);
+            }
         }
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         const float m_new = fmaxf(m_run, mloc);
@@ -287,10 +302,13 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
         lsum += __shfl_xor(lsum, 32, 64);
         l_run = l_run * alpha + lsum;
         m_run = m_new;
+        // alpha == 1 exactly when no lane's running max moved: skipping the multiply is then exact
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
 #pragma unroll
-        for (int d = 0; d < A::NDB; ++d)
+            for (int d = 0; d < A::NDB; ++d)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+                for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        }
 
         // ---- O^T += V^T P^T: two 16-key chunks ----
 #pragma unroll

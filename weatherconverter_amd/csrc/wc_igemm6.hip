@@ -18,6 +18,8 @@
 //   * LDS images are [piece][k-half][row][8 bf16] (16-byte row slots): the ds_read_b128 lane
 //     groups {0-3,12-15,20-27} / {4-11,16-19,28-31} read 16 rows distinct mod 16 ->
 //     conflict-free with no swizzle.
+#include <type_traits>
+
 #include "wc_x6.hpp"
 
 namespace {
@@ -47,6 +49,7 @@ struct IgDev {
     int Ho, Wo, osy, osx, ooy, oox, out_nchw;
     int ident;
     int steps0, steps;
+    int cpt;             // 16-channel chunks per tap of segment 0
     int ntiles_n;
     float ascale;        // f16x3: 2^a_exp applied to the A values before splitting (else 1)
     float ainv;          // 2^-a_exp
@@ -58,17 +61,19 @@ struct IgDev {
     int gn_ncb, gn_sw, gn_c0, gn_p64, gn_np64;
 };
 
-// F3: segment 0 in f16x3 (2 fp16 pieces), else bf16x6; segment 1 is always bf16x6.
-template <int BM, int BN, bool F3>
+// F3: segment 0 in f16x3 (2 fp16 pieces), else bf16x6; segment 1 is always bf16x6.  NPL: LDS
+// planes per operand stage (piece x k-half): 4 for an f16x3 launch without segment 1, else 6.
+template <int BM, int BN, bool F3, int NPL>
 struct IgTile {
     static constexpr int WAVES_M = BM / 64;
     static constexpr int WAVES_N = BN / 64;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
+    static_assert(NPL == 6 || (F3 && NPL == 4), "4-plane stages hold f16x3 segment-0 steps only");
     static constexpr int A_PER_T = BM * (BK / 4) / NT;  // float4 per thread per step
     static constexpr int APLANE = BM * 16;              // bytes of one (piece, k-half) plane
     static constexpr int BPLANE = BN * 16;
-    static constexpr int ASTAGE = 6 * APLANE;
-    static constexpr int BSTAGE = 6 * BPLANE;
+    static constexpr int ASTAGE = NPL * APLANE;
+    static constexpr int BSTAGE = NPL * BPLANE;
     static constexpr int STAGE = ASTAGE + BSTAGE;
     static constexpr int BSTEP0 = (F3 ? 4 : 6) * BPLANE;  // weight bytes of a segment-0 step
     static constexpr int BSTEP1 = 6 * BPLANE;             // ... of a segment-1 step
@@ -78,9 +83,9 @@ struct IgTile {
 
 // PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU.  UNIB: tiles never straddle images.  ACT: epilogue
 // activation (template, see wc_conv.hip).  F3: segment 0 on f16x3 (caller bounds |a| 2^a_exp).
-template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3>
+template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
-    using T = IgTile<BM, BN, F3>;
+    using T = IgTile<BM, BN, F3, NPL>;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
 
     const int tid = threadIdx.x;
@@ -145,85 +150,102 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.src0);
     const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
 
-    f32x4 ra[T::A_PER_T];
-    u32x4 rb[T::B_PER_T];
-    f32x4 rsc[UNIB ? 1 : T::A_PER_T], rsh[UNIB ? 1 : T::A_PER_T];
-    unsigned aval = 0;
-    int ky = 0, kx = 0, c0 = 0, c1 = 0, bstep = 0;
+    // Two register stages: the loads of K-step s + 2 are issued before the MFMAs of step s and
+    // written to LDS after those of step s + 1, so a load has two K-steps (not one) to land.
+    constexpr int NSC = UNIB ? 1 : T::A_PER_T;
+    f32x4 ra[2][T::A_PER_T];
+    u32x4 rb[2][T::B_PER_T];
+    f32x4 rsc[2][NSC], rsh[2][NSC];
+    unsigned aval0 = 0u, aval1 = 0u;
 
     const unsigned wtile =
         (unsigned)tile_n * (unsigned)(p.steps0 * T::BSTEP0 + (p.steps - p.steps0) * T::BSTEP1);
-    auto load_w = [&]() {
-        const bool s1 = bstep >= p.steps0;
-        const unsigned base = wtile + (s1 ? (unsigned)(p.steps0 * T::BSTEP0 + (bstep - p.steps0) * T::BSTEP1)
-                                          : (unsigned)(bstep * T::BSTEP0));
+    auto load_w = [&](int st, auto RS) {
+        constexpr int rs = decltype(RS)::value;
+        const bool s1 = st >= p.steps0;
+        const unsigned base = wtile + (s1 ? (unsigned)(p.steps0 * T::BSTEP0 + (st - p.steps0) * T::BSTEP1)
+                                          : (unsigned)(st * T::BSTEP0));
         const int items = (s1 ? T::BSTEP1 : T::BSTEP0) / 16;
+        const bool live = st < p.steps;
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            rb[j] = bload_u4(srdw, (j < T::B_FULL || i < items) ? base + (unsigned)i * 16u : OOB);
+            rb[rs][j] = bload_u4(srdw, live && (j < T::B_FULL || i < items) ? base + (unsigned)i * 16u : OOB);
         }
-        ++bstep;
     };
-    auto load0 = [&]() {
+    auto load0 = [&](int st, auto RS) {
+        constexpr int rs = decltype(RS)::value;
+        // K-step st = (tap, 16-channel chunk), tap-major; taps row-major over the kh x kw grid
+        const int tap = st / p.cpt;
+        const int c0 = (st - tap * p.cpt) * BK;
+        const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
         const int dy = p.ty0 + ky * p.tdy, dx = p.tx0 + kx * p.tdx;
         const int tap_off = (dy * p.W0 + dx) * p.ldc0 + c0;
-        aval = 0;
+        const bool live = st < p.steps;
+        unsigned av = 0;
 #pragma unroll
         for (int j = 0; j < T::A_PER_T; ++j) {
             const int iy = ys[j] + dy, ix = xs[j] + dx;
-            const bool ok = (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
-            aval |= (ok ? 1u : 0u) << j;
-            ra[j] = bload_f4(srd0, ok ? (unsigned)(org0[j] + tap_off) * 4u : OOB);
+            const bool ok = live && (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
+            av |= (ok ? 1u : 0u) << j;
+            ra[rs][j] = bload_f4(srd0, ok ? (unsigned)(org0[j] + tap_off) * 4u : OOB);
         }
+        if constexpr (rs == 0) aval0 = av; else aval1 = av;
         if constexpr (PRO != 0) {
             const int c = c0 + q4 * 4;
             if constexpr (UNIB) {
-                rsc[0] = bload_f4(srdsc, (unsigned)(b_tile * p.C0 + c) * 4u);
-                rsh[0] = bload_f4(srdsh, (unsigned)(b_tile * p.C0 + c) * 4u);
+                const unsigned o = live ? (unsigned)(b_tile * p.C0 + c) * 4u : OOB;
+                rsc[rs][0] = bload_f4(srdsc, o);
+                rsh[rs][0] = bload_f4(srdsh, o);
             } else {
 #pragma unroll
                 for (int j = 0; j < T::A_PER_T; ++j) {
-                    const unsigned o = pb[j] >= 0 ? (unsigned)(pb[j] * p.C0 + c) * 4u : OOB;
-                    rsc[j] = bload_f4(srdsc, o);
-                    rsh[j] = bload_f4(srdsh, o);
+                    const unsigned o = live && pb[j] >= 0 ? (unsigned)(pb[j] * p.C0 + c) * 4u : OOB;
+                    rsc[rs][j] = bload_f4(srdsc, o);
+                    rsh[rs][j] = bload_f4(srdsh, o);
                 }
             }
         }
-        load_w();
-        c0 += BK;
-        const bool wc = c0 == p.C0;
-        c0 = wc ? 0 : c0;
-        kx += wc ? 1 : 0;
-        const bool wx = kx == p.kw;
-        kx = wx ? 0 : kx;
-        ky += wx ? 1 : 0;
+        load_w(st, RS);
     };
-    auto load1 = [&]() {
-        aval = 0;
+    auto load1 = [&](int st, auto RS) {
+        constexpr int rs = decltype(RS)::value;
+        const int c1 = (st - p.steps0) * BK;
+        const bool live = st < p.steps;
+        unsigned av = 0;
 #pragma unroll
         for (int j = 0; j < T::A_PER_T; ++j) {
-            aval |= (pb[j] >= 0 ? 1u : 0u) << j;
-            ra[j] = bload_f4(srd1, pb[j] >= 0 ? (unsigned)(org1[j] + c1) * 4u : OOB);
+            av |= (pb[j] >= 0 ? 1u : 0u) << j;
+            ra[rs][j] = bload_f4(srd1, live && pb[j] >= 0 ? (unsigned)(org1[j] + c1) * 4u : OOB);
         }
-        load_w();
-        c1 += BK;
+        if constexpr (rs == 0) aval0 = av; else aval1 = av;
+        load_w(st, RS);
+    };
+    // Every K-loop iteration issues its loads unconditionally (steps past the end load nothing:
+    // all offsets out of range), so the compiler's vmcnt waits see one straight-line issue order
+    // and count only the younger stage's loads (a conditional issue made it wait for vmcnt(0)).
+    auto load_step = [&](int st, auto RS) {
+        if (NPL == 4 || st < p.steps0) load0(st, RS);
+        else load1(st, RS);
     };
 
-    auto store = [&](unsigned char* buf, bool pro) {
+    // register stage rs (holding K-step st) -> LDS stage buf
+    auto store = [&](unsigned char* buf, int st, auto RS) {
+        constexpr int rs = decltype(RS)::value;
+        const bool pro = st < p.steps0;
 #pragma unroll
         for (int j = 0; j < T::A_PER_T; ++j) {
-            f32x4 v = ra[j];
+            f32x4 v = ra[rs][j];
             if constexpr (PRO != 0) {
                 if (pro) {
-                    v = v * rsc[UNIB ? 0 : j] + rsh[UNIB ? 0 : j];
+                    v = v * rsc[rs][UNIB ? 0 : j] + rsh[rs][UNIB ? 0 : j];
                     if constexpr (PRO == 2) {
                         v.x = silu_fast(v.x); v.y = silu_fast(v.y);
                         v.z = silu_fast(v.z); v.w = silu_fast(v.w);
                     }
                 }
             }
-            if (!((aval >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+            if (!(((rs == 0 ? aval0 : aval1) >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
             unsigned char* d = buf + a_wr + j * 64 * 16;
             if constexpr (F3) v = v * ascale;
             if (F3 && pro) {
@@ -231,7 +253,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                 split2_f16(v, a0, a1);
                 *reinterpret_cast<u32x2*>(d) = a0;
                 *reinterpret_cast<u32x2*>(d + 2 * T::APLANE) = a1;
-            } else {
+            } else if constexpr (NPL == 6) {
                 u32x2 a0, a1, a2;
                 split3(v, a0, a1, a2);
                 *reinterpret_cast<u32x2*>(d) = a0;
@@ -240,11 +262,11 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
             }
         }
         unsigned char* bb = buf + T::ASTAGE;
-        const int items = ((bstep - 1 >= p.steps0) ? T::BSTEP1 : T::BSTEP0) / 16;  // the step just loaded
+        const int items = (pro ? T::BSTEP0 : T::BSTEP1) / 16;
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
-            if (j < T::B_FULL || i < items) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[j];
+            if (j < T::B_FULL || i < items) *reinterpret_cast<u32x4*>(bb + i * 16) = rb[rs][j];
         }
     };
 
@@ -262,35 +284,37 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     const int b_rd = T::ASTAGE + half * T::BPLANE + (wn * 64 + l32) * 16;
 
     auto compute6 = [&](const unsigned char* buf) {
-        u32x4 fa[2][3], fb[2][3];
+        if constexpr (NPL == 6) {
+            u32x4 fa[2][3], fb[2][3];
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc) {
+            for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+                    fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * T::APLANE);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * T::BPLANE);
+            }
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb)
-                fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * T::APLANE);
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-                fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * T::BPLANE);
+                for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                    acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][2], acc[mb][nb]);
+                    acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][1], acc[mb][nb]);
+                    acc[mb][nb] = mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
+                }
         }
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][0], acc[mb][nb]);
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][1], acc[mb][nb]);
-                acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][0], acc[mb][nb]);
-            }
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                acc[mb][nb] = mfma_bf16(fa[mb][0], fb[nb][2], acc[mb][nb]);
-                acc[mb][nb] = mfma_bf16(fa[mb][1], fb[nb][1], acc[mb][nb]);
-                acc[mb][nb] = mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
-            }
     };
     auto compute3 = [&](const unsigned char* buf) {
         u32x4 fa[2][2], fb[2][2];
@@ -321,27 +345,25 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
         else compute6(buf);
     };
 
-    // ---- K loop: one barrier per step ----
-    if (p.steps0 > 0) { load0(); store(smem, true); } else { load1(); store(smem, false); }
+    // ---- K loop: one barrier per step, two steps per iteration (register stages 0 / 1) ----
+    const std::integral_constant<int, 0> R0;
+    const std::integral_constant<int, 1> R1;
+    load_step(0, R0);
+    load_step(1, R1);
+    store(smem, 0, R0);
     __syncthreads();
-    int step = 0;
-    for (; step < p.steps0 - 1; ++step) {
-        unsigned char* cur = smem + (step & 1) * T::STAGE;
-        unsigned char* nxt = smem + ((step & 1) ^ 1) * T::STAGE;
-        load0();
-        compute(cur, true);
-        store(nxt, true);
+    for (int step = 0; step < p.steps; step += 2) {
+        load_step(step + 2, R0);
+        compute(smem, step < p.steps0);
+        if (step + 1 >= p.steps) break;
+        store(smem + T::STAGE, step + 1, R1);
+        __syncthreads();
+        load_step(step + 3, R1);
+        compute(smem + T::STAGE, step + 1 < p.steps0);
+        if (step + 2 >= p.steps) break;
+        store(smem, step + 2, R0);
         __syncthreads();
     }
-    for (; step < p.steps - 1; ++step) {
-        unsigned char* cur = smem + (step & 1) * T::STAGE;
-        unsigned char* nxt = smem + ((step & 1) ^ 1) * T::STAGE;
-        load1();
-        compute(cur, step < p.steps0);
-        store(nxt, false);
-        __syncthreads();
-    }
-    compute(smem + (step & 1) * T::STAGE, step < p.steps0);
 
     // ---- epilogue (as wc_conv.hip) ----
     const int HWo = p.Ho * p.Wo;
@@ -413,7 +435,10 @@ int launch(const IgDev& d, hipStream_t stream) {
     const int tiles_m = (p.M + BM - 1) / BM;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(tiles_m * p.ntiles_n);
-    hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3>), grid, dim3(NT), 0, stream, p);
+    if (F3 && p.steps == p.steps0)  // f16x3 segment 0 only: 4-plane LDS stages
+        hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, F3 ? 4 : 6>), grid, dim3(NT), 0, stream, p);
+    else
+        hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 6>), grid, dim3(NT), 0, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -499,6 +524,7 @@ int prepare(const wc_conv_args* a, const void* w6, IgDev& d, long& k) {
     d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
               a->Ho == a->Hm && a->Wo == a->Wm;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
+    d.cpt = s0.C / BK;
     d.steps = (int)(k / BK);
     d.wsinv = nullptr; d.abound = nullptr; d.a_exp = 0;
     d.absmax = a->absmax_out;

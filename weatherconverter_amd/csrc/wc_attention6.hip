@@ -216,15 +216,15 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
             if (v_key[j] >= KT) continue;
             const int pos = v_pos[j];
             if constexpr (F3) {
-                unsigned ha[4], la[4], hb[4], lb[4];
-                split2_f16_elems(rv[j][0] * vs, ha, la);
-                split2_f16_elems(rv[j][1] * vs, hb, lb);
+                const f32x4 va = rv[j][0] * vs, vb4 = rv[j][1] * vs;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int d = v_d[j] + e;
                     const int off = d * (KT * 2) + (((pos >> 3) ^ ((d >> 2) & 3)) << 4) + (pos & 7) * 2;
-                    *reinterpret_cast<unsigned*>(vb + off) = ha[e] | (hb[e] << 16);
-                    *reinterpret_cast<unsigned*>(vb + A::VPLANE + off) = la[e] | (lb[e] << 16);
+                    unsigned h, l;  // keys 2kp (low half) and 2kp + 1 of dim d, split as one pair
+                    split2_pair(f32x2{va[e], vb4[e]}, h, l);
+                    *reinterpret_cast<unsigned*>(vb + off) = h;
+                    *reinterpret_cast<unsigned*>(vb + A::VPLANE + off) = l;
                 }
             } else {
                 unsigned ua[3][4], ub[3][4];
@@ -291,11 +291,11 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
         }
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         const float m_new = fmaxf(m_run, mloc);
-        const float alpha = exp2f(m_run - m_new);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // v_exp_f32 (results < 2^-126 flush: negligible)
         float lsum = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const float pv = exp2f(s[r] - m_new);
+            const float pv = __builtin_amdgcn_exp2f(s[r] - m_new);
             s[r] = pv;
             lsum += pv;
         }

@@ -63,30 +63,22 @@ WC_DEVICE void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
 
 // Two-piece fp16 split by round-to-nearest: h = fp16(v), l = fp16(v - h) (v - h is exact in fp32),
 // so v = h + l to 2^-22 |v| (or 2^-25 absolute when l is subnormal).  Callers bound |v| < 2^15.
-WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
-    unsigned h[4], l[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float x = v[e];
-        const _Float16 hh = (_Float16)x;
-        const _Float16 ll = (_Float16)(x - (float)hh);
-        h[e] = __builtin_bit_cast(unsigned short, hh);
-        l[e] = __builtin_bit_cast(unsigned short, ll);
-    }
-    ph = u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-    pl = u32x2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+// Two values at a time: v_cvt_pk_f16_f32 (gfx950, RNE) -> 2 x v_cvt_f32_f16 -> v_pk_add_f32 ->
+// v_cvt_pk_f16_f32, 2.5 VALU per value, already packed as the MFMA operand wants.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+WC_DEVICE void split2_pair(f32x2 v, unsigned& h, unsigned& l) {
+    const f16x2v hh = __builtin_convertvector(v, f16x2v);
+    const f32x2 r = v - __builtin_convertvector(hh, f32x2);
+    h = __builtin_bit_cast(unsigned, hh);
+    l = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2v));
 }
-
-// Per-element form of split2_f16: the fp16 bit patterns (low 16 bits) of h and l for 4 floats.
-WC_DEVICE void split2_f16_elems(f32x4 v, unsigned (&h)[4], unsigned (&l)[4]) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float x = v[e];
-        const _Float16 hh = (_Float16)x;
-        const _Float16 ll = (_Float16)(x - (float)hh);
-        h[e] = __builtin_bit_cast(unsigned short, hh);
-        l[e] = __builtin_bit_cast(unsigned short, ll);
-    }
+WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
+    unsigned h0, l0, h1, l1;
+    split2_pair(f32x2{v.x, v.y}, h0, l0);
+    split2_pair(f32x2{v.z, v.w}, h1, l1);
+    ph = u32x2{h0, h1};
+    pl = u32x2{l0, l1};
 }
 
 // Raise absmax[b] to the wave's max of m (|values| >= 0: their float bits order like unsigned ints).

@@ -289,9 +289,11 @@ def main():
                     'parallelism': f'batch-sharded x{world}, 1 RCCL all-gather of x0' if world > 1 else 'single GPU',
                     'hip_graph': bool(args.graph),
                     'arithmetic': {
-                        'f16x3': 'fp32-class: GN-prologue 3x3 convs on f16x3 (2-piece fp16 split, Samuelson-bounded '
-                                 'scale), all other convs and attention on bf16x6 (exact 3-piece bf16 split); fp32 '
-                                 'accumulation; fp32 activations in HBM',
+                        'f16x3': 'fp32-class: 3x3 convs, attention projections and attention on f16x3 (2-piece fp16 '
+                                 'split under static power-of-two range bounds: Samuelson GN bound, in-projection row '
+                                 'norms); down convs / ConvT on f16x3 under the producer\'s per-image absmax; '
+                                 'unbounded operands on bf16x6 (exact 3-piece bf16 split); fp32 accumulation; fp32 '
+                                 'activations in HBM',
                         'bf16x6': 'fp32-class: every conv and attention on bf16x6 (exact 3-piece bf16 split), fp32 '
                                   'accumulation; fp32 activations in HBM',
                         'fp32': 'fp32 MFMA (v_mfma_f32_32x32x2_f32) everywhere'}[precision],

@@ -103,11 +103,12 @@ WC_DEVICE float gn_seg_sum(float v, int sw) {
     for (int o = 1; o < sw; o <<= 1) v += __shfl_xor(v, o, 64);
     return v + __shfl_xor(v, 32, 64);
 }
-WC_DEVICE void gn_tile_partials(const f32x16 (&acc)[2][2], const GnTile& g, int nvalid) {
+template <int NB>
+WC_DEVICE void gn_tile_partials(const f32x16 (&acc)[2][NB], const GnTile& g, int nvalid) {
     const int lane = threadIdx.x & 63;
     const float inv_n = 1.0f / (64.0f * (float)g.sw);
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
         if (nb >= nvalid) break;
         float s = 0.f;
 #pragma unroll

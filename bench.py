@@ -103,7 +103,9 @@ def roofline_leg(model, x, t_dev):
     traffic, traffic_src = None, None
     for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
                                               '*_hbm_traffic.json')))[-1:]:
-        rec = json.load(open(path)).get(name)
+        recs = json.load(open(path))
+        # rocprof names carry every template argument; the profile label may omit trailing defaults
+        rec = recs.get(name) or next((v for k, v in recs.items() if k.startswith(name[:-1] + ',')), None)
         if rec:
             traffic = round(rec['total_bytes'] / 1e9, 4)
             traffic_src = (f'{os.path.relpath(path, os.path.dirname(os.path.abspath(__file__)))}: GB per launch '

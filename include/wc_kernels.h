@@ -149,6 +149,19 @@ int wc_conv_igemm_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes,
  * down-sampling convs (:231) and the up-sampling transposed convs (:300). */
 int wc_conv_igemm_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
                         const float* w_inv_scale, const float* a_bound, void* stream);
+/* wc_conv_igemm_f16x3 for the attention in-projection (1x1, N = 3C output channels [q | k | v],
+ * unet_base.py:115,159 in_proj_weight/in_proj_bias), whose epilogue writes the projection already
+ * in the f16x3 form wc_attention_fwd_f16x3_presplit reads instead of fp32 rows: value v of part
+ * p (q, k, v) is scaled by 2^exps[p] and split into two round-to-nearest fp16 pieces (h, l) that
+ * are stored per image b (image stride 6*C*HW fp16 elements) as
+ *   q, k:  [part 2][head][piece 2][d / 8][pixel HW][d % 8]
+ *   v:     at 4*C*HW: [head][piece 2][d][HW] with pixels permuted inside every 32-pixel group into
+ *          the key order of the attention kernel's P V^T MFMA (so its V^T tiles are contiguous rows).
+ * args->out is ignored (may be NULL); requires args->N == 3*C, C % heads == 0, (C/heads) % 32 == 0,
+ * HW % 128 == 0 and no residual / temb / absmax / GN partial outputs. */
+int wc_conv_igemm_f16x3_qkv(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
+                            const float* w_inv_scale, void* qkv3, int C, int heads, const int* exps,
+                            void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */
@@ -197,6 +210,12 @@ int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, in
  * the scales are removed in the softmax multiplier and the final 1/l. */
 int wc_attention_fwd_f16x3(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
                            int heads, float scale, int q_exp, int k_exp, int v_exp, void* stream);
+/* wc_attention_fwd_f16x3 reading the pre-split projection written by wc_conv_igemm_f16x3_qkv with
+ * exponents (q_exp, k_exp, v_exp): the K and V^T tiles are copied into LDS by LDS-DMA (no split
+ * or transpose work in the key loop); results are bit-identical to wc_attention_fwd_f16x3 on the
+ * fp32 projection.  N % 32 == 0, head dim % 32 == 0. */
+int wc_attention_fwd_f16x3_presplit(const void* qkv3, float* out, int ld_out, int B, int N, int C, int heads,
+                                    float scale, int q_exp, int k_exp, int v_exp, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Time embedding: sinusoid + t_proj MLP + every ResBlock's SiLU→Linear projection in one launch */

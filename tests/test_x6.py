@@ -757,3 +757,49 @@ def test_unet_gn_partials_equal_stats_pass(precision):
         net.engine().gn_partials = False
         y0 = net(x, torch.tensor([400]).cuda())
     assert rel_l2(y1, y0) < 2e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,C,heads', [(2, 16, 128, 4), (2, 16, 512, 4), (1, 16, 768, 4), (2, 32, 256, 4),
+                                         (1, 16, 64, 2)])
+def test_qkv_presplit_attention_bit_identical(B, H, C, heads):
+    """The pre-split path (in_proj epilogue writes scaled fp16 pieces, attention copies K / V^T tiles
+    by LDS-DMA) against the fp32-projection path: the same split values and MFMA order, so the
+    attention output is bit-identical; and both within the fp32 tolerance of float64."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(77)
+    N = H * H
+    x = torch.randn((B, C, H, H), generator=g) * 2 + 1
+    gamma = 1 + 0.3 * torch.randn(C, generator=g)
+    beta = 0.3 * torch.randn(C, generator=g)
+    sc, sh = _gn_affine(x, gamma, beta)
+    w_in = torch.randn((3 * C, C), generator=g) / C**0.5
+    b_in = 0.1 * torch.randn(3 * C, generator=g)
+    ga, ba = float(gamma.abs().max()), float(beta.abs().max())
+    a_exp = K.f16x3_a_exp(ga, ba, N * C // 8)
+    exps = K.attention_f16x3_exps(w_in, b_in, ga, ba, N * C // 8)
+    xd = x.permute(0, 2, 3, 1).contiguous().cuda()
+    seg = K.Seg(K.View.full(xd), [(0, 0)], scale=sc.float().cuda(), shift=sh.float().cuda())
+    w3 = K.pack_f16x3(w_in.cuda(), C, ntaps=1, order='natural')
+    bias = b_in.cuda()
+    assert K.qkv_presplit_ok(B, N, C, heads)
+    qkv = torch.empty((B, H, H, 3 * C), device='cuda')
+    K.conv_igemm_f16x3([seg], w3, bias, K.View.full(qkv), Hm=H, Wm=H, a_exp=a_exp)
+    ref_out = torch.empty((B * N, C), device='cuda')
+    K.attention(qkv.view(B * N, 3 * C), ref_out, B, N, C, heads, 'f16x3', exps)
+    qkv3 = torch.empty(B * 6 * C * N, dtype=torch.int16, device='cuda')
+    K.conv_igemm_f16x3_qkv(seg, w3, bias, qkv3, Hm=H, Wm=H, a_exp=a_exp, C=C, heads=heads, exps=exps)
+    out = torch.full((B * N, C), 7.0, device='cuda')
+    K.attention_presplit(qkv3, out, B, N, C, heads, exps)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref_out)
+    # the pre-split pieces are the scaled projection: q piece h + l == fp32 q * 2^eq (to 2^-22)
+    D = C // heads
+    q3 = qkv3.view(B, 6 * C * N)[:, :2 * D * N].view(B, 2, D // 8, N, 8)  # head 0, pieces of q
+    qh = q3.view(torch.float16).float()
+    q_rec = (qh[:, 0] + qh[:, 1]).permute(0, 2, 1, 3).reshape(B, N, D)
+    q_ref = qkv.view(B, N, 3 * C)[:, :, :D] * 2.0**exps[0]
+    assert rel_l2(q_rec.double().cpu(), q_ref.double().cpu()) < 1e-6
+    a = (x.double() * sc[:, :, None, None] + sh[:, :, None, None]).permute(0, 2, 3, 1).reshape(B, N, C)
+    ref64 = _attn_ref((a @ w_in.double().t() + b_in.double()).float(), B, N, C, heads)
+    assert rel_l2(out.cpu().double().reshape(B, N, C), ref64) < 1e-5

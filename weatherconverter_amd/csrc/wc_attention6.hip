@@ -48,10 +48,7 @@ struct Ax6 {
 };
 
 // position of key k (0..31) in the permuted K16 order of the PV MFMA (see header)
-WC_DEVICE int key_pos(int k) {
-    const int c = k >> 4, kk = k & 15;
-    return 16 * c + 8 * ((kk >> 2) & 1) + (kk & 3) + 4 * (kk >> 3);
-}
+WC_DEVICE int key_pos(int k) { return attn_key_pos(k); }
 
 // The three bf16 piece bit patterns (hi16 = the piece) of 4 floats, per element.
 WC_DEVICE void split3_elems(f32x4 v, unsigned (&u)[3][4]) {
@@ -107,11 +104,14 @@ WC_DEVICE void mfma_split(f32x16& acc, const u32x4 (&a)[F3 ? 2 : 3], const u32x4
 // raw S^T accumulator into the exp2 domain; out_mul multiplies O / l at the end.
 // f16x3 up to D = 128 fits 256 registers (two waves per SIMD: one wave's softmax / staging VALU
 // runs under the other's MFMAs); the larger forms keep Q and O in 512 registers at one wave.
-template <int D, bool F3>
+// PRE (f16x3 only): qkv is the pre-split projection of wc_conv_igemm_f16x3_qkv (already scaled by
+// 2^exps; qs, ks, vs unused); K and V^T tiles are copied into LDS by LDS-DMA in their final image.
+template <int D, bool F3, bool PRE = false>
 __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
                                                              float* __restrict__ out, int ldo, int N,
                                                              int C, float score_mul, float qs, float ks,
                                                              float vs, float ps, float out_mul) {
+    static_assert(!PRE || F3, "pre-split operands are f16x3");
     using A = Ax6<D, F3>;
     constexpr int NP = A::NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -140,17 +140,57 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     const int kcol = C + head * D;
     const int vcol = 2 * C + head * D;
     const __amdgpu_buffer_rsrc_t srd = make_srd(base);
+    // pre-split layout (wc_kernels.h, wc_conv_igemm_f16x3_qkv), in fp16 elements
+    const unsigned short* q3 = reinterpret_cast<const unsigned short*>(qkv) + (long)b * 6 * C * N;
+    const long hplane = (long)D * N;  // one piece of one head
+    const unsigned short* Qp = q3 + (long)(head * 2) * hplane;
+    const unsigned short* Kp = q3 + (long)((C / D + head) * 2) * hplane;
+    const unsigned short* Vp = q3 + 4L * C * N + (long)(head * 2) * hplane;
 
     // ---- Q pieces: lane (query l32, half) holds Q[q][16 ch + 8 half + j] ----
     const int qrow = q0 + l32;
     u32x4 qp[A::NCH][NP];
 #pragma unroll
     for (int ch = 0; ch < A::NCH; ++ch) {
-        const unsigned o = (unsigned)(qrow * ldq + qcol + 16 * ch + 8 * half) * 4u;
-        const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB) * qs;
-        const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB) * qs;
-        pieces8<F3>(v0, v1, qp[ch]);
+        if constexpr (PRE) {
+#pragma unroll
+            for (int pc = 0; pc < NP; ++pc) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(Qp + pc * hplane + ((long)(2 * ch + half) * N + qrow) * 8);
+                qp[ch][pc] = qrow < N ? *src : u32x4{0u, 0u, 0u, 0u};
+            }
+        } else {
+            const unsigned o = (unsigned)(qrow * ldq + qcol + 16 * ch + 8 * half) * 4u;
+            const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB) * qs;
+            const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB) * qs;
+            pieces8<F3>(v0, v1, qp[ch]);
+        }
     }
+    // LDS-DMA of tile t into buf (PRE): D/16 wave-instructions per wave, half K (plane pairs, key
+    // slots XOR-swizzled as write_tile does), half V^T (16 dim rows, 16-byte slots swizzled)
+    auto dma_tile = [&](int t, unsigned char* buf) {
+        const int kv0 = t * KT;
+        constexpr int G = D / 8;  // K planes per piece = V^T row groups of 16 per piece x 2
+#pragma unroll
+        for (int j = 0; j < G / 4; ++j) {
+            const int i = wave + 4 * j;  // 0 .. G-1: (piece, plane pair)
+            const int pc = i / (G / 2), pp = i % (G / 2);
+            const int pl = 2 * pp + (lane >> 5), key = (lane & 31) ^ (pl & 15);
+            const unsigned short* src = Kp + pc * hplane + ((long)pl * N + kv0 + key) * 8;
+            unsigned char* dst = buf + (pc * G + 2 * pp) * A::KPLANE;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < G / 4; ++j) {
+            const int i = wave + 4 * j;  // 0 .. G-1: (piece, 16-row block)
+            const int pc = i / (D / 16), r0 = 16 * (i % (D / 16));
+            const int row = r0 + (lane >> 2), slot = (lane & 3) ^ ((row >> 2) & 3);
+            const unsigned short* src = Vp + pc * hplane + (long)row * N + kv0 + slot * 8;
+            unsigned char* dst = buf + A::KBYTES + pc * A::VPLANE + r0 * (KT * 2);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+    };
 
     // ---- staging coordinates ----
     // K: item i -> key i / (D/4), dims 4*(i % (D/4)) .. +3 (a wave reads whole key rows).  In LDS
@@ -250,13 +290,22 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     float m_run = -INFINITY, l_run = 0.f;
 
     const int ntiles = (N + KT - 1) / KT;
-    load_tile(0);
-    write_tile(smem);
+    if constexpr (PRE) {
+        dma_tile(0, smem);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        load_tile(0);
+        write_tile(smem);
+    }
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const unsigned char* cur = smem + (t & 1) * A::STAGE;
         const int kv0 = t * KT;
-        if (t + 1 < ntiles) load_tile(t + 1);
+        if constexpr (PRE) {
+            if (t + 1 < ntiles) dma_tile(t + 1, smem + ((t + 1) & 1) * A::STAGE);  // buffer last read in tile t - 1
+        } else {
+            if (t + 1 < ntiles) load_tile(t + 1);
+        }
 
         // ---- S^T = K Q^T ----
         f32x16 s;
@@ -328,7 +377,11 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
             }
         }
 
-        if (t + 1 < ntiles) write_tile(smem + ((t + 1) & 1) * A::STAGE);
+        if constexpr (PRE) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t + 1 landed
+        } else {
+            if (t + 1 < ntiles) write_tile(smem + ((t + 1) & 1) * A::STAGE);
+        }
         __syncthreads();
     }
 
@@ -348,13 +401,13 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     }
 }
 
-template <int D, bool F3>
+template <int D, bool F3, bool PRE = false>
 int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
                 float scale, int eq, int ek, int ev, hipStream_t stream) {
     using A = Ax6<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3, PRE>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, A::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -362,7 +415,7 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
     constexpr int EP = F3 ? 14 : 0;  // P scale: keeps small probabilities in the fp16 normal range
     const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
     dim3 grid(((N + 127) / 128) * heads * B);
-    hipLaunchKernelGGL((attention_x6_kernel<D, F3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
+    hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
                        score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), ldexpf(1.f, EP),
                        ldexpf(1.f, -(ev + EP)));
     WC_CHECK_LAUNCH();
@@ -389,7 +442,32 @@ int dispatch_att6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, i
     }
 }
 
+int dispatch_att_presplit(const void* qkv3, float* out, int ld_out, int B, int N, int C, int heads, float scale,
+                          int eq, int ek, int ev, hipStream_t s) {
+    if (!qkv3 || !out) return WC_E_ARG;
+    if (heads <= 0 || C % heads != 0 || ld_out % 4 != 0 || ld_out < C || N <= 0 || B <= 0 || N % KT) return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(qkv3) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return WC_E_SHAPE;
+    if (eq < -60 || eq > 60 || ek < -60 || ek > 60 || ev < -60 || ev > 60) return WC_E_ARG;
+    const float* q = reinterpret_cast<const float*>(qkv3);
+    switch (C / heads) {
+        case 32: return launch_att6<32, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 64: return launch_att6<64, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 96: return launch_att6<96, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 128: return launch_att6<128, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 160: return launch_att6<160, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 192: return launch_att6<192, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        default: return WC_E_SHAPE;
+    }
+}
+
 }  // namespace
+
+extern "C" int wc_attention_fwd_f16x3_presplit(const void* qkv3, float* out, int ld_out, int B, int N, int C,
+                                               int heads, float scale, int q_exp, int k_exp, int v_exp,
+                                               void* stream) {
+    return dispatch_att_presplit(qkv3, out, ld_out, B, N, C, heads, scale, q_exp, k_exp, v_exp,
+                                 reinterpret_cast<hipStream_t>(stream));
+}
 
 extern "C" int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N,
                                    int C, int heads, float scale, void* stream) {

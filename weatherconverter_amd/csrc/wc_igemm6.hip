@@ -59,6 +59,9 @@ struct IgDev {
     float* absmax;       // optional per-image max |out| (atomic)
     float* gn_part;      // optional GroupNorm tile partials (UNIB only; wcx6::gn_tile_partials)
     int gn_ncb, gn_sw, gn_c0, gn_p64, gn_np64;
+    unsigned short* qkv3;  // optional: attention in-projection written pre-split (wc_conv_igemm_f16x3_qkv)
+    int qC, qD;            // C and the head dim of that projection
+    float qscale[3];       // 2^exps of q, k, v
 };
 
 // F3: segment 0 in f16x3 (2 fp16 pieces), else bf16x6; segment 1 is always bf16x6.  NPL: LDS
@@ -83,7 +86,9 @@ struct IgTile {
 
 // PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU.  UNIB: tiles never straddle images.  ACT: epilogue
 // activation (template, see wc_conv.hip).  F3: segment 0 on f16x3 (caller bounds |a| 2^a_exp).
-template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL>
+// TR (the pre-split qkv epilogue only): accumulate the transposed block (lanes = pixels, rows =
+// channels; the same products, B and A fragments swapped in the MFMA).
+template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     using T = IgTile<BM, BN, F3, NPL>;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
@@ -330,13 +335,14 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+            for (int nb = 0; nb < 2; ++nb)
+                acc[mb][nb] = TR ? mfma_f16(fb[nb][0], fa[mb][0], acc[mb][nb]) : mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
-                acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
-                acc[mb][nb] = mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                acc[mb][nb] = TR ? mfma_f16(fb[nb][1], fa[mb][0], acc[mb][nb]) : mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = TR ? mfma_f16(fb[nb][0], fa[mb][1], acc[mb][nb]) : mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
             }
     };
     // the data of K-step `step` is segment 0 iff step < steps0
@@ -363,6 +369,64 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
         if (step + 2 >= p.steps) break;
         store(smem, step + 2, R0);
         __syncthreads();
+    }
+
+    // ---- epilogue: pre-split attention projection (wc_conv_igemm_f16x3_qkv, TR) ----
+    // acc[mb][nb][r] = output (pixel m-block col l32, channel n-block row); a 32-channel block lies
+    // in one (part, head) since D % 32 == 0.  q / k: rows 8j + 4 half + 0..3 are 4 consecutive
+    // dims of one 8-dim group -> one 8-byte store per piece, 64 lanes = 512 contiguous bytes.
+    // v: 2-byte stores at the pixel's key-order position, 64 contiguous bytes per half-wave.
+    if constexpr (TR) {
+        if (UNIB && p.qkv3) {
+            const long img = (long)b_tile * 6 * p.qC * HWm;
+            const long plane = (long)p.qD * HWm;  // one piece of one head
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int nblk = n0 + wn * 64 + nb * 32;
+                if (nblk >= p.N) continue;
+                const int part = nblk / p.qC;
+                const int c0 = nblk - part * p.qC;
+                const int head = c0 / p.qD, d0 = c0 - head * p.qD;
+                const float sc = p.qscale[part];
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) {
+                    const int pix = m0 - b_tile * HWm + wm * 64 + mb * 32 + l32;
+                    if (part < 2) {
+                        unsigned short* dst = p.qkv3 + img + (long)((part * (p.qC / p.qD) + head) * 2) * plane +
+                                              ((long)(d0 >> 3) * HWm + pix) * 8 + 4 * half;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            f32x4 v;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const int n = nblk + 8 * j + 4 * half + e;
+                                v[e] = ((F3 ? acc[mb][nb][4 * j + e] * p.wsinv[n] * ainv : acc[mb][nb][4 * j + e]) +
+                                        (p.bias ? p.bias[n] : 0.f)) * sc;
+                            }
+                            u32x2 ph, pl;
+                            split2_f16(v, ph, pl);
+                            *reinterpret_cast<u32x2*>(dst + (long)j * HWm * 8) = ph;
+                            *reinterpret_cast<u32x2*>(dst + plane + (long)j * HWm * 8) = pl;
+                        }
+                    } else {
+                        const long pos = (pix & ~31) + attn_key_pos(pix & 31);
+                        unsigned short* dst = p.qkv3 + img + 4L * p.qC * HWm + (long)(head * 2) * plane + pos;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                            const int n = nblk + row;
+                            const float v = ((F3 ? acc[mb][nb][r] * p.wsinv[n] * ainv : acc[mb][nb][r]) +
+                                             (p.bias ? p.bias[n] : 0.f)) * sc;
+                            const _Float16 h = (_Float16)v;
+                            const _Float16 l = (_Float16)(v - (float)h);
+                            dst[(long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, h);
+                            dst[plane + (long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, l);
+                        }
+                    }
+                }
+            }
+        }
+        return;
     }
 
     // ---- epilogue (as wc_conv.hip) ----
@@ -435,6 +499,14 @@ int launch(const IgDev& d, hipStream_t stream) {
     const int tiles_m = (p.M + BM - 1) / BM;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(tiles_m * p.ntiles_n);
+    if constexpr (F3 && UNIB && PRO == 1 && ACT == WC_ACT_NONE) {
+        if (p.qkv3) {  // pre-split attention projection
+            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true>), grid, dim3(NT), 0, stream, p);
+            WC_CHECK_LAUNCH();
+            return WC_OK;
+        }
+    }
+    if (p.qkv3) return WC_E_ARG;
     if (F3 && p.steps == p.steps0)  // f16x3 segment 0 only: 4-plane LDS stages
         hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, F3 ? 4 : 6>), grid, dim3(NT), 0, stream, p);
     else
@@ -527,6 +599,7 @@ int prepare(const wc_conv_args* a, const void* w6, IgDev& d, long& k) {
     d.cpt = s0.C / BK;
     d.steps = (int)(k / BK);
     d.wsinv = nullptr; d.abound = nullptr; d.a_exp = 0;
+    d.qkv3 = nullptr; d.qC = d.qD = 0;
     d.absmax = a->absmax_out;
     d.gn_part = a->gn_part;
     if (a->gn_part) {  // N whole 32-channel blocks at a 32-aligned offset, NHWC output
@@ -554,6 +627,40 @@ extern "C" int wc_conv_igemm_x6(const wc_conv_args* a, const void* w6, int64_t w
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (BN == 64) return dispatch<256, 64>(d, pro, a->act, false, s);
     return dispatch<128, 128>(d, pro, a->act, false, s);
+}
+
+extern "C" int wc_conv_igemm_f16x3_qkv(const wc_conv_args* a, const void* w3, int64_t w3_bytes, int a_exp,
+                                       const float* w_inv_scale, void* qkv3, int C, int heads, const int* exps,
+                                       void* stream) {
+    if (!a || !qkv3 || !exps || !w_inv_scale) return WC_E_ARG;
+    if (C <= 0 || heads <= 0 || C % heads || (C / heads) % 32 || a->N != 3 * C) return WC_E_SHAPE;
+    if (a->nseg != 1 || a->res || a->temb || a->absmax_out || a->gn_part || a->out_nchw || a->act) return WC_E_ARG;
+    if (a->seg[0].ntaps != 1 || a->seg[0].dy[0] || a->seg[0].dx[0] || a->seg[0].sy != 1 || a->seg[0].sx != 1)
+        return WC_E_SHAPE;
+    if ((a->Hm * a->Wm) % 128 || (reinterpret_cast<uintptr_t>(qkv3) & 15)) return WC_E_SHAPE;
+    if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    for (int i = 0; i < 3; ++i)
+        if (exps[i] < -60 || exps[i] > 60) return WC_E_ARG;
+    IgDev d;
+    long k;
+    wc_conv_args aa = *a;
+    aa.out = reinterpret_cast<float*>(qkv3);  // unused by the split epilogue; keeps prepare's checks uniform
+    aa.ldo = a->N;
+    aa.Ho = a->Hm; aa.Wo = a->Wm; aa.osy = aa.osx = 1; aa.ooy = aa.oox = 0;
+    const int st = prepare(&aa, w3, d, k);
+    if (st != WC_OK) return st;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    if (BN != 128) return WC_E_SHAPE;
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w3_bytes != ntn * (long)d.steps0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    d.a_exp = a_exp;
+    d.wsinv = w_inv_scale;
+    d.qkv3 = reinterpret_cast<unsigned short*>(qkv3);
+    d.qC = C;
+    d.qD = C / heads;
+    for (int i = 0; i < 3; ++i) d.qscale[i] = ldexpf(1.0f, exps[i]);
+    const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
+    return dispatch<128, 128>(d, pro, WC_ACT_NONE, true, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int wc_conv_igemm_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, int a_exp,

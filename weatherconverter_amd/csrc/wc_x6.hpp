@@ -81,6 +81,13 @@ WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
     pl = u32x2{l0, l1};
 }
 
+// Position of key k (0..31) of a 32-key tile in the K16 order of the attention P V^T MFMA: inside
+// each 16-key half, keys 4-7 and 8-11 swap places (wc_attention6.hip header).
+WC_DEVICE int attn_key_pos(int k) {
+    const int c = k >> 4, kk = k & 15;
+    return 16 * c + 8 * ((kk >> 2) & 1) + (kk & 3) + 4 * (kk >> 3);
+}
+
 // Raise absmax[b] to the wave's max of m (|values| >= 0: their float bits order like unsigned ints).
 WC_DEVICE void wave_absmax_atomic(float* absmax, int b, float m) {
 #pragma unroll

@@ -109,6 +109,9 @@ class UnetEngine:
         self.model = model
         self.device = params[0].device
         self.precision = getattr(model, 'conv_precision', None) or K.default_conv_precision()
+        # f16x3 attention on the pre-split in-projection (WC_ATTN_PRESPLIT=0: fp32 projection + split
+        # in the attention kernel, the bit-identical reference path)
+        self.attn_presplit = os.environ.get('WC_ATTN_PRESPLIT', '1') != '0'
         # GroupNorm statistics from the producers' epilogue tile partials (False: a stats pass per GN)
         self.gn_partials = os.environ.get('WC_GN_PARTIALS', '1') != '0'
         self._sig = self._signature()
@@ -335,21 +338,31 @@ class UnetEngine:
         B, H, W, C = Y.B, Y.H, Y.W, Y.C
         N = H * W
         sc, sh = self._gn(Y, p.g, p.be)
-        qkv = self._new(B, H, W, 3 * C)
         o = self._new(B, H, W, C)
         if p.w_in_f3 is not None:
             # in_proj: GN output bound; attention: q/k/v bounds; out_proj: |O| <= max|V| (convex
             # combination of V rows), so the V exponent bounds it
-            K.conv_igemm_f16x3([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in_f3, p.b_in, View.full(qkv),
-                               Hm=H, Wm=W, a_exp=K.f16x3_a_exp(p.gb[0], p.gb[1], N * C // 8))
+            a_exp = K.f16x3_a_exp(p.gb[0], p.gb[1], N * C // 8)
             exps = K.attention_exps_from_norms(p.qkv_l1, p.qkv_babs, p.gb[0], p.gb[1], N * C // 8)
-            K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
+            seg = Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)
+            if self.attn_presplit and K.qkv_presplit_ok(B, N, C, p.heads):
+                # the in_proj epilogue writes Q, K, V already scaled and split (fp16 pieces, V
+                # transposed in the PV key order); the attention copies K / V^T tiles by LDS-DMA
+                qkv3 = torch.empty(B * 6 * C * N, dtype=torch.int16, device=self.device)
+                K.conv_igemm_f16x3_qkv(seg, p.w_in_f3, p.b_in, qkv3, Hm=H, Wm=W, a_exp=a_exp, C=C, heads=p.heads,
+                                       exps=exps)
+                K.attention_presplit(qkv3, o.view(B * N, C), B, N, C, p.heads, exps)
+            else:
+                qkv = self._new(B, H, W, 3 * C)
+                K.conv_igemm_f16x3([seg], p.w_in_f3, p.b_in, View.full(qkv), Hm=H, Wm=W, a_exp=a_exp)
+                K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
             gp = K.GnPart.of(Y)
             fused = K.gn_conv_ok(Y, gp, p.w_out_f3.N, H, W, 256 if p.w_out_f3.N <= 64 else 128)
             K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y,
                                absmax=absmax, gn=gp if fused else None)
             self._gn_fill(Y, fused)
             return absmax is not None
+        qkv = self._new(B, H, W, 3 * C)
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
         return self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y, absmax=absmax)[0]

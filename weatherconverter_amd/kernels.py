@@ -154,7 +154,8 @@ class GnPart:
 def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: Optional[View], Hm: int, Wm: int,
                temb: Optional[torch.Tensor], temb_ld: int, res: Optional[View], out_map,
                out_nchw: Optional[torch.Tensor], act: int, absmax: Optional[torch.Tensor] = None,
-               act_param: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None, gn_p64: int = 0) -> ConvArgs:
+               act_param: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None, gn_p64: int = 0,
+               out_dummy: bool = False) -> ConvArgs:
     a = ConvArgs()
     _req(1 <= len(segs) <= 2, 'conv takes 1 or 2 K segments')
     B = segs[0].view.B
@@ -207,6 +208,8 @@ def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: O
         a.ldo = 0
         a.Ho, a.Wo = out_nchw.shape[2], out_nchw.shape[3]
         a.out_nchw = 1
+    elif out_dummy:  # the kernel writes its own output format (e.g. the pre-split qkv)
+        a.out, a.ldo, a.Ho, a.Wo = None, N, Hm, Wm
     else:
         out.check()
         _req(out.C == N and out.B == B, 'output view shape')
@@ -439,6 +442,39 @@ def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Ten
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, 0, true>', 'wc_conv_igemm_f16x3',
            _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
+
+
+def qkv_presplit_ok(B: int, N: int, C: int, heads: int) -> bool:
+    """True when the attention of (B, N tokens, C, heads) can run on the pre-split projection
+    (wc_conv_igemm_f16x3_qkv + wc_attention_fwd_f16x3_presplit)."""
+    return C % heads == 0 and (C // heads) % 32 == 0 and N % 128 == 0 and 3 * C > 64
+
+
+def conv_igemm_f16x3_qkv(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], qkv3: torch.Tensor, *, Hm: int,
+                         Wm: int, a_exp: int, C: int, heads: int, exps: Tuple[int, int, int]):
+    """The attention in-projection (1x1 conv, GN prologue) on f16x3 writing the pre-split form
+    (wc_conv_igemm_f16x3_qkv): qkv3 is an int16 tensor of B * 6 * C * Hm * Wm elements."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3n' and w3.N == 3 * C, 'f16x3 qkv weight')
+    B = seg.view.B
+    _req(qkv3.is_cuda and qkv3.dtype == torch.int16 and qkv3.is_contiguous() and qkv3.numel() == B * 6 * C * Hm * Wm,
+         'pre-split qkv buffer: int16, B * 6 * C * HW elements')
+    a = _conv_args([seg], w3.N, bias, None, Hm, Wm, None, 0, None, (1, 1, 0, 0), None, 0, out_dummy=True)
+    ex = (ctypes.c_int * 3)(*[int(e) for e in exps])  # host array, read during the call
+    pro = 0 if seg.scale is None else (2 if seg.silu else 1)
+    _timed(f'conv_igemm_x6_kernel<128, 128, {pro}, true, 0, true> (qkv pre-split)', 'wc_conv_igemm_f16x3_qkv',
+           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), qkv3.data_ptr(), C, heads,
+           ctypes.cast(ex, ctypes.c_void_p), _stream())
+
+
+def attention_presplit(qkv3: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int,
+                       exps: Tuple[int, int, int]):
+    """f16x3 attention on the pre-split projection of conv_igemm_f16x3_qkv (same exps)."""
+    _req(qkv3.is_cuda and qkv3.dtype == torch.int16 and qkv3.numel() == B * 6 * C * N, 'pre-split qkv buffer')
+    _req(out.shape == (B * N, C) and out.is_contiguous(), 'attention output shape')
+    d = C // heads
+    _timed(f'attention_x6_kernel<{d}, true> (pre-split)', 'wc_attention_fwd_f16x3_presplit', 4.0 * B * N * N * C,
+           qkv3.data_ptr(), out.data_ptr(), C, B, N, C, heads, float(d)**-0.5, *[int(e) for e in exps], _stream())
 
 
 def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:

@@ -7,7 +7,7 @@ def main(path, steps=None):
     rows = list(csv.DictReader(open(path)))
     tot = sum(float(r['TotalDurationNs']) for r in rows)
     if steps is None:  # conv_in runs once per UNet forward
-        steps = next(int(r['Calls']) for r in rows if 'conv_in_kernel' in r['Name'])
+        steps = next(int(r['Calls']) for r in rows if 'conv_in' in r['Name'] and 'kernel' in r['Name'])
     print(f'{"kernel":48s} {"calls/fwd":>9s} {"avg_us":>9s} {"ms/fwd":>7s} {"pct":>6s}')
     for r in rows:
         n = r['Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0]

@@ -66,8 +66,59 @@ __global__ __launch_bounds__(TE_THREADS) void temb_kernel(const int64_t* __restr
 
 // --------------------------------------------------------------------------------------------
 // conv_in: 3x3 pad-1 conv from the NCHW image to an NHWC view (unet_base.py:400,456).  The
-// NCHW->NHWC transpose is fused here.  Thread = (pixel, 4 output channels).
+// NCHW->NHWC transpose is fused here.
+// conv_in_px_kernel<COUT>: thread = pixel, all COUT outputs in registers; the Cin*9 inputs are
+// loaded once per pixel (coalesced across the wave), weights are LDS broadcasts, and the pixel's
+// COUT outputs leave as 16-byte stores: HBM-bound (12 B in + 4*COUT B out per pixel).
+// conv_in_kernel (any Cout % 4): thread = (pixel, 4 output channels).
+// Both accumulate bias, then (ci, ky, kx) in order, one fma each (out-of-image taps add 0 * w).
 // --------------------------------------------------------------------------------------------
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_in_px_kernel(const float* __restrict__ x, int B, int Cin, int H, int W,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         float* __restrict__ out, int ldo) {
+    extern __shared__ float ws[];  // [Cin*9][COUT]
+    const int K = Cin * 9;
+    for (int i = threadIdx.x; i < K * COUT; i += blockDim.x) {
+        const int co = i % COUT, k = i / COUT;
+        ws[i] = w[(long)co * K + k];
+    }
+    __syncthreads();
+    const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= (long)B * H * W) return;
+    const int xw = (int)(pix % W);
+    const int yh = (int)((pix / W) % H);
+    const int b = (int)(pix / ((long)W * H));
+    float acc[COUT];
+#pragma unroll
+    for (int c = 0; c < COUT; ++c) acc[c] = bias[c];
+    for (int ci = 0; ci < Cin; ++ci) {
+        const float* plane = x + ((long)b * Cin + ci) * H * W;
+        // one tap per iteration: its COUT weights are consumed before the next tap's are read
+#pragma unroll 1
+        for (int t = 0; t < 9; ++t) {
+            const int ky = t / 3, kx = t - 3 * (t / 3);
+            const int iy = yh + ky - 1;
+            const int ix = xw + kx - 1;
+            {
+                const float v = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? plane[(long)iy * W + ix] : 0.f;
+                const f32x4* wr = reinterpret_cast<const f32x4*>(ws + (ci * 9 + t) * COUT);
+#pragma unroll
+                for (int q = 0; q < COUT / 4; ++q) {
+                    const f32x4 wv = wr[q];
+                    acc[4 * q + 0] = fmaf(v, wv.x, acc[4 * q + 0]);
+                    acc[4 * q + 1] = fmaf(v, wv.y, acc[4 * q + 1]);
+                    acc[4 * q + 2] = fmaf(v, wv.z, acc[4 * q + 2]);
+                    acc[4 * q + 3] = fmaf(v, wv.w, acc[4 * q + 3]);
+                }
+            }
+        }
+    }
+    f32x4* o = reinterpret_cast<f32x4*>(out + pix * ldo);
+#pragma unroll
+    for (int q = 0; q < COUT / 4; ++q) o[q] = f32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+}
+
 __global__ __launch_bounds__(256) void conv_in_kernel(const float* __restrict__ x, int B, int Cin,
                                                       int H, int W, const float* __restrict__ w,
                                                       const float* __restrict__ bias, int Cout,
@@ -93,15 +144,16 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const float* __restrict__ 
             const float* plane = x + ((long)b * Cin + ci) * H * W;
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky) {
-                int iy = yh + ky - 1;
-                if (iy < 0 || iy >= H) continue;
+                const int iy = yh + ky - 1;
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
-                    int ix = xw + kx - 1;
-                    if (ix < 0 || ix >= W) continue;
-                    float v = plane[(long)iy * W + ix];
+                    const int ix = xw + kx - 1;
+                    const float v = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? plane[(long)iy * W + ix] : 0.f;
                     const f32x4 wv = *reinterpret_cast<const f32x4*>(ws + ((ci * 3 + ky) * 3 + kx) * Cout + q * 4);
-                    acc += v * wv;
+                    acc.x = fmaf(v, wv.x, acc.x);
+                    acc.y = fmaf(v, wv.y, acc.y);
+                    acc.z = fmaf(v, wv.z, acc.z);
+                    acc.w = fmaf(v, wv.w, acc.w);
                 }
             }
         }
@@ -378,6 +430,13 @@ extern "C" int wc_conv_in(const float* x, int B, int Cin, int H, int W, const fl
     if (Cin < 1 || Cin > 16 || Cout % 4 != 0 || ldo % 4 != 0) return WC_E_SHAPE;
     size_t lds = (size_t)Cin * 9 * Cout * sizeof(float);
     if (lds > 64 * 1024) return WC_E_SHAPE;
+    if (Cout == 64 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(b) & 15) == 0) {
+        const long npix = (long)B * H * W;
+        hipLaunchKernelGGL(conv_in_px_kernel<64>, dim3((unsigned)((npix + 255) / 256)), dim3(256), lds,
+                           reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, out, ldo);
+        WC_CHECK_LAUNCH();
+        return WC_OK;
+    }
     long total = (long)B * H * W * (Cout / 4);
     hipLaunchKernelGGL(conv_in_kernel, dim3(grid_for(total, 256)), dim3(256), lds,
                        reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, Cout, out, ldo);

@@ -143,10 +143,26 @@ def roofline_leg(model, x, t_dev):
         'mean_launch_ms_events': round(mean_events * 1e3, 4),
         'gflop_per_launch': round(fl / n / 1e9, 3),
         'share_of_mfma_event_time': round(sec / max(total_conv, 1e-12), 3),
-        'mfma_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1)}
+        'mfma_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1),
+                             'peak': _mode_peak(k), 'frac': round(v[1] / v[2] / 1e12 / _mode_peak(k), 4)}
                          for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])},
         'hbm_kernels': hbm_leg(hbm),
     }
+
+
+def _mode_peak(name: str) -> float:
+    """The emulated-fp32 ceiling of a profiled MFMA kernel instantiation: f16x3 (3 f16 MFMAs per
+    block), bf16x6 (6 bf16 MFMAs) or plain fp32 MFMA."""
+    if '<' not in name:
+        return FP32_PEAK_TFLOPS
+    targs = name[name.index('<') + 1:name.rindex('>')].split(', ')
+    if name.startswith('conv3x3_x6'):
+        return F16X3_PEAK_TFLOPS if len(targs) >= 5 and targs[4] == 'true' else BF16X6_PEAK_TFLOPS
+    if name.startswith('conv_igemm_x6'):
+        return F16X3_PEAK_TFLOPS if targs[-1] == 'true' else BF16X6_PEAK_TFLOPS
+    if name.startswith('attention_x6'):
+        return F16X3_PEAK_TFLOPS if targs[1] == 'true' else BF16X6_PEAK_TFLOPS
+    return FP32_PEAK_TFLOPS
 
 
 def hbm_leg(hbm):

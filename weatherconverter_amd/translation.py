@@ -20,11 +20,36 @@ from .sgg.sgg import apply_gsg, apply_lcg
 from .srgan_model.models import inference as srgan_inference
 
 
+class _Replay:
+    """fn(x) captured into a HIP graph over a static input buffer: a call copies x in and replays
+    (the per-kernel host launch cost of a B=1 UNet / SRGAN forward is most of its eager time).  The
+    returned tensor is the graph's static output: consumed before the next call."""
+
+    def __init__(self, fn, x: torch.Tensor):
+        self.x = x.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # allocations and weight packing outside the capture
+                self.y = fn(self.x)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.y = fn(self.x)
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        self.x.copy_(x)
+        self.graph.replay()
+        return self.y
+
+
 @torch.no_grad()
 def sample_with_sgg(input_tensor: torch.Tensor, diff_model, diff_scheduler, seg_model, gt: torch.Tensor,
                     srgan_model, *, LAMBDA: float = 60.0, N: int = 500, mode: str = 'applied', use_lcg: bool = False,
                     t_start: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
-                    progress=None, return_latent: bool = False):
+                    progress=None, return_latent: bool = False, graph: bool = True):
+    """graph=True replays the UNet and SRGAN forwards from HIP graphs (same kernels, same results);
+    the segmenter's autograd pass stays eager."""
     if mode not in ('reference', 'applied'):
         raise ValueError("mode must be 'reference' or 'applied'")
     dev = diff_scheduler.device
@@ -34,13 +59,18 @@ def sample_with_sgg(input_tensor: torch.Tensor, diff_model, diff_scheduler, seg_
     nz = torch.randn_like(x0) if noise is None else noise.to(dev)
     xt = diff_scheduler.add_noise2(x0, nz, t.to(dev))
     ts = torch.arange(N, device=dev, dtype=torch.long)
+    unet_run = sr_run = None
+    if graph and xt.is_cuda:
+        from .diffusion_model.sample_ddpm import _GraphStep
+        unet_run = _GraphStep(diff_model, xt)
+        sr_run = _Replay(lambda v: srgan_inference(srgan_model, v), xt)
     for i in reversed(range(N)):
-        eps = diff_model(xt, ts[i:i + 1])
+        eps = unet_run(xt, ts[i:i + 1]) if unet_run is not None else diff_model(xt, ts[i:i + 1])
         mu, sigma, _ = diff_scheduler.sample_prev_timestep(xt, eps, i)
         if i == 0:
             xt = mu
             break
-        sr_xt = srgan_inference(srgan_model, xt)
+        sr_xt = sr_run(xt) if sr_run is not None else srgan_inference(srgan_model, xt)
         guided = None
         if i % 2 == 1:
             guided = apply_gsg(seg_model, mu, sigma, sr_xt, gt, LAMBDA)

@@ -436,9 +436,15 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     }
 
     // ---- epilogue: (F3: x 2^-(sA + sW[n])) + bias + temb, activation, + residual, NHWC store ----
+    // 32-bit buffer offsets from the image's base (the tile is one image): one multiply per row,
+    // no 64-bit address arithmetic per element
+    const long img_px = (long)b * p.H * p.W;
+    const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + img_px * p.ldo);
+    const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + img_px * p.ldres : p.out);
     float vmax = 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
+        const int pix0 = (y0 + 4 * wm + 2 * mb) * p.W + x0;  // pixel (dy 0, dx 0) of this 32-row block
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             const int n = n0 + wn * 64 + nb * 32 + l32;
@@ -449,14 +455,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int oy = y0 + 4 * wm + 2 * mb + row_dy(row);
-                const int ox = x0 + row_dx(row);
-                const long m = (long)(b * p.H + oy) * p.W + ox;
+                const int pix = pix0 + (row_dy(row) ? p.W : 0) + row_dx(row);
                 float v = (F3 ? acc[mb][nb][r] * mul : acc[mb][nb][r]) + add;
                 if (p.act == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
                 else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
-                if (p.res) v += p.res[m * p.ldres + n];
-                p.out[m * p.ldo + n] = v;
+                if (p.res) v += bload_f1(srd_res, (unsigned)(pix * p.ldres + n) * 4u);
+                bstore_f1(srd_out, (unsigned)(pix * p.ldo + n) * 4u, v);
                 vmax = fmaxf(vmax, fabsf(v));
                 acc[mb][nb][r] = v;
             }
@@ -571,6 +575,9 @@ int prepare(const wc_conv_args* a, const void* w, X6Dev& d, int& BN, int& TH) {
         d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc; d.nck1 = s1.C / 16;
     }
     if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox)
+        return WC_E_SHAPE;
+    // the epilogue addresses one image of the output / residual with 32-bit buffer offsets
+    if ((long)a->Hm * a->Wm * a->ldo * 4 >= (1L << 31) || (a->res && (long)a->Hm * a->Wm * a->ldres * 4 >= (1L << 31)))
         return WC_E_SHAPE;
     d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
     d.w6 = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;

@@ -1,6 +1,6 @@
 #!/bin/bash
 mkdir -p gpurun_out
-timeout -k 10 200 python -u tools/bench_conv.py --check --modes f3,x6 --no-misc > gpurun_out/epi_conv.log 2>&1
+timeout -k 10 200 python -u tools/bench_conv.py --check --modes igf3,igx6 --no-misc > gpurun_out/epi_conv.log 2>&1
 rc=$?; echo conv_rc=$rc; grep -E "relL2|aggregate" gpurun_out/epi_conv.log | grep -v amdgpu
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python -u tools/conv_shape_probe.py > gpurun_out/epi_shape.log 2>&1

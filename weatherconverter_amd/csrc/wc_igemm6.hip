@@ -432,6 +432,61 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
     // ---- epilogue (as wc_conv.hip) ----
     const int HWo = p.Ho * p.Wo;
     float vmax = 0.f;  // absmax: per image; tiles straddling images take the per-value atomic below
+    if constexpr (UNIB) {
+        // the tile is one image: 32-bit buffer offsets from that image's base, temb hoisted, and the
+        // output position of a 32-row block from one division (32 | Wm) instead of one per element
+        const __amdgpu_buffer_rsrc_t srd_out =
+            make_srd(p.out + (p.out_nchw ? (long)b_tile * p.N * HWo : (long)b_tile * HWo * p.ldo));
+        const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + (long)b_tile * HWo * p.ldres : p.out);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int rr0 = m0 - b_tile * HWm + wm * 64 + mb * 32;  // pixel of row 0 in the image
+            const bool fast = (p.Wm & 31) == 0;
+            const int my0 = rr0 / p.Wm, mx0 = rr0 - my0 * p.Wm;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int n = n0 + wn * 64 + nb * 32 + l32;
+                if (n >= p.N) continue;
+                float bn = p.bias ? p.bias[n] : 0.f;
+                if (p.temb) bn += p.temb[b_tile * p.temb_ld + n];
+                const float mul = F3 ? p.wsinv[n] * ainv : 1.0f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                    float v = (F3 ? acc[mb][nb][r] * mul : acc[mb][nb][r]) + bn;
+                    if constexpr (ACT == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+                    else if constexpr (ACT == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
+                    int opix;  // output pixel within the image
+                    int oy = 0, ox = 0;
+                    if (p.ident) {
+                        opix = rr0 + row;
+                    } else {
+                        int my = my0, mx = mx0 + row;
+                        if (!fast) {
+                            my = (rr0 + row) / p.Wm;
+                            mx = rr0 + row - my * p.Wm;
+                        }
+                        oy = my * p.osy + p.ooy;
+                        ox = mx * p.osx + p.oox;
+                        opix = oy * p.Wo + ox;
+                    }
+                    if (p.res) v += bload_f1(srd_res, (unsigned)(opix * p.ldres + n) * 4u);
+                    if (p.out_nchw) bstore_f1(srd_out, (unsigned)(n * HWo + opix) * 4u, v);
+                    else bstore_f1(srd_out, (unsigned)(opix * p.ldo + n) * 4u, v);
+                    vmax = fmaxf(vmax, fabsf(v));
+                    acc[mb][nb][r] = v;
+                }
+            }
+        }
+        if (p.absmax) wave_absmax_atomic(p.absmax, b_tile, vmax);
+        if (p.gn_part) {  // this wave's 64 GEMM rows are one pixel block of image b_tile
+            GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
+                     (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + wm,
+                     (p.gn_c0 + n0 + wn * 64) / 32};
+            gn_tile_partials(acc, g, min(2, max(0, (p.N - n0 - wn * 64) / 32)));
+        }
+        return;
+    }
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
         const int mbase = m0 + wm * 64 + mb * 32;
@@ -480,15 +535,6 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                     acc[mb][nb][r] = v;
                 }
             }
-        }
-    }
-    if constexpr (UNIB) {
-        if (p.absmax) wave_absmax_atomic(p.absmax, b_tile, vmax);
-        if (p.gn_part) {  // this wave's 64 GEMM rows are one pixel block of image b_tile
-            GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
-                     (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + wm,
-                     (p.gn_c0 + n0 + wn * 64) / 32};
-            gn_tile_partials(acc, g, min(2, max(0, (p.N - n0 - wn * 64) / 32)));
         }
     }
 }
@@ -595,6 +641,10 @@ int prepare(const wc_conv_args* a, const void* w6, IgDev& d, long& k) {
     d.out_nchw = a->out_nchw;
     d.ident = !a->out_nchw && a->osy == 1 && a->osx == 1 && a->ooy == 0 && a->oox == 0 &&
               a->Ho == a->Hm && a->Wo == a->Wm;
+    // the single-image-tile epilogue addresses one image of the output / residual with 32-bit offsets
+    const long hwo = (long)a->Ho * a->Wo;
+    if ((a->out_nchw ? hwo * a->N : hwo * a->ldo) * 4 >= (1L << 31) || (a->res && hwo * a->ldres * 4 >= (1L << 31)))
+        return WC_E_SHAPE;
     d.steps0 = (int)((long)s0.ntaps * s0.C / BK);
     d.cpt = s0.C / BK;
     d.steps = (int)(k / BK);

@@ -107,6 +107,8 @@ struct X6Tile {
     static constexpr int LDS = 2 * HSTAGE + 2 * BSTAGE;
     static constexpr int H_ITEMS = HPIX * 4;             // float4 items of one halo chunk
     static constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
+    static constexpr int C_PER_T = TH * 16 * 4 / NT;      // float4 items of one residual centre chunk
+    static_assert(C_PER_T * NT == TH * 16 * 4, "whole centre items per thread");
     static constexpr int B_PER_T = (BSTAGE / 16 + NT - 1) / NT;
     // weight items j < B_FULL of every thread are valid in every step (both segments; the last
     // K-step of a chunk may carry a single tap)
@@ -121,8 +123,11 @@ WC_DEVICE int row_dx(int r) {
 }
 
 // PRO: 0 = raw segment 0, 1 = GN affine, 2 = GN affine + SiLU.  RES: segment 1 present.
+// TH = 8 tiles without a residual or with an fp16 one are held to 3 waves per SIMD (<= 168
+// VGPRs; the two-deep residual staging would otherwise take the R16 form to 178 and 2 waves, and
+// 3 waves cost it one spilled VGPR); the other forms run at 2.
 template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL>
-__global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
+__global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(X6Dev p) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
 
     // ---- halo staging coordinates: item i = tid + NT*j is halo pixel i>>2, channels 4*(i&3).. ----
     const int q = tid & 3;
-    int hoff0[T::H_PER_T], hoff1[T::H_PER_T], hlds[T::H_PER_T];
+    int hoff0[T::H_PER_T], hlds[T::H_PER_T];
     unsigned hin = 0, hval = 0;
 #pragma unroll
     for (int j = 0; j < T::H_PER_T; ++j) {
@@ -179,7 +184,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
         hin |= (inb ? 1u : 0u) << j;
         const int pix = (b * p.H + iy) * p.W + ix;
         hoff0[j] = inb ? pix * p.ldc0 + 4 * q : 0;
-        hoff1[j] = inb ? pix * p.ldc1 + 4 * q : 0;
         hlds[j] = (q >> 1) * T::HPLANE + P * 16 + (q & 1) * 8;
     }
 
@@ -190,6 +194,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
     const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
 
     f32x4 rh[T::H_PER_T];
+    // residual (segment-1) chunks: only the TH x 16 halo centre is read (1x1 tap), so they are
+    // staged as centre items, two register sets deep (chunk c in set c & 1): a chunk's loads have
+    // two K-steps to land instead of one
+    f32x4 rc[RES ? 2 : 1][RES ? T::C_PER_T : 1];
+    const int cq = tid & 3, cpx = (tid >> 2) & 15, cpy = tid >> 6;  // item tid + NT j: row cpy + 4 j
+    const unsigned coff0 = (unsigned)(((b * p.H + y0 + cpy) * p.W + x0 + cpx) * p.ldc1 + 4 * cq);
+    const unsigned cstep = (unsigned)(4 * p.W * p.ldc1);
+    const int clds0 = (cq >> 1) * T::HPLANE + ((cpy + 1) * HWD + cpx + 1) * 16 + (cq & 1) * 8;
     f32x4 rsc = {1.f, 1.f, 1.f, 1.f}, rsh = {0.f, 0.f, 0.f, 0.f};
     u32x4 rb[GL ? 1 : T::B_PER_T];
 
@@ -202,11 +214,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             rsc = bload_f4(srdsc, o);
             rsh = bload_f4(srdsh, o);
         }
-    };
-    auto load_halo1 = [&](int c) {
-#pragma unroll
-        for (int j = 0; j < T::H_PER_T; ++j)
-            rh[j] = bload_f4(srd1, ((hin >> j) & 1u) ? (unsigned)(hoff1[j] + c * 16) * 4u : OOB);
     };
     // seg0: prologue + (F3: scale, 2 fp16 pieces | 3 bf16 pieces); seg1: (F3: scale) 3 bf16 pieces
     auto write_halo = [&](int hs, bool seg0) {
@@ -240,6 +247,37 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             }
         }
     };
+    auto load_center = [&](auto P, int c) {
+        constexpr int PV = decltype(P)::value;
+#pragma unroll
+        for (int j = 0; j < T::C_PER_T; ++j)
+            rc[PV][j] = bload_f4(srd1, (coff0 + (unsigned)j * cstep + (unsigned)c * 16u) * 4u);
+    };
+    // segment-1 centre -> halo buffer hs: raw input (F3: scaled), R16: 2 fp16 pieces, else 3 bf16
+    auto write_center = [&](auto P, int hs) {
+        constexpr int PV = decltype(P)::value;
+        unsigned char* base = smem + hs * T::HSTAGE + clds0;
+#pragma unroll
+        for (int j = 0; j < T::C_PER_T; ++j) {
+            f32x4 v = rc[PV][j];
+            if constexpr (F3) v = v * ascale;
+            unsigned char* d = base + j * 4 * HWD * 16;
+            if constexpr (R16) {
+                u32x2 a0, a1;
+                split2_f16(v, a0, a1);
+                *reinterpret_cast<u32x2*>(d) = a0;
+                *reinterpret_cast<u32x2*>(d + 2 * T::HPLANE) = a1;
+            } else {
+                u32x2 a0, a1, a2;
+                split3(v, a0, a1, a2);
+                *reinterpret_cast<u32x2*>(d) = a0;
+                *reinterpret_cast<u32x2*>(d + 2 * T::HPLANE) = a1;
+                *reinterpret_cast<u32x2*>(d + 4 * T::HPLANE) = a2;
+            }
+        }
+    };
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, 1> I1;
     // weight step s (segment-0 steps are BSTEP0 bytes, segment-1 steps BSTEP1)
     // K-step s -> (byte offset of its weights, 16-byte items): segment-0 step s is taps
     // TPS*(s % NMT) .. of chunk s / NMT (the host packs taps of a chunk contiguously)
@@ -397,9 +435,13 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             // The next chunk's halo loads go out one K-step before the last, after that step's
             // weight loads: vmcnt drains in issue order, so a halo load issued earlier would be
             // waited for by every later step's weight-tile wait (an HBM-latency stall per chunk).
+            // After the last chunk come residual centres 0 (one step early) and 1 (in the last).
             if (mt == T::NMT - 2) {
                 if (c + 1 < p.nck0) load_halo0(c + 1);
-                else if (RES) load_halo1(0);
+                else if constexpr (RES) load_center(I0, 0);
+            }
+            if constexpr (RES) {
+                if (mt == T::NMT - 1 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
             }
 #pragma unroll
             for (int tt = 0; tt < T::TPS; ++tt) {
@@ -409,30 +451,39 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_x6_kernel(X6Dev p) {
             if (more) write_b((s + 1) & 1, s + 1);
             if (mt == T::NMT - 1) {
                 if (c + 1 < p.nck0) write_halo(hs ^ 1, true);
-                else if (RES) write_halo(hs ^ 1, false);
+                else if constexpr (RES) write_center(I0, hs ^ 1);
             }
             __syncthreads();
             ++s;
         }
     }
     if constexpr (RES) {
-        for (int c = 0; c < p.nck1; ++c) {
+        // residual chunk c (centre set c & 1): issue centre c + 2 into this set, compute, write
+        // centre c + 1 (loaded a step earlier) into the other halo buffer
+        auto rstep = [&](auto P, int c) {
+            constexpr int PV = decltype(P)::value;
             const int hs = (p.nck0 + c) & 1;
             const bool more = s + 1 < S;
             if (more) {
                 if constexpr (GL) glds_b(s + 1);
                 load_b(s + 1);
-                load_halo1(c + 1);
             }
+            if (c + 2 < p.nck1) load_center(P, c + 2);
             if constexpr (R16) compute3(hs, HWD + 1, s & 1, 0);  // the halo centre = the output pixel
             else compute6(hs, HWD + 1, s & 1);
             if (more) {
                 write_b((s + 1) & 1, s + 1);
-                write_halo(hs ^ 1, false);
+                write_center(std::integral_constant<int, PV ^ 1>{}, hs ^ 1);
             }
             __syncthreads();
             ++s;
+        };
+        int c = 0;
+        for (; c + 1 < p.nck1; c += 2) {
+            rstep(I0, c);
+            rstep(I1, c + 1);
         }
+        if (c < p.nck1) rstep(I0, c);
     }
 
     // ---- epilogue: (F3: x 2^-(sA + sW[n])) + bias + temb, activation, + residual, NHWC store ----

@@ -98,6 +98,21 @@ def test_graph_replay_matches_eager():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+def test_graph_stream_groups_equal_unsplit(precision):
+    # the graph step with the batch as 2 / 4 concurrent image groups (bench --split) is bit-exact
+    from weatherconverter_amd.diffusion_model.sample_ddpm import _GraphStep
+    mc, net = _model('default_64', precision=precision)
+    x = _x(mc, 8, seed=5).cuda()
+    t = torch.tensor([321], device='cuda')
+    with torch.no_grad():
+        ref = _GraphStep(net, x, split=1)(x, t).clone()
+        for sp in (2, 4):
+            step = _GraphStep(net, x, split=sp)
+            assert step.split == sp
+            assert torch.equal(step(x, t).clone(), ref)
+
+
 def test_sharded_sampling_equals_single_rank():
     """Batch sharding with per-sample keyed noise: rows [2, 4) of a B=4 run == a B=2 run at sample0=2."""
     from weatherconverter_amd.diffusion_model.sample_ddpm import sample_tensor

@@ -149,6 +149,17 @@ int wc_conv_igemm_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes,
  * down-sampling convs (:231) and the up-sampling transposed convs (:300). */
 int wc_conv_igemm_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
                         const float* w_inv_scale, const float* a_bound, void* stream);
+/* The down-sampling Conv2d(C, N, 4, stride 2, padding 1) (unet_base.py:129,163) on f16x3 as a
+ * 2x2 stride-1 conv over the space-to-depth view of its raw input: block (BY, BX) = input pixels
+ * (2BY-1+py, 2BX-1+px), 4C channels phase-major (py, px, c), run by the halo-tiled kernel of
+ * wc_conv3x3_f16x3 with a 2x2 tap grid.  args: one raw segment with the 16 taps (ky-1, kx-1),
+ * stride 2, input 2Hm x 2Wm; Hm % 8 == 0, Wm % 16 == 0, N > 64 (else WC_E_SHAPE: use
+ * wc_conv_igemm_f16x3); no residual, activation or output map.  a_bound[b] >= max |x| of image b
+ * (the producer's absmax_out) sets its scale as in wc_conv_igemm_f16x3.  w3 layout per N tile:
+ * [(4C/16) chunks x 4 taps (a, b) steps][piece 2][k-half 2][BN][8] fp16 bits of the weight
+ * w[n][c][2a+py][2b+px] at s2d channel (2py+px)C + c, scaled by 2^sW[n]; w_inv_scale[n] = 2^-sW[n]. */
+int wc_conv4x4s2_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, const float* w_inv_scale,
+                       const float* a_bound, void* stream);
 /* wc_conv_igemm_f16x3 for the attention in-projection (1x1, N = 3C output channels [q | k | v],
  * unet_base.py:115,159 in_proj_weight/in_proj_bias), whose epilogue writes the projection already
  * in the f16x3 form wc_attention_fwd_f16x3_presplit reads instead of fp32 rows: value v of part

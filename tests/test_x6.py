@@ -647,9 +647,13 @@ def test_igemm_f16x3_resampling_with_producer_bound():
     ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1)
     seg = [K.Seg(K.View.full(xp), TAPS4S2, stride=2)]
     outs = {}
-    for mode in ('f16x3', 'fp32'):
+    for mode in ('f16x3', 's2d', 'fp32'):
         o = torch.empty((B, H // 2, H // 2, Co), device='cuda')
-        if mode == 'f16x3':
+        if mode == 's2d':  # the halo kernel over the space-to-depth view (wc_conv4x4s2_f16x3)
+            assert K.conv4x4s2_f16x3_ok(seg[0], Co, H // 2, H // 2)
+            K.conv4x4s2_f16x3(seg[0], K.pack_f16x3_s2d(_pack(w).cuda(), Ci), b.cuda(), K.View.full(o),
+                              Hm=H // 2, Wm=H // 2, a_bound=am)
+        elif mode == 'f16x3':
             K.conv_igemm_f16x3(seg, K.pack_f16x3(_pack(w).cuda(), Ci, ntaps=16, order='natural'), b.cuda(),
                                K.View.full(o), Hm=H // 2, Wm=H // 2, a_exp=60, a_bound=am)
         else:
@@ -657,8 +661,10 @@ def test_igemm_f16x3_resampling_with_producer_bound():
         torch.cuda.synchronize()
         outs[mode] = _nchw(o.cpu()).double()
     for i in range(B):  # per image: each one's own scale
-        e3, e32 = rel_l2(outs['f16x3'][i], ref[i]), rel_l2(outs['fp32'][i], ref[i])
-        assert e3 < 1e-5 and e3 <= 4 * e32 + 2e-7, (i, e3, e32)
+        e32 = rel_l2(outs['fp32'][i], ref[i])
+        for mode in ('f16x3', 's2d'):
+            e3 = rel_l2(outs[mode][i], ref[i])
+            assert e3 < 1e-5 and e3 <= 4 * e32 + 2e-7, (mode, i, e3, e32)
 
     # transposed conv (ConvTranspose2d(Ci, Co2, 4, 2, 1)) from the same producer output
     Co2 = 64
@@ -690,6 +696,49 @@ def test_igemm_f16x3_resampling_with_producer_bound():
         K.conv_igemm_f16x3([K.Seg(xs, [(0, 0)])], K.pack_f16x3(torch.randn(Co, Ci).cuda(), Ci, ntaps=1,
                            order='natural'), None, K.View.full(torch.empty((B, 12, 12, Co), device='cuda')),
                            Hm=12, Wm=12, a_exp=60, a_bound=am)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,ldc', [(2, 16, 32, 128, 128, 256), (1, 32, 32, 256, 256, 256),
+                                             (2, 16, 64, 64, 192, 64)])
+def test_conv4x4s2_s2d_vs_float64(B, H, W, Ci, Co, ldc):
+    """wc_conv4x4s2_f16x3 (the down conv as a 2x2 conv over the space-to-depth input on the halo
+    kernel) against float64 and the implicit-GEMM f16x3 path: strided input views, non-square
+    grids, a ragged N tile (192 = 128 + 64), border blocks on every side, GN tile partials from the
+    epilogue vs a stats pass; shapes outside its tiling are refused."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(7 + Ci)
+    x = torch.randn((B, Ci, H, W), generator=g) * torch.tensor([3.0, 0.01][:B])[:, None, None, None]
+    buf = torch.randn((B, H, W, ldc), generator=g).cuda()
+    buf[..., :Ci] = _nhwc(x).cuda()
+    xv = K.View(buf, 0, Ci)
+    am = _img_amax(_nhwc(x)).cuda()
+    w = torch.randn((Co, Ci, 4, 4), generator=g) / (16 * Ci)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1)
+    seg = K.Seg(xv, TAPS4S2, stride=2)
+    Hm, Wm = H // 2, W // 2
+    assert K.conv4x4s2_f16x3_ok(seg, Co, Hm, Wm)
+    o = torch.empty((B, Hm, Wm, Co), device='cuda')
+    gp = K.GnPart.attach(o, 8) if Co % 32 == 0 else None
+    K.conv4x4s2_f16x3(seg, K.pack_f16x3_s2d(_pack(w).cuda(), Ci), b.cuda(), K.View.full(o), Hm=Hm, Wm=Wm,
+                      a_bound=am, gn=gp)
+    oi = torch.empty_like(o)
+    K.conv_igemm_f16x3([seg], K.pack_f16x3(_pack(w).cuda(), Ci, ntaps=16, order='natural'), b.cuda(),
+                       K.View.full(oi), Hm=Hm, Wm=Wm, a_exp=60, a_bound=am)
+    torch.cuda.synchronize()
+    got, gi = _nchw(o.cpu()).double(), _nchw(oi.cpu()).double()
+    for i in range(B):
+        assert rel_l2(got[i], ref[i]) < 1e-5, (i, rel_l2(got[i], ref[i]))
+        assert rel_l2(got[i], gi[i]) < 1e-5
+    if gp is not None:  # epilogue partials give the stats pass's GroupNorm affine
+        gam, bet = torch.randn(Co).cuda(), torch.randn(Co).cuda()
+        s1, h1 = K.gn_affine(K.View.full(o), gam, bet, part=gp)
+        s2, h2 = K.gn_affine(K.View.full(o), gam, bet)
+        torch.cuda.synchronize()
+        assert torch.allclose(s1, s2, rtol=1e-5, atol=0) and torch.allclose(h1, h2, rtol=1e-5, atol=1e-6)
+    bad = K.Seg(K.View.full(torch.randn((B, 12, 32, Ci), device='cuda')), TAPS4S2, stride=2)
+    assert not K.conv4x4s2_f16x3_ok(bad, Co, 6, 16)
 
 
 # ---------------------------------------------------------------- GroupNorm tile partials (epilogue-fused statistics)

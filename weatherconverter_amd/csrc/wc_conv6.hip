@@ -77,6 +77,7 @@ struct X6Dev {
     float* gn_part;       // optional GroupNorm tile partials of the output (wcx6::gn_tile_partials)
     int gn_ncb, gn_sw, gn_c0, gn_np64;
     int tiles_x, tiles_y, ntiles_n;
+    int s2d_cpp, Hi, Wi;  // S2D: 16-channel chunks per phase (C / 16) and the input's H, W
 };
 
 // F3: segment 0 in f16x3 (2 pieces), else bf16x6 (3 pieces).  R16: segment 1 in f16x3 too (needs
@@ -84,7 +85,7 @@ struct X6Dev {
 // GL: weights staged by LDS-DMA (global_load_lds_dwordx4 straight into the LDS image the host
 // pre-laid out) at three taps (one halo row) per K-step: 36 MFMAs per wave between barriers and
 // no weight registers; else register-staged, one tap per K-step.
-template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false>
+template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, bool S2D = false>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
@@ -101,7 +102,8 @@ struct X6Tile {
     static constexpr int BSTEP1 = 2 * NP1 * BPLANE;      // one segment-1 weight step
     // taps per K-step (2 for f16x3 measured slower: 302 vs 322 TF/s, larger LDS weight stage)
     static constexpr int TPS = GL ? 3 : 1;
-    static constexpr int NMT = (9 + TPS - 1) / TPS;       // K-steps per 16-channel chunk
+    static constexpr int NTAP = S2D ? 4 : 9;             // taps per chunk (S2D: the 2x2 block taps)
+    static constexpr int NMT = (NTAP + TPS - 1) / TPS;    // K-steps per 16-channel chunk
     static constexpr int BSTEPM = TPS * BSTEP0;           // weight bytes of a full segment-0 K-step
     static constexpr int BSTAGE = (RES && BSTEP1 > BSTEPM) ? BSTEP1 : BSTEPM;  // LDS weight buffer
     static constexpr int LDS = 2 * HSTAGE + 2 * BSTAGE;
@@ -126,9 +128,10 @@ WC_DEVICE int row_dx(int r) {
 // TH = 8 tiles without a residual or with an fp16 one are held to 3 waves per SIMD (<= 168
 // VGPRs; the two-deep residual staging would otherwise take the R16 form to 178 and 2 waves, and
 // 3 waves cost it one spilled VGPR); the other forms run at 2.
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, bool S2D = false>
 __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(X6Dev p) {
-    using T = X6Tile<TH, BN, RES, F3, R16, GL>;
+    using T = X6Tile<TH, BN, RES, F3, R16, GL, S2D>;
+    static_assert(!S2D || (!RES && !GL && PRO == 0), "S2D: raw single-segment register-staged form");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -164,13 +167,15 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     const float ascale = ldexpf(1.0f, s_exp), ainv = ldexpf(1.0f, -s_exp);
     const int S0 = T::NMT * p.nck0;  // segment-0 K-steps
     const int S = S0 + (RES ? p.nck1 : 0);
-    const unsigned seg0_bytes = (unsigned)(9 * p.nck0 * T::BSTEP0);
+    const unsigned seg0_bytes = (unsigned)(T::NTAP * p.nck0 * T::BSTEP0);
     const unsigned wtile = (unsigned)tile_n * (seg0_bytes + (unsigned)((RES ? p.nck1 : 0) * T::BSTEP1));
 
     // ---- halo staging coordinates: item i = tid + NT*j is halo pixel i>>2, channels 4*(i&3).. ----
     const int q = tid & 3;
+    // S2D: halo pixel (hy, hx) is the 2x2 input block (BY, BX) = (y0 - 1 + hy, x0 - 1 + hx) of
+    // input pixels (2 BY - 1 + py, 2 BX - 1 + px); its in-bounds bits per phase row / column
     int hoff0[T::H_PER_T], hlds[T::H_PER_T];
-    unsigned hin = 0, hval = 0;
+    unsigned hin = 0, hval = 0, hr0 = 0, hr1 = 0, hc0 = 0, hc1 = 0;
 #pragma unroll
     for (int j = 0; j < T::H_PER_T; ++j) {
         const int i = tid + NT * j;
@@ -179,13 +184,23 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         const int hx = P - hy * HWD;
         const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
         const bool valid = i < T::H_ITEMS;
-        const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
         hval |= (valid ? 1u : 0u) << j;
-        hin |= (inb ? 1u : 0u) << j;
-        const int pix = (b * p.H + iy) * p.W + ix;
-        hoff0[j] = inb ? pix * p.ldc0 + 4 * q : 0;
         hlds[j] = (q >> 1) * T::HPLANE + P * 16 + (q & 1) * 8;
+        if constexpr (S2D) {
+            const int y2 = 2 * iy - 1, x2 = 2 * ix - 1;
+            hr0 |= (valid && (unsigned)y2 < (unsigned)p.Hi ? 1u : 0u) << j;
+            hr1 |= (valid && (unsigned)(y2 + 1) < (unsigned)p.Hi ? 1u : 0u) << j;
+            hc0 |= ((unsigned)x2 < (unsigned)p.Wi ? 1u : 0u) << j;
+            hc1 |= ((unsigned)(x2 + 1) < (unsigned)p.Wi ? 1u : 0u) << j;
+            hoff0[j] = ((b * p.Hi + y2) * p.Wi + x2) * p.ldc0 + 4 * q;  // used only with a phase in bounds
+        } else {
+            const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+            hin |= (inb ? 1u : 0u) << j;
+            const int pix = (b * p.H + iy) * p.W + ix;
+            hoff0[j] = inb ? pix * p.ldc0 + 4 * q : 0;
+        }
     }
+    unsigned hinc = hin;  // in-bounds bits of the chunk in the halo registers
 
     const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
     const __amdgpu_buffer_rsrc_t srd1 = make_srd(RES ? p.src1 : p.src0);
@@ -206,9 +221,19 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     u32x4 rb[GL ? 1 : T::B_PER_T];
 
     auto load_halo0 = [&](int c) {
+        if constexpr (S2D) {  // chunk c = (phase (py, px), 16 channels): phase-major over 4C channels
+            const int ph = c / p.s2d_cpp;
+            const int py = ph >> 1, px = ph & 1;
+            hinc = (py ? hr1 : hr0) & (px ? hc1 : hc0);
+            const int d = (py * p.Wi + px) * p.ldc0 + (c - ph * p.s2d_cpp) * 16;
 #pragma unroll
-        for (int j = 0; j < T::H_PER_T; ++j)
-            rh[j] = bload_f4(srd0, ((hin >> j) & 1u) ? (unsigned)(hoff0[j] + c * 16) * 4u : OOB);
+            for (int j = 0; j < T::H_PER_T; ++j)
+                rh[j] = bload_f4(srd0, ((hinc >> j) & 1u) ? (unsigned)(hoff0[j] + d) * 4u : OOB);
+        } else {
+#pragma unroll
+            for (int j = 0; j < T::H_PER_T; ++j)
+                rh[j] = bload_f4(srd0, ((hin >> j) & 1u) ? (unsigned)(hoff0[j] + c * 16) * 4u : OOB);
+        }
         if constexpr (PRO != 0) {
             const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
             rsc = bload_f4(srdsc, o);
@@ -231,7 +256,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                     }
                 }
             }
-            if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+            if (!((hinc >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
             if constexpr (F3) v = v * ascale;
             if ((F3 && seg0) || (R16 && !seg0)) {
                 u32x2 a0, a1;
@@ -287,8 +312,8 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             items = T::BSTEP1 / 16;
         } else {
             const int c = s / T::NMT, t0 = (s - c * T::NMT) * T::TPS;
-            const int nt = 9 - t0 < T::TPS ? 9 - t0 : T::TPS;
-            off = wtile + (unsigned)((c * 9 + t0) * T::BSTEP0);
+            const int nt = T::NTAP - t0 < T::TPS ? T::NTAP - t0 : T::TPS;
+            off = wtile + (unsigned)((c * T::NTAP + t0) * T::BSTEP0);
             items = nt * T::BSTEP0 / 16;
         }
     };
@@ -446,7 +471,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
 #pragma unroll
             for (int tt = 0; tt < T::TPS; ++tt) {
                 const int tp = mt * T::TPS + tt;
-                if (tp < 9) compute0(hs, (tp / 3) * HWD + tp % 3, s & 1, tt);
+                if (tp < T::NTAP) compute0(hs, S2D ? ((tp >> 1) + 1) * HWD + (tp & 1) + 1 : (tp / 3) * HWD + tp % 3, s & 1, tt);
             }
             if (more) write_b((s + 1) & 1, s + 1);
             if (mt == T::NMT - 1) {
@@ -526,12 +551,12 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, bool S2D = false>
 int launch6(const X6Dev& d, hipStream_t stream) {
-    using T = X6Tile<TH, BN, RES, F3, R16, GL>;
+    using T = X6Tile<TH, BN, RES, F3, R16, GL, S2D>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, S2D>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -541,7 +566,7 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL>), grid, dim3(NT), T::LDS, stream, p);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, S2D>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -683,4 +708,50 @@ extern "C" int wc_conv3x3_f16x3(const wc_conv_args* a, const void* w3, int64_t w
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (BN == 64) return dispatch6<16, 64>(d, pro, a->nseg == 2, true, s);
     return dispatch6<8, 128>(d, pro, a->nseg == 2, true, s);
+}
+
+// 4x4 stride-2 pad-1 conv (the UNet down-sampling conv) as a 2x2 stride-1 conv over the
+// space-to-depth view of its input: output (oy, ox) = sum over taps (a, b) in {0,1}^2 of block
+// (oy + a, ox + b), block (BY, BX) = input pixels (2 BY - 1 + py, 2 BX - 1 + px) as 4C channels
+// (phase-major), so the weight tap (ky, kx) = (2a + py, 2b + px).  The halo kernel runs it with a
+// 2x2 tap grid and the block -> pixel map in its halo loader: each input value is staged once per
+// tile instead of once per tap.  Raw input on f16x3 under the producer's per-image bound.
+extern "C" int wc_conv4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, const float* w_inv_scale,
+                                  const float* a_bound, void* stream) {
+    if (!a || !w3 || !a->out || !w_inv_scale || !a_bound) return WC_E_ARG;
+    if (a->nseg != 1 || a->act != WC_ACT_NONE) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src || s0.scale || s0.shift) return WC_E_ARG;
+    if (s0.ntaps != 16 || s0.sy != 2 || s0.sx != 2 || s0.kbase != 0) return WC_E_SHAPE;
+    for (int t = 0; t < 16; ++t)
+        if (s0.dy[t] != t / 4 - 1 || s0.dx[t] != t % 4 - 1) return WC_E_SHAPE;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    if (BN != 128) return WC_E_SHAPE;  // the TH = 8 x BN = 128 form only (N > 64)
+    if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
+    if (a->B <= 0 || a->Hm % 8 || a->Wm % 16 || s0.H != 2 * a->Hm || s0.W != 2 * a->Wm) return WC_E_SHAPE;
+    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+    if (reinterpret_cast<uintptr_t>(w3) & 15) return WC_E_SHAPE;
+    if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox || a->res)
+        return WC_E_SHAPE;
+    if ((long)a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;
+    X6Dev d{};
+    d.src0 = s0.src; d.C0 = 4 * s0.C; d.ldc0 = s0.ldc;
+    d.nck0 = 4 * s0.C / 16;
+    d.s2d_cpp = s0.C / 16; d.Hi = s0.H; d.Wi = s0.W;
+    d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
+    d.w6 = w3; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
+    d.out = a->out; d.ldo = a->ldo; d.act = WC_ACT_NONE;
+    d.a_exp = 60; d.abound = a_bound; d.wsinv = w_inv_scale;
+    d.absmax = a->absmax_out;
+    d.gn_part = a->gn_part;
+    if (a->gn_part) {
+        const int sw = a->gn_sw;
+        if ((sw != 4 && sw != 8 && sw != 16 && sw != 32) || a->N % 32 || a->gn_c0 % 32 || a->gn_c0 < 0 ||
+            a->gn_c0 + a->N > a->gn_ncb * 32 || a->gn_p64 != 0 || a->gn_np64 * 64 != a->Hm * a->Wm)
+            return WC_E_SHAPE;
+        d.gn_ncb = a->gn_ncb; d.gn_sw = sw; d.gn_c0 = a->gn_c0; d.gn_np64 = a->gn_np64;
+    }
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w3_bytes != ntn * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    return launch6<8, 128, 0, false, true, false, false, true>(d, reinterpret_cast<hipStream_t>(stream));
 }

@@ -134,7 +134,8 @@ class UnetEngine:
                     w = pack_conv(blk.down_sample_conv.weight)
                     ci = blk.down_sample_conv.in_channels
                     self.down_convs.append((w, blk.down_sample_conv.bias.detach().float(),
-                                            self._x6(w, ci, len(TAPS4S2)), self._f3n(w, ci, len(TAPS4S2))))
+                                            self._x6(w, ci, len(TAPS4S2)), self._f3n(w, ci, len(TAPS4S2)),
+                                            self._f3s(w, ci)))
                 else:
                     self.down_convs.append(None)
             self.mids = [self._pack_stage(blk, n_res=blk.num_layers + 1, attn=True) for blk in m.mids]
@@ -205,6 +206,14 @@ class UnetEngine:
         if self.precision != 'f16x3' or c0 % 16:
             return None
         return K.pack_f16x3(w, c0, ntaps=ntaps, order='natural')
+
+    def _f3s(self, w: torch.Tensor, c0: int) -> Optional[K.X6Weight]:
+        """f16x3 space-to-depth pack of a 4x4 / stride-2 down conv for wc_conv4x4s2_f16x3 (the halo
+        kernel), or None (outside f16x3 mode, N <= 64, or WC_DOWN_S2D=0: the implicit GEMM)."""
+        if (self.precision != 'f16x3' or c0 % 16 or K.x6_tile(w.shape[0])[1] != 128
+                or os.environ.get('WC_DOWN_S2D', '1') == '0'):
+            return None
+        return K.pack_f16x3_s2d(w, c0)
 
     def _pack_attn(self, blk, i: int) -> AttnPack:
         mha, gn = blk.attentions[i], blk.attention_norms[i]
@@ -426,9 +435,16 @@ class UnetEngine:
                     bnd = slot if self.attention(tgt, att[li], absmax=slot) else None
                 cur = tgt
             if self.down_convs[i] is not None:
-                w, b, w6, w3 = self.down_convs[i]
-                self.resample([Seg(cur, TAPS4S2, stride=2)], (w, w6, w3), b, final, sizes[i + 1][0], sizes[i + 1][1],
-                              bnd)
+                w, b, w6, w3, w3s = self.down_convs[i]
+                seg = Seg(cur, TAPS4S2, stride=2)
+                Hm, Wm = sizes[i + 1]
+                if w3s is not None and bnd is not None and K.conv4x4s2_f16x3_ok(seg, w3s.N, Hm, Wm):
+                    gp = K.GnPart.of(final)
+                    fused = K.gn_conv_ok(final, gp, w3s.N, Hm, Wm)
+                    K.conv4x4s2_f16x3(seg, w3s, b, final, Hm=Hm, Wm=Wm, a_bound=bnd, gn=gp if fused else None)
+                    self._gn_fill(final, fused)
+                else:
+                    self.resample([seg], (w, w6, w3), b, final, Hm, Wm, bnd)
                 cur = final
 
         # ---------------- mid path

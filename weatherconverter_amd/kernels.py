@@ -346,7 +346,7 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     bound, wc_conv3x3_f16x3)."""
     N, K = w.shape
     _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'f16x3 weight shape')
-    _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
+    _req(order == 'natural' or ntaps in (9, 4), "order 'halo' is for 3x3 (or s2d 2x2) weights")
     _, BN = x6_tile(N)
     Np = -(-N // BN) * BN
     T = Np // BN
@@ -360,7 +360,7 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     ws = wp * torch.ldexp(torch.ones_like(wp[:, :1]), sw[:, None].float())  # exact power-of-two scaling
     S0, S1 = K0 // 16, C1 // 16
     if order == 'halo':
-        main = ws[:, :K0].reshape(Np, 9, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, S0, 2, 8)
+        main = ws[:, :K0].reshape(Np, ntaps, C0 // 16, 2, 8).permute(0, 2, 1, 3, 4).reshape(Np, S0, 2, 8)
     else:
         _req(order == 'natural', f'unknown f16x3 order {order!r}')
         main = ws[:, :K0].reshape(Np, S0, 2, 8)
@@ -378,7 +378,8 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
         parts.append(pr.permute(1, 3, 0, 4, 2, 5).reshape(T, -1))
     data = torch.cat(parts, 1).contiguous()
     wsinv = torch.ldexp(torch.ones(Np, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
-    return X6Weight(data, N, BN, C0, C1, 'f16x3' if order == 'halo' else 'f16x3n', wsinv, res_f16)
+    order_tag = ('f16x3' if ntaps == 9 else 'f16x3s') if order == 'halo' else 'f16x3n'
+    return X6Weight(data, N, BN, C0, C1, order_tag, wsinv, res_f16)
 
 
 def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
@@ -442,6 +443,36 @@ def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Ten
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, 0, true>', 'wc_conv_igemm_f16x3',
            _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
+
+
+def pack_f16x3_s2d(w: torch.Tensor, C: int) -> X6Weight:
+    """f16x3 pack of a 4x4 stride-2 conv weight for wc_conv4x4s2_f16x3.  w is [N][(ky*4 + kx)*C + c]
+    (engine.pack_conv); the kernel's view is a 2x2 conv over the space-to-depth input, tap (a, b),
+    channel (2py + px)*C + c <- w[n][c][2a + py][2b + px]."""
+    N = w.shape[0]
+    _req(w.shape[1] == 16 * C and C % 16 == 0, '4x4 conv weight shape')
+    w2 = w.reshape(N, 2, 2, 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, 16 * C)  # (a, py, b, px) -> (a, b, py, px)
+    return pack_f16x3(w2, 4 * C, ntaps=4, order='halo')
+
+
+def conv4x4s2_f16x3_ok(seg: Seg, N: int, Hm: int, Wm: int) -> bool:
+    """Shapes wc_conv4x4s2_f16x3 takes (else use conv_igemm_f16x3)."""
+    v = seg.view
+    return (x6_tile(N)[1] == 128 and Hm % 8 == 0 and Wm % 16 == 0 and v.H == 2 * Hm and v.W == 2 * Wm
+            and v.C % 16 == 0 and seg.scale is None and seg.stride == 2)
+
+
+def conv4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
+                    a_bound: torch.Tensor, absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None):
+    """Down-sampling 4x4 / stride-2 / pad-1 conv of a raw input on f16x3 (wc_conv4x4s2_f16x3): the
+    halo-tiled kernel over the space-to-depth view; a_bound = per-image max |x| (the producer's absmax)."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3s', 'f16x3 s2d weight')
+    _req(w3.C0 == 4 * seg.view.C and w3.C1 == 0, 'f16x3 s2d weight channels')
+    _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == seg.view.B, 'A bound')
+    a = _conv_args([seg], w3.N, bias, out, Hm, Wm, None, 0, None, (1, 1, 0, 0), None, 0, absmax, gn=gn)
+    _timed('conv3x3_x6_kernel<8, 128, 0, false, true, false, false, true> (s2d 4x4/s2)', 'wc_conv4x4s2_f16x3',
+           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
 
 
 def qkv_presplit_ok(B: int, N: int, C: int, heads: int) -> bool:

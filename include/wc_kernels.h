@@ -160,6 +160,18 @@ int wc_conv_igemm_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_byt
  * w[n][c][2a+py][2b+px] at s2d channel (2py+px)C + c, scaled by 2^sW[n]; w_inv_scale[n] = 2^-sW[n]. */
 int wc_conv4x4s2_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, const float* w_inv_scale,
                        const float* a_bound, void* stream);
+/* The up-sampling ConvTranspose2d(C, N, 4, stride 2, padding 1) (unet_base.py:333-334,348) on
+ * f16x3 in one launch of the halo-tiled kernel: output parity (py, px) is a 2x2 stride-1 conv over
+ * the raw input, tap (i, j) at input offset (py - i, px - j) with weight rows ky = 1, 3 (py 0) or
+ * 0, 2 (py 1) for i = 0, 1, columns likewise, stored at output pixel
+ * (2y + py, 2x + px).  args: one raw segment (taps ignored, stride 1) over the Hm x Wm input grid;
+ * output view Ho = 2Hm, Wo = 2Wm with osy = osx = 2, ooy = oox = 0; Hm % TH == 0 (TH = 16 for
+ * N <= 64 else 8), Wm % 16 == 0; no residual, temb or activation.  GN partials: gn_np64 = 4HmWm/64,
+ * gn_p64 = 0 (parity p writes blocks p*HmWm/64 ..).  a_bound as wc_conv4x4s2_f16x3.  w3 layout
+ * per N tile: [parity 4][(C/16) chunks x 4 taps][piece 2][k-half 2][BN][8] fp16 bits, one scale
+ * 2^sW[n] for all parities; w_inv_scale[n] = 2^-sW[n]. */
+int wc_convtr4x4s2_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, const float* w_inv_scale,
+                        const float* a_bound, void* stream);
 /* wc_conv_igemm_f16x3 for the attention in-projection (1x1, N = 3C output channels [q | k | v],
  * unet_base.py:115,159 in_proj_weight/in_proj_bias), whose epilogue writes the projection already
  * in the f16x3 form wc_attention_fwd_f16x3_presplit reads instead of fp32 rows: value v of part

@@ -741,6 +741,53 @@ def test_conv4x4s2_s2d_vs_float64(B, H, W, Ci, Co, ldc):
     assert not K.conv4x4s2_f16x3_ok(bad, Co, 6, 16)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co', [(2, 8, 16, 64, 128), (2, 16, 32, 128, 64), (1, 8, 32, 32, 192)])
+def test_convT4x4s2_one_launch_vs_float64(B, H, W, Ci, Co):
+    """wc_convtr4x4s2_f16x3 (all four output parities in one launch of the halo kernel) against
+    float64 and the four implicit-GEMM parities, writing the first half of a wider (skip-concat)
+    buffer whose other half stays untouched; both tile forms (N <= 64: TH 16), a ragged N tile;
+    GN tile partials from the epilogue vs a stats pass."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.models.engine import pack_convT
+    g = torch.Generator().manual_seed(11 + Co)
+    x = torch.randn((B, Ci, H, W), generator=g) * torch.tensor([2.0, 1e-2][:B])[:, None, None, None]
+    xin = _nhwc(x).cuda()
+    am = _img_amax(_nhwc(x)).cuda()
+    wt = torch.randn((Ci, Co, 4, 4), generator=g) / (4 * Ci)**0.5
+    bt = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv_transpose2d(x.double(), wt.double(), bt.double(), stride=2, padding=1)
+    seg = K.Seg(K.View.full(xin), [(0, 0)])
+    assert K.convT4x4s2_f16x3_ok(seg, Co)
+    outs = {}
+    for mode in ('one', 'parities'):
+        buf = torch.full((B, 2 * H, 2 * W, 2 * Co), 5.0, device='cuda')
+        dst = K.View(buf, 0, Co)
+        gp = K.GnPart.attach(buf, 8) if mode == 'one' else None
+        if mode == 'one':
+            K.convT4x4s2_f16x3(seg, K.pack_f16x3_convT(wt.cuda()), bt.cuda(), dst, a_bound=am, gn=gp)
+        else:
+            for py in (0, 1):
+                for px in (0, 1):
+                    taps, wp = pack_convT(wt, py, px)
+                    K.conv_igemm_f16x3([K.Seg(K.View.full(xin), taps)], K.pack_f16x3(wp.cuda(), Ci, ntaps=4,
+                                       order='natural'), bt.cuda(), dst, Hm=H, Wm=W, a_exp=60, a_bound=am,
+                                       out_map=(2, 2, py, px))
+        torch.cuda.synchronize()
+        bc = buf.cpu()
+        assert bool((bc[..., Co:] == 5.0).all())
+        outs[mode] = _nchw(bc[..., :Co]).double()
+        if gp is not None:
+            gam, bet = torch.randn(Co).cuda(), torch.randn(Co).cuda()
+            s1, h1 = K.gn_affine(dst, gam, bet, part=gp)
+            s2, h2 = K.gn_affine(dst, gam, bet)
+            torch.cuda.synchronize()
+            assert torch.allclose(s1, s2, rtol=1e-5, atol=0) and torch.allclose(h1, h2, rtol=1e-5, atol=1e-6)
+    for i in range(B):
+        assert rel_l2(outs['one'][i], ref[i]) < 1e-5, (i, rel_l2(outs['one'][i], ref[i]))
+        assert rel_l2(outs['one'][i], outs['parities'][i]) < 1e-5
+
+
 # ---------------------------------------------------------------- GroupNorm tile partials (epilogue-fused statistics)
 
 @pytest.mark.gpu

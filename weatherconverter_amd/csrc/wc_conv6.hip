@@ -85,7 +85,9 @@ struct X6Dev {
 // GL: weights staged by LDS-DMA (global_load_lds_dwordx4 straight into the LDS image the host
 // pre-laid out) at three taps (one halo row) per K-step: 36 MFMAs per wave between barriers and
 // no weight registers; else register-staged, one tap per K-step.
-template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, bool S2D = false>
+// MAP: 0 = 3x3 stride 1; 1 = 4x4/s2 down conv over the space-to-depth input (2x2 taps); 2 = the
+// 4x4/s2 transposed conv, one output parity per workgroup (2x2 taps of the 3x3 frame).
+template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, int MAP = 0>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
@@ -102,7 +104,7 @@ struct X6Tile {
     static constexpr int BSTEP1 = 2 * NP1 * BPLANE;      // one segment-1 weight step
     // taps per K-step (2 for f16x3 measured slower: 302 vs 322 TF/s, larger LDS weight stage)
     static constexpr int TPS = GL ? 3 : 1;
-    static constexpr int NTAP = S2D ? 4 : 9;             // taps per chunk (S2D: the 2x2 block taps)
+    static constexpr int NTAP = MAP ? 4 : 9;             // taps per chunk (MAP 1, 2: 2x2 taps)
     static constexpr int NMT = (NTAP + TPS - 1) / TPS;    // K-steps per 16-channel chunk
     static constexpr int BSTEPM = TPS * BSTEP0;           // weight bytes of a full segment-0 K-step
     static constexpr int BSTAGE = (RES && BSTEP1 > BSTEPM) ? BSTEP1 : BSTEPM;  // LDS weight buffer
@@ -128,10 +130,11 @@ WC_DEVICE int row_dx(int r) {
 // TH = 8 tiles without a residual or with an fp16 one are held to 3 waves per SIMD (<= 168
 // VGPRs; the two-deep residual staging would otherwise take the R16 form to 178 and 2 waves, and
 // 3 waves cost it one spilled VGPR); the other forms run at 2.
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, bool S2D = false>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP = 0>
 __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(X6Dev p) {
-    using T = X6Tile<TH, BN, RES, F3, R16, GL, S2D>;
-    static_assert(!S2D || (!RES && !GL && PRO == 0), "S2D: raw single-segment register-staged form");
+    using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP>;
+    constexpr bool S2D = MAP == 1, CT = MAP == 2;
+    static_assert(!MAP || (!RES && !GL && PRO == 0), "MAP 1, 2: raw single-segment register-staged forms");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -148,6 +151,9 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     }
+    // CT: the four output parities of one tile are consecutive blocks (one halo, one L2)
+    const int par = CT ? (bid & 3) : 0;
+    if (CT) bid >>= 2;
     const int tile_n = bid % p.ntiles_n;
     int tt = bid / p.ntiles_n;
     const int txi = tt % p.tiles_x;
@@ -168,7 +174,8 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     const int S0 = T::NMT * p.nck0;  // segment-0 K-steps
     const int S = S0 + (RES ? p.nck1 : 0);
     const unsigned seg0_bytes = (unsigned)(T::NTAP * p.nck0 * T::BSTEP0);
-    const unsigned wtile = (unsigned)tile_n * (seg0_bytes + (unsigned)((RES ? p.nck1 : 0) * T::BSTEP1));
+    const unsigned wtile = CT ? (unsigned)(tile_n * 4 + par) * seg0_bytes
+                              : (unsigned)tile_n * (seg0_bytes + (unsigned)((RES ? p.nck1 : 0) * T::BSTEP1));
 
     // ---- halo staging coordinates: item i = tid + NT*j is halo pixel i>>2, channels 4*(i&3).. ----
     const int q = tid & 3;
@@ -471,7 +478,13 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
 #pragma unroll
             for (int tt = 0; tt < T::TPS; ++tt) {
                 const int tp = mt * T::TPS + tt;
-                if (tp < T::NTAP) compute0(hs, S2D ? ((tp >> 1) + 1) * HWD + (tp & 1) + 1 : (tp / 3) * HWD + tp % 3, s & 1, tt);
+                if (tp < T::NTAP) {
+                    // CT parity (py, px): tap (i, j) reads input offset (py - i, px - j) (engine._CT_TAPS)
+                    const int toff = S2D ? ((tp >> 1) + 1) * HWD + (tp & 1) + 1
+                                   : CT  ? ((par >> 1) - (tp >> 1) + 1) * HWD + (par & 1) - (tp & 1) + 1
+                                         : (tp / 3) * HWD + tp % 3;
+                    compute0(hs, toff, s & 1, tt);
+                }
             }
             if (more) write_b((s + 1) & 1, s + 1);
             if (mt == T::NMT - 1) {
@@ -514,13 +527,15 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     // ---- epilogue: (F3: x 2^-(sA + sW[n])) + bias + temb, activation, + residual, NHWC store ----
     // 32-bit buffer offsets from the image's base (the tile is one image): one multiply per row,
     // no 64-bit address arithmetic per element
-    const long img_px = (long)b * p.H * p.W;
+    const long img_px = (long)b * p.H * p.W * (CT ? 4 : 1);
     const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + img_px * p.ldo);
     const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + img_px * p.ldres : p.out);
     float vmax = 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
-        const int pix0 = (y0 + 4 * wm + 2 * mb) * p.W + x0;  // pixel (dy 0, dx 0) of this 32-row block
+        // pixel (dy 0, dx 0) of this 32-row block; CT: output pixel (2y + py, 2x + px) of 2H x 2W
+        const int pix0 = CT ? (2 * (y0 + 4 * wm + 2 * mb) + (par >> 1)) * 2 * p.W + 2 * x0 + (par & 1)
+                            : (y0 + 4 * wm + 2 * mb) * p.W + x0;
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             const int n = n0 + wn * 64 + nb * 32 + l32;
@@ -531,7 +546,8 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int pix = pix0 + (row_dy(row) ? p.W : 0) + row_dx(row);
+                const int pix = CT ? pix0 + (row_dy(row) ? 4 * p.W : 0) + 2 * row_dx(row)
+                                   : pix0 + (row_dy(row) ? p.W : 0) + row_dx(row);
                 float v = (F3 ? acc[mb][nb][r] * mul : acc[mb][nb][r]) + add;
                 if (p.act == WC_ACT_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
                 else if (p.act == WC_ACT_SILU) v = v / (1.0f + __expf(-v));
@@ -546,17 +562,18 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     if (p.gn_part) {
         // this wave's 64 pixels (4 rows x 16 columns of the tile) are pixel block p64 of image b
         GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
-                 (long)b * p.gn_np64 + (tyi * p.tiles_x + txi) * T::WAVES_M + wm, (p.gn_c0 + n0 + wn * 64) / 32};
+                 (long)b * p.gn_np64 + par * (p.H * p.W / 64) + (tyi * p.tiles_x + txi) * T::WAVES_M + wm,
+                 (p.gn_c0 + n0 + wn * 64) / 32};
         gn_tile_partials(acc, g, min(2, max(0, (p.N - n0 - wn * 64) / 32)));
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, bool S2D = false>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0>
 int launch6(const X6Dev& d, hipStream_t stream) {
-    using T = X6Tile<TH, BN, RES, F3, R16, GL, S2D>;
+    using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, S2D>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -565,8 +582,8 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_x = p.W / 16;
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
-    dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, S2D>), grid, dim3(NT), T::LDS, stream, p);
+    dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n * (MAP == 2 ? 4 : 1));
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -753,5 +770,48 @@ extern "C" int wc_conv4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64_t
     }
     const long ntn = (a->N + BN - 1) / BN;
     if (w3_bytes != ntn * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
-    return launch6<8, 128, 0, false, true, false, false, true>(d, reinterpret_cast<hipStream_t>(stream));
+    return launch6<8, 128, 0, false, true, false, false, 1>(d, reinterpret_cast<hipStream_t>(stream));
+}
+
+// ConvTranspose2d(C, N, 4, stride 2, padding 1) (the UNet up-sampling conv) in one launch: output
+// parity (py, px) is a 2x2 stride-1 conv over the input, tap (i, j) at input offset (py - i, px - j)
+// (engine._CT_TAPS), written to pixels (2y + py, 2x + px); the four parities of a tile are four
+// consecutive workgroups of the halo kernel reading one halo.
+extern "C" int wc_convtr4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64_t w3_bytes, const float* w_inv_scale,
+                                   const float* a_bound, void* stream) {
+    if (!a || !w3 || !a->out || !w_inv_scale || !a_bound) return WC_E_ARG;
+    if (a->nseg != 1 || a->act != WC_ACT_NONE) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src || s0.scale || s0.shift) return WC_E_ARG;
+    if (s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
+    const int BN = wc_conv3x3_x6_tile_n(a->N);
+    const int TH = BN == 64 ? 16 : 8;
+    if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
+    if (a->B <= 0 || a->N <= 0 || s0.H != a->Hm || s0.W != a->Wm || a->Hm % TH || a->Wm % 16) return WC_E_SHAPE;
+    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+    if (reinterpret_cast<uintptr_t>(w3) & 15) return WC_E_SHAPE;
+    if (a->out_nchw || a->Ho != 2 * a->Hm || a->Wo != 2 * a->Wm || a->osy != 2 || a->osx != 2 || a->ooy || a->oox ||
+        a->res || a->temb)
+        return WC_E_SHAPE;
+    if (4L * a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;
+    X6Dev d{};
+    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.nck0 = s0.C / 16;
+    d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
+    d.w6 = w3; d.bias = a->bias;
+    d.out = a->out; d.ldo = a->ldo; d.act = WC_ACT_NONE;
+    d.a_exp = 60; d.abound = a_bound; d.wsinv = w_inv_scale;
+    d.absmax = a->absmax_out;
+    d.gn_part = a->gn_part;
+    if (a->gn_part) {  // the parities' pixel blocks: parity p owns blocks p*HW/64 .. of the 4HW/64
+        const int sw = a->gn_sw;
+        if ((sw != 4 && sw != 8 && sw != 16 && sw != 32) || a->N % 32 || a->gn_c0 % 32 || a->gn_c0 < 0 ||
+            a->gn_c0 + a->N > a->gn_ncb * 32 || a->gn_p64 != 0 || a->gn_np64 * 64 != 4 * a->Hm * a->Wm)
+            return WC_E_SHAPE;
+        d.gn_ncb = a->gn_ncb; d.gn_sw = sw; d.gn_c0 = a->gn_c0; d.gn_np64 = a->gn_np64;
+    }
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w3_bytes != ntn * 4L * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return launch6<16, 64, 0, false, true, false, false, 2>(d, st);
+    return launch6<8, 128, 0, false, true, false, false, 2>(d, st);
 }

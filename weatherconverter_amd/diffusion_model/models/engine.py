@@ -146,7 +146,8 @@ class UnetEngine:
                     ci = blk.up_sample_conv.in_channels
                     parts = [pack_convT(blk.up_sample_conv.weight, py, px) for py in (0, 1) for px in (0, 1)]
                     parts = [(taps, w, self._x6(w, ci, len(taps)), self._f3n(w, ci, len(taps))) for taps, w in parts]
-                    self.up_convs.append((parts, blk.up_sample_conv.bias.detach().float()))
+                    self.up_convs.append((parts, blk.up_sample_conv.bias.detach().float(),
+                                          self._f3t(blk.up_sample_conv.weight, ci)))
                 else:
                     self.up_convs.append(None)
             self.conv_in_w = m.conv_in.weight.detach().float().contiguous()
@@ -214,6 +215,14 @@ class UnetEngine:
                 or os.environ.get('WC_DOWN_S2D', '1') == '0'):
             return None
         return K.pack_f16x3_s2d(w, c0)
+
+    def _f3t(self, wt: torch.Tensor, c0: int) -> Optional[K.X6Weight]:
+        """f16x3 pack of a 4x4 / stride-2 ConvTranspose for wc_convtr4x4s2_f16x3 (all four parities in
+        one launch of the halo kernel), or None (outside f16x3 mode or WC_UP_CT=0: the four
+        implicit-GEMM parities)."""
+        if self.precision != 'f16x3' or c0 % 16 or os.environ.get('WC_UP_CT', '1') == '0':
+            return None
+        return K.pack_f16x3_convT(wt.detach().float())
 
     def _pack_attn(self, blk, i: int) -> AttnPack:
         mha, gn = blk.attentions[i], blk.attention_norms[i]
@@ -469,15 +478,22 @@ class UnetEngine:
             i = L - 1 - k
             H, W = sizes[i]
             if self.up_convs[k] is not None:
-                parts, b = self.up_convs[k]
+                parts, b, w3t = self.up_convs[k]
                 dst = View(U[i], 0, dc[i])
-                np_in = cur.H * cur.W // 64 if (cur.H * cur.W) % 64 == 0 else 0
-                fused = []
-                for par, ((py, px), (taps, w, w6, w3)) in enumerate(zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts)):
-                    # each parity covers a quarter of the output pixels: its own range of pixel blocks
-                    fused.append(self.resample([Seg(cur, taps)], (w, w6, w3), b, dst, cur.H, cur.W, bnd,
-                                               gn_p64=par * np_in, gn_defer=True, out_map=(2, 2, py, px)))
-                self._gn_fill(dst, all(fused) and np_in > 0)
+                seg = Seg(cur, [(0, 0)])
+                if w3t is not None and bnd is not None and K.convT4x4s2_f16x3_ok(seg, w3t.N):
+                    gp = K.GnPart.of(dst)
+                    fused = K.gn_conv_ok(dst, gp, w3t.N, dst.H, dst.W)
+                    K.convT4x4s2_f16x3(seg, w3t, b, dst, a_bound=bnd, gn=gp if fused else None)
+                    self._gn_fill(dst, fused)
+                else:
+                    np_in = cur.H * cur.W // 64 if (cur.H * cur.W) % 64 == 0 else 0
+                    fused = []
+                    for par, ((py, px), (taps, w, w6, w3)) in enumerate(zip(((0, 0), (0, 1), (1, 0), (1, 1)), parts)):
+                        # each parity covers a quarter of the output pixels: its own range of pixel blocks
+                        fused.append(self.resample([Seg(cur, taps)], (w, w6, w3), b, dst, cur.H, cur.W, bnd,
+                                                   gn_p64=par * np_in, gn_defer=True, out_map=(2, 2, py, px)))
+                    self._gn_fill(dst, all(fused) and np_in > 0)
             else:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
             cur = View.full(U[i])

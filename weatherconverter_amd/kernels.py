@@ -336,7 +336,7 @@ def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str
 
 
 def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo',
-               res_f16: bool = False) -> X6Weight:
+               res_f16: bool = False, amax: Optional[torch.Tensor] = None) -> X6Weight:
     """Re-pack a [N][ntaps*C0 + C1] conv (+ 1x1 residual) weight for the f16x3 kernels: per output
     channel n a power-of-two scale 2^sW[n] with max_k |w[n, k]| * 2^sW[n] <= 2^14 over the fp16-packed
     columns (segment 0, and the residual with res_f16); segment 0
@@ -354,7 +354,10 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     wp[:N] = w.float()
     K0 = ntaps * C0
     # the scale must keep every fp16-packed column <= 2^14: segment 0, plus the residual with res_f16
-    amax = (wp if res_f16 else wp[:, :K0]).abs().amax(1).double()
+    if amax is None:  # (a caller packing several weights under one scale passes their common max)
+        amax = (wp if res_f16 else wp[:, :K0]).abs().amax(1).double()
+    else:
+        amax = torch.cat([amax.double().to(w.device), torch.zeros(Np - N, dtype=torch.float64, device=w.device)])
     sw = torch.where(amax > 0, torch.floor(torch.log2(2.0**14 / amax.clamp_min(1e-300))), torch.zeros_like(amax))
     sw = sw.clamp(-60, 60).to(torch.int32)
     ws = wp * torch.ldexp(torch.ones_like(wp[:, :1]), sw[:, None].float())  # exact power-of-two scaling
@@ -453,6 +456,43 @@ def pack_f16x3_s2d(w: torch.Tensor, C: int) -> X6Weight:
     _req(w.shape[1] == 16 * C and C % 16 == 0, '4x4 conv weight shape')
     w2 = w.reshape(N, 2, 2, 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, 16 * C)  # (a, py, b, px) -> (a, b, py, px)
     return pack_f16x3(w2, 4 * C, ntaps=4, order='halo')
+
+
+def pack_f16x3_convT(wt: torch.Tensor) -> X6Weight:
+    """f16x3 pack of a ConvTranspose2d(Ci, N, 4, 2, 1) weight [Ci][N][4][4] for wc_convtr4x4s2_f16x3:
+    per N tile the four parities (py, px) in order, each the 2x2-tap halo pack of
+    engine.pack_convT(wt, py, px), under one per-channel scale."""
+    from .diffusion_model.models.engine import pack_convT
+    Ci, N = wt.shape[0], wt.shape[1]
+    _req(Ci % 16 == 0, 'ConvT input channels % 16')
+    parts = [pack_convT(wt, py, px)[1].to(wt.device) for py in (0, 1) for px in (0, 1)]
+    amax = torch.stack([p.abs().amax(1) for p in parts]).amax(0)
+    packs = [pack_f16x3(p, Ci, ntaps=4, order='halo', amax=amax) for p in parts]
+    T = packs[0].data.shape[0]
+    data = torch.stack([pk.data for pk in packs], 1).reshape(T, -1).contiguous()
+    return X6Weight(data, N, packs[0].BN, Ci, 0, 'f16x3t', packs[0].wsinv)
+
+
+def convT4x4s2_f16x3_ok(seg: Seg, N: int) -> bool:
+    """Shapes wc_convtr4x4s2_f16x3 takes (else the four implicit-GEMM parities)."""
+    v = seg.view
+    TH = x6_tile(N)[0]
+    return v.H % TH == 0 and v.W % 16 == 0 and v.C % 16 == 0 and seg.scale is None and seg.stride == 1
+
+
+def convT4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, a_bound: torch.Tensor,
+                     gn: Optional[GnPart] = None):
+    """Up-sampling 4x4 / stride-2 / pad-1 transposed conv of a raw input on f16x3 in one launch
+    (wc_convtr4x4s2_f16x3); out is the 2H x 2W view; a_bound = per-image max |x|."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3t', 'f16x3 ConvT weight')
+    v = seg.view
+    _req(w3.C0 == v.C and out.H == 2 * v.H and out.W == 2 * v.W, 'ConvT shapes')
+    _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == v.B, 'A bound')
+    a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, None, (2, 2, 0, 0), None, 0, None, gn=gn)
+    TH, BN = x6_tile(w3.N)
+    _timed(f'conv3x3_x6_kernel<{TH}, {BN}, 0, false, true, false, false, 2> (ConvT 4x4/s2)', 'wc_convtr4x4s2_f16x3',
+           2.0 * v.B * v.H * v.W * w3.N * 16 * v.C if PROFILE is not None else 0.0, ctypes.byref(a),
+           w3.data.data_ptr(), w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
 
 
 def conv4x4s2_f16x3_ok(seg: Seg, N: int, Hm: int, Wm: int) -> bool:

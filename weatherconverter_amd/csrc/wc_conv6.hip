@@ -558,7 +558,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             }
         }
     }
-    if (p.absmax) wave_absmax_atomic(p.absmax, b, vmax);  // the whole tile is image b
+    if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);  // the whole tile is image b
     if (p.gn_part) {
         // this wave's 64 pixels (4 rows x 16 columns of the tile) are pixel block p64 of image b
         GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,

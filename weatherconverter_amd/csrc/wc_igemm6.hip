@@ -88,8 +88,9 @@ struct IgTile {
 // activation (template, see wc_conv.hip).  F3: segment 0 on f16x3 (caller bounds |a| 2^a_exp).
 // TR (the pre-split qkv epilogue only): accumulate the transposed block (lanes = pixels, rows =
 // channels; the same products, B and A fragments swapped in the MFMA).
+// The pre-split qkv form (TR, BN 128) is held to 3 waves per SIMD (174 -> 168 VGPRs, 5 spilled).
 template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false>
-__global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
+__global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_kernel(IgDev p) {
     using T = IgTile<BM, BN, F3, NPL>;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
 
@@ -438,6 +439,25 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
         const __amdgpu_buffer_rsrc_t srd_out =
             make_srd(p.out + (p.out_nchw ? (long)b_tile * p.N * HWo : (long)b_tile * HWo * p.ldo));
         const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + (long)b_tile * HWo * p.ldres : p.out);
+        // identity output map: every residual value of the tile is loaded before the first store
+        // (vmcnt counts stores too, so a load issued after a store waits for that store's ack --
+        // one residual load per element between the stores serialised the epilogue on them)
+        float rv[2][2][16];
+        const bool pre = p.res && p.ident;
+        if (pre) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const int rr0 = m0 - b_tile * HWm + wm * 64 + mb * 32;
+                    const int n = n0 + wn * 64 + nb * 32 + l32;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                        rv[mb][nb][r] = bload_f1(srd_res, n < p.N ? (unsigned)((rr0 + row) * p.ldres + n) * 4u : OOB);
+                    }
+                }
+        }
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
             const int rr0 = m0 - b_tile * HWm + wm * 64 + mb * 32;  // pixel of row 0 in the image
@@ -470,7 +490,8 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                         ox = mx * p.osx + p.oox;
                         opix = oy * p.Wo + ox;
                     }
-                    if (p.res) v += bload_f1(srd_res, (unsigned)(opix * p.ldres + n) * 4u);
+                    if (pre) v += rv[mb][nb][r];
+                    else if (p.res) v += bload_f1(srd_res, (unsigned)(opix * p.ldres + n) * 4u);
                     if (p.out_nchw) bstore_f1(srd_out, (unsigned)(n * HWo + opix) * 4u, v);
                     else bstore_f1(srd_out, (unsigned)(opix * p.ldo + n) * 4u, v);
                     vmax = fmaxf(vmax, fabsf(v));
@@ -478,7 +499,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_x6_kernel(IgDev p) {
                 }
             }
         }
-        if (p.absmax) wave_absmax_atomic(p.absmax, b_tile, vmax);
+        if (p.absmax) block_absmax_atomic(p.absmax, b_tile, vmax);  // the tile is image b_tile
         if (p.gn_part) {  // this wave's 64 GEMM rows are one pixel block of image b_tile
             GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
                      (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + wm,

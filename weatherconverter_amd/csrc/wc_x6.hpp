@@ -102,6 +102,22 @@ WC_DEVICE void wave_absmax_atomic(float* absmax, int b, float m) {
     if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(absmax) + b, __float_as_uint(m));
 }
 
+// The workgroup's max |value| in one atomic (the wave maxima meet in LDS): many same-address
+// device atomics serialise -- one per wave cost the attention out-projection up to 40 % of its
+// time (tools/probes/proj_epi_probe.py).  Every thread of the block must call it.
+WC_DEVICE void block_absmax_atomic(float* absmax, int b, float m) {
+    __shared__ float wmax[16];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = wmax[0];
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, wmax[i]);
+        atomicMax(reinterpret_cast<unsigned*>(absmax) + b, __float_as_uint(r));
+    }
+}
+
 // GroupNorm tile partials from a wave's 64 x 64 output block (2 x 2 MFMA 32x32 blocks whose
 // acc[mb][nb][r] already hold the FINAL stored values).  For each valid 32-channel column block nb
 // and each sub-slot of sw channels in it: (mean, M2) over the 64 pixels x sw channels, two passes

@@ -531,6 +531,17 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + img_px * p.ldo);
     const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + img_px * p.ldres : p.out);
     float vmax = 0.f;
+    // per-channel bias / temb / scale of both column blocks loaded before the first store (a load
+    // issued after stores waits for their acks: vmcnt counts both)
+    float eadd[2], emul[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        const int n = n0 + wn * 64 + nb * 32 + l32;
+        const bool ok = n < p.N;
+        eadd[nb] = (ok && p.bias) ? p.bias[n] : 0.f;
+        if (ok && p.temb) eadd[nb] += p.temb[b * p.temb_ld + n];
+        emul[nb] = (F3 && ok) ? p.wsinv[n] * ainv : 1.0f;
+    }
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
         // pixel (dy 0, dx 0) of this 32-row block; CT: output pixel (2y + py, 2x + px) of 2H x 2W
@@ -540,9 +551,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         for (int nb = 0; nb < 2; ++nb) {
             const int n = n0 + wn * 64 + nb * 32 + l32;
             if (n >= p.N) continue;
-            float add = p.bias ? p.bias[n] : 0.f;
-            if (p.temb) add += p.temb[b * p.temb_ld + n];
-            const float mul = F3 ? p.wsinv[n] * ainv : 1.0f;
+            const float add = eadd[nb], mul = emul[nb];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * half;

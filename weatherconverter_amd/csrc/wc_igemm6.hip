@@ -444,6 +444,15 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
         // one residual load per element between the stores serialised the epilogue on them)
         float rv[2][2][16];
         const bool pre = p.res && p.ident;
+        float ebn[2], emul[2];  // per-channel terms of both column blocks, also before any store
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int n = n0 + wn * 64 + nb * 32 + l32;
+            const bool ok = n < p.N;
+            ebn[nb] = (ok && p.bias) ? p.bias[n] : 0.f;
+            if (ok && p.temb) ebn[nb] += p.temb[b_tile * p.temb_ld + n];
+            emul[nb] = (F3 && ok) ? p.wsinv[n] * ainv : 1.0f;
+        }
         if (pre) {
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb)
@@ -467,9 +476,7 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
             for (int nb = 0; nb < 2; ++nb) {
                 const int n = n0 + wn * 64 + nb * 32 + l32;
                 if (n >= p.N) continue;
-                float bn = p.bias ? p.bias[n] : 0.f;
-                if (p.temb) bn += p.temb[b_tile * p.temb_ld + n];
-                const float mul = F3 ? p.wsinv[n] * ainv : 1.0f;
+                const float bn = ebn[nb], mul = emul[nb];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = (r & 3) + 8 * (r >> 2) + 4 * half;

@@ -379,6 +379,16 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
     // v: 2-byte stores at the pixel's key-order position, 64 contiguous bytes per half-wave.
     if constexpr (TR) {
         if (UNIB && p.qkv3) {
+            // the tile's bias and 2^-(sA + sW[n]) through LDS: global loads between the stores
+            // would wait for the stores' acks (vmcnt counts both), LDS reads do not
+            __syncthreads();  // the last K-step's fragment reads are done
+            float* sbias = reinterpret_cast<float*>(smem);
+            if (tid < BN) {
+                const int n = n0 + tid;
+                sbias[tid] = (n < p.N && p.bias) ? p.bias[n] : 0.f;
+                sbias[BN + tid] = n < p.N ? (F3 ? p.wsinv[n] * ainv : 1.0f) : 0.f;
+            }
+            __syncthreads();
             const long img = (long)b_tile * 6 * p.qC * HWm;
             const long plane = (long)p.qD * HWm;  // one piece of one head
 #pragma unroll
@@ -401,8 +411,7 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
                                 const int n = nblk + 8 * j + 4 * half + e;
-                                v[e] = ((F3 ? acc[mb][nb][4 * j + e] * p.wsinv[n] * ainv : acc[mb][nb][4 * j + e]) +
-                                        (p.bias ? p.bias[n] : 0.f)) * sc;
+                                v[e] = (acc[mb][nb][4 * j + e] * sbias[BN + n - n0] + sbias[n - n0]) * sc;
                             }
                             u32x2 ph, pl;
                             split2_f16(v, ph, pl);
@@ -416,8 +425,7 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
                         for (int r = 0; r < 16; ++r) {
                             const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
                             const int n = nblk + row;
-                            const float v = ((F3 ? acc[mb][nb][r] * p.wsinv[n] * ainv : acc[mb][nb][r]) +
-                                             (p.bias ? p.bias[n] : 0.f)) * sc;
+                            const float v = (acc[mb][nb][r] * sbias[BN + n - n0] + sbias[n - n0]) * sc;
                             const _Float16 h = (_Float16)v;
                             const _Float16 l = (_Float16)(v - (float)h);
                             dst[(long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, h);

@@ -171,37 +171,66 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const float* __restrict__ 
 // --------------------------------------------------------------------------------------------
 constexpr int HD_T = 16;
 
+// The next chunk's halo (raw values and their GN affine) is loaded into registers while the
+// current chunk computes, so the loads' latency is hidden; NOC = 3 skips the padded 4th output.
+constexpr int HD_ITEMS = (HD_T + 2) * (HD_T + 2) * 4;
+constexpr int HD_PER_T = (HD_ITEMS + 255) / 256;
+
+template <int NOC>
 __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict__ x, int ldx,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int B, int H, int W,
                                                         int C, const float* __restrict__ w,
                                                         const float* __restrict__ bias, int NO,
                                                         float* __restrict__ out, int tiles_x, int tiles_y) {
-    __shared__ f32x4 halo[(HD_T + 2) * (HD_T + 2) * 4];
+    __shared__ f32x4 halo[HD_ITEMS];
     const int tile = blockIdx.x;
     const int tx = tile % tiles_x, ty = (tile / tiles_x) % tiles_y, b = tile / (tiles_x * tiles_y);
     const int x0 = tx * HD_T, y0 = ty * HD_T;
     const int px = threadIdx.x % HD_T, py = threadIdx.x / HD_T;
     float acc0 = bias[0], acc1 = NO > 1 ? bias[1] : 0.f, acc2 = NO > 2 ? bias[2] : 0.f,
-          acc3 = NO > 3 ? bias[3] : 0.f;
+          acc3 = (NOC > 3 && NO > 3) ? bias[3] : 0.f;
+    // halo item i = threadIdx.x + 256 k: pixel i >> 2, channels 4 (i & 3) ..
+    long goff[HD_PER_T];
+    unsigned inb = 0, val = 0;
+#pragma unroll
+    for (int k = 0; k < HD_PER_T; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        const int hp = i >> 2;
+        const int hx = hp % (HD_T + 2), hy = hp / (HD_T + 2);
+        const int gy = y0 + hy - 1, gx = x0 + hx - 1;
+        const bool ok = i < HD_ITEMS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        val |= (i < HD_ITEMS ? 1u : 0u) << k;
+        inb |= (ok ? 1u : 0u) << k;
+        goff[k] = ok ? ((long)(b * H + gy) * W + gx) * ldx + 4 * (i & 3) : 0;
+    }
+    f32x4 ra[HD_PER_T], rs[HD_PER_T], rh[HD_PER_T];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int k = 0; k < HD_PER_T; ++k) {
+            const int c = c0 + 4 * ((threadIdx.x + 256 * k) & 3);
+            if ((inb >> k) & 1u) {
+                ra[k] = *reinterpret_cast<const f32x4*>(x + goff[k] + c0);
+                rs[k] = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
+                rh[k] = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
+            }
+        }
+    };
+    load(0);
     for (int c0 = 0; c0 < C; c0 += 16) {
         __syncthreads();  // previous chunk's reads done
-        for (int i = threadIdx.x; i < (HD_T + 2) * (HD_T + 2) * 4; i += 256) {
-            const int q = i & 3, hp = i >> 2;
-            const int hx = hp % (HD_T + 2), hy = hp / (HD_T + 2);
-            const int gy = y0 + hy - 1, gx = x0 + hx - 1;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-                const int c = c0 + 4 * q;
-                const f32x4 a = *reinterpret_cast<const f32x4*>(x + ((long)(b * H + gy) * W + gx) * ldx + c);
-                const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
-                const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(a[e], sc[e], sh[e]));
+        for (int k = 0; k < HD_PER_T; ++k) {
+            if (!((val >> k) & 1u)) continue;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((inb >> k) & 1u) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(ra[k][e], rs[k][e], rh[k][e]));
             }
-            halo[i] = v;  // zero padding is applied after the prologue, as the reference's conv pads
+            halo[threadIdx.x + 256 * k] = v;  // zero padding after the prologue, as the reference pads
         }
         __syncthreads();
+        if (c0 + 16 < C) load(c0 + 16);
         const float* wc = w + (long)(c0 / 16) * 9 * 16 * 4;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
@@ -215,7 +244,7 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
                     acc0 = fmaf(a[e], wv.x, acc0);
                     acc1 = fmaf(a[e], wv.y, acc1);
                     acc2 = fmaf(a[e], wv.z, acc2);
-                    acc3 = fmaf(a[e], wv.w, acc3);
+                    if constexpr (NOC > 3) acc3 = fmaf(a[e], wv.w, acc3);
                 }
             }
         }
@@ -227,7 +256,7 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
         out[o] = acc0;
         if (NO > 1) out[o + ps] = acc1;
         if (NO > 2) out[o + 2 * ps] = acc2;
-        if (NO > 3) out[o + 3 * ps] = acc3;
+        if (NOC > 3 && NO > 3) out[o + 3 * ps] = acc3;
     }
 }
 
@@ -454,8 +483,12 @@ extern "C" int wc_head_conv(const float* x, int ldx, const float* scale, const f
     const int tiles_x = (W + HD_T - 1) / HD_T, tiles_y = (H + HD_T - 1) / HD_T;
     const long n = (long)B * tiles_x * tiles_y;
     if (n >= (1L << 31)) return WC_E_SHAPE;
-    hipLaunchKernelGGL(head_conv_kernel, dim3((unsigned)n), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x,
-                       ldx, scale, shift, B, H, W, C, w, bias, NO, out, tiles_x, tiles_y);
+    if (NO == 3)
+        hipLaunchKernelGGL(head_conv_kernel<3>, dim3((unsigned)n), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                           x, ldx, scale, shift, B, H, W, C, w, bias, NO, out, tiles_x, tiles_y);
+    else
+        hipLaunchKernelGGL(head_conv_kernel<4>, dim3((unsigned)n), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                           x, ldx, scale, shift, B, H, W, C, w, bias, NO, out, tiles_x, tiles_y);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -11,21 +11,30 @@ Workload (BASELINE config 2 at N=1, config 5 at N=8): S=256, 16 images per GPU (
 fp32, the default config.yaml UNet (110.08 M params) with keyed synthetic weights, Philox device
 noise keyed by (seed, global sample, step).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run (RCCL).
-Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
+Launch: python bench.py [--gpus N --steps K --warmup W].  N>1: under torch.distributed.run (RCCL,
+WORLD_SIZE must equal --gpus); without WORLD_SIZE in the environment bench.py starts
+``torch.distributed.run --nproc-per-node N`` itself as a child process (before any GPU call) and exits
+with its code.  Rank 0 prints ONE JSON line.  Extra legs (rank 0, after the timed region):
   roofline      per-launch HIP events around every conv of one UNet forward; the dominant kernel
                 is the conv instantiation with the most time (the GN+SiLU-prologue 3x3 convs) —
                 achieved = its algorithmic (fp32-equivalent) FLOPs per launch / its mean launch
                 duration, against its own ceiling: 157.3 TF for the fp32-MFMA conv, 2516.6/6 =
                 419.4 TF for bf16x6 kernels (6 bf16 MFMAs per fp32 product), 2516.6/3 = 838.9 TF
                 for the f16x3 conv (3 f16 MFMAs per product; MI355X_MICROARCH.md).
-  cpu_baseline  the oracle's PyTorch-CPU restatement of the reference UNet step (N=1 only), on a
-                bounded sample (a few 256-px UNet steps), extrapolated x T.
+  parity        the committed 256-px golden input (reference unet_base.Unet output, tests/golden/
+                unet_256.npz) through the same engine / arithmetic that was timed: rel-L2 vs the golden.
+  cpu_baseline  the oracle's PyTorch-CPU restatement of the reference UNet step (N=1 only), at the
+                timed batch (B=16) on every CPU this process may use, a bounded sample (1-3 steps
+                after one warmup, ~10-30 s), extrapolated x T.
 """
 import argparse
 import glob
 import json
+import math
 import os
+import socket
+import subprocess
+import sys
 import time
 
 import torch
@@ -43,7 +52,8 @@ GFLOP_PER_IMAGE_STEP_256 = 590.61  # SURVEY.md §8(d) algorithmic FLOPs (probe h
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='GPUs of this node (default: WORLD_SIZE, else 1); N>1 without WORLD_SIZE self-launches')
     ap.add_argument('--steps', type=int, default=1000)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=16, help='images per GPU')
@@ -55,8 +65,10 @@ def parse():
                     help='image groups per GPU run concurrently on their own streams inside the graph')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-batch', type=int, default=2)
-    ap.add_argument('--cpu-steps', type=int, default=2)
+    ap.add_argument('--cpu-batch', type=int, default=None, help='CPU baseline batch (default: --batch)')
+    ap.add_argument('--cpu-steps', type=int, default=3, help='at most this many timed CPU steps')
+    ap.add_argument('--cpu-budget', type=float, default=20.0, help='stop timing CPU steps after ~this many s')
+    ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--precision', default=None, choices=['f16x3', 'bf16x6', 'fp32'],
                     help='conv/attention arithmetic (default: kernels.default_conv_precision(), i.e. f16x3)')
     return ap.parse_args()
@@ -182,38 +194,115 @@ def hbm_leg(hbm):
     return out
 
 
+def _cpu_share() -> dict:
+    """CPUs this process may actually use: its affinity mask, capped by the cgroup CPU quota (a GPU box
+    shows the whole machine in nproc / os.cpu_count() but grants each GPU a share of it)."""
+    host = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = host
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(math.floor(quota))))
+    model = None
+    try:
+        for line in subprocess.run(['lscpu'], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith('Model name:'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    nproc = None
+    try:
+        nproc = int(subprocess.run(['nproc'], capture_output=True, text=True, timeout=10).stdout.strip())
+    except (OSError, subprocess.SubprocessError, ValueError):
+        pass
+    return {'host_cpus': host, 'nproc': nproc, 'affinity_cpus': affinity, 'cgroup_cpu_quota': quota,
+            'usable_cpus': usable, 'cpu_model': model}
+
+
 def cpu_baseline_leg(args):
-    import sys
+    """The reference UNet step restated op for op in PyTorch-CPU (oracle/, bitwise-equal to the reference
+    import, tests/test_oracle_golden.py), at the timed batch, on every CPU this process may use."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle.unet_oracle import unet_forward, unet_state_dict_keys
     from weatherconverter_amd.diffusion_model.config import model_config
     from weatherconverter_amd.synthetic import synth_tensor
-    threads = min(16, os.cpu_count() or 1)
+    share = _cpu_share()
+    threads = share['usable_cpus']
     torch.set_num_threads(threads)
+    B = args.cpu_batch or args.batch
     mc = model_config(args.size)
     sd = {k: synth_tensor(k, s) for k, s in unet_state_dict_keys(mc).items()}
-    x = torch.randn((args.cpu_batch, 3, args.size, args.size), generator=torch.Generator().manual_seed(1))
+    x = torch.randn((B, 3, args.size, args.size), generator=torch.Generator().manual_seed(1))
     t = torch.tensor([500])
+    times = []
     with torch.no_grad():
         unet_forward(sd, mc, x, t)  # warm
-        t0 = time.perf_counter()
-        for _ in range(args.cpu_steps):
+        t_start = time.perf_counter()
+        while len(times) < max(1, args.cpu_steps):
+            t0 = time.perf_counter()
             unet_forward(sd, mc, x, t)
-        dt = (time.perf_counter() - t0) / args.cpu_steps
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_start > args.cpu_budget:
+                break
+    dt = sum(times) / len(times)
     return {
-        'value': round(args.cpu_batch / (dt * args.timesteps), 7),
+        'value': round(B / (dt * args.timesteps), 7),
         'unit': 'images/s',
         'cores': threads,
         'kind': 'port',
         'ms_per_step': round(dt * 1e3, 1),
-        'sample': f'oracle PyTorch-CPU UNet step (reference unet_base.Unet restated), {args.size}px, '
-                  f'B={args.cpu_batch}, {args.cpu_steps} timed steps after 1 warmup, extrapolated x{args.timesteps}'
+        'host': share,
+        'sample': f'oracle PyTorch-CPU UNet step (reference unet_base.Unet restated op for op), {args.size}px, '
+                  f'B={B}, {len(times)} timed step(s) after 1 warmup on {threads} threads (the CPUs this process '
+                  f'may use: affinity capped by the cgroup quota), extrapolated x{args.timesteps} (T) -- '
+                  f'extrapolated, not a full sample'
     }
+
+
+def parity_leg(model, dev):
+    """The committed 256-px golden (reference unet_base.Unet on the keyed synthetic weights,
+    tests/golden/make_golden.py) through the engine and arithmetic that was just timed."""
+    import numpy as np
+    from weatherconverter_amd.synthetic import state_dict_digest, synthetic_images
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'tests', 'golden', 'unet_256.npz')
+    g = np.load(path)
+    digest_ok = state_dict_digest({k: v.detach().cpu() for k, v in model.state_dict().items()}) == str(g['digest'])
+    x = synthetic_images((1, 3, 256, 256), seed=301).to(dev)
+    with torch.no_grad():
+        y = model(x, torch.tensor([611], device=dev)).double().cpu()
+    ref = torch.from_numpy(g['y']).double()
+    rel = float((y - ref).norm() / ref.norm())
+    return {'rel_l2': float(f'{rel:.3e}'), 'tolerance': 1e-5, 'pass': bool(digest_ok and rel <= 1e-5),
+            'weights_digest_match': digest_ok,
+            'case': 'tests/golden/unet_256.npz: reference Unet (config.yaml @256px) forward, x seed 301, t=611, B=1'}
+
+
+def _self_launch(args) -> int:
+    """--gpus N>1 outside torch.distributed.run: start it as a child (nothing here has touched the GPU;
+    the parent only waits and passes the exit code on)."""
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
     args = parse()
+    if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(_self_launch(args))
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
@@ -261,6 +350,11 @@ def main():
             xw, nxt = nxt, xw
         del xw
         gathered = None
+        gather_sec = 0.0
+        if world > 1:  # RCCL communicator set up outside the timed region
+            warm = torch.empty((B * world, ) + shape[1:], device=dev)
+            dist.all_gather_into_tensor(warm, x)
+            del warm
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -272,16 +366,27 @@ def main():
                 sched.step(x, eps, i, out=nxt, noise='philox', seed=args.seed, sample0=sample0)
             x, nxt = nxt, x
         if world > 1:
+            torch.cuda.synchronize()
+            g0 = time.perf_counter()
             gathered = torch.empty((B * world, ) + shape[1:], device=dev)
             dist.all_gather_into_tensor(gathered, x)
+            torch.cuda.synchronize()
+            gather_sec = time.perf_counter() - g0
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
+        per_rank = [elapsed]
+        per_rank_gather = [gather_sec]
         if world > 1:
-            tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
+            tt = torch.tensor([elapsed, gather_sec], device=dev, dtype=torch.float64)
+            allt = torch.empty((world, 2), device=dev, dtype=torch.float64)
+            dist.all_gather_into_tensor(allt, tt)
+            per_rank = [float(v) for v in allt[:, 0].tolist()]
+            per_rank_gather = [float(v) for v in allt[:, 1].tolist()]
+            elapsed = max(per_rank)
         finite = bool(torch.isfinite(x).all())
+        if gathered is not None:
+            finite = finite and bool(torch.isfinite(gathered).all())
 
         result = None
         if rank == 0:
@@ -301,6 +406,8 @@ def main():
                 'vs_baseline': None,
                 'dtype': 'f32',
                 'data': 'synthetic (keyed random-init weights, Philox N(0,1) x_T and per-step noise)',
+                'extrapolated_from_steps': None if K == T else
+                f'{K} of T={T} steps timed; images/s = images x {K}/{T} / elapsed (UNet cost does not depend on t)',
                 'config': {
                     'workload': f'DDPM reverse sampling, UNet config.yaml @ {args.size}px, {B} images/GPU, '
                                 f'T={T}, {K} timed steps from t={T - 1}' + (' (complete sample)' if K == T else ''),
@@ -311,23 +418,27 @@ def main():
                     'hip_graph': bool(args.graph),
                     'stream_groups': runner.split if runner is not None else 1,
                     'arithmetic': {
-                        'f16x3': 'fp32-class: 3x3 convs, attention projections and attention on f16x3 (2-piece fp16 '
-                                 'split under static power-of-two range bounds: Samuelson GN bound, in-projection row '
-                                 'norms); down convs / ConvT on f16x3 under the producer\'s per-image absmax; '
-                                 'unbounded operands on bf16x6 (exact 3-piece bf16 split); fp32 accumulation; fp32 '
-                                 'activations in HBM',
+                        'f16x3': 'fp32-class: 3x3 convs (with the fused 1x1 residual), attention projections and '
+                                 'attention on f16x3 (2-piece fp16 split under power-of-two range bounds: Samuelson '
+                                 'GN bound, in-projection row norms, per-image GN/absmax bounds measured by the '
+                                 'producer for the residual, down convs and ConvT); operands without a bound on '
+                                 'bf16x6 (exact 3-piece bf16 split); fp32 accumulation; fp32 activations in HBM',
                         'bf16x6': 'fp32-class: every conv and attention on bf16x6 (exact 3-piece bf16 split), fp32 '
                                   'accumulation; fp32 activations in HBM',
                         'fp32': 'fp32 MFMA (v_mfma_f32_32x32x2_f32) everywhere'}[precision],
                     'x_finite': finite,
                 },
                 'ms_per_unet_step': round(ms_step, 3),
+                'per_rank_ms_per_step': [round(v / K * 1e3, 3) for v in per_rank],
+                'all_gather_ms': [round(v * 1e3, 3) for v in per_rank_gather] if world > 1 else None,
                 'unet_step_tflops_algorithmic': round(unet_tflops, 2) if unet_tflops else None,
             }
             if not args.no_roofline:
                 # the dominant kernel as the timed graph launches it: one image group
                 g = runner.split if runner is not None else 1
                 result['roofline'] = roofline_leg(model, x[:B // g], ts[500:501], groups=g)
+            if not args.no_parity and args.size == 256:
+                result['parity'] = parity_leg(model, dev)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             result['cpu_baseline'] = cpu_baseline_leg(args)

@@ -12,6 +12,8 @@ weatherconverter_amd/synthetic.py, so only outputs + digests are stored):
   unet_64.npz           64-px default-config Unet forward, B=2 (config 1 model)
   unet_256.npz          256-px default-config Unet forward, B=1 (BASELINE architecture)
   traj_64_T50.npz       config 1: 64 px, B=2, T=50 reverse trajectory (sample_ddpm.py:35-44 loop)
+  traj_64_T1000.npz     64 px default config, B=1, the full T=1000 schedule, same loop and RNG stream
+                        (--only-traj1000; ~5 min on 8 CPU threads)
 The reference modules imported: diffusion_model.models.unet_base, diffusion_model.scheduler.
 linear_noise_scheduler, diffusion_model.config.models.  ``Tensor.cuda`` is shimmed to a no-op
 (unet_base.py:461 hard-codes .cuda()); nothing in the reference is modified.
@@ -49,6 +51,7 @@ def main():
     ap.add_argument('--skip-traj', action='store_true')
     ap.add_argument('--only-guided', action='store_true')
     ap.add_argument('--only-old', action='store_true')
+    ap.add_argument('--only-traj1000', action='store_true')
     args = ap.parse_args()
     sys.path.insert(0, args.reference)
     torch.Tensor.cuda = lambda self, *a, **k: self  # harness shim for unet_base.py:461
@@ -57,6 +60,8 @@ def main():
         return guided(args)
     if args.only_old:
         return old_unet(args)
+    if args.only_traj1000:
+        return traj1000(args)
     from diffusion_model.config import models as ref_models
     from diffusion_model.models.unet_base import Unet, get_time_embedding
     from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
@@ -154,6 +159,34 @@ def main():
                 xt = mean + sigma if i != 0 else mean
         np.savez(os.path.join(HERE, 'traj_64_T50.npz'), x0=xt.numpy(), eps_first=eps_first.numpy(), seed=3455)
         print('traj done', float(xt.abs().max()))
+
+
+def traj1000(args):
+    """traj_64_T1000.npz: the sample_ddpm.py:35-44 loop over the full T=1000 schedule (64-px default
+    config, B=1, torch.manual_seed(3455) CPU stream), x at a few checkpoints and the final x0."""
+    from diffusion_model.config import models as ref_models
+    from diffusion_model.models.unet_base import Unet
+    from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    mc = default_model(ref_models, 64)
+    net = Unet(mc)
+    sd = synthetic_state_dict(net.state_dict(), seed=0)
+    net.load_state_dict(sd)
+    net.eval()
+    s = LinearNoiseScheduler(1000, 0.0001, 0.02)
+    torch.manual_seed(3455)
+    xt = torch.randn((1, 3, 64, 64))  # sample_ddpm.py:35-36
+    out = {'seed': 3455, 'digest': state_dict_digest(sd)}
+    marks = {999, 900, 500, 100}
+    with torch.no_grad():
+        for i in reversed(range(1000)):  # sample_ddpm.py:37-44
+            noise_pred = net(xt, torch.as_tensor(i).unsqueeze(0))
+            mean, sigma, _ = s.sample_prev_timestep(xt, noise_pred, torch.as_tensor(i))
+            xt = mean + sigma if i != 0 else mean
+            if i in marks:
+                out[f'x_after_t{i}'] = xt.numpy().copy()
+    out['x0'] = xt.numpy()
+    np.savez(os.path.join(HERE, 'traj_64_T1000.npz'), **out)
+    print('traj1000 done', float(xt.abs().max()))
 
 
 def old_unet(args):

@@ -125,3 +125,46 @@ def test_sharded_sampling_equals_single_rank():
     fc = sample_tensor(net, s, 4, 3, 32, noise='torch_cpu', seed=22)
     pc = sample_tensor(net, s, 2, 3, 32, noise='torch_cpu', seed=22, sample0=2, total_batch=4)
     assert rel_l2(fc[2:], pc) < 1e-6
+
+
+def test_unet_256_batch_above_descriptor_limit_chunks():
+    """B=64 at 256 px puts the level-0 skip buffer at 2 GiB (past one buffer descriptor's 32-bit range):
+    the engine runs it as chunks of max_batch (63) images; rows equal singleton runs bit for bit."""
+    mc, net = _model('default_256')
+    eng_cap = net.engine().max_batch(256, 256)
+    x = _x(mc, 64, 303).cuda()
+    t = torch.tensor([250]).cuda()
+    with torch.no_grad():
+        y = net(x, t)
+        y0 = net(x[:1].contiguous(), t)
+        y63 = net(x[63:].contiguous(), t)
+    assert eng_cap == 63
+    assert torch.isfinite(y).all()
+    assert torch.equal(y[:1], y0) and torch.equal(y[63:], y63)
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'bf16x6'])
+def test_trajectory_T1000_reference_rng(precision):
+    """The full T=1000 schedule (64-px default config, B=1, reference RNG stream seed 3455) in the benched
+    split-precision arithmetic: x0 (and x at intermediate checkpoints) within SURVEY §8(c)'s trajectory
+    tolerance rel-L2 <= 1e-4 of the reference's fp32 CPU trajectory (tests/golden/traj_64_T1000.npz)."""
+    from weatherconverter_amd.diffusion_model.sample_ddpm import sample_tensor
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    from weatherconverter_amd.synthetic import state_dict_digest
+    path = os.path.join(GOLDEN, 'traj_64_T1000.npz')
+    g = np.load(path)
+    mc, net = _model('default_64', precision=precision)
+    assert state_dict_digest(net.state_dict()) == str(g['digest'])
+    s = LinearNoiseScheduler(1000, 0.0001, 0.02)
+    seen = {}
+
+    def grab(i, x):
+        if f'x_after_t{i}' in g.files:
+            seen[i] = x.cpu().clone()
+
+    x0 = sample_tensor(net, s, 1, 3, 64, noise='torch_cpu', seed=int(g['seed']), graph=True, progress_x=grab)
+    errs = {i: rel_l2(v, g[f'x_after_t{i}']) for i, v in sorted(seen.items(), reverse=True)}
+    err = rel_l2(x0.cpu(), g['x0'])
+    print(f'{precision}: T=1000 trajectory rel-L2 checkpoints {errs}, x0 {err:.3e}')
+    assert len(errs) == 4 and all(e < 1e-4 for e in errs.values()), errs
+    assert err < 1e-4

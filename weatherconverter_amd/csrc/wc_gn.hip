@@ -16,19 +16,16 @@ namespace {
 
 constexpr int GN_THREADS = 256;
 
-int splits_for(int B, int HW, int C) {
+// Splits per image depend on the image only (not on B), so the partials of one image merge in the
+// same order whatever batch it runs in: a batch-sharded run is bit-identical to a single-rank run.
+// The counts are what the former "~2048 workgroups" rule gave at the benched B=16.
+int splits_for(int /*B*/, int HW, int C) {
     if (C / 4 > GN_THREADS) {  // fallback kernel: B * splits * G workgroups
-        int target = 2048 / (B * 8);
-        target = target < 1 ? 1 : target;
         const int max_by_hw = HW / 64 < 1 ? 1 : HW / 64;
-        target = target > max_by_hw ? max_by_hw : target;
-        return target > 256 ? 256 : target;
+        return max_by_hw > 16 ? 16 : max_by_hw;
     }
-    int target = 2048 / B;  // ~2048 workgroups of whole pixel rows
-    target = target < 1 ? 1 : target;
-    const int max_by_hw = HW / 16 < 1 ? 1 : HW / 16;
-    target = target > max_by_hw ? max_by_hw : target;
-    return target > 256 ? 256 : target;
+    const int max_by_hw = HW / 16 < 1 ? 1 : HW / 16;  // whole pixel rows per workgroup
+    return max_by_hw > 128 ? 128 : max_by_hw;
 }
 
 // Whole-row kernel: thread t handles channel quad q = t % Q of pixels p_begin + t / Q + k * R.

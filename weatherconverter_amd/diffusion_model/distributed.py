@@ -26,19 +26,35 @@ def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def gather_samples(x_local: torch.Tensor, total: int, group=None) -> torch.Tensor:
-    """All-gather the per-rank sample blocks into the full (total, ...) batch on every rank."""
+    """All-gather the per-rank sample blocks into the full (total, ...) batch on every rank.
+
+    RCCL (backend ``nccl``) gathers device tensors in place over xGMI.  gloo cannot gather device
+    tensors, so under gloo (CPU tests, or several ranks sharing one GPU) the blocks are staged through
+    host memory and the result is copied back to ``x_local``'s device.
+    """
     world = dist.get_world_size(group)
     counts = [shard_range(total, world, r)[1] for r in range(world)]
+    if x_local.shape[0] != counts[dist.get_rank(group)]:
+        raise ValueError(f'gather_samples: rank holds {x_local.shape[0]} samples, shard_range says '
+                         f'{counts[dist.get_rank(group)]}')
+    dev = x_local.device
+    staged = dist.get_backend(group) == 'gloo' and dev.type != 'cpu'
+    xs = x_local.detach().to('cpu') if staged else x_local
     if all(c == counts[0] for c in counts):
-        out = torch.empty((total, ) + tuple(x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
-        dist.all_gather_into_tensor(out, x_local.contiguous(), group=group)
-        return out
-    cmax = max(counts)
-    pad = torch.zeros((cmax, ) + tuple(x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
-    pad[:x_local.shape[0]] = x_local
-    parts: List[torch.Tensor] = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+        out = torch.empty((total, ) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
+        if dist.get_backend(group) == 'gloo':
+            parts = list(out.split(counts[0]))
+            dist.all_gather(parts, xs.contiguous(), group=group)
+        else:
+            dist.all_gather_into_tensor(out, xs.contiguous(), group=group)
+    else:
+        cmax = max(counts)
+        pad = torch.zeros((cmax, ) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
+        pad[:xs.shape[0]] = xs
+        parts: List[torch.Tensor] = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        out = torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+    return out.to(dev) if staged else out
 
 
 @torch.no_grad()

@@ -386,19 +386,52 @@ class UnetEngine:
         return self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y, absmax=absmax)[0]
 
     # ------------------------------------------------------------------ forward
+    def max_batch(self, S: int, S2: int) -> int:
+        """Largest batch one pass can take: the kernels address each source tensor of the whole batch
+        through one buffer descriptor (32-bit byte offsets, < 2 GiB).  Per image, the widest tensor at
+        level i is the skip buffer (2*dc[i] channels), a ResBlock output (dc[i+1]) or an attention
+        in-projection (3*C; 6*C fp16 pieces pre-split, the same bytes)."""
+        m = self.model
+        dc, mids = m.down_channels, m.mid_channels
+        h, w = S, S2
+        per_image = 0
+        L = len(dc) - 1
+        for i in range(L):
+            att = m.downs[i].use_attn or m.ups[L - 1 - i].use_attn
+            wide = max(2 * dc[i], dc[i + 1], 3 * max(dc[i], dc[i + 1]) if att else 0)
+            per_image = max(per_image, h * w * 4 * wide)
+            if m.down_sample[i]:
+                h, w = h // 2, w // 2
+        per_image = max(per_image, h * w * 4 * 3 * max(mids + [dc[-1]]))
+        return max(1, ((1 << 31) - 1) // per_image)
+
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
+        """Batches above max_batch run as consecutive chunks: every op is per image, and every kernel's
+        reduction order is independent of the batch, so the result equals one pass bit for bit."""
+        m = self.model
+        if x.dim() != 4 or x.shape[1] != m.model_config.im_channels:
+            raise RuntimeError(f'Unet expects (B, {m.model_config.im_channels}, H, W), got {tuple(x.shape)}')
+        B = x.shape[0]
+        tt = torch.as_tensor(t).long().reshape(-1).to(self.device)
+        if tt.shape[0] not in (1, B):
+            raise RuntimeError(f'timestep tensor has {tt.shape[0]} entries for a batch of {B}')
+        cap = self.max_batch(x.shape[2], x.shape[3])
+        if B <= cap:
+            return self._forward(x, tt)
+        outs = []
+        for b0 in range(0, B, cap):
+            tc = tt if tt.shape[0] == 1 else tt[b0:b0 + cap]
+            outs.append(self._forward(x[b0:b0 + cap], tc))
+        return torch.cat(outs)
+
+    def _forward(self, x: torch.Tensor, tt: torch.Tensor) -> torch.Tensor:
         if self._signature() != self._sig:  # parameters changed in place: repack
             self._sig = self._signature()
             self._pack()
         m = self.model
-        if x.dim() != 4 or x.shape[1] != m.model_config.im_channels:
-            raise RuntimeError(f'Unet expects (B, {m.model_config.im_channels}, H, W), got {tuple(x.shape)}')
         x = x.to(device=self.device, dtype=torch.float32).contiguous()
         B, _, S, S2 = x.shape
-        tt = torch.as_tensor(t).long().reshape(-1).to(self.device)
         nt = tt.shape[0]
-        if nt not in (1, B):
-            raise RuntimeError(f'timestep tensor has {nt} entries for a batch of {B}')
         temb = K.temb(tt, *self.tproj, self.temb_w, self.temb_b)
         temb_ld = temb.shape[1] if nt > 1 else 0
 

@@ -162,7 +162,10 @@ class Unet(nn.Module):
         return self._engine
 
     def set_conv_precision(self, precision: str) -> 'Unet':
-        """'bf16x6' (default) or 'fp32' arithmetic for the 3x3 convs (see kernels.conv3x3_x6)."""
+        """Conv / attention arithmetic: 'f16x3' (the default: 2-piece fp16 split under power-of-two
+        range bounds, bf16x6 where no bound exists), 'bf16x6' (exact 3-piece bf16 split everywhere) or
+        'fp32' (fp32 MFMA).  The default comes from kernels.default_conv_precision(), which the
+        WC_CONV_PRECISION environment variable overrides; see DESIGN.md §3.1."""
         from ... import kernels
         if precision not in kernels.CONV_PRECISIONS:
             raise ValueError(f'conv precision must be one of {kernels.CONV_PRECISIONS}')

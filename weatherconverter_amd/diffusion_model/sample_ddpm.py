@@ -27,7 +27,14 @@ def _device() -> torch.device:
 
 # ----------------------------------------------------------------------------------- image output
 def make_grid(ims: torch.Tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> torch.Tensor:
-    """torchvision.utils.make_grid semantics for a (B, C, H, W) batch (torchvision is not a dependency)."""
+    """torchvision.utils.make_grid (torchvision==0.18.0, reference requirements.txt:6; not a dependency
+    here) for a (B, C, H, W) batch with its defaults normalize=False, scale_each=False: one image is
+    returned as is, a 1-channel batch is repeated to 3 channels, images are laid out row-major
+    ``min(nrow, B)`` per row with ``padding`` pixels of ``pad_value`` around each."""
+    if ims.dim() == 3:
+        ims = ims.unsqueeze(0)
+    if ims.shape[1] == 1:
+        ims = torch.cat((ims, ims, ims), 1)
     B, C, H, W = ims.shape
     if B == 1:
         return ims[0]
@@ -46,9 +53,14 @@ def make_grid(ims: torch.Tensor, nrow: int = 8, padding: int = 2, pad_value: flo
 
 
 def save_png(grid: torch.Tensor, path: str):
-    """ToPILImage semantics for float CHW in [0, 1]: mul(255).byte(), then PNG."""
+    """torchvision.transforms.ToPILImage()(grid).save(path) for a CHW tensor: a float tensor becomes
+    ``mul(255).byte()`` (truncation, wrapping above 255 as the reference's does), a uint8 tensor is
+    taken as is; 1 channel -> mode 'L', 3 -> 'RGB'."""
     from PIL import Image
-    arr = grid.mul(255).byte().permute(1, 2, 0).cpu().numpy()
+    g = grid.detach().cpu()
+    if g.is_floating_point():
+        g = g.mul(255).byte()
+    arr = g.permute(1, 2, 0).numpy()
     Image.fromarray(arr.squeeze(-1) if arr.shape[-1] == 1 else arr).save(path)
 
 
@@ -112,7 +124,7 @@ class _GraphStep:
 def sample_tensor(model: Unet, scheduler: LinearNoiseScheduler, batch: int, im_channels: int, im_size: int, *,
                   noise: str = 'torch_cpu', seed: Optional[int] = None, sample0: int = 0,
                   x_T: Optional[torch.Tensor] = None, graph: bool = False, total_batch: Optional[int] = None,
-                  progress=None) -> torch.Tensor:
+                  progress=None, progress_x=None) -> torch.Tensor:
     """The reverse loop of reference ``sample_ddpm.py:35-44``; returns x0 (not clamped).
 
     noise='torch_cpu': x_T and every z come from the CPU generator in the reference's order
@@ -157,6 +169,8 @@ def sample_tensor(model: Unet, scheduler: LinearNoiseScheduler, batch: int, im_c
         xt, nxt = nxt, xt
         if progress is not None:
             progress(i)
+        if progress_x is not None:  # (t, x_{t-1}) after each step (tests / diagnostics)
+            progress_x(i, xt)
     return xt
 
 

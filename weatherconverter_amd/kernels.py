@@ -740,20 +740,31 @@ def head_conv(x: View, scale: torch.Tensor, shift: torch.Tensor, w_packed: torch
 def ddpm_step(x: torch.Tensor, eps: torch.Tensor, out: torch.Tensor, beta: float, s1m: float, sqrt_alpha: float,
               sigma: float, *, z: Optional[torch.Tensor] = None, mode: int = _native.NOISE_NONE, seed: int = 0,
               sample0: int = 0, step: int = 0, sz_out: Optional[torch.Tensor] = None):
-    _req(x.shape == eps.shape == out.shape and x.is_contiguous() and eps.is_contiguous() and out.is_contiguous(),
-         'ddpm_step shapes')
+    def dev_f32(v, what):  # the kernel reads / writes float4 vectors of device memory
+        _req(v.is_cuda and v.dtype == torch.float32 and v.is_contiguous() and v.data_ptr() % 16 == 0,
+             f'ddpm_step {what}: contiguous 16-byte-aligned fp32 device tensor')
+
+    _req(x.shape == eps.shape == out.shape, 'ddpm_step shapes')
+    for v, what in ((x, 'x'), (eps, 'eps'), (out, 'out')):
+        dev_f32(v, what)
     if mode == _native.NOISE_TENSOR:
-        _req(z is not None and z.shape == x.shape and z.is_contiguous() and z.is_cuda, 'noise tensor shape')
+        _req(z is not None and z.shape == x.shape, 'noise tensor shape')
+        dev_f32(z, 'z')
     B = x.shape[0]
     per = x.numel() // B
     if sz_out is not None:
-        _req(sz_out.shape == x.shape and sz_out.is_contiguous(), 'sz_out shape')
+        _req(sz_out.shape == x.shape, 'sz_out shape')
+        dev_f32(sz_out, 'sz_out')
     _native.call('wc_ddpm_step', x.data_ptr(), eps.data_ptr(), _ptr(z), out.data_ptr(), _ptr(sz_out), B, per, beta, s1m,
                  sqrt_alpha, sigma, mode, seed & ((1 << 64) - 1), sample0, step, _stream())
 
 
 def add_noise(x0: torch.Tensor, noise: torch.Tensor, coef_a: torch.Tensor, coef_b: torch.Tensor) -> torch.Tensor:
     _req(x0.shape == noise.shape and x0.is_contiguous() and noise.is_contiguous(), 'add_noise shapes')
+    _req(x0.is_cuda and noise.is_cuda and x0.dtype == torch.float32 and noise.dtype == torch.float32
+         and x0.data_ptr() % 16 == 0 and noise.data_ptr() % 16 == 0, 'add_noise: 16-byte-aligned fp32 device tensors')
+    _req(coef_a.is_cuda and coef_b.is_cuda and coef_a.dtype == torch.float32 and coef_b.dtype == torch.float32,
+         'add_noise coefficients: fp32 device tensors')
     B = x0.shape[0]
     _req(coef_a.numel() == B and coef_b.numel() == B, 'add_noise coefficient count')
     out = torch.empty_like(x0)

@@ -336,6 +336,76 @@ int wc_mse_workspace_doubles(void);
 int wc_mse_loss(const float* a, const float* b, int64_t n, float* grad, float grad_scale,
                 double* workspace, float* loss, void* stream);
 
+/* ---- UNet backward (loss.backward(), train_ddpm.py:110; the layers of unet_base.py:87-488) ---- */
+
+/* Conv weight gradient: dW[m][k] = sum over the B*Hm*Wm pixel grid of g[pixel][m] * X_k[pixel],
+ * where X_k is column k of the conv's own input exactly as the forward read it (wc_conv_args
+ * segments: segment 0 through its taps / stride / zero padding, optionally through the forward's
+ * GroupNorm(+SiLU) prologue scale/shift/silu, then the raw 1x1 segment 1).  K column order as the
+ * forward's packed weight: (tap, channel) of segment 0, then segment 1's channels.  fp32 MFMA.
+ * g: NHWC view with M channels (M % 4 == 0) and pixel stride ldg.  The pixel sum is split over
+ * `splits` workgroup rows (wc_conv_wgrad_splits); partial sums go to part[splits][M][Kc] and
+ * wc_wgrad_reduce adds them in a fixed order (deterministic).
+ * Replaces the weight gradients of every nn.Conv2d / ConvTranspose2d / in_proj / out_proj. */
+typedef struct wc_wgrad_args {
+    const float* g;
+    int M, ldg;
+    wc_conv_seg seg[2];
+    int nseg;
+    int B, Hm, Wm;
+} wc_wgrad_args;
+int wc_conv_wgrad(const wc_wgrad_args* args, float* part, int splits, void* stream);
+/* The split count wc_conv_wgrad accepts for (M, Kc, P = B*Hm*Wm) aiming at ~target_blocks workgroups. */
+int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks);
+/* dW = sum_split part: column k < K0 is (tap t = k / C0, channel c = k % C0), written (c < Cw only)
+ * to dw0[m*sM0 + c*sC0 + t*sT0]; columns k >= K0 to dw1[m*sM1 + k - K0].  accumulate: += . */
+int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,
+                    int64_t sM0, int64_t sC0, int64_t sT0, float* dw1, int64_t sM1, int accumulate,
+                    void* stream);
+
+/* GroupNorm(groups)(+SiLU) backward over NHWC views (reference nn.GroupNorm(8, C) -> nn.SiLU()).
+ * sc0/sh0 [B][C]: the normalisation without affine (rstd, -mean*rstd: wc_gn_finalize with NULL
+ * gamma/beta), so xhat = x*sc0 + sh0; y = gamma*xhat + beta; dy = dz * SiLU'(y) (silu) or dz.
+ * reduce: part[B][splits][C][2] = (sum dy, sum dy*xhat) per pixel split (wc_gn_bwd_splits);
+ *         x == NULL: plain per-(b, c) sums of dz (bias / time-embedding gradients).
+ * finalize: sums[B][C][2] in a fixed order; with coef: coef[B][C][4] = (rstd*gamma, -rstd*A/n,
+ *         -rstd*Bs/n, 0), A / Bs the group sums of gamma*sum dy / gamma*sum dy*xhat.
+ * bsum: out[c] (+)= sum_b sums[b][c][idx]  (idx 0: dbeta / bias grad, 1: dgamma).
+ * apply: dx (+)= coef0*dy + coef1 + coef2*xhat.  C % 4 == 0, 16-byte aligned views. */
+int wc_gn_bwd_splits(int B, int HW);
+int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
+                     const float* gamma, const float* beta, int silu, int B, int HW, int C, int splits,
+                     float* part, void* stream);
+int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, int HW, const float* sc0,
+                       const float* gamma, float* sums, float* coef, void* stream);
+int wc_bsum(const float* sums, int B, int C, int idx, float* out, int accumulate, void* stream);
+int wc_gn_bwd_apply(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
+                    const float* gamma, const float* beta, int silu, const float* coef, int B, int HW, int C,
+                    float* dx, int lddx, int accumulate, void* stream);
+
+/* Attention forward that also writes lse[b][h][q] = log2 sum_k exp2(s_qk * scale * log2 e) (fp32
+ * MFMA kernel of wc_attention_fwd), and its backward: dqkv (same [q | k | v] column layout as
+ * qkv) from qkv, the forward output `out`, its gradient dout and lse; dv_work: B*heads*N floats.
+ * Head dims 8, 16, 32, 64, 128, 192.  Deterministic (no atomics).
+ * Replaces the backward of nn.MultiheadAttention's attention core (unet_base.py:115,159). */
+int wc_attention_fwd_lse(const float* qkv, int ld_qkv, float* out, int ld_out, float* lse, int B, int N, int C,
+                         int heads, float scale, void* stream);
+int wc_attention_bwd(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout, int ld_dout,
+                     const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C, int heads,
+                     float scale, void* stream);
+
+/* Small dense helpers for the time-embedding MLP backward (t_proj, t_emb_layers: B x 128):
+ * C[m][n] = alpha*sum_k A[m*sam + k*sak]*B[k*sbk + n*sbn] + beta*C[m][n] (beta 0: C not read);
+ * silu: mode 0 out = silu(y), mode 1 out = dz*silu'(y); colsum: out[n] (+)= sum_r X[r*ldx + n];
+ * time embedding: get_time_embedding (unet_base.py:7-30) of nt timesteps, D columns. */
+int wc_gemm_small(int M, int N, int K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                  int64_t sbn, float* C, int64_t ldc, float alpha, float beta, void* stream);
+int wc_silu(const float* y, const float* dz, float* out, int64_t n, int mode, void* stream);
+int wc_colsum(const float* X, int R, int N, int64_t ldx, float* out, int accumulate, void* stream);
+int wc_time_embedding(const int64_t* t, int nt, int D, float* out, void* stream);
+/* NCHW (B, C, H, W) -> NHWC with ldc >= C channels per pixel, channels C..ldc-1 zero. */
+int wc_nchw_to_nhwc(const float* src, int B, int C, int H, int W, float* dst, int ldc, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Swift-SRGAN generator (srgan_model/models.py:6-92)                                         */
 /* ------------------------------------------------------------------------------------------ */

@@ -64,13 +64,14 @@ def level_has_attn(mc, i: int) -> bool:  # unet_base.py:404-405,434-435
 
 
 def unet_forward(sd: Dict[str, torch.Tensor], mc, x: torch.Tensor, t) -> torch.Tensor:
-    """Reference Unet.forward (unet_base.py:451-488) on CPU fp32."""
-    x = x.float()
+    """Reference Unet.forward (unet_base.py:451-488) on CPU fp32 (float64 when x is float64: the
+    autograd reference of the training-backward tests)."""
+    x = x if x.dtype == torch.float64 else x.float()
     dc: List[int] = list(mc.down_channels)
     L = len(dc) - 1
     heads = mc.num_heads
     out = F.conv2d(x, sd['conv_in.weight'], sd['conv_in.bias'], padding=1)
-    temb = time_embedding(torch.as_tensor(t).long(), mc.time_emb_dim)
+    temb = time_embedding(torch.as_tensor(t).long(), mc.time_emb_dim).to(x.dtype)
     temb = F.linear(F.silu(F.linear(temb, sd['t_proj.0.weight'], sd['t_proj.0.bias'])), sd['t_proj.2.weight'],
                     sd['t_proj.2.bias'])
     skips = []

@@ -21,7 +21,10 @@ EXPORTS = [
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
-    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version'
+    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
+    'wc_conv_wgrad', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
+    'wc_gn_bwd_finalize', 'wc_bsum', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
+    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
@@ -46,6 +49,13 @@ class ConvArgs(ctypes.Structure):
         ('out_nchw', ctypes.c_int), ('act', ctypes.c_int), ('absmax_out', ctypes.c_void_p),
         ('act_param', ctypes.c_void_p), ('gn_part', ctypes.c_void_p), ('gn_ncb', ctypes.c_int),
         ('gn_sw', ctypes.c_int), ('gn_c0', ctypes.c_int), ('gn_p64', ctypes.c_int), ('gn_np64', ctypes.c_int)
+    ]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [
+        ('g', ctypes.c_void_p), ('M', ctypes.c_int), ('ldg', ctypes.c_int), ('seg', ConvSeg * 2),
+        ('nseg', ctypes.c_int), ('B', ctypes.c_int), ('Hm', ctypes.c_int), ('Wm', ctypes.c_int)
     ]
 
 
@@ -90,6 +100,21 @@ _SIGS = {
     'wc_mse_workspace_doubles': [],
     'wc_mse_loss': [_P, _P, _L, _P, _F, _P, _P, _P],
     'wc_dwconv': [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
+    'wc_conv_wgrad': [ctypes.POINTER(WgradArgs), _P, _I, _P],
+    'wc_conv_wgrad_splits': [_I, _I, _L, _I],
+    'wc_wgrad_reduce': [_P, _I, _I, _I, _I, _I, _I, _P, _L, _L, _L, _P, _L, _I, _P],
+    'wc_gn_bwd_splits': [_I, _I],
+    'wc_gn_bwd_reduce': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P],
+    'wc_gn_bwd_finalize': [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    'wc_bsum': [_P, _I, _I, _I, _P, _I, _P],
+    'wc_gn_bwd_apply': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P],
+    'wc_attention_fwd_lse': [_P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P],
+    'wc_attention_bwd': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
+    'wc_gemm_small': [_I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _F, _F, _P],
+    'wc_silu': [_P, _P, _P, _L, _I, _P],
+    'wc_colsum': [_P, _I, _I, _L, _P, _I, _P],
+    'wc_time_embedding': [_P, _I, _I, _P, _P],
+    'wc_nchw_to_nhwc': [_P, _I, _I, _I, _I, _P, _I, _P],
 }
 
 _lib = None

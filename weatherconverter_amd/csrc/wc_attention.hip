@@ -34,7 +34,7 @@ template <int D>
 __global__ __launch_bounds__(ATT_THREADS, 1) void attention_kernel(const float* __restrict__ qkv,
                                                                    int ldq, float* __restrict__ out,
                                                                    int ldo, int N, int C,
-                                                                   float scale_log2) {
+                                                                   float scale_log2, float* __restrict__ lse) {
     using Cf = AttCfg<D>;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* Ks = smem;                       // [KT][KS]
@@ -169,6 +169,8 @@ __global__ __launch_bounds__(ATT_THREADS, 1) void attention_kernel(const float* 
     // ---- epilogue: O[q][dv] = O^T[dv][q] / l ----
     if (qrow < N) {
         const float inv = 1.0f / l_run;
+        // log2-domain log-sum-exp of the scaled scores (training backward): P = exp2(s*scale_log2 - lse)
+        if (lse && half == 0) lse[((long)b * gridDim.y + head) * N + qrow] = m_run + __log2f(l_run);
         float* orow = out + ((long)b * N + qrow) * ldo + head * D;
 #pragma unroll
         for (int d = 0; d < Cf::NDB; ++d) {
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(ATT_THREADS, 1) void attention_kernel(const float* 
 
 template <int D>
 int launch_att(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
-               float scale, hipStream_t stream) {
+               float scale, hipStream_t stream, float* lse = nullptr) {
     using Cf = AttCfg<D>;
     size_t lds = (size_t)(KT * Cf::KS + KT * Cf::DP) * sizeof(float);
     if (!Cf::QREG) lds += (size_t)128 * Cf::QS * sizeof(float);
@@ -200,31 +202,42 @@ int launch_att(const float* qkv, int ldq, float* out, int ldo, int B, int N, int
     dim3 grid((N + 127) / 128, heads, B);
     const float scale_log2 = scale * 1.4426950408889634f;
     hipLaunchKernelGGL(attention_kernel<D>, grid, dim3(ATT_THREADS), lds, stream, qkv, ldq, out,
-                       ldo, N, C, scale_log2);
+                       ldo, N, C, scale_log2, lse);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 }  // namespace
 
-extern "C" int wc_attention_fwd(const float* qkv, int ld_qkv, float* out, int ld_out, int B,
-                                int N, int C, int heads, float scale, void* stream) {
+static int attention_fwd_any(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C, int heads,
+                             float scale, void* stream, float* lse) {
     if (!qkv || !out) return WC_E_ARG;
     if (heads <= 0 || C % heads != 0 || ld_qkv % 4 != 0 || ld_out % 4 != 0) return WC_E_SHAPE;
     if (ld_qkv < 3 * C || ld_out < C) return WC_E_SHAPE;
     const int D = C / heads;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     switch (D) {
-        case 8: return launch_att<8>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 16: return launch_att<16>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 24: return launch_att<24>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 48: return launch_att<48>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 96: return launch_att<96>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 160: return launch_att<160>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 32: return launch_att<32>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 64: return launch_att<64>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 128: return launch_att<128>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
-        case 192: return launch_att<192>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s);
+        case 8: return launch_att<8>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 16: return launch_att<16>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 24: return launch_att<24>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 48: return launch_att<48>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 96: return launch_att<96>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 160: return launch_att<160>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 32: return launch_att<32>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 64: return launch_att<64>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 128: return launch_att<128>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
+        case 192: return launch_att<192>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, s, lse);
         default: return WC_E_SHAPE;
     }
+}
+
+extern "C" int wc_attention_fwd(const float* qkv, int ld_qkv, float* out, int ld_out, int B,
+                                int N, int C, int heads, float scale, void* stream) {
+    return attention_fwd_any(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, stream, nullptr);
+}
+
+extern "C" int wc_attention_fwd_lse(const float* qkv, int ld_qkv, float* out, int ld_out, float* lse, int B, int N,
+                                    int C, int heads, float scale, void* stream) {
+    if (!lse) return WC_E_ARG;
+    return attention_fwd_any(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, stream, lse);
 }

@@ -1,0 +1,331 @@
+// Self-attention backward on fp32 MFMA for gfx950 (the training backward of the softmax(QK^T*s)V
+// core of nn.MultiheadAttention, reference unet_base.py:115,159; train_ddpm.py:110 loss.backward()).
+//
+// Forward contract (wc_attention_fwd_lse): lse[b][h][q] = log2 sum_k exp2(s_qk * scale*log2(e)), so
+// P_qk = exp2(s_qk*scale_log2 - lse_q) is recomputed exactly without storing the N x N scores.
+// With Dv_q = sum_d dO_qd O_qd (attn_bwd_prep_kernel):
+//     dS = P o (dP - Dv),  dP = dO V^T,  dV = P^T dO,  dK = scale dS^T Q,  dQ = scale dS K.
+// Two kernels, no atomics (deterministic):
+//   attn_bwd_dkdv_kernel  a wave owns 32 keys; loops over 32-query tiles (Q, dO, lse, Dv staged in
+//       LDS): S = Q K^T and dP = dO V^T with keys on the lanes (the accumulator register r holds
+//       query (r&3)+8(r>>2)+4*half), so P and dS are directly the B operand of
+//       dV^T += dO^T P and dK^T += Q^T dS (the forward kernel's register-reuse trick, transposed).
+//   attn_bwd_dq_kernel    a wave owns 32 queries; loops over 32-key tiles: S^T = K Q^T and
+//       dP^T = V dO^T with queries on the lanes, dS^T feeds dQ^T += K^T dS^T.
+// All operands come from LDS (K/V of the workgroup's keys or Q/dO of its queries staged once, the
+// other side per tile), so head dims up to 192 fit without spilling; exact fp32 products.
+#include "wc_common.hpp"
+
+namespace {
+
+template <int D>
+struct BwdCfg {
+    static constexpr int DH = D / 2;                // d-values per lane half in the QK^T / dO V^T loops
+    static constexpr int DP = (D + 31) / 32 * 32;   // padded head dim of the d-row accumulators
+    static constexpr int NDB = DP / 32;
+    static constexpr int RS = D + 4;                // LDS row stride (floats)
+    static constexpr int W = D >= 128 ? 2 : 4;      // waves per workgroup
+    static constexpr int SLACK = 32;                // reads of pad columns d >= D stay inside LDS
+};
+
+template <int D>
+__global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dkdv_kernel(
+    const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
+    using Cf = BwdCfg<D>;
+    constexpr int W = Cf::W, RS = Cf::RS, NT = W * 64;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Ks = smem;                     // [W*32][RS]  this workgroup's keys
+    float* Vs = Ks + W * 32 * RS;         // [W*32][RS]
+    float* Qs = Vs + W * 32 * RS;         // [32][RS]    query tile
+    float* Os = Qs + 32 * RS;             // [32][RS]    dO tile
+    float* Ls = Os + 32 * RS + Cf::SLACK; // [32] lse, then [32] Dv
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, half = lane >> 5;
+    const int head = blockIdx.y, b = blockIdx.z, H = gridDim.y;
+    const int kb0 = blockIdx.x * W * 32;
+    const float* base = qkv + (long)b * N * ldq;
+    const float* dob = dO + (long)b * N * lddo;
+    const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
+
+    for (int i = tid; i < W * 32 * (D / 4); i += NT) {
+        const int r = i / (D / 4), c4 = i % (D / 4);
+        const int key = kb0 + r;
+        f32x4 kv = f32x4{0.f, 0.f, 0.f, 0.f}, vv = kv;
+        if (key < N) {
+            kv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + kcol + c4 * 4);
+            vv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + vcol + c4 * 4);
+        }
+        *reinterpret_cast<f32x4*>(Ks + r * RS + c4 * 4) = kv;
+        *reinterpret_cast<f32x4*>(Vs + r * RS + c4 * 4) = vv;
+    }
+
+    f32x16 dvT[Cf::NDB], dkT[Cf::NDB];
+#pragma unroll
+    for (int d = 0; d < Cf::NDB; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dvT[d][r] = 0.f; dkT[d][r] = 0.f; }
+
+    const float* krow = Ks + (wave * 32 + l32) * RS + half * Cf::DH;
+    const float* vrow = Vs + (wave * 32 + l32) * RS + half * Cf::DH;
+    const int ntiles = (N + 31) / 32;
+    for (int t = 0; t < ntiles; ++t) {
+        const int q0 = t * 32;
+        __syncthreads();  // previous tile consumed (and the key block staged on t == 0)
+        for (int i = tid; i < 32 * (D / 4); i += NT) {
+            const int r = i / (D / 4), c4 = i % (D / 4);
+            const int q = q0 + r;
+            f32x4 qv = f32x4{0.f, 0.f, 0.f, 0.f}, ov = qv;
+            if (q < N) {
+                qv = *reinterpret_cast<const f32x4*>(base + (long)q * ldq + qcol + c4 * 4);
+                ov = *reinterpret_cast<const f32x4*>(dob + (long)q * lddo + head * D + c4 * 4);
+            }
+            *reinterpret_cast<f32x4*>(Qs + r * RS + c4 * 4) = qv;
+            *reinterpret_cast<f32x4*>(Os + r * RS + c4 * 4) = ov;
+        }
+        if (tid < 32) {
+            const int q = q0 + tid;
+            Ls[tid] = q < N ? lse[((long)b * H + head) * N + q] : INFINITY;  // P = 0 for padding queries
+            Ls[32 + tid] = q < N ? Dv[((long)b * H + head) * N + q] : 0.f;
+        }
+        __syncthreads();
+
+        // S = Q K^T, dP = dO V^T: rows = queries, lane = key
+        f32x16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+        const float* qr = Qs + l32 * RS + half * Cf::DH;
+        const float* orw = Os + l32 * RS + half * Cf::DH;
+#pragma unroll
+        for (int i = 0; i < Cf::DH; i += 4) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(qr + i);
+            const f32x4 kk = *reinterpret_cast<const f32x4*>(krow + i);
+            const f32x4 a2 = *reinterpret_cast<const f32x4*>(orw + i);
+            const f32x4 vv = *reinterpret_cast<const f32x4*>(vrow + i);
+            s = mfma32(a.x, kk.x, s); s = mfma32(a.y, kk.y, s); s = mfma32(a.z, kk.z, s); s = mfma32(a.w, kk.w, s);
+            dp = mfma32(a2.x, vv.x, dp); dp = mfma32(a2.y, vv.y, dp);
+            dp = mfma32(a2.z, vv.z, dp); dp = mfma32(a2.w, vv.w, dp);
+        }
+        // P and dS in place (register r <-> query row (r&3) + 8(r>>2) + 4 half of the tile)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int qi = (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float pr = exp2f(s[r] * scale_log2 - Ls[qi]);
+            s[r] = pr;
+            dp[r] = pr * (dp[r] - Ls[32 + qi]);
+        }
+        // dV^T += dO^T P, dK^T += Q^T dS
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int qi = (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float* op = Os + qi * RS + l32;
+            const float* qp = Qs + qi * RS + l32;
+#pragma unroll
+            for (int d = 0; d < Cf::NDB; ++d) {
+                dvT[d] = mfma32(op[d * 32], s[r], dvT[d]);
+                dkT[d] = mfma32(qp[d * 32], dp[r], dkT[d]);
+            }
+        }
+    }
+
+    const int key = kb0 + wave * 32 + l32;
+    if (key < N) {
+        float* row = dqkv + ((long)b * N + key) * lddq;
+#pragma unroll
+        for (int d = 0; d < Cf::NDB; ++d) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 4) {
+                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                if (dv < D) {
+                    *reinterpret_cast<f32x4*>(row + kcol + dv) =
+                        f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * scale;
+                    *reinterpret_cast<f32x4*>(row + vcol + dv) = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
+                }
+            }
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dq_kernel(
+    const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
+    using Cf = BwdCfg<D>;
+    constexpr int W = Cf::W, RS = Cf::RS, NT = W * 64;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Qs = smem;                 // [W*32][RS] this workgroup's queries
+    float* Os = Qs + W * 32 * RS;     // [W*32][RS] their dO
+    float* Ks = Os + W * 32 * RS;     // [32][RS]   key tile
+    float* Vs = Ks + 32 * RS;         // [32][RS]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, half = lane >> 5;
+    const int head = blockIdx.y, b = blockIdx.z, H = gridDim.y;
+    const int qb0 = blockIdx.x * W * 32;
+    const float* base = qkv + (long)b * N * ldq;
+    const float* dob = dO + (long)b * N * lddo;
+    const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
+
+    for (int i = tid; i < W * 32 * (D / 4); i += NT) {
+        const int r = i / (D / 4), c4 = i % (D / 4);
+        const int q = qb0 + r;
+        f32x4 qv = f32x4{0.f, 0.f, 0.f, 0.f}, ov = qv;
+        if (q < N) {
+            qv = *reinterpret_cast<const f32x4*>(base + (long)q * ldq + qcol + c4 * 4);
+            ov = *reinterpret_cast<const f32x4*>(dob + (long)q * lddo + head * D + c4 * 4);
+        }
+        *reinterpret_cast<f32x4*>(Qs + r * RS + c4 * 4) = qv;
+        *reinterpret_cast<f32x4*>(Os + r * RS + c4 * 4) = ov;
+    }
+    const int qme = qb0 + wave * 32 + l32;
+    const float lq = qme < N ? lse[((long)b * H + head) * N + qme] : INFINITY;
+    const float dq = qme < N ? Dv[((long)b * H + head) * N + qme] : 0.f;
+
+    f32x16 dqT[Cf::NDB];
+#pragma unroll
+    for (int d = 0; d < Cf::NDB; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dqT[d][r] = 0.f;
+
+    const float* qrow = Qs + (wave * 32 + l32) * RS + half * Cf::DH;
+    const float* orow = Os + (wave * 32 + l32) * RS + half * Cf::DH;
+    const int ntiles = (N + 31) / 32;
+    for (int t = 0; t < ntiles; ++t) {
+        const int k0 = t * 32;
+        __syncthreads();
+        for (int i = tid; i < 32 * (D / 4); i += NT) {
+            const int r = i / (D / 4), c4 = i % (D / 4);
+            const int key = k0 + r;
+            f32x4 kv = f32x4{0.f, 0.f, 0.f, 0.f}, vv = kv;
+            if (key < N) {
+                kv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + kcol + c4 * 4);
+                vv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + vcol + c4 * 4);
+            }
+            *reinterpret_cast<f32x4*>(Ks + r * RS + c4 * 4) = kv;
+            *reinterpret_cast<f32x4*>(Vs + r * RS + c4 * 4) = vv;
+        }
+        __syncthreads();
+
+        // S^T = K Q^T, dP^T = V dO^T: rows = keys, lane = query
+        f32x16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+        const float* kr = Ks + l32 * RS + half * Cf::DH;
+        const float* vr = Vs + l32 * RS + half * Cf::DH;
+#pragma unroll
+        for (int i = 0; i < Cf::DH; i += 4) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(kr + i);
+            const f32x4 qq = *reinterpret_cast<const f32x4*>(qrow + i);
+            const f32x4 a2 = *reinterpret_cast<const f32x4*>(vr + i);
+            const f32x4 oo = *reinterpret_cast<const f32x4*>(orow + i);
+            s = mfma32(a.x, qq.x, s); s = mfma32(a.y, qq.y, s); s = mfma32(a.z, qq.z, s); s = mfma32(a.w, qq.w, s);
+            dp = mfma32(a2.x, oo.x, dp); dp = mfma32(a2.y, oo.y, dp);
+            dp = mfma32(a2.z, oo.z, dp); dp = mfma32(a2.w, oo.w, dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float pr = key < N ? exp2f(s[r] * scale_log2 - lq) : 0.f;
+            dp[r] = pr * (dp[r] - dq);
+        }
+        // dQ^T += K^T dS^T
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int ki = (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float* kp = Ks + ki * RS + l32;
+#pragma unroll
+            for (int d = 0; d < Cf::NDB; ++d) dqT[d] = mfma32(kp[d * 32], dp[r], dqT[d]);
+        }
+    }
+
+    if (qme < N) {
+        float* row = dqkv + ((long)b * N + qme) * lddq + qcol;
+#pragma unroll
+        for (int d = 0; d < Cf::NDB; ++d) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 4) {
+                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                if (dv < D)
+                    *reinterpret_cast<f32x4*>(row + dv) = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * scale;
+            }
+        }
+    }
+}
+
+// Dv[b][h][q] = sum_d dO[b, q, h*D + d] * O[b, q, h*D + d]
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ O, int ldo,
+                                                            const float* __restrict__ dO, int lddo, int B, int N,
+                                                            int H, int D, float* __restrict__ Dv) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)B * H * N) return;
+    const int q = (int)(i % N);
+    const long bh = i / N;
+    const int h = (int)(bh % H);
+    const int b = (int)(bh / H);
+    const float* o = O + ((long)b * N + q) * ldo + h * D;
+    const float* g = dO + ((long)b * N + q) * lddo + h * D;
+    float s = 0.f;
+    for (int d = 0; d < D; d += 4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(o + d);
+        const f32x4 c = *reinterpret_cast<const f32x4*>(g + d);
+        s = fmaf(a.x, c.x, s); s = fmaf(a.y, c.y, s); s = fmaf(a.z, c.z, s); s = fmaf(a.w, c.w, s);
+    }
+    Dv[i] = s;
+}
+
+template <int D>
+int launch_bwd(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
+               int lddq, int B, int N, int C, int heads, float scale, hipStream_t s) {
+    using Cf = BwdCfg<D>;
+    const size_t lds = (size_t)(2 * Cf::W * 32 * Cf::RS + 2 * 32 * Cf::RS + Cf::SLACK + 64) * sizeof(float);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<D>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    const dim3 grid((N + Cf::W * 32 - 1) / (Cf::W * 32), heads, B);
+    const float scale_log2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, grid, dim3(Cf::W * 64), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq,
+                       N, C, scale_log2, scale);
+    WC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(Cf::W * 64), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N,
+                       C, scale_log2, scale);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+}  // namespace
+
+extern "C" int wc_attention_bwd(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
+                                int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
+                                int C, int heads, float scale, void* stream) {
+    if (!qkv || !out || !dout || !lse || !dv_work || !dqkv) return WC_E_ARG;
+    if (heads <= 0 || C % heads || B <= 0 || N <= 0) return WC_E_SHAPE;
+    if (ld_qkv % 4 || ld_out % 4 || ld_dout % 4 || ld_dqkv % 4 || ld_qkv < 3 * C || ld_dqkv < 3 * C || ld_out < C ||
+        ld_dout < C)
+        return WC_E_SHAPE;
+    const int D = C / heads;
+    if (D % 4) return WC_E_SHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const long n = (long)B * heads * N;
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, ld_out, dout,
+                       ld_dout, B, N, heads, D, dv_work);
+    WC_CHECK_LAUNCH();
+    switch (D) {
+        case 8: return launch_bwd<8>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 16: return launch_bwd<16>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 32: return launch_bwd<32>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 64: return launch_bwd<64>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 128:
+            return launch_bwd<128>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 192:
+            return launch_bwd<192>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        default: return WC_E_SHAPE;
+    }
+}

@@ -1,0 +1,676 @@
+// Backward-pass kernels of the DDPM UNet training step (reference diffusion_model/train_ddpm.py:106-114:
+// loss.backward() through unet_base.Unet, then Adam).  gfx950 / CDNA4, wave64.
+//
+//  * conv_wgrad_kernel  dW[m][k] = sum over pixels of G[pixel][m] * X_k[pixel], where X_k is the
+//    conv's own input as the forward read it: column k = (tap, channel) of segment 0 with the same
+//    tap offsets, stride and zero padding, optionally through the forward's GroupNorm(+SiLU)
+//    prologue (the activation is recomputed, not stored), then the raw 1x1 residual segment.
+//    One GEMM with M = G channels, N = K columns, K = B*Hm*Wm pixels on fp32 MFMA
+//    (v_mfma_f32_32x32x2_f32, exact fp32 products): both operands are NHWC pixel rows, which is
+//    exactly the [k][m] / [k][n] order the 32x32x2 fragments read (lane = m or n, lane half = k),
+//    so the tiles are staged straight from HBM rows into LDS with no transpose.  The pixel
+//    reduction is split across workgroups (partials [split][M][K]) and summed in a fixed order
+//    by wgrad_reduce_kernel, which also scatters into the parameter's own layout: results are
+//    deterministic run to run.
+//  * gnb_*  GroupNorm(8)(+SiLU) backward: per-(b, c) sums of dy and dy*xhat over pixel splits,
+//    per-image coefficients (dx = a*dy + k0 + k1*xhat), dgamma / dbeta, and the elementwise
+//    apply that recomputes xhat and the SiLU derivative from the stored pre-norm input.  The
+//    same reduction without a normalised input is the per-(b, c) channel sum (bias / temb grads).
+//  * gemm_small / silu / colsum / temb helpers for the time-embedding MLP (B x 128 matrices).
+//  * nchw_to_nhwc: the loss gradient (NCHW, the UNet output layout) into a padded NHWC view.
+#include "wc_common.hpp"
+
+namespace {
+
+constexpr unsigned OOB = 0x80000000u;
+constexpr int SRD_BYTES = 0x7FFFFFFF;
+constexpr int SRD_FLAGS = 0x00020000;
+
+WC_DEVICE __amdgpu_buffer_rsrc_t make_srd(const float* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, SRD_BYTES, SRD_FLAGS);
+}
+WC_DEVICE f32x4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+WC_DEVICE float silu_grad(float y) {  // d/dy [y * sigmoid(y)]
+    const float s = 1.0f / (1.0f + __expf(-y));
+    return s * (1.0f + y * (1.0f - s));
+}
+
+// ============================================================================================
+// conv weight gradient
+// ============================================================================================
+constexpr int WG_THREADS = 256;
+constexpr int WG_KP = 32;  // pixels per K-step
+
+struct WgDev {
+    const float* g;
+    int M, ldg;
+    const float* src0;
+    int C0, ldc0, H0, W0, sy, sx, ntaps;
+    int dy[WC_MAX_TAPS], dx[WC_MAX_TAPS];
+    const float* scale;
+    const float* shift;
+    const float* src1;
+    int C1, ldc1, H1, W1;
+    int Hm, Wm;
+    long P;     // pixels = B*Hm*Wm
+    int K0, Kc; // segment-0 columns (ntaps*C0), all columns (+ C1)
+    float* part;
+    long pps;   // pixels per split (multiple of WG_KP)
+    int ntm, ntn;
+};
+
+// PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU (segment 0 only, as the forward prologue).
+template <int BM, int BN, int PRO>
+__global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
+    constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;
+    static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
+    constexpr int AS = BM + 32, BS = BN + 32;  // LDS row strides: lane halves on disjoint banks
+    constexpr int A_PER_T = WG_KP * BM / 4 / WG_THREADS;
+    constexpr int B_PER_T = WG_KP * BN / 4 / WG_THREADS;
+    constexpr int STAGE = WG_KP * (AS + BS);
+    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int l32 = lane & 31, half = lane >> 5;
+
+    int t = blockIdx.x;
+    const int tn = t % p.ntn;
+    t /= p.ntn;
+    const int tm = t % p.ntm;
+    const int sp = t / p.ntm;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const long pbeg = (long)sp * p.pps;
+    long pend = pbeg + p.pps;
+    if (pend > p.P) pend = p.P;
+    const int nsteps = (int)((pend - pbeg + WG_KP - 1) / WG_KP);
+    const int HWm = p.Hm * p.Wm;
+
+    // fixed per-thread column coordinates
+    int arow[A_PER_T], acol[A_PER_T];
+#pragma unroll
+    for (int j = 0; j < A_PER_T; ++j) {
+        const int i = tid + WG_THREADS * j;
+        arow[j] = i / (BM / 4);
+        acol[j] = 4 * (i % (BM / 4));
+    }
+    int brow[B_PER_T], bcol[B_PER_T], bseg[B_PER_T], bc[B_PER_T], bdy[B_PER_T], bdx[B_PER_T];
+#pragma unroll
+    for (int j = 0; j < B_PER_T; ++j) {
+        const int i = tid + WG_THREADS * j;
+        brow[j] = i / (BN / 4);
+        bcol[j] = 4 * (i % (BN / 4));
+        const int k = n0 + bcol[j];
+        if (k < p.K0) {
+            const int tp = k / p.C0;
+            bseg[j] = 0;
+            bc[j] = k - tp * p.C0;
+            bdy[j] = p.dy[tp];
+            bdx[j] = p.dx[tp];
+        } else if (k < p.Kc) {
+            bseg[j] = 1;
+            bc[j] = k - p.K0;
+            bdy[j] = 0;
+            bdx[j] = 0;
+        } else {
+            bseg[j] = 2;  // past the last column
+            bc[j] = 0;
+            bdy[j] = 0;
+            bdx[j] = 0;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t srdg = make_srd(p.g);
+    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
+    const __amdgpu_buffer_rsrc_t srd1 = make_srd(p.src1 ? p.src1 : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
+
+    f32x4 ra[A_PER_T], rb[B_PER_T];
+    auto load = [&](int s) {
+        const long pb0 = pbeg + (long)s * WG_KP;
+#pragma unroll
+        for (int j = 0; j < A_PER_T; ++j) {
+            const long px = pb0 + arow[j];
+            const bool ok = px < pend && m0 + acol[j] < p.M;
+            ra[j] = bload4(srdg, ok ? (unsigned)(px * p.ldg + m0 + acol[j]) * 4u : OOB);
+        }
+#pragma unroll
+        for (int j = 0; j < B_PER_T; ++j) {
+            const long px = pb0 + brow[j];
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (px < pend && bseg[j] < 2) {
+                const int b = (int)(px / HWm);
+                const int r = (int)(px - (long)b * HWm);
+                const int y = r / p.Wm;
+                const int x = r - y * p.Wm;
+                if (bseg[j] == 0) {
+                    const int iy = y * p.sy + bdy[j], ix = x * p.sx + bdx[j];
+                    const bool inb = (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
+                    v = bload4(srd0, inb ? (unsigned)(((b * p.H0 + iy) * p.W0 + ix) * p.ldc0 + bc[j]) * 4u : OOB);
+                    if constexpr (PRO != 0) {
+                        const unsigned o = (unsigned)(b * p.C0 + bc[j]) * 4u;
+                        const f32x4 sc = bload4(srdsc, o), sh = bload4(srdsh, o);
+                        v = v * sc + sh;
+                        if constexpr (PRO == 2) {
+                            v.x = wc_silu(v.x); v.y = wc_silu(v.y); v.z = wc_silu(v.z); v.w = wc_silu(v.w);
+                        }
+                        if (!inb) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+                    }
+                } else {
+                    const int iy = y * p.sy, ix = x * p.sx;
+                    v = bload4(srd1, (unsigned)(((b * p.H1 + iy) * p.W1 + ix) * p.ldc1 + bc[j]) * 4u);
+                }
+            }
+            rb[j] = v;
+        }
+    };
+    auto store = [&](int buf) {
+        float* a = lds + buf * STAGE;
+        float* bb = a + WG_KP * AS;
+#pragma unroll
+        for (int j = 0; j < A_PER_T; ++j) *reinterpret_cast<f32x4*>(a + arow[j] * AS + acol[j]) = ra[j];
+#pragma unroll
+        for (int j = 0; j < B_PER_T; ++j) *reinterpret_cast<f32x4*>(bb + brow[j] * BS + bcol[j]) = rb[j];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (nsteps > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nsteps) load(s + 1);
+        const float* a = lds + buf * STAGE + wm * 64 + l32;
+        const float* bb = lds + buf * STAGE + WG_KP * AS + wn * 64 + l32;
+#pragma unroll
+        for (int kk = 0; kk < WG_KP / 2; ++kk) {
+            const int row = 2 * kk + half;
+            const float a0 = a[row * AS], a1 = a[row * AS + 32];
+            const float b0 = bb[row * BS], b1 = bb[row * BS + 32];
+            acc[0][0] = mfma32(a0, b0, acc[0][0]);
+            acc[0][1] = mfma32(a0, b1, acc[0][1]);
+            acc[1][0] = mfma32(a1, b0, acc[1][0]);
+            acc[1][1] = mfma32(a1, b1, acc[1][1]);
+        }
+        if (s + 1 < nsteps) store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // partial[sp][m][k]
+    float* out = p.part + (long)sp * p.M * p.Kc;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int k = n0 + wn * 64 + nb * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 64 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (m < p.M && k < p.Kc) out[(long)m * p.Kc + k] = acc[mb][nb][r];
+            }
+        }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int M, int Kc,
+                                                           int K0, int C0, int Cw, float* __restrict__ dw0, long sM0,
+                                                           long sC0, long sT0, float* __restrict__ dw1, long sM1,
+                                                           int accumulate) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    const long n = (long)M * Kc;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += part[(long)sp * n + i];
+    const int m = (int)(i / Kc);
+    const int k = (int)(i - (long)m * Kc);
+    float* dst;
+    if (k < K0) {
+        const int t = k / C0, c = k - t * C0;
+        if (c >= Cw) return;
+        dst = dw0 + m * sM0 + c * sC0 + t * sT0;
+    } else {
+        if (!dw1) return;
+        dst = dw1 + m * sM1 + (k - K0);
+    }
+    *dst = accumulate ? *dst + s : s;
+}
+
+template <int BM, int BN>
+int wgrad_dispatch(const WgDev& d, int pro, int grid, hipStream_t s) {
+    switch (pro) {
+        case 0: hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 0>), dim3(grid), dim3(WG_THREADS), 0, s, d); break;
+        case 1: hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 1>), dim3(grid), dim3(WG_THREADS), 0, s, d); break;
+        default: hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 2>), dim3(grid), dim3(WG_THREADS), 0, s, d); break;
+    }
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+// ============================================================================================
+// GroupNorm(+SiLU) backward and per-(b, c) channel sums
+// ============================================================================================
+constexpr int GB_THREADS = 256;
+
+// part[((b*splits + sp)*C + c)*2 + {0, 1}] = (sum dy, sum dy*xhat) over the split's pixels, with
+// xhat = x*sc0[b,c] + sh0[b,c] (sc0 = rstd, sh0 = -mean*rstd), y = gamma*xhat + beta and
+// dy = dz * SiLU'(y) (or dz).  HAS_X = false: plain sums of dz (second entry 0).
+template <bool HAS_X, bool SILU>
+__global__ __launch_bounds__(GB_THREADS) void gnb_reduce_kernel(const float* __restrict__ dz, int ldz,
+                                                                 const float* __restrict__ x, int ldx,
+                                                                 const float* __restrict__ sc0,
+                                                                 const float* __restrict__ sh0,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, int HW, int C,
+                                                                 int splits, int pps, int nq, float* __restrict__ part) {
+    __shared__ f32x4 red[2][GB_THREADS];
+    const int ncb = C / 4 / nq;
+    int t = blockIdx.x;
+    const int cb = t % ncb;
+    t /= ncb;
+    const int sp = t % splits;
+    const int b = t / splits;
+    const int q = threadIdx.x % nq;
+    const int r = threadIdx.x / nq;
+    const int R = GB_THREADS / nq;
+    const int c = (cb * nq + q) * 4;
+    const int p0 = sp * pps;
+    const int p1 = min(HW, p0 + pps);
+    f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    f32x4 a = s1, o = s1, g = f32x4{1.f, 1.f, 1.f, 1.f}, be = s1;
+    if constexpr (HAS_X) {
+        a = *reinterpret_cast<const f32x4*>(sc0 + (long)b * C + c);
+        o = *reinterpret_cast<const f32x4*>(sh0 + (long)b * C + c);
+        if (gamma) g = *reinterpret_cast<const f32x4*>(gamma + c);
+        if (beta) be = *reinterpret_cast<const f32x4*>(beta + c);
+    }
+    for (int px = p0 + r; px < p1; px += R) {
+        const long pix = (long)b * HW + px;
+        f32x4 d = *reinterpret_cast<const f32x4*>(dz + pix * ldz + c);
+        if constexpr (HAS_X) {
+            const f32x4 xh = *reinterpret_cast<const f32x4*>(x + pix * ldx + c) * a + o;
+            if constexpr (SILU) {
+                const f32x4 y = g * xh + be;
+                d.x *= silu_grad(y.x); d.y *= silu_grad(y.y); d.z *= silu_grad(y.z); d.w *= silu_grad(y.w);
+            }
+            s2 += d * xh;
+        }
+        s1 += d;
+    }
+    red[0][threadIdx.x] = s1;
+    red[1][threadIdx.x] = s2;
+    __syncthreads();
+    if (r == 0) {
+        for (int k = 1; k < R; ++k) {
+            s1 += red[0][k * nq + q];
+            s2 += red[1][k * nq + q];
+        }
+        float* dst = part + (((long)b * splits + sp) * C + c) * 2;
+        *reinterpret_cast<f32x4*>(dst) = f32x4{s1.x, s2.x, s1.y, s2.y};
+        *reinterpret_cast<f32x4*>(dst + 4) = f32x4{s1.z, s2.z, s1.w, s2.w};
+    }
+}
+
+// One workgroup per image: sums[b][c] = (sum dy, sum dy*xhat) over the splits (fixed order); with
+// coef: per group A = sum_c gamma_c s1_c, Bs = sum_c gamma_c s2_c, n = (C/G)*HW, and
+// coef[b][c] = (rstd*gamma_c, -rstd*A/n, -rstd*Bs/n) so that dx = c0*dy + c1 + c2*xhat.
+__global__ __launch_bounds__(GB_THREADS) void gnb_finalize_kernel(const float* __restrict__ part, int splits, int C,
+                                                                   int G, int HW, const float* __restrict__ sc0,
+                                                                   const float* __restrict__ gamma,
+                                                                   float* __restrict__ sums, float* __restrict__ coef) {
+    extern __shared__ float sh[];  // [C][2] then [G][2]
+    const int b = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += GB_THREADS) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int sp = 0; sp < splits; ++sp) {
+            const float* pp = part + (((long)b * splits + sp) * C + c) * 2;
+            s1 += pp[0];
+            s2 += pp[1];
+        }
+        sums[((long)b * C + c) * 2] = s1;
+        sums[((long)b * C + c) * 2 + 1] = s2;
+        const float ga = gamma ? gamma[c] : 1.f;
+        sh[2 * c] = ga * s1;
+        sh[2 * c + 1] = ga * s2;
+    }
+    if (!coef) return;
+    __syncthreads();
+    float* gs = sh + 2 * C;
+    const int cpg = C / G;
+    if (threadIdx.x < G) {
+        float A = 0.f, Bs = 0.f;
+        for (int c = threadIdx.x * cpg; c < (threadIdx.x + 1) * cpg; ++c) {
+            A += sh[2 * c];
+            Bs += sh[2 * c + 1];
+        }
+        gs[2 * threadIdx.x] = A;
+        gs[2 * threadIdx.x + 1] = Bs;
+    }
+    __syncthreads();
+    const float inv_n = 1.0f / ((float)cpg * (float)HW);
+    for (int c = threadIdx.x; c < C; c += GB_THREADS) {
+        const int g = c / cpg;
+        const float rstd = sc0[(long)b * C + c];
+        const float ga = gamma ? gamma[c] : 1.f;
+        float* cf = coef + ((long)b * C + c) * 4;
+        *reinterpret_cast<f32x4*>(cf) = f32x4{rstd * ga, -rstd * gs[2 * g] * inv_n, -rstd * gs[2 * g + 1] * inv_n, 0.f};
+    }
+}
+
+// out[c] (+)= sum_b sums[(b*C + c)*2 + idx]   (fixed order)
+__global__ __launch_bounds__(256) void bsum_kernel(const float* __restrict__ sums, int B, int C, int idx,
+                                                   float* __restrict__ out, int accumulate) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += sums[((long)b * C + c) * 2 + idx];
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+// dx (+)= coef0*dy + coef1 + coef2*xhat, elementwise over (b, pixel, 4 channels)
+template <bool SILU, bool ACC>
+__global__ __launch_bounds__(256) void gnb_apply_kernel(const float* __restrict__ dz, int ldz, const float* __restrict__ x,
+                                                        int ldx, const float* __restrict__ sc0,
+                                                        const float* __restrict__ sh0, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float* __restrict__ coef,
+                                                        float* __restrict__ dx, int lddx, long n4, int HW, int C) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const int C4 = C / 4;
+    const long pix = i / C4;
+    const int c = (int)(i - pix * C4) * 4;
+    const int b = (int)(pix / HW);
+    const long bc = (long)b * C + c;
+    f32x4 d = *reinterpret_cast<const f32x4*>(dz + pix * ldz + c);
+    const f32x4 xh = *reinterpret_cast<const f32x4*>(x + pix * ldx + c) * *reinterpret_cast<const f32x4*>(sc0 + bc) +
+                     *reinterpret_cast<const f32x4*>(sh0 + bc);
+    if constexpr (SILU) {
+        const f32x4 g = gamma ? *reinterpret_cast<const f32x4*>(gamma + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+        const f32x4 be = beta ? *reinterpret_cast<const f32x4*>(beta + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 y = g * xh + be;
+        d.x *= silu_grad(y.x); d.y *= silu_grad(y.y); d.z *= silu_grad(y.z); d.w *= silu_grad(y.w);
+    }
+    f32x4 res;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const f32x4 cf = *reinterpret_cast<const f32x4*>(coef + (bc + e) * 4);
+        res[e] = cf.x * d[e] + cf.y + cf.z * xh[e];
+    }
+    f32x4* o = reinterpret_cast<f32x4*>(dx + pix * lddx + c);
+    if constexpr (ACC) res += *o;
+    *o = res;
+}
+
+// ============================================================================================
+// small dense helpers (time-embedding MLP: B x 128 rows)
+// ============================================================================================
+// C[m][n] = alpha * sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] + beta*C[m][n]  (beta = 0: no read)
+__global__ __launch_bounds__(256) void gemm_small_kernel(int M, int N, int K, const float* __restrict__ A, long sam,
+                                                         long sak, const float* __restrict__ Bm, long sbk, long sbn,
+                                                         float* __restrict__ Cm, long ldc, float alpha, float beta) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)M * N) return;
+    const int m = (int)(i / N), n = (int)(i - (long)m * N);
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s = fmaf(A[m * sam + k * sak], Bm[k * sbk + n * sbn], s);
+    float* c = Cm + m * ldc + n;
+    *c = beta != 0.f ? alpha * s + beta * *c : alpha * s;
+}
+
+// mode 0: out = silu(y); mode 1: out = dz * silu'(y)
+__global__ __launch_bounds__(256) void silu_kernel(const float* __restrict__ y, const float* __restrict__ dz,
+                                                   float* __restrict__ out, long n, int mode) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] = mode == 0 ? wc_silu(y[i]) : dz[i] * silu_grad(y[i]);
+}
+
+// out[n] (+)= sum_r X[r*ldx + n]
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, int R, int N, long ldx,
+                                                     float* __restrict__ out, int accumulate) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += X[r * ldx + n];
+    out[n] = accumulate ? out[n] + s : s;
+}
+
+// reference get_time_embedding (unet_base.py:7-30): [sin(t/f_k), cos(t/f_k)], f_k = 10000^(k/half)
+__global__ __launch_bounds__(256) void time_embedding_kernel(const int64_t* __restrict__ t, int nt, int D,
+                                                             float* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int half = D / 2;
+    if (i >= nt * half) return;
+    const int row = i / half, k = i - row * half;
+    const float f = powf(10000.0f, (float)k / (float)half);
+    const float a = (float)t[row] / f;
+    out[(long)row * D + k] = sinf(a);
+    out[(long)row * D + k + half] = cosf(a);
+}
+
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ src, int C, int HW, long total,
+                                                           float* __restrict__ dst, int ldc) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;  // total = B*HW*ldc
+    const long pix = i / ldc;
+    const int c = (int)(i - pix * ldc);
+    const long b = pix / HW;
+    const long p = pix - b * HW;
+    dst[i] = c < C ? src[(b * C + c) * HW + p] : 0.f;
+}
+
+inline unsigned blocks_for(long n, int per) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+extern "C" int wc_conv_wgrad(const wc_wgrad_args* a, float* part, int splits, void* stream) {
+    if (!a || !a->g || !part || a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src) return WC_E_ARG;
+    if (a->M <= 0 || a->M % 4 || a->ldg % 4 || s0.C <= 0 || s0.C % 4 || s0.ldc % 4) return WC_E_SHAPE;
+    if (s0.ntaps < 1 || s0.ntaps > WC_MAX_TAPS || splits < 1 || s0.sy < 1 || s0.sx < 1) return WC_E_SHAPE;
+    if (a->B < 1 || a->Hm < 1 || a->Wm < 1) return WC_E_SHAPE;
+    if ((s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
+    if (((reinterpret_cast<uintptr_t>(a->g) | reinterpret_cast<uintptr_t>(s0.src)) & 15) != 0) return WC_E_SHAPE;
+    const long P = (long)a->B * a->Hm * a->Wm;
+    if (P <= 0 || (long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31) || P * a->ldg * 4 >= (1L << 31))
+        return WC_E_SHAPE;
+    WgDev d{};
+    d.g = a->g; d.M = a->M; d.ldg = a->ldg;
+    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.H0 = s0.H; d.W0 = s0.W; d.sy = s0.sy; d.sx = s0.sx;
+    d.ntaps = s0.ntaps;
+    for (int t = 0; t < s0.ntaps; ++t) { d.dy[t] = s0.dy[t]; d.dx[t] = s0.dx[t]; }
+    d.scale = s0.scale; d.shift = s0.shift;
+    d.K0 = s0.ntaps * s0.C;
+    d.Kc = d.K0;
+    if (a->nseg == 2) {
+        const wc_conv_seg& s1 = a->seg[1];
+        if (!s1.src || s1.scale) return WC_E_ARG;
+        if (s1.C <= 0 || s1.C % 4 || s1.ldc % 4 || (reinterpret_cast<uintptr_t>(s1.src) & 15) != 0) return WC_E_SHAPE;
+        if (s1.ntaps != 1 || s1.dy[0] != 0 || s1.dx[0] != 0) return WC_E_SHAPE;
+        // the 1x1 residual segment is read at the pixel itself (stride 1, the gradient's grid)
+        if (s0.sy != 1 || s0.sx != 1 || s1.sy != 1 || s1.sx != 1 || s1.H != a->Hm || s1.W != a->Wm)
+            return WC_E_SHAPE;
+        if ((long)a->B * s1.H * s1.W * s1.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+        d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc; d.H1 = s1.H; d.W1 = s1.W;
+        d.Kc += s1.C;
+    }
+    d.Hm = a->Hm; d.Wm = a->Wm; d.P = P;
+    const bool narrow = a->M <= 64;
+    const int BM = narrow ? 64 : 128, BN = narrow ? 256 : 128;
+    d.ntm = (a->M + BM - 1) / BM;
+    d.ntn = (d.Kc + BN - 1) / BN;
+    d.pps = ((P + splits - 1) / splits + WG_KP - 1) / WG_KP * WG_KP;
+    const long nsp = (P + d.pps - 1) / d.pps;
+    if (nsp != splits) return WC_E_SHAPE;  // the caller sizes part by wc_conv_wgrad_splits
+    d.part = part;
+    const long grid = (long)d.ntm * d.ntn * splits;
+    if (grid > (1L << 30)) return WC_E_SHAPE;
+    const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return narrow ? wgrad_dispatch<64, 256>(d, pro, (int)grid, s) : wgrad_dispatch<128, 128>(d, pro, (int)grid, s);
+}
+
+extern "C" int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks) {
+    const bool narrow = M <= 64;
+    const int BM = narrow ? 64 : 128, BN = narrow ? 256 : 128;
+    const long tiles = (long)((M + BM - 1) / BM) * ((Kc + BN - 1) / BN);
+    long sp = (target_blocks + tiles - 1) / tiles;
+    const long maxsp = (P + 255) / 256;  // at least 8 K-steps per split
+    if (sp > maxsp) sp = maxsp;
+    if (sp < 1) sp = 1;
+    // the kernel's pixels-per-split rounding may need fewer splits to cover P
+    const long pps = ((P + sp - 1) / sp + WG_KP - 1) / WG_KP * WG_KP;
+    return (int)((P + pps - 1) / pps);
+}
+
+extern "C" int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,
+                               int64_t sM0, int64_t sC0, int64_t sT0, float* dw1, int64_t sM1, int accumulate,
+                               void* stream) {
+    if (!part || !dw0 || splits < 1 || M <= 0 || Kc <= 0 || K0 <= 0 || C0 <= 0 || K0 % C0 || K0 > Kc) return WC_E_ARG;
+    if (Kc > K0 && !dw1) return WC_E_ARG;
+    const long n = (long)M * Kc;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       part, splits, M, Kc, K0, C0, Cw, dw0, (long)sM0, (long)sC0, (long)sT0, dw1, (long)sM1, accumulate);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+static int gnb_nq(int C) {
+    const int q = C / 4;
+    const int nq = q < 64 ? q : 64;
+    if (C % 4 || nq < 1 || GB_THREADS % nq || q % nq) return -1;
+    return nq;
+}
+
+extern "C" int wc_gn_bwd_splits(int B, int HW) {
+    int sp = 1024 / (B < 1 ? 1 : B);
+    const int maxsp = HW / 16 < 1 ? 1 : HW / 16;
+    sp = sp > maxsp ? maxsp : sp;
+    sp = sp > 256 ? 256 : sp;
+    return sp < 1 ? 1 : sp;
+}
+
+extern "C" int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
+                                const float* gamma, const float* beta, int silu, int B, int HW, int C, int splits,
+                                float* part, void* stream) {
+    if (!dz || !part || (x && (!sc0 || !sh0))) return WC_E_ARG;
+    const int nq = gnb_nq(C);
+    if (nq < 0 || ldz % 4 || (x && ldx % 4) || splits < 1 || B < 1 || HW < 1) return WC_E_SHAPE;
+    const int pps = (HW + splits - 1) / splits;
+    const long grid = (long)B * splits * (C / 4 / nq);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!x)
+        hipLaunchKernelGGL((gnb_reduce_kernel<false, false>), dim3((unsigned)grid), dim3(GB_THREADS), 0, s, dz, ldz, x,
+                           ldx, sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part);
+    else if (silu)
+        hipLaunchKernelGGL((gnb_reduce_kernel<true, true>), dim3((unsigned)grid), dim3(GB_THREADS), 0, s, dz, ldz, x, ldx,
+                           sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part);
+    else
+        hipLaunchKernelGGL((gnb_reduce_kernel<true, false>), dim3((unsigned)grid), dim3(GB_THREADS), 0, s, dz, ldz, x,
+                           ldx, sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, int HW, const float* sc0,
+                                  const float* gamma, float* sums, float* coef, void* stream) {
+    if (!part || !sums || (coef && !sc0)) return WC_E_ARG;
+    if (C < 1 || (coef && (groups < 1 || groups > GB_THREADS || C % groups))) return WC_E_SHAPE;
+    const size_t lds = (size_t)(2 * C + 2 * (groups > 0 ? groups : 1)) * sizeof(float);
+    if (lds > 64 * 1024) return WC_E_SHAPE;
+    hipLaunchKernelGGL(gnb_finalize_kernel, dim3(B), dim3(GB_THREADS), lds, reinterpret_cast<hipStream_t>(stream), part,
+                       splits, C, groups, HW, sc0, gamma, sums, coef);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_bsum(const float* sums, int B, int C, int idx, float* out, int accumulate, void* stream) {
+    if (!sums || !out || idx < 0 || idx > 1) return WC_E_ARG;
+    hipLaunchKernelGGL(bsum_kernel, dim3(blocks_for(C, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), sums,
+                       B, C, idx, out, accumulate);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_gn_bwd_apply(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
+                               const float* gamma, const float* beta, int silu, const float* coef, int B, int HW, int C,
+                               float* dx, int lddx, int accumulate, void* stream) {
+    if (!dz || !x || !sc0 || !sh0 || !coef || !dx) return WC_E_ARG;
+    if (C % 4 || ldz % 4 || ldx % 4 || lddx % 4) return WC_E_SHAPE;
+    if (((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx)) & 15) != 0)
+        return WC_E_SHAPE;
+    const long n4 = (long)B * HW * (C / 4);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 g(blocks_for(n4, 256));
+#define WC_GNB_APPLY(S, A) \
+    hipLaunchKernelGGL((gnb_apply_kernel<S, A>), g, dim3(256), 0, s, dz, ldz, x, ldx, sc0, sh0, gamma, beta, coef, dx, lddx, n4, HW, C)
+    if (silu) {
+        if (accumulate) WC_GNB_APPLY(true, true); else WC_GNB_APPLY(true, false);
+    } else {
+        if (accumulate) WC_GNB_APPLY(false, true); else WC_GNB_APPLY(false, false);
+    }
+#undef WC_GNB_APPLY
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_gemm_small(int M, int N, int K, const float* A, int64_t sam, int64_t sak, const float* Bm, int64_t sbk,
+                             int64_t sbn, float* Cm, int64_t ldc, float alpha, float beta, void* stream) {
+    if (!A || !Bm || !Cm) return WC_E_ARG;
+    if (M <= 0 || N <= 0 || K <= 0) return WC_E_SHAPE;
+    hipLaunchKernelGGL(gemm_small_kernel, dim3(blocks_for((long)M * N, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), M, N, K, A, (long)sam, (long)sak, Bm, (long)sbk,
+                       (long)sbn, Cm, (long)ldc, alpha, beta);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_silu(const float* y, const float* dz, float* out, int64_t n, int mode, void* stream) {
+    if (!y || !out || (mode == 1 && !dz) || mode < 0 || mode > 1) return WC_E_ARG;
+    if (n <= 0) return WC_E_SHAPE;
+    hipLaunchKernelGGL(silu_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), y, dz,
+                       out, (long)n, mode);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_colsum(const float* X, int R, int N, int64_t ldx, float* out, int accumulate, void* stream) {
+    if (!X || !out) return WC_E_ARG;
+    if (R <= 0 || N <= 0) return WC_E_SHAPE;
+    hipLaunchKernelGGL(colsum_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), X, R,
+                       N, (long)ldx, out, accumulate);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_time_embedding(const int64_t* t, int nt, int D, float* out, void* stream) {
+    if (!t || !out) return WC_E_ARG;
+    if (nt <= 0 || D <= 0 || D % 2) return WC_E_SHAPE;
+    hipLaunchKernelGGL(time_embedding_kernel, dim3(blocks_for((long)nt * (D / 2), 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), t, nt, D, out);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_nchw_to_nhwc(const float* src, int B, int C, int H, int W, float* dst, int ldc, void* stream) {
+    if (!src || !dst) return WC_E_ARG;
+    if (B <= 0 || C <= 0 || ldc < C || H <= 0 || W <= 0) return WC_E_SHAPE;
+    const long total = (long)B * H * W * ldc;
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(blocks_for(total, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), src, C, H * W, total, dst, ldc);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}

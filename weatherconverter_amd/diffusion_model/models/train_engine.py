@@ -1,0 +1,465 @@
+"""TrainEngine: the reference ``Unet`` training step's forward (with saved activations) and its
+backward, as gfx950 HIP kernels — ``loss.backward()`` of ``train_ddpm.py:106-110``.
+
+Forward (same layout as ``UnetEngine``: NHWC fp32 activations, one skip buffer ``U[i]`` per level so
+the up path's ``torch.cat`` is free) records a tape; every GroupNorm keeps both its affine
+(scale, shift) and the plain normalisation (rstd, -mean*rstd) so the backward recomputes
+SiLU(GN(x)) from the stored pre-norm tensor instead of keeping the activation.  Attention keeps its
+pre-residual input, q/k/v, its output and the softmax log-sum-exp.
+
+Backward, per layer type (reference modules of unet_base.py):
+  Conv2d 3x3 / 1x1 / 4x4-s2, ConvTranspose2d 4x4-s2, in/out projections
+      data gradient   the forward implicit-GEMM kernels on re-packed weights: a 3x3 conv's is the
+                      3x3 conv of dY with W flipped and transposed; a 4x4/s2 conv's is the
+                      transposed conv of dY (four parity sub-convs); a transposed conv's is the
+                      4x4/s2 conv of dY with its own weight; a linear layer's is dY W.
+      weight gradient wc_conv_wgrad (fp32-MFMA GEMM over the pixels, input re-read through the
+                      forward's taps and GN prologue), scattered into the parameter's layout.
+      bias            per-(b, c) pixel sums, summed over b in a fixed order.
+  GroupNorm(+SiLU)    wc_gn_bwd_* (dx, dgamma, dbeta).
+  attention core      wc_attention_bwd (dq, dk, dv from lse; no N x N matrix).
+  time embedding MLP  small GEMM / SiLU kernels (B x 128).
+Arithmetic: the forward and data-gradient convs on bf16x6 (exact 3-piece bf16 split, fp32
+accumulation) where channels allow (else fp32 MFMA), weight gradients and attention on fp32 MFMA:
+fp32-class gradients, checked against PyTorch autograd of the reference restatement.
+Every gradient buffer is written in a fixed order: results are deterministic run to run.
+"""
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ... import kernels as K
+from ...kernels import Seg, View
+from .engine import TAPS1, TAPS3, TAPS4S2, pack_conv, pack_convT
+
+_PARITIES = ((0, 0), (0, 1), (1, 0), (1, 1))
+
+
+class TrainEngine:
+
+    def __init__(self, model, precision: Optional[str] = None):
+        params = list(model.parameters())
+        if not params or not params[0].is_cuda:
+            raise RuntimeError('weatherconverter_amd.Unet trains on the GPU only (HIP kernels, no CPU fallback)')
+        K._native.load()
+        self.model = model
+        self.device = params[0].device
+        p = precision or getattr(model, 'conv_precision', None) or 'bf16x6'
+        # f16x3 needs range bounds that gradients do not have: split-precision training runs bf16x6
+        self.precision = 'fp32' if p == 'fp32' else 'bf16x6'
+        self.tape: List[tuple] = []
+
+    # ------------------------------------------------------------------ packing (per step)
+    def _pk(self, w2d: torch.Tensor, C0: int, ntaps: int, C1: int = 0):
+        w2d = w2d.contiguous().float()
+        x6 = None
+        if self.precision == 'bf16x6' and C0 % 16 == 0 and C1 % 16 == 0:
+            x6 = K.pack_x6(w2d, C0, C1, ntaps=ntaps, order='natural')
+        elif C0 % 32 or C1 % 32:
+            raise RuntimeError(f'fp32 implicit GEMM needs channel counts % 32 (got {C0}, {C1})')
+        return (w2d, x6)
+
+    def _conv(self, segs, pk, bias, out: Optional[View], H: int, W: int, **kw):
+        w, x6 = pk
+        if x6 is not None:
+            K.conv_igemm_x6(segs, x6, bias, out, Hm=H, Wm=W, **kw)
+        else:
+            K.conv_igemm(segs, w, bias, out, Hm=H, Wm=W, **kw)
+
+    def _pack_res(self, blk, i: int):
+        f, s, r = blk.resnet_conv_first[i], blk.resnet_conv_second[i], blk.residual_input_conv[i]
+        w1, w2, wr = f[2].weight.detach(), s[2].weight.detach(), r.weight.detach()
+        ci, co = w1.shape[1], w1.shape[0]
+        wr2 = wr.reshape(co, ci)
+        return dict(
+            ci=ci, co=co, gn1=f[0], conv1=f[2], gn2=s[0], conv2=s[2], resc=r, temb=blk.t_emb_layers[i][1],
+            pk1=self._pk(pack_conv(w1), ci, 9),
+            pk2=self._pk(torch.cat([pack_conv(w2), wr2], 1), co, 9, ci),
+            b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
+            pk1T=self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9),
+            pk2T=self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9),
+            pkrT=self._pk(wr2.t(), co, 1))
+
+    def _pack_attn(self, blk, i: int):
+        mha, gn = blk.attentions[i], blk.attention_norms[i]
+        C = mha.embed_dim
+        w_in, w_out = mha.in_proj_weight.detach(), mha.out_proj.weight.detach()
+        return dict(C=C, heads=mha.num_heads, gn=gn, mha=mha, pk_in=self._pk(w_in, C, 1), pk_out=self._pk(w_out, C, 1),
+                    pk_inT=self._pk(w_in.t(), 3 * C, 1), pk_outT=self._pk(w_out.t(), C, 1))
+
+    def _pack(self):
+        m = self.model
+        self.P = 0
+
+        def stage(blk, n_res):
+            res = []
+            for i in range(n_res):
+                rp = self._pack_res(blk, i)
+                rp['off'] = self.P
+                self.P += rp['co']
+                res.append(rp)
+            att = [self._pack_attn(blk, i) for i in range(len(blk.attentions))] if blk.use_attn else []
+            return res, att
+
+        with torch.no_grad():
+            self.downs = [stage(blk, blk.num_layers) for blk in m.downs]
+            self.mids = [stage(blk, blk.num_layers + 1) for blk in m.mids]
+            self.ups = [stage(blk, blk.num_layers) for blk in m.ups]
+            self.down_pk = []
+            for blk in m.downs:
+                if blk.down_sample:
+                    w = blk.down_sample_conv.weight.detach()
+                    ci = w.shape[1]
+                    parts = [pack_convT(w, py, px) for py, px in _PARITIES]  # dgrad: ConvT of dY (in = Co)
+                    self.down_pk.append(dict(mod=blk.down_sample_conv, pk=self._pk(pack_conv(w), ci, 16),
+                                             dT=[(taps, self._pk(wp, w.shape[0], len(taps))) for taps, wp in parts]))
+                else:
+                    self.down_pk.append(None)
+            self.up_pk = []
+            for blk in m.ups:
+                if blk.up_sample:
+                    wt = blk.up_sample_conv.weight.detach()  # [Cin][Cout][4][4]
+                    ci = wt.shape[0]
+                    parts = [pack_convT(wt, py, px) for py, px in _PARITIES]
+                    self.up_pk.append(dict(mod=blk.up_sample_conv,
+                                           fw=[(taps, self._pk(wp, ci, len(taps))) for taps, wp in parts],
+                                           dT=self._pk(pack_conv(wt), wt.shape[1], 16)))
+                else:
+                    self.up_pk.append(None)
+            tp = m.t_proj
+            self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
+                          tp[2].weight.detach().float().contiguous(), tp[2].bias.detach().float().contiguous()]
+            rows = [rp for st in self.downs + self.mids + self.ups for rp in st[0]]
+            self.temb_w = torch.cat([rp['temb'].weight.detach().float() for rp in rows], 0).contiguous()
+            self.temb_b = torch.cat([rp['temb'].bias.detach().float() for rp in rows], 0).contiguous()
+            self.res_rows = rows
+            co = m.conv_out.weight.detach()  # [NO][C][3][3]
+            NO, C = co.shape[0], co.shape[1]
+            self.head_pk = self._pk(pack_conv(co), C, 9)
+            wt = torch.zeros((C, 32, 3, 3), dtype=torch.float32, device=self.device)
+            wt[:, :NO] = co.flip([2, 3]).transpose(0, 1)
+            self.head_T = self._pk(pack_conv(wt), 32, 9)  # dgrad over the 32-channel padded loss gradient
+
+    # ------------------------------------------------------------------ helpers
+    def _new(self, B, H, W, C) -> torch.Tensor:
+        return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
+
+    def _grad(self, v: View) -> View:
+        """The gradient view of a forward view (zero-initialised tensors, allocated on first use)."""
+        key = id(v.t)
+        if key not in self.gmap:
+            self.gmap[key] = (torch.zeros_like(v.t), 0)
+        g, off = self.gmap[key]
+        return View(g, v.c0 + off, v.C)
+
+    def _alias_grad(self, t: torch.Tensor, v: View):
+        """The full tensor t's gradient IS the gradient of view v (t feeds v through an identity path
+        and everything else adds into it afterwards in backward order)."""
+        g = self._grad(v)
+        self.gmap[id(t)] = (g.t, g.c0)
+        self.keep.append(t)
+
+    def _pgrad(self, p: torch.nn.Parameter) -> torch.Tensor:
+        g = self.pgrads.get(id(p))
+        if g is None:
+            g = torch.zeros_like(p, dtype=torch.float32)
+            self.pgrads[id(p)] = g
+        return g
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, t) -> torch.Tensor:
+        m = self.model
+        mc = m.model_config
+        self._pack()
+        self.tape = []
+        x = x.to(device=self.device, dtype=torch.float32).contiguous()
+        B, _, S, S2 = x.shape
+        tt = torch.as_tensor(t).long().reshape(-1).to(self.device)
+        if tt.numel() == 1 and B > 1:
+            tt = tt.expand(B).contiguous()
+        if tt.numel() != B:
+            raise RuntimeError(f'timestep tensor has {tt.numel()} entries for a batch of {B}')
+        self.tt = tt
+        temb = K.temb(tt, *self.tproj, self.temb_w, self.temb_b)  # (B, P)
+        self.x = x
+        dc = m.down_channels
+        L = len(dc) - 1
+        sizes = [(S, S2)]
+        for i in range(L):
+            h, w = sizes[-1]
+            sizes.append((h // 2, w // 2) if m.down_sample[i] else (h, w))
+        U = [self._new(B, sizes[i][0], sizes[i][1], 2 * dc[i]) for i in range(L)]
+        self.U = U
+        cur = View(U[0], dc[0], dc[0])
+        K.conv_in(x, m.conv_in.weight.detach().float().contiguous(), m.conv_in.bias.detach().float().contiguous(), cur)
+        self.tape.append(('conv_in', cur))
+
+        def block(X: View, tgt: View, rp, att) -> View:
+            if att is None:
+                self._res_fwd(X, tgt, rp, temb)
+            else:
+                ypre = View.full(self._new(B, X.H, X.W, rp['co']))
+                self._res_fwd(X, ypre, rp, temb)
+                self._attn_fwd(ypre, tgt, att)
+            return tgt
+
+        for i in range(L):
+            res, att = self.downs[i]
+            H, W = sizes[i]
+            final = View(U[i + 1], dc[i + 1], dc[i + 1]) if i < L - 1 else View.full(
+                self._new(B, sizes[i + 1][0], sizes[i + 1][1], dc[i + 1]))
+            for li, rp in enumerate(res):
+                last = li == len(res) - 1
+                tgt = final if (last and self.down_pk[i] is None) else View.full(self._new(B, H, W, rp['co']))
+                cur = block(cur, tgt, rp, att[li] if att else None)
+            if self.down_pk[i] is not None:
+                dp = self.down_pk[i]
+                self._conv([Seg(cur, TAPS4S2, stride=2)], dp['pk'], dp['mod'].bias.detach().float().contiguous(), final,
+                           sizes[i + 1][0], sizes[i + 1][1])
+                self.tape.append(('down', cur, final, dp))
+                cur = final
+
+        for j, (res, att) in enumerate(self.mids):
+            last_mid = j == len(self.mids) - 1
+            H, W = cur.H, cur.W
+            for li, rp in enumerate(res):
+                if last_mid and li == len(res) - 1 and self.up_pk[0] is None:
+                    tgt = View(U[L - 1], 0, dc[L - 1])
+                else:
+                    tgt = View.full(self._new(B, H, W, rp['co']))
+                self._res_fwd(cur, tgt, rp, temb)
+                cur = tgt
+                if li < len(att):
+                    nxt = View.full(self._new(B, H, W, rp['co']))
+                    self._attn_fwd(cur, nxt, att[li])
+                    cur = nxt
+
+        for k, (res, att) in enumerate(self.ups):
+            i = L - 1 - k
+            H, W = sizes[i]
+            if self.up_pk[k] is not None:
+                up = self.up_pk[k]
+                dst = View(U[i], 0, dc[i])
+                b = up['mod'].bias.detach().float().contiguous()
+                for (py, px), (taps, pk) in zip(_PARITIES, up['fw']):
+                    self._conv([Seg(cur, taps)], pk, b, dst, cur.H, cur.W, out_map=(2, 2, py, px))
+                self.tape.append(('up', cur, dst, up))
+            else:
+                assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
+            cur = View.full(U[i])
+            next_in_place = i > 0 and self.up_pk[k + 1] is None
+            for li, rp in enumerate(res):
+                last = li == len(res) - 1
+                tgt = View(U[i - 1], 0, dc[i - 1]) if (last and next_in_place) else View.full(
+                    self._new(B, H, W, rp['co']))
+                cur = block(cur, tgt, rp, att[li] if att else None)
+
+        # head: GN -> SiLU -> conv_out, NCHW output
+        gn = m.norm_out
+        sc, sh, a0, o0 = K.gn_stats_pair(cur, gn.weight.detach().float(), gn.bias.detach().float())
+        out = torch.empty((B, mc.im_channels, S, S2), dtype=torch.float32, device=self.device)
+        self._conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.head_pk,
+                   m.conv_out.bias.detach().float().contiguous(), None, S, S2, out_nchw=out)
+        self.tape.append(('head', cur, (sc, sh, a0, o0)))
+        return out
+
+    def _res_fwd(self, X: View, Y: View, rp, temb: torch.Tensor):
+        B, H, W = X.B, X.H, X.W
+        g1, g2 = rp['gn1'], rp['gn2']
+        st1 = K.gn_stats_pair(X, g1.weight.detach().float(), g1.bias.detach().float())
+        h = View.full(self._new(B, H, W, rp['co']))
+        self._conv([Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], rp['pk1'],
+                   rp['conv1'].bias.detach().float().contiguous(), h, H, W, temb=temb[:, rp['off']:],
+                   temb_ld=temb.shape[1])
+        st2 = K.gn_stats_pair(h, g2.weight.detach().float(), g2.bias.detach().float())
+        self._conv([Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * rp['co'])],
+                   rp['pk2'], rp['b2'], Y, H, W)
+        self.tape.append(('res', X, h, Y, rp, st1, st2))
+
+    def _attn_fwd(self, Ypre: View, Yout: View, ap):
+        B, H, W, C = Ypre.B, Ypre.H, Ypre.W, Ypre.C
+        N = H * W
+        gn, mha = ap['gn'], ap['mha']
+        st = K.gn_stats_pair(Ypre, gn.weight.detach().float(), gn.bias.detach().float())
+        qkv = self._new(B, H, W, 3 * C)
+        self._conv([Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], ap['pk_in'],
+                   mha.in_proj_bias.detach().float().contiguous(), View.full(qkv), H, W)
+        o = self._new(B, H, W, C)
+        lse = torch.empty((B, ap['heads'], N), dtype=torch.float32, device=self.device)
+        K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'])
+        self._conv([Seg(View.full(o), TAPS1)], ap['pk_out'], mha.out_proj.bias.detach().float().contiguous(), Yout, H,
+                   W, res=Ypre)
+        self.tape.append(('attn', Ypre, Yout, qkv, o, lse, st, ap))
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, gout: torch.Tensor) -> Dict[int, torch.Tensor]:
+        """Gradients of every parameter given d loss / d output (B, C, S, S); returns {id(param): grad}."""
+        m = self.model
+        self.gmap: Dict[int, Tuple[torch.Tensor, int]] = {}
+        self.pgrads: Dict[int, torch.Tensor] = {}
+        self.keep = []
+        B = gout.shape[0]
+        self.dproj = torch.zeros((B, self.P), dtype=torch.float32, device=self.device)
+        gout = gout.to(self.device, torch.float32).contiguous()
+        for rec in reversed(self.tape):
+            getattr(self, '_bwd_' + rec[0])(rec, gout)
+        self._temb_bwd()
+        self.tape = []
+        self.gmap = {}
+        self.keep = []
+        return self.pgrads
+
+    def _bias_grad(self, g: View, *params):
+        sums = K.channel_sums(g)
+        for p in params:
+            K.bsum(sums, 0, self._pgrad(p), accumulate=True)
+        return sums
+
+    def _bwd_head(self, rec, gout):
+        m = self.model
+        _, cur, (sc, sh, a0, o0) = rec
+        B, NO, S, S2 = gout.shape
+        C = cur.C
+        g32 = K.nchw_to_nhwc(gout, 32)
+        g4 = View(g32, 0, 4)
+        wtmp = torch.zeros((4, C, 3, 3), dtype=torch.float32, device=self.device)
+        K.conv_wgrad(g4, [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], wtmp, (C * 9, 9, 1))
+        self._pgrad(m.conv_out.weight).copy_(wtmp[:NO])
+        btmp = torch.zeros(4, dtype=torch.float32, device=self.device)
+        K.bsum(K.channel_sums(g4), 0, btmp)
+        self._pgrad(m.conv_out.bias).copy_(btmp[:NO])
+        dz = View.full(self._new(B, S, S2, C))
+        self._conv([Seg(View.full(g32), TAPS3)], self.head_T, None, dz, S, S2)
+        gn = m.norm_out
+        K.gn_backward(dz, cur, a0, o0, gn.weight.detach().float(), gn.bias.detach().float(), True, self._grad(cur),
+                      dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias))
+
+    def _bwd_res(self, rec, gout):
+        _, X, h, Y, rp, st1, st2 = rec
+        B, H, W = X.B, X.H, X.W
+        ci, co = rp['ci'], rp['co']
+        gY = self._grad(Y)
+        gX = self._grad(X)
+        self._bias_grad(gY, rp['conv2'].bias, rp['resc'].bias)
+        K.conv_wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
+                     self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci)
+        dz2 = View.full(self._new(B, H, W, co))
+        self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
+        self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX)
+        g2 = rp['gn2']
+        dh = View.full(self._new(B, H, W, co))
+        K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
+                      dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False)
+        sums = self._bias_grad(dh, rp['conv1'].bias)
+        self.dproj[:, rp['off']:rp['off'] + co].copy_(sums[:, :, 0])
+        K.conv_wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
+                     (ci * 9, 9, 1))
+        dz1 = View.full(self._new(B, H, W, ci))
+        self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
+        g1 = rp['gn1']
+        K.gn_backward(dz1, X, st1[2], st1[3], g1.weight.detach().float(), g1.bias.detach().float(), True, gX,
+                      dgamma=self._pgrad(g1.weight), dbeta=self._pgrad(g1.bias), accumulate=True)
+
+    def _bwd_attn(self, rec, gout):
+        _, Ypre, Yout, qkv, o, lse, st, ap = rec
+        B, H, W, C = Ypre.B, Ypre.H, Ypre.W, Ypre.C
+        N = H * W
+        mha, gn = ap['mha'], ap['gn']
+        gY = self._grad(Yout)
+        self._bias_grad(gY, mha.out_proj.bias)
+        K.conv_wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0))
+        do = self._new(B, H, W, C)
+        self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W)
+        dqkv = self._new(B, H, W, 3 * C)
+        K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C), B,
+                        N, C, ap['heads'])
+        gq = View.full(dqkv)
+        self._bias_grad(gq, mha.in_proj_bias)
+        K.conv_wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),
+                     (C, 1, 0))
+        da = View.full(self._new(B, H, W, C))
+        self._conv([Seg(gq, TAPS1)], ap['pk_inT'], None, da, H, W)
+        # Yout = Ypre + out_proj(...): Ypre's gradient is Yout's plus the GroupNorm path
+        self._alias_grad(Ypre.t, Yout)
+        K.gn_backward(da, Ypre, st[2], st[3], gn.weight.detach().float(), gn.bias.detach().float(), False,
+                      self._grad(Ypre), dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), accumulate=True)
+
+    def _bwd_down(self, rec, gout):
+        _, cur, final, dp = rec
+        gF = self._grad(final)
+        gc = self._grad(cur)
+        w = dp['mod'].weight
+        self._bias_grad(gF, dp['mod'].bias)
+        K.conv_wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1))
+        for (py, px), (taps, pk) in zip(_PARITIES, dp['dT']):
+            self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=gc)
+
+    def _bwd_up(self, rec, gout):
+        _, cur, dst, up = rec
+        gD = self._grad(dst)
+        gc = self._grad(cur)
+        wt = up['mod'].weight  # [Cin][Cout][4][4]
+        self._bias_grad(gD, up['mod'].bias)
+        # dW[ci][co][ky][kx] = sum_pixels x[ci] * dY[co] at (2y - 1 + ky, 2x - 1 + kx): the 4x4/s2 tap
+        # grid over dY with x in the gradient role
+        K.conv_wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1))
+        self._conv([Seg(gD, TAPS4S2, stride=2)], up['dT'], None, gc, cur.H, cur.W, res=gc)
+
+    def _bwd_conv_in(self, rec, gout):
+        m = self.model
+        _, cur = rec
+        g = self._grad(cur)
+        self._bias_grad(g, m.conv_in.bias)
+        xn = K.nchw_to_nhwc(self.x, 4)
+        w = m.conv_in.weight
+        K.conv_wgrad(g, [Seg(View.full(xn), TAPS3)], self._pgrad(w), (w.shape[1] * 9, 9, 1), Cw=w.shape[1])
+
+    def _temb_bwd(self):
+        """t_proj (Linear, SiLU, Linear) and the t_emb_layers (SiLU, Linear) backward (B x 128)."""
+        m = self.model
+        w1, b1, w2, b2 = self.tproj
+        D = w1.shape[0]
+        B, P = self.dproj.shape
+        e = K.time_embedding(self.tt, D)
+        a1 = b1.expand(B, D).contiguous()
+        K.gemm_small(B, D, D, e, (D, 1), w1, (1, D), a1, D, beta=1.0)
+        h1 = K.silu_map(a1)
+        a2 = b2.expand(B, D).contiguous()
+        K.gemm_small(B, D, D, h1, (D, 1), w2, (1, D), a2, D, beta=1.0)
+        s = K.silu_map(a2)
+        dp = self.dproj
+        for rp in self.res_rows:
+            off, co = rp['off'], rp['co']
+            lin = rp['temb']
+            K.gemm_small(co, D, B, dp, (1, P), s, (D, 1), self._pgrad(lin.weight), D, offs=(off, 0, 0))
+            K.colsum(dp, self._pgrad(lin.bias), col0=off, ncol=co)
+        ds = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        K.gemm_small(B, D, P, dp, (P, 1), self.temb_w, (D, 1), ds, D)
+        da2 = K.silu_map(a2, ds)
+        tp = m.t_proj
+        K.gemm_small(D, D, B, da2, (1, D), h1, (D, 1), self._pgrad(tp[2].weight), D)
+        K.colsum(da2, self._pgrad(tp[2].bias))
+        dh1 = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        K.gemm_small(B, D, D, da2, (D, 1), w2, (D, 1), dh1, D)
+        da1 = K.silu_map(a1, dh1)
+        K.gemm_small(D, D, B, da1, (1, D), e, (D, 1), self._pgrad(tp[0].weight), D)
+        K.colsum(da1, self._pgrad(tp[0].bias))
+
+
+class UnetTrainFunction(torch.autograd.Function):
+    """Unet.forward in training mode: the HIP forward records its tape, and autograd's backward runs
+    TrainEngine.backward, returning one gradient per parameter (so the reference's own
+    ``loss.backward(); optimizer.step()`` loop works unchanged)."""
+
+    @staticmethod
+    def forward(ctx, engine: TrainEngine, x: torch.Tensor, t, *params):
+        with torch.no_grad():
+            out = engine.forward(x, t)
+        ctx.engine = engine
+        ctx.param_ids = [id(p) for p in engine.model.parameters()]
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        grads = ctx.engine.backward(gout)
+        return (None, None, None) + tuple(grads.get(i) for i in ctx.param_ids)

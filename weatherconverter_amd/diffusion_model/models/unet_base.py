@@ -171,17 +171,27 @@ class Unet(nn.Module):
             raise ValueError(f'conv precision must be one of {kernels.CONV_PRECISIONS}')
         self.conv_precision = precision
         self._engine = None
+        self._train_engine = None
         return self
+
+    def train_engine(self):
+        from .train_engine import TrainEngine
+        if getattr(self, '_train_engine', None) is None:
+            self._train_engine = TrainEngine(self)
+        return self._train_engine
 
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
         if self.training and torch.is_grad_enabled():
-            raise RuntimeError('weatherconverter_amd.Unet implements the inference (denoising) path; '
-                               'the training backward is not implemented yet (SURVEY.md §8(f) #1)')
+            # training (train_ddpm.py:106-110): the HIP forward records its tape and loss.backward()
+            # runs the HIP backward (models/train_engine.py), one gradient per parameter
+            from .train_engine import UnetTrainFunction
+            return UnetTrainFunction.apply(self.train_engine(), x, t, *self.parameters())
         return self.engine().forward(x, t)
 
     def _apply(self, fn, *args, **kwargs):
         # device / dtype moves invalidate the packed GPU weights
         self._engine = None
+        self._train_engine = None
         return super()._apply(fn, *args, **kwargs)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):

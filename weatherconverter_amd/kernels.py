@@ -851,3 +851,193 @@ def noise_embed(noise: torch.Tensor, ang: torch.Tensor, out: View):
          'noise_embed shapes')
     _native.call('wc_noise_embed', noise.data_ptr(), ang.data_ptr(), K, out.ptr, out.ldc, out.B, out.H * out.W,
                  _stream())
+
+
+# ---- UNet backward (csrc/wc_backward.hip, csrc/wc_attention_bwd.hip) ----
+
+def _fill_seg(cs, s: Seg, B: int):
+    v = s.view
+    v.check()
+    _req(v.B == B, 'segment batch mismatch')
+    _req(len(s.taps) <= _native.MAX_TAPS, 'too many taps')
+    cs.src, cs.C, cs.ldc, cs.H, cs.W = v.ptr, v.C, v.ldc, v.H, v.W
+    cs.sy = cs.sx = s.stride
+    cs.ntaps = len(s.taps)
+    for j, (dy, dx) in enumerate(s.taps):
+        cs.dy[j], cs.dx[j] = dy, dx
+    if s.scale is not None:
+        _req(s.scale.shape == (B, v.C) and s.shift.shape == (B, v.C), 'GN affine shape')
+        cs.scale, cs.shift = s.scale.data_ptr(), s.shift.data_ptr()
+    cs.silu = int(s.silu)
+    cs.kbase = s.kbase
+
+
+def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, int, int], *, Cw: Optional[int] = None,
+               dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False):
+    """Weight gradient of a conv whose input segments are `segs` (as the forward read them, prologue
+    included) and whose output gradient is the view g (pixel grid = g's H x W): fp32-MFMA GEMM over
+    the pixels, split and reduced in a fixed order.  Column (tap t, channel c < Cw) of segment 0 is
+    written to dw0.flat[m*s0[0] + c*s0[1] + t*s0[2]], segment 1's columns to dw1.flat[m*s1 + c]."""
+    g.check()
+    _req(1 <= len(segs) <= 2, 'wgrad takes 1 or 2 segments')
+    _req(dw0.is_cuda and dw0.dtype == torch.float32 and dw0.is_contiguous(), 'dw0: contiguous fp32 device tensor')
+    a = _native.WgradArgs()
+    B = g.B
+    for i, s in enumerate(segs):
+        _fill_seg(a.seg[i], s, B)
+    a.nseg = len(segs)
+    a.g, a.M, a.ldg = g.ptr, g.C, g.ldc
+    a.B, a.Hm, a.Wm = B, g.H, g.W
+    C0, T = segs[0].view.C, len(segs[0].taps)
+    K0 = T * C0
+    C1 = segs[1].view.C if len(segs) == 2 else 0
+    Kc = K0 + C1
+    Cw = C0 if Cw is None else Cw
+    # the reduce kernel's writes must stay inside the destination tensors
+    _req((g.C - 1) * s0[0] + (Cw - 1) * s0[1] + (T - 1) * s0[2] < dw0.numel(), 'dw0 too small for its strides')
+    if C1:
+        _req(dw1 is not None and dw1.is_cuda and dw1.is_contiguous() and (g.C - 1) * s1 + C1 <= dw1.numel(),
+             'dw1: the residual segment gradient')
+    lib = _native.load()
+    P = B * g.H * g.W
+    splits = lib.wc_conv_wgrad_splits(g.C, Kc, P, 2048)
+    part = torch.empty(splits * g.C * Kc, dtype=torch.float32, device=g.t.device)
+    s = _stream()
+    _timed('conv_wgrad_kernel', 'wc_conv_wgrad', 2.0 * P * g.C * Kc, ctypes.byref(a), part.data_ptr(), splits, s)
+    _native.call('wc_wgrad_reduce', part.data_ptr(), splits, g.C, Kc, K0, C0, Cw, dw0.data_ptr(), s0[0], s0[1], s0[2],
+                 _ptr(dw1), s1, int(accumulate), s)
+
+
+def gn_stats_pair(v: View, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5, groups: int = 8):
+    """GroupNorm statistics of v once, finalized twice: (scale, shift) of the affine GN and
+    (sc0, sh0) = (rstd, -mean*rstd) of the plain normalisation (what the backward needs)."""
+    v.check()
+    B, HW, C = v.B, v.H * v.W, v.C
+    lib = _native.load()
+    splits = lib.wc_gn_num_splits(B, HW, C)
+    part = torch.empty((B, splits, groups, 2), dtype=torch.float32, device=v.t.device)
+    s = _stream()
+    _native.call('wc_gn_stats', v.ptr, B, HW, C, v.ldc, groups, part.data_ptr(), s)
+    out = [torch.empty((B, C), dtype=torch.float32, device=v.t.device) for _ in range(4)]
+    _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps, out[0].data_ptr(),
+                 out[1].data_ptr(), s)
+    _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, None, None, eps, out[2].data_ptr(),
+                 out[3].data_ptr(), s)
+    return tuple(out)
+
+
+def channel_sums(g: View) -> torch.Tensor:
+    """Per-(b, c) sums over pixels of view g -> float32 [B][C][2] (second entry 0), fixed order."""
+    g.check()
+    B, HW, C = g.B, g.H * g.W, g.C
+    lib = _native.load()
+    splits = lib.wc_gn_bwd_splits(B, HW)
+    part = torch.empty(B * splits * C * 2, dtype=torch.float32, device=g.t.device)
+    sums = torch.empty((B, C, 2), dtype=torch.float32, device=g.t.device)
+    s = _stream()
+    _native.call('wc_gn_bwd_reduce', g.ptr, g.ldc, None, 0, None, None, None, None, 0, B, HW, C, splits,
+                 part.data_ptr(), s)
+    _native.call('wc_gn_bwd_finalize', part.data_ptr(), B, splits, C, 0, HW, None, None, sums.data_ptr(), None, s)
+    return sums
+
+
+def bsum(sums: torch.Tensor, idx: int, out: torch.Tensor, accumulate: bool = False):
+    """out[c] (+)= sum_b sums[b][c][idx] (fixed order)."""
+    B, C, _ = sums.shape
+    _req(out.is_cuda and out.is_contiguous() and out.numel() == C, 'bsum output')
+    _native.call('wc_bsum', sums.data_ptr(), B, C, idx, out.data_ptr(), int(accumulate), _stream())
+
+
+def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+                silu: bool, dx: View, *, dgamma: Optional[torch.Tensor] = None, dbeta: Optional[torch.Tensor] = None,
+                accumulate: bool = True, groups: int = 8):
+    """Backward of SiLU(GroupNorm(x)) (silu) or GroupNorm(x): dx (+)= d/dx given dz = d/d output;
+    dgamma / dbeta (+)= their gradients."""
+    for v in (dz, x, dx):
+        v.check()
+    B, HW, C = x.B, x.H * x.W, x.C
+    _req(dz.C == C and dx.C == C and dz.B == B and dx.B == B, 'GN backward view shapes')
+    lib = _native.load()
+    splits = lib.wc_gn_bwd_splits(B, HW)
+    dev = x.t.device
+    part = torch.empty(B * splits * C * 2, dtype=torch.float32, device=dev)
+    sums = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
+    coef = torch.empty((B, C, 4), dtype=torch.float32, device=dev)
+    s = _stream()
+    _timed('gnb_reduce_kernel', 'wc_gn_bwd_reduce', 8.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc, sc0.data_ptr(),
+           sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), B, HW, C, splits, part.data_ptr(), s)
+    _native.call('wc_gn_bwd_finalize', part.data_ptr(), B, splits, C, groups, HW, sc0.data_ptr(), _ptr(gamma),
+                 sums.data_ptr(), coef.data_ptr(), s)
+    if dbeta is not None:
+        bsum(sums, 0, dbeta, accumulate=True)
+    if dgamma is not None:
+        bsum(sums, 1, dgamma, accumulate=True)
+    _timed('gnb_apply_kernel', 'wc_gn_bwd_apply', 16.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc, sc0.data_ptr(),
+           sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), coef.data_ptr(), B, HW, C, dx.ptr, dx.ldc,
+           int(accumulate), s)
+
+
+def attention_fwd_lse(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, B: int, N: int, C: int, heads: int):
+    """fp32-MFMA attention (wc_attention_fwd) that also writes lse[b][h][q] (log2 domain) for the backward."""
+    _req(qkv.shape == (B * N, 3 * C) and qkv.is_contiguous() and out.shape == (B * N, C) and out.is_contiguous(),
+         'attention shapes')
+    _req(lse.is_contiguous() and lse.numel() == B * heads * N, 'lse: B*heads*N floats')
+    d = C // heads
+    _timed(f'attention_kernel<{d}> (lse)', 'wc_attention_fwd_lse', 4.0 * B * N * N * C, qkv.data_ptr(), 3 * C,
+           out.data_ptr(), C, lse.data_ptr(), B, N, C, heads, float(d**-0.5), _stream())
+
+
+def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, dqkv: torch.Tensor,
+                  B: int, N: int, C: int, heads: int):
+    """d qkv (same [q | k | v] rows as qkv) of softmax(Q K^T / sqrt(d)) V from the forward's output and lse."""
+    for t_, w in ((qkv, 3 * C), (out, C), (dout, C), (dqkv, 3 * C)):
+        _req(t_.is_cuda and t_.dtype == torch.float32 and t_.is_contiguous() and t_.numel() == B * N * w,
+             'attention backward operands')
+    d = C // heads
+    dv = torch.empty(B * heads * N, dtype=torch.float32, device=qkv.device)
+    _timed(f'attention_bwd<{d}>', 'wc_attention_bwd', 10.0 * B * N * N * C, qkv.data_ptr(), 3 * C, out.data_ptr(), C,
+           dout.data_ptr(), C, lse.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), 3 * C, B, N, C, heads, float(d**-0.5),
+           _stream())
+
+
+def gemm_small(M: int, N: int, K: int, A: torch.Tensor, sa: Tuple[int, int], Bm: torch.Tensor, sb: Tuple[int, int],
+               Cm: torch.Tensor, ldc: int, alpha: float = 1.0, beta: float = 0.0, offs: Tuple[int, int, int] = (0, 0, 0)):
+    """C[m][n] = alpha*sum_k A[m*sa0 + k*sa1] B[k*sb0 + n*sb1] + beta*C (small matrices; element offsets offs)."""
+    for t_ in (A, Bm, Cm):
+        _req(t_.is_cuda and t_.dtype == torch.float32 and t_.is_contiguous(), 'gemm_small operands')
+    _native.call('wc_gemm_small', M, N, K, A.data_ptr() + 4 * offs[0], sa[0], sa[1], Bm.data_ptr() + 4 * offs[1], sb[0],
+                 sb[1], Cm.data_ptr() + 4 * offs[2], ldc, alpha, beta, _stream())
+
+
+def silu_map(y: torch.Tensor, dz: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(y), or dz * silu'(y) when dz is given."""
+    _req(y.is_cuda and y.dtype == torch.float32 and y.is_contiguous(), 'silu operand')
+    out = torch.empty_like(y)
+    if dz is not None:
+        _req(dz.shape == y.shape and dz.is_contiguous(), 'silu gradient operand')
+    _native.call('wc_silu', y.data_ptr(), _ptr(dz), out.data_ptr(), y.numel(), 0 if dz is None else 1, _stream())
+    return out
+
+
+def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False, col0: int = 0, ncol: Optional[int] = None):
+    """out[n] (+)= sum_r X[r][col0 + n] over a 2-D contiguous X."""
+    R, Ntot = X.shape
+    n = Ntot - col0 if ncol is None else ncol
+    _req(out.is_contiguous() and out.numel() == n, 'colsum output')
+    _native.call('wc_colsum', X.data_ptr() + 4 * col0, R, n, Ntot, out.data_ptr(), int(accumulate), _stream())
+
+
+def time_embedding(t: torch.Tensor, D: int) -> torch.Tensor:
+    tt = t.reshape(-1).to(torch.int64).contiguous()
+    out = torch.empty((tt.numel(), D), dtype=torch.float32, device=tt.device)
+    _native.call('wc_time_embedding', tt.data_ptr(), tt.numel(), D, out.data_ptr(), _stream())
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, ldc: int) -> torch.Tensor:
+    """(B, C, H, W) -> (B, H, W, ldc) with zero channels C..ldc-1."""
+    _req(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4, 'NCHW fp32 device tensor')
+    B, C, H, W = x.shape
+    out = torch.empty((B, H, W, ldc), dtype=torch.float32, device=x.device)
+    _native.call('wc_nchw_to_nhwc', x.data_ptr(), B, C, H, W, out.data_ptr(), ldc, _stream())
+    return out

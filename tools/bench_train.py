@@ -1,10 +1,15 @@
-"""BASELINE config 3 measurement: one training-loss iteration (train_ddpm.py:94-108: add_noise + UNet
-forward + MSE) at 256 px, B=32, per-sample timesteps, HIP-graph replay; prints one JSON line.
+"""BASELINE config 3 measurement at 256 px, B=32, per-sample timesteps; prints one JSON line.
 
-  python tools/bench_train.py [--batch 32] [--steps 20] [--warmup 3]
+  python tools/bench_train.py [--mode step|forward] [--batch 32] [--steps 10] [--warmup 2]
 
-The backward and the optimizer step are not part of config 3 as BASELINE.json states it ("forward
-add_noise + UNet + MSE"); the arithmetic is the engine's fp32-class mode (>= the config's bf16).
+mode 'step' (default): the reference's whole training iteration (train_ddpm.py:94-114) —
+    opt.zero_grad(); noisy = scheduler.add_noise(images, noise, t); pred = model(noisy, t);
+    loss = MSELoss()(pred, noise); loss.backward(); opt.step()
+  with the HIP forward-with-tape and HIP backward (models/train_engine.py) and torch Adam, timed per
+  phase with events.  Arithmetic: convs / projections bf16x6 (fp32-class), weight gradients and
+  attention fp32 MFMA.
+mode 'forward': the training-loss forward only (add_noise + UNet fwd + MSE), HIP-graph replay (the
+  round-1 line).
 """
 import argparse
 import json
@@ -25,7 +30,11 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--seed', type=int, default=3455)
+    ap.add_argument('--mode', default='step', choices=['step', 'forward'])
+    ap.add_argument('--profile', action='store_true', help='per-kernel-class event times of one step')
     args = ap.parse_args()
+    if args.mode == 'step':
+        return train_step(args)
     from weatherconverter_amd import kernels
     from weatherconverter_amd.diffusion_model.config import model_config
     from weatherconverter_amd.diffusion_model.models.unet_base import Unet
@@ -68,6 +77,87 @@ def main():
         'unet_tflops_algorithmic': round(GFLOP_PER_IMAGE_STEP_256 * B / (ms * 1e-3) / 1e3, 1) if S == 256 else None,
         'loss_finite': bool(torch.isfinite(torch.stack(losses)).all()),
         'loss_mean': float(torch.stack(losses).mean()),
+    }))
+
+
+def train_step(args):
+    from weatherconverter_amd import kernels
+    from weatherconverter_amd.diffusion_model.config import model_config
+    from weatherconverter_amd.diffusion_model.models.unet_base import Unet
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    from weatherconverter_amd.synthetic import init_synthetic_
+    dev = torch.device('cuda', 0)
+    mc = model_config(args.size)
+    net = Unet(mc)
+    init_synthetic_(net, seed=0)
+    net = net.to(dev).train()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)  # train_ddpm.py:176 (lr from config.yaml)
+    crit = torch.nn.MSELoss()
+    sched = LinearNoiseScheduler(1000, 0.0001, 0.02)
+    B, S = args.batch, args.size
+    g = torch.Generator().manual_seed(args.seed)
+    nb = 4
+    imgs = [(torch.rand((B, 3, S, S), generator=g) * 2 - 1).to(dev) for _ in range(nb)]
+    noises = [kernels.philox_normal((B, 3, S, S), dev, args.seed, step=i) for i in range(nb)]
+    ts = [torch.randint(0, 1000, (B, ), generator=g).to(dev) for _ in range(nb)]
+
+    def step(i, ev=None):
+        opt.zero_grad(set_to_none=True)
+        noisy = sched.add_noise(imgs[i % nb], noises[i % nb], ts[i % nb])
+        pred = net(noisy, ts[i % nb])
+        loss = crit(pred, noises[i % nb])
+        if ev:
+            ev[0].record()
+        loss.backward()
+        if ev:
+            ev[1].record()
+        opt.step()
+        return loss.detach()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    losses, evs = [], []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[2].record()
+        losses.append(step(i, (e[0], e[1])))
+        evs.append(e)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = el / args.steps * 1e3
+    fwd = sum(e[2].elapsed_time(e[0]) for e in evs) / len(evs)
+    bwd = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
+    prof = None
+    if args.profile:
+        rec = kernels.profile_conv(True)
+        step(0)
+        torch.cuda.synchronize()
+        kernels.profile_conv(False)
+        per = {}
+        for name, flops, e0, e1 in rec:
+            key = name.split('<')[0].split(' ')[0]
+            d = per.setdefault(key, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += flops
+            d[2] += e0.elapsed_time(e1)
+        prof = {k: {'launches': v[0], 'ms': round(v[2], 2), 'tflops_or_gbs': round(v[1] / (v[2] * 1e-3) / 1e12, 1)}
+                for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])}
+    ls = torch.stack(losses)
+    print(json.dumps({
+        'metric': 'train_ddpm config 3: training iterations/s (add_noise + UNet fwd + MSE + backward + Adam)',
+        'value': round(args.steps / el, 4), 'unit': 'iter/s', 'ms_per_iter': round(ms, 2),
+        'ms_forward': round(fwd, 2), 'ms_backward': round(bwd, 2), 'ms_adam_and_host': round(ms - fwd - bwd, 2),
+        'images_per_s': round(B * args.steps / el, 2), 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'higher_is_better': True,
+        'dtype': 'f32 (fp32-class: bf16x6 convs/projections, fp32-MFMA weight gradients and attention)',
+        'data': 'synthetic (keyed random-init weights; images U[-1,1], Philox N(0,1) noise, t ~ U[0,1000))',
+        'config': {'workload': 'BASELINE config 3 full training iteration', 'global_batch': B, 'image_size': S,
+                   'backward': True, 'optimizer': 'torch.optim.Adam lr 1e-4'},
+        'train_tflops_algorithmic': round(3 * GFLOP_PER_IMAGE_STEP_256 * B / (ms * 1e-3) / 1e3, 1) if S == 256 else None,
+        'loss_finite': bool(torch.isfinite(ls).all()), 'loss_first': float(ls[0]), 'loss_last': float(ls[-1]),
+        'kernel_classes': prof,
     }))
 
 

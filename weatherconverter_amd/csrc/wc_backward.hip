@@ -548,10 +548,13 @@ extern "C" int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int
     return WC_OK;
 }
 
+// channel quads per workgroup: the largest power of two <= 64 dividing C/4 (the threads' rows then
+// tile the 256-thread workgroup exactly)
 static int gnb_nq(int C) {
     const int q = C / 4;
-    const int nq = q < 64 ? q : 64;
-    if (C % 4 || nq < 1 || GB_THREADS % nq || q % nq) return -1;
+    if (C % 4 || q < 1) return -1;
+    int nq = 64;
+    while (q % nq) nq >>= 1;
     return nq;
 }
 

@@ -12,8 +12,9 @@
 //       dV^T += dO^T P and dK^T += Q^T dS (the forward kernel's register-reuse trick, transposed).
 //   attn_bwd_dq_kernel    a wave owns 32 queries; loops over 32-key tiles: S^T = K Q^T and
 //       dP^T = V dO^T with queries on the lanes, dS^T feeds dQ^T += K^T dS^T.
-// All operands come from LDS (K/V of the workgroup's keys or Q/dO of its queries staged once, the
-// other side per tile), so head dims up to 192 fit without spilling; exact fp32 products.
+// The wave's own rows (K, V for dK/dV; Q, dO for dQ) stay in registers for the whole loop and the
+// other side's 32-row tiles go through LDS, shared by the workgroup's 4 waves (one per SIMD); exact
+// fp32 products.
 #include "wc_common.hpp"
 
 namespace {
@@ -24,41 +25,42 @@ struct BwdCfg {
     static constexpr int DP = (D + 31) / 32 * 32;   // padded head dim of the d-row accumulators
     static constexpr int NDB = DP / 32;
     static constexpr int RS = D + 4;                // LDS row stride (floats)
-    static constexpr int W = D >= 128 ? 2 : 4;      // waves per workgroup
+    static constexpr int W = 4;                     // waves per workgroup (one per SIMD)
     static constexpr int SLACK = 32;                // reads of pad columns d >= D stay inside LDS
+    static constexpr int LDS_FLOATS = 2 * 32 * RS + SLACK + 64;
 };
 
+// A wave owns 32 keys: its K and V rows stay in registers (lane = key, the half's d range), the
+// 32-query tiles of Q and dO go through LDS, shared by the workgroup's 4 waves.
 template <int D>
-__global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dkdv_kernel(
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
     using Cf = BwdCfg<D>;
-    constexpr int W = Cf::W, RS = Cf::RS, NT = W * 64;
+    constexpr int RS = Cf::RS, NT = 256;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* Ks = smem;                     // [W*32][RS]  this workgroup's keys
-    float* Vs = Ks + W * 32 * RS;         // [W*32][RS]
-    float* Qs = Vs + W * 32 * RS;         // [32][RS]    query tile
-    float* Os = Qs + 32 * RS;             // [32][RS]    dO tile
+    float* Qs = smem;                     // [32][RS] query tile
+    float* Os = Qs + 32 * RS;             // [32][RS] dO tile
     float* Ls = Os + 32 * RS + Cf::SLACK; // [32] lse, then [32] Dv
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l32 = lane & 31, half = lane >> 5;
     const int head = blockIdx.y, b = blockIdx.z, H = gridDim.y;
-    const int kb0 = blockIdx.x * W * 32;
     const float* base = qkv + (long)b * N * ldq;
     const float* dob = dO + (long)b * N * lddo;
     const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
+    const int key = blockIdx.x * 128 + wave * 32 + l32;
 
-    for (int i = tid; i < W * 32 * (D / 4); i += NT) {
-        const int r = i / (D / 4), c4 = i % (D / 4);
-        const int key = kb0 + r;
+    float kreg[Cf::DH], vreg[Cf::DH];
+#pragma unroll
+    for (int i = 0; i < Cf::DH; i += 4) {
         f32x4 kv = f32x4{0.f, 0.f, 0.f, 0.f}, vv = kv;
         if (key < N) {
-            kv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + kcol + c4 * 4);
-            vv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + vcol + c4 * 4);
+            kv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + kcol + half * Cf::DH + i);
+            vv = *reinterpret_cast<const f32x4*>(base + (long)key * ldq + vcol + half * Cf::DH + i);
         }
-        *reinterpret_cast<f32x4*>(Ks + r * RS + c4 * 4) = kv;
-        *reinterpret_cast<f32x4*>(Vs + r * RS + c4 * 4) = vv;
+        kreg[i] = kv.x; kreg[i + 1] = kv.y; kreg[i + 2] = kv.z; kreg[i + 3] = kv.w;
+        vreg[i] = vv.x; vreg[i + 1] = vv.y; vreg[i + 2] = vv.z; vreg[i + 3] = vv.w;
     }
 
     f32x16 dvT[Cf::NDB], dkT[Cf::NDB];
@@ -67,12 +69,10 @@ __global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) { dvT[d][r] = 0.f; dkT[d][r] = 0.f; }
 
-    const float* krow = Ks + (wave * 32 + l32) * RS + half * Cf::DH;
-    const float* vrow = Vs + (wave * 32 + l32) * RS + half * Cf::DH;
     const int ntiles = (N + 31) / 32;
     for (int t = 0; t < ntiles; ++t) {
         const int q0 = t * 32;
-        __syncthreads();  // previous tile consumed (and the key block staged on t == 0)
+        __syncthreads();  // previous tile consumed
         for (int i = tid; i < 32 * (D / 4); i += NT) {
             const int r = i / (D / 4), c4 = i % (D / 4);
             const int q = q0 + r;
@@ -100,12 +100,11 @@ __global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
         for (int i = 0; i < Cf::DH; i += 4) {
             const f32x4 a = *reinterpret_cast<const f32x4*>(qr + i);
-            const f32x4 kk = *reinterpret_cast<const f32x4*>(krow + i);
             const f32x4 a2 = *reinterpret_cast<const f32x4*>(orw + i);
-            const f32x4 vv = *reinterpret_cast<const f32x4*>(vrow + i);
-            s = mfma32(a.x, kk.x, s); s = mfma32(a.y, kk.y, s); s = mfma32(a.z, kk.z, s); s = mfma32(a.w, kk.w, s);
-            dp = mfma32(a2.x, vv.x, dp); dp = mfma32(a2.y, vv.y, dp);
-            dp = mfma32(a2.z, vv.z, dp); dp = mfma32(a2.w, vv.w, dp);
+            s = mfma32(a.x, kreg[i], s); s = mfma32(a.y, kreg[i + 1], s);
+            s = mfma32(a.z, kreg[i + 2], s); s = mfma32(a.w, kreg[i + 3], s);
+            dp = mfma32(a2.x, vreg[i], dp); dp = mfma32(a2.y, vreg[i + 1], dp);
+            dp = mfma32(a2.z, vreg[i + 2], dp); dp = mfma32(a2.w, vreg[i + 3], dp);
         }
         // P and dS in place (register r <-> query row (r&3) + 8(r>>2) + 4 half of the tile)
 #pragma unroll
@@ -129,7 +128,6 @@ __global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dkdv_kernel(
         }
     }
 
-    const int key = kb0 + wave * 32 + l32;
     if (key < N) {
         float* row = dqkv + ((long)b * N + key) * lddq;
 #pragma unroll
@@ -147,38 +145,36 @@ __global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dkdv_kernel(
     }
 }
 
+// A wave owns 32 queries: Q and dO rows in registers, 32-key tiles of K and V through LDS.
 template <int D>
-__global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dq_kernel(
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
     using Cf = BwdCfg<D>;
-    constexpr int W = Cf::W, RS = Cf::RS, NT = W * 64;
+    constexpr int RS = Cf::RS, NT = 256;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* Qs = smem;                 // [W*32][RS] this workgroup's queries
-    float* Os = Qs + W * 32 * RS;     // [W*32][RS] their dO
-    float* Ks = Os + W * 32 * RS;     // [32][RS]   key tile
-    float* Vs = Ks + 32 * RS;         // [32][RS]
+    float* Ks = smem;             // [32][RS] key tile
+    float* Vs = Ks + 32 * RS;     // [32][RS]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l32 = lane & 31, half = lane >> 5;
     const int head = blockIdx.y, b = blockIdx.z, H = gridDim.y;
-    const int qb0 = blockIdx.x * W * 32;
     const float* base = qkv + (long)b * N * ldq;
     const float* dob = dO + (long)b * N * lddo;
     const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
+    const int qme = blockIdx.x * 128 + wave * 32 + l32;
 
-    for (int i = tid; i < W * 32 * (D / 4); i += NT) {
-        const int r = i / (D / 4), c4 = i % (D / 4);
-        const int q = qb0 + r;
+    float qreg[Cf::DH], oreg[Cf::DH];
+#pragma unroll
+    for (int i = 0; i < Cf::DH; i += 4) {
         f32x4 qv = f32x4{0.f, 0.f, 0.f, 0.f}, ov = qv;
-        if (q < N) {
-            qv = *reinterpret_cast<const f32x4*>(base + (long)q * ldq + qcol + c4 * 4);
-            ov = *reinterpret_cast<const f32x4*>(dob + (long)q * lddo + head * D + c4 * 4);
+        if (qme < N) {
+            qv = *reinterpret_cast<const f32x4*>(base + (long)qme * ldq + qcol + half * Cf::DH + i);
+            ov = *reinterpret_cast<const f32x4*>(dob + (long)qme * lddo + head * D + half * Cf::DH + i);
         }
-        *reinterpret_cast<f32x4*>(Qs + r * RS + c4 * 4) = qv;
-        *reinterpret_cast<f32x4*>(Os + r * RS + c4 * 4) = ov;
+        qreg[i] = qv.x; qreg[i + 1] = qv.y; qreg[i + 2] = qv.z; qreg[i + 3] = qv.w;
+        oreg[i] = ov.x; oreg[i + 1] = ov.y; oreg[i + 2] = ov.z; oreg[i + 3] = ov.w;
     }
-    const int qme = qb0 + wave * 32 + l32;
     const float lq = qme < N ? lse[((long)b * H + head) * N + qme] : INFINITY;
     const float dq = qme < N ? Dv[((long)b * H + head) * N + qme] : 0.f;
 
@@ -188,8 +184,6 @@ __global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) dqT[d][r] = 0.f;
 
-    const float* qrow = Qs + (wave * 32 + l32) * RS + half * Cf::DH;
-    const float* orow = Os + (wave * 32 + l32) * RS + half * Cf::DH;
     const int ntiles = (N + 31) / 32;
     for (int t = 0; t < ntiles; ++t) {
         const int k0 = t * 32;
@@ -216,12 +210,11 @@ __global__ __launch_bounds__(BwdCfg<D>::W * 64, 1) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int i = 0; i < Cf::DH; i += 4) {
             const f32x4 a = *reinterpret_cast<const f32x4*>(kr + i);
-            const f32x4 qq = *reinterpret_cast<const f32x4*>(qrow + i);
             const f32x4 a2 = *reinterpret_cast<const f32x4*>(vr + i);
-            const f32x4 oo = *reinterpret_cast<const f32x4*>(orow + i);
-            s = mfma32(a.x, qq.x, s); s = mfma32(a.y, qq.y, s); s = mfma32(a.z, qq.z, s); s = mfma32(a.w, qq.w, s);
-            dp = mfma32(a2.x, oo.x, dp); dp = mfma32(a2.y, oo.y, dp);
-            dp = mfma32(a2.z, oo.z, dp); dp = mfma32(a2.w, oo.w, dp);
+            s = mfma32(a.x, qreg[i], s); s = mfma32(a.y, qreg[i + 1], s);
+            s = mfma32(a.z, qreg[i + 2], s); s = mfma32(a.w, qreg[i + 3], s);
+            dp = mfma32(a2.x, oreg[i], dp); dp = mfma32(a2.y, oreg[i + 1], dp);
+            dp = mfma32(a2.z, oreg[i + 2], dp); dp = mfma32(a2.w, oreg[i + 3], dp);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -278,9 +271,9 @@ template <int D>
 int launch_bwd(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
                int lddq, int B, int N, int C, int heads, float scale, hipStream_t s) {
     using Cf = BwdCfg<D>;
-    const size_t lds = (size_t)(2 * Cf::W * 32 * Cf::RS + 2 * 32 * Cf::RS + Cf::SLACK + 64) * sizeof(float);
+    const size_t lds = (size_t)Cf::LDS_FLOATS * sizeof(float);
     static bool attr_set = false;
-    if (!attr_set) {
+    if (!attr_set && lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
@@ -289,13 +282,13 @@ int launch_bwd(const float* qkv, int ldq, const float* dO, int lddo, const float
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
-    const dim3 grid((N + Cf::W * 32 - 1) / (Cf::W * 32), heads, B);
+    const dim3 grid((N + 127) / 128, heads, B);
     const float scale_log2 = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, grid, dim3(Cf::W * 64), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq,
-                       N, C, scale_log2, scale);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, grid, dim3(256), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N, C,
+                       scale_log2, scale);
     WC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(Cf::W * 64), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N,
-                       C, scale_log2, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(256), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N, C,
+                       scale_log2, scale);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

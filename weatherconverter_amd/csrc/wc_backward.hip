@@ -130,23 +130,31 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
 
     f32x4 ra[A_PER_T], rb[B_PER_T];
+    // pixel coordinates of each B item, advanced by WG_KP pixels per K-step (no per-step division)
+    int bb_[B_PER_T], by_[B_PER_T], bx_[B_PER_T];
+#pragma unroll
+    for (int j = 0; j < B_PER_T; ++j) {
+        const int px = (int)pbeg + brow[j];
+        bb_[j] = px / HWm;
+        const int r = px - bb_[j] * HWm;
+        by_[j] = r / p.Wm;
+        bx_[j] = r - by_[j] * p.Wm;
+    }
+    const int ipend = (int)pend;
     auto load = [&](int s) {
-        const long pb0 = pbeg + (long)s * WG_KP;
+        const int pb0 = (int)pbeg + s * WG_KP;
 #pragma unroll
         for (int j = 0; j < A_PER_T; ++j) {
-            const long px = pb0 + arow[j];
-            const bool ok = px < pend && m0 + acol[j] < p.M;
+            const int px = pb0 + arow[j];
+            const bool ok = px < ipend && m0 + acol[j] < p.M;
             ra[j] = bload4(srdg, ok ? (unsigned)(px * p.ldg + m0 + acol[j]) * 4u : OOB);
         }
 #pragma unroll
         for (int j = 0; j < B_PER_T; ++j) {
-            const long px = pb0 + brow[j];
+            const int px = pb0 + brow[j];
+            const int b = bb_[j], y = by_[j], x = bx_[j];
             f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (px < pend && bseg[j] < 2) {
-                const int b = (int)(px / HWm);
-                const int r = (int)(px - (long)b * HWm);
-                const int y = r / p.Wm;
-                const int x = r - y * p.Wm;
+            if (px < ipend && bseg[j] < 2) {
                 if (bseg[j] == 0) {
                     const int iy = y * p.sy + bdy[j], ix = x * p.sx + bdx[j];
                     const bool inb = (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
@@ -161,11 +169,22 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
                         if (!inb) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
                     }
                 } else {
-                    const int iy = y * p.sy, ix = x * p.sx;
-                    v = bload4(srd1, (unsigned)(((b * p.H1 + iy) * p.W1 + ix) * p.ldc1 + bc[j]) * 4u);
+                    v = bload4(srd1, (unsigned)(((b * p.H1 + y) * p.W1 + x) * p.ldc1 + bc[j]) * 4u);
                 }
             }
             rb[j] = v;
+            // advance to the next K-step's pixel
+            int nx = x + WG_KP, ny = y, nb = b;
+            while (nx >= p.Wm) {
+                nx -= p.Wm;
+                if (++ny == p.Hm) {
+                    ny = 0;
+                    ++nb;
+                }
+            }
+            bb_[j] = nb;
+            by_[j] = ny;
+            bx_[j] = nx;
         }
     };
     auto store = [&](int buf) {

@@ -141,6 +141,10 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
         bx_[j] = r - by_[j] * p.Wm;
     }
     const int ipend = (int)pend;
+    // raw loads of the next K-step are issued before the current step's MFMAs; the GroupNorm(+SiLU)
+    // prologue runs after them, in store(), so the loads' latency hides under the MFMAs
+    unsigned binb = 0;  // bit j: B item j is a real (in-image) input value
+    f32x4 bsc[PRO ? B_PER_T : 1], bsh[PRO ? B_PER_T : 1];
     auto load = [&](int s) {
         const int pb0 = (int)pbeg + s * WG_KP;
 #pragma unroll
@@ -149,30 +153,31 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
             const bool ok = px < ipend && m0 + acol[j] < p.M;
             ra[j] = bload4(srdg, ok ? (unsigned)(px * p.ldg + m0 + acol[j]) * 4u : OOB);
         }
+        binb = 0;
 #pragma unroll
         for (int j = 0; j < B_PER_T; ++j) {
             const int px = pb0 + brow[j];
             const int b = bb_[j], y = by_[j], x = bx_[j];
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            unsigned off = OOB;
             if (px < ipend && bseg[j] < 2) {
                 if (bseg[j] == 0) {
                     const int iy = y * p.sy + bdy[j], ix = x * p.sx + bdx[j];
-                    const bool inb = (unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0;
-                    v = bload4(srd0, inb ? (unsigned)(((b * p.H0 + iy) * p.W0 + ix) * p.ldc0 + bc[j]) * 4u : OOB);
-                    if constexpr (PRO != 0) {
-                        const unsigned o = (unsigned)(b * p.C0 + bc[j]) * 4u;
-                        const f32x4 sc = bload4(srdsc, o), sh = bload4(srdsh, o);
-                        v = v * sc + sh;
-                        if constexpr (PRO == 2) {
-                            v.x = wc_silu(v.x); v.y = wc_silu(v.y); v.z = wc_silu(v.z); v.w = wc_silu(v.w);
-                        }
-                        if (!inb) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+                    if ((unsigned)iy < (unsigned)p.H0 && (unsigned)ix < (unsigned)p.W0) {
+                        off = (unsigned)(((b * p.H0 + iy) * p.W0 + ix) * p.ldc0 + bc[j]) * 4u;
+                        binb |= 1u << j;
                     }
                 } else {
-                    v = bload4(srd1, (unsigned)(((b * p.H1 + y) * p.W1 + x) * p.ldc1 + bc[j]) * 4u);
+                    off = (unsigned)(((b * p.H1 + y) * p.W1 + x) * p.ldc1 + bc[j]) * 4u;
                 }
             }
-            rb[j] = v;
+            // the buffer descriptor must be wave-uniform: one load per segment, the other masked off
+            rb[j] = bload4(srd0, bseg[j] == 0 ? off : OOB) + bload4(srd1, bseg[j] == 1 ? off : OOB);
+            if constexpr (PRO != 0) {
+                const unsigned o = (unsigned)(b * p.C0 + bc[j]) * 4u;
+                const bool pro = bseg[j] == 0 && px < ipend;
+                bsc[j] = bload4(srdsc, pro ? o : OOB);
+                bsh[j] = bload4(srdsh, pro ? o : OOB);
+            }
             // advance to the next K-step's pixel
             int nx = x + WG_KP, ny = y, nb = b;
             while (nx >= p.Wm) {
@@ -193,7 +198,19 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
 #pragma unroll
         for (int j = 0; j < A_PER_T; ++j) *reinterpret_cast<f32x4*>(a + arow[j] * AS + acol[j]) = ra[j];
 #pragma unroll
-        for (int j = 0; j < B_PER_T; ++j) *reinterpret_cast<f32x4*>(bb + brow[j] * BS + bcol[j]) = rb[j];
+        for (int j = 0; j < B_PER_T; ++j) {
+            f32x4 v = rb[j];
+            if constexpr (PRO != 0) {
+                if (bseg[j] == 0) {
+                    v = v * bsc[j] + bsh[j];
+                    if constexpr (PRO == 2) {
+                        v.x = wc_silu(v.x); v.y = wc_silu(v.y); v.z = wc_silu(v.z); v.w = wc_silu(v.w);
+                    }
+                    if (!((binb >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+                }
+            }
+            *reinterpret_cast<f32x4*>(bb + brow[j] * BS + bcol[j]) = v;
+        }
     };
 
     f32x16 acc[2][2];

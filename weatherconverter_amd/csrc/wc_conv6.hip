@@ -87,7 +87,7 @@ struct X6Dev {
 // no weight registers; else register-staged, one tap per K-step.
 // MAP: 0 = 3x3 stride 1; 1 = 4x4/s2 down conv over the space-to-depth input (2x2 taps); 2 = the
 // 4x4/s2 transposed conv, one output parity per workgroup (2x2 taps of the 3x3 frame).
-template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, int MAP = 0>
+template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, int MAP = 0, bool WR = false>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
@@ -108,7 +108,8 @@ struct X6Tile {
     static constexpr int NMT = (NTAP + TPS - 1) / TPS;    // K-steps per 16-channel chunk
     static constexpr int BSTEPM = TPS * BSTEP0;           // weight bytes of a full segment-0 K-step
     static constexpr int BSTAGE = (RES && BSTEP1 > BSTEPM) ? BSTEP1 : BSTEPM;  // LDS weight buffer
-    static constexpr int LDS = 2 * HSTAGE + 2 * BSTAGE;
+    // WR: weight fragments go from global (L2) straight into registers, no LDS weight stage
+    static constexpr int LDS = 2 * HSTAGE + (WR ? 0 : 2 * BSTAGE);
     static constexpr int H_ITEMS = HPIX * 4;             // float4 items of one halo chunk
     static constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
     static constexpr int C_PER_T = TH * 16 * 4 / NT;      // float4 items of one residual centre chunk
@@ -130,9 +131,12 @@ WC_DEVICE int row_dx(int r) {
 // TH = 8 tiles without a residual or with an fp16 one are held to 3 waves per SIMD (<= 168
 // VGPRs; the two-deep residual staging would otherwise take the R16 form to 178 and 2 waves, and
 // 3 waves cost it one spilled VGPR); the other forms run at 2.
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP = 0>
-__global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(X6Dev p) {
-    using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP>;
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP = 0, bool WR = false>
+__global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16)) && !(WR && RES)) ? 3 : 2) void conv3x3_x6_kernel(
+    X6Dev p) {
+    using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
+    static_assert(!WR || (F3 && (!RES || R16) && !GL && MAP == 0 && T::TPS == 1),
+                  "WR: the f16x3 3x3 forms with 2-piece weights in every step");
     constexpr bool S2D = MAP == 1, CT = MAP == 2;
     static_assert(!MAP || (!RES && !GL && PRO == 0), "MAP 1, 2: raw single-segment register-staged forms");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -447,81 +451,178 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         else compute6(hs, toff, bs);
     };
 
-    // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
-    load_halo0(0);
-    if constexpr (GL) glds_b(0);
-    load_b(0);
-    write_halo(0, true);
-    write_b(0, 0);
-    __syncthreads();
-    int s = 0;
-    for (int c = 0; c < p.nck0; ++c) {
-        const int hs = c & 1;
+    if constexpr (WR) {
+        // ---- K loop, weights in registers: a K-step (chunk, tap) reads its A fragments from the
+        // chunk's halo image in LDS and its B fragments from a register set filled one step ahead
+        // straight from L2 (the host's weight image is already in fragment order); the only LDS
+        // writes are the next chunk's halo at the chunk's last tap, so there is ONE barrier per
+        // chunk (9 taps x 12 MFMAs) instead of one per tap.  Set parity is compile-time: step
+        // s = 9c + mt uses set (c + mt) & 1, and chunks run in pairs.
+        u32x4 wreg[2][2][2];  // [set][nb][piece]
+        const unsigned wlane = (unsigned)(half * T::BPLANE + (wn * 64 + l32) * 16);
+        auto load_w = [&](int set, int st) {
+            unsigned off;
+            int items_unused;
+            step_w(st, off, items_unused);
+            off += wlane;
 #pragma unroll
-        for (int mt = 0; mt < T::NMT; ++mt) {
-            const bool more = s + 1 < S;
-            if constexpr (GL) {
-                if (more) glds_b(s + 1);  // buffer (s+1)&1 was last read in step s-1
-            }
-            if (more) load_b(s + 1);
-            // The next chunk's halo loads go out one K-step before the last, after that step's
-            // weight loads: vmcnt drains in issue order, so a halo load issued earlier would be
-            // waited for by every later step's weight-tile wait (an HBM-latency stall per chunk).
-            // After the last chunk come residual centres 0 (one step early) and 1 (in the last).
-            if (mt == T::NMT - 2) {
-                if (c + 1 < p.nck0) load_halo0(c + 1);
-                else if constexpr (RES) load_center(I0, 0);
-            }
-            if constexpr (RES) {
-                if (mt == T::NMT - 1 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
-            }
+            for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int tt = 0; tt < T::TPS; ++tt) {
-                const int tp = mt * T::TPS + tt;
-                if (tp < T::NTAP) {
-                    // CT parity (py, px): tap (i, j) reads input offset (py - i, px - j) (engine._CT_TAPS)
-                    const int toff = S2D ? ((tp >> 1) + 1) * HWD + (tp & 1) + 1
-                                   : CT  ? ((par >> 1) - (tp >> 1) + 1) * HWD + (par & 1) - (tp & 1) + 1
-                                         : (tp / 3) * HWD + tp % 3;
-                    compute0(hs, toff, s & 1, tt);
+                for (int pc = 0; pc < 2; ++pc)
+                    wreg[set][nb][pc] = bload_u4(srdw, off + (unsigned)(nb * 32 * 16 + pc * 2 * T::BPLANE));
+        };
+        auto compute_w = [&](int set, int hs, int toff) {
+            const unsigned char* ha = smem + hs * T::HSTAGE + toff * 16;
+            u32x4 fa[2][2];
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+                    fa[mb][pc] = *reinterpret_cast<const u32x4*>(ha + abase[mb] + pc * 2 * T::HPLANE);
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma_f16(fa[mb][0], wreg[set][nb][0], acc[mb][nb]);
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    acc[mb][nb] = mfma_f16(fa[mb][0], wreg[set][nb][1], acc[mb][nb]);
+                    acc[mb][nb] = mfma_f16(fa[mb][1], wreg[set][nb][0], acc[mb][nb]);
                 }
+        };
+        load_halo0(0);
+        load_w(0, 0);
+        write_halo(0, true);
+        __syncthreads();
+        auto chunk = [&](auto P, int c) {
+            constexpr int PV = decltype(P)::value;  // c & 1: the chunk's halo buffer and set parity
+#pragma unroll
+            for (int mt = 0; mt < 9; ++mt) {
+                const int st = 9 * c + mt;
+                if (st + 1 < S) load_w((mt + 1 + PV) & 1, st + 1);
+                if (mt == 7) {
+                    if (c + 1 < p.nck0) load_halo0(c + 1);
+                    else if constexpr (RES) load_center(I0, 0);
+                }
+                if constexpr (RES) {
+                    if (mt == 8 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
+                }
+                compute_w((mt + PV) & 1, PV, (mt / 3) * HWD + mt % 3);
             }
-            if (more) write_b((s + 1) & 1, s + 1);
-            if (mt == T::NMT - 1) {
-                if (c + 1 < p.nck0) write_halo(hs ^ 1, true);
-                else if constexpr (RES) write_center(I0, hs ^ 1);
-            }
+            if (c + 1 < p.nck0) write_halo(PV ^ 1, true);
+            else if constexpr (RES) write_center(I0, PV ^ 1);
             __syncthreads();
-            ++s;
-        }
-    }
-    if constexpr (RES) {
-        // residual chunk c (centre set c & 1): issue centre c + 2 into this set, compute, write
-        // centre c + 1 (loaded a step earlier) into the other halo buffer
-        auto rstep = [&](auto P, int c) {
-            constexpr int PV = decltype(P)::value;
-            const int hs = (p.nck0 + c) & 1;
-            const bool more = s + 1 < S;
-            if (more) {
-                if constexpr (GL) glds_b(s + 1);
-                load_b(s + 1);
-            }
-            if (c + 2 < p.nck1) load_center(P, c + 2);
-            if constexpr (R16) compute3(hs, HWD + 1, s & 1, 0);  // the halo centre = the output pixel
-            else compute6(hs, HWD + 1, s & 1);
-            if (more) {
-                write_b((s + 1) & 1, s + 1);
-                write_center(std::integral_constant<int, PV ^ 1>{}, hs ^ 1);
-            }
-            __syncthreads();
-            ++s;
         };
         int c = 0;
-        for (; c + 1 < p.nck1; c += 2) {
-            rstep(I0, c);
-            rstep(I1, c + 1);
+        for (; c + 1 < p.nck0; c += 2) {
+            chunk(I0, c);
+            chunk(I1, c + 1);
         }
-        if (c < p.nck1) rstep(I0, c);
+        if (c < p.nck0) chunk(I0, c);
+        if constexpr (RES) {
+            // residual chunk c: centre register set c & 1, halo buffer and weight set (nck0 + c) & 1
+            const int S0w = 9 * p.nck0;
+            auto rstep = [&](auto P, auto Q, int cc) {
+                constexpr int PV = decltype(P)::value, QV = decltype(Q)::value;
+                const int st = S0w + cc;
+                const bool more = st + 1 < S;
+                if (more) load_w(QV ^ 1, st + 1);
+                if (cc + 2 < p.nck1) load_center(P, cc + 2);
+                compute_w(QV, QV, HWD + 1);  // the halo centre = the output pixel
+                if (more) write_center(std::integral_constant<int, PV ^ 1>{}, QV ^ 1);
+                __syncthreads();
+            };
+            auto rloop = [&](auto Q0) {
+                constexpr int Q = decltype(Q0)::value;
+                int cc = 0;
+                for (; cc + 1 < p.nck1; cc += 2) {
+                    rstep(I0, std::integral_constant<int, Q>{}, cc);
+                    rstep(I1, std::integral_constant<int, Q ^ 1>{}, cc + 1);
+                }
+                if (cc < p.nck1) rstep(I0, std::integral_constant<int, Q>{}, cc);
+            };
+            if (p.nck0 & 1) rloop(I1);
+            else rloop(I0);
+        }
+    } else {
+        // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
+        load_halo0(0);
+        if constexpr (GL) glds_b(0);
+        load_b(0);
+        write_halo(0, true);
+        write_b(0, 0);
+        __syncthreads();
+        int s = 0;
+        for (int c = 0; c < p.nck0; ++c) {
+            const int hs = c & 1;
+    #pragma unroll
+            for (int mt = 0; mt < T::NMT; ++mt) {
+                const bool more = s + 1 < S;
+                if constexpr (GL) {
+                    if (more) glds_b(s + 1);  // buffer (s+1)&1 was last read in step s-1
+                }
+                if (more) load_b(s + 1);
+                // The next chunk's halo loads go out one K-step before the last, after that step's
+                // weight loads: vmcnt drains in issue order, so a halo load issued earlier would be
+                // waited for by every later step's weight-tile wait (an HBM-latency stall per chunk).
+                // After the last chunk come residual centres 0 (one step early) and 1 (in the last).
+                if (mt == T::NMT - 2) {
+                    if (c + 1 < p.nck0) load_halo0(c + 1);
+                    else if constexpr (RES) load_center(I0, 0);
+                }
+                if constexpr (RES) {
+                    if (mt == T::NMT - 1 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
+                }
+    #pragma unroll
+                for (int tt = 0; tt < T::TPS; ++tt) {
+                    const int tp = mt * T::TPS + tt;
+                    if (tp < T::NTAP) {
+                        // CT parity (py, px): tap (i, j) reads input offset (py - i, px - j) (engine._CT_TAPS)
+                        const int toff = S2D ? ((tp >> 1) + 1) * HWD + (tp & 1) + 1
+                                       : CT  ? ((par >> 1) - (tp >> 1) + 1) * HWD + (par & 1) - (tp & 1) + 1
+                                             : (tp / 3) * HWD + tp % 3;
+                        compute0(hs, toff, s & 1, tt);
+                    }
+                }
+                if (more) write_b((s + 1) & 1, s + 1);
+                if (mt == T::NMT - 1) {
+                    if (c + 1 < p.nck0) write_halo(hs ^ 1, true);
+                    else if constexpr (RES) write_center(I0, hs ^ 1);
+                }
+                __syncthreads();
+                ++s;
+            }
+        }
+        if constexpr (RES) {
+            // residual chunk c (centre set c & 1): issue centre c + 2 into this set, compute, write
+            // centre c + 1 (loaded a step earlier) into the other halo buffer
+            auto rstep = [&](auto P, int c) {
+                constexpr int PV = decltype(P)::value;
+                const int hs = (p.nck0 + c) & 1;
+                const bool more = s + 1 < S;
+                if (more) {
+                    if constexpr (GL) glds_b(s + 1);
+                    load_b(s + 1);
+                }
+                if (c + 2 < p.nck1) load_center(P, c + 2);
+                if constexpr (R16) compute3(hs, HWD + 1, s & 1, 0);  // the halo centre = the output pixel
+                else compute6(hs, HWD + 1, s & 1);
+                if (more) {
+                    write_b((s + 1) & 1, s + 1);
+                    write_center(std::integral_constant<int, PV ^ 1>{}, hs ^ 1);
+                }
+                __syncthreads();
+                ++s;
+            };
+            int c = 0;
+            for (; c + 1 < p.nck1; c += 2) {
+                rstep(I0, c);
+                rstep(I1, c + 1);
+            }
+            if (c < p.nck1) rstep(I0, c);
+        }
+
     }
 
     // ---- epilogue: (F3: x 2^-(sA + sW[n])) + bias + temb, activation, + residual, NHWC store ----
@@ -577,12 +678,12 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0, bool WR = false>
 int launch6(const X6Dev& d, hipStream_t stream) {
-    using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP>;
+    using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -592,7 +693,7 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n * (MAP == 2 ? 4 : 1));
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP>), grid, dim3(NT), T::LDS, stream, p);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -603,6 +704,16 @@ bool conv3_glds() {
     static const int v = [] {
         const char* e = getenv("WC_CONV3_GL");
         return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v != 0;
+}
+
+// f16x3 weight fragments straight from L2 into registers, one barrier per 16-channel chunk instead of
+// one per tap (WC_CONV3_WR=0: the LDS-staged form, kept for A/B measurement)
+bool conv3_wr() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_WR");
+        return (e && e[0] == '0') ? 0 : 1;
     }();
     return v != 0;
 }
@@ -618,6 +729,17 @@ int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
             case 3: return launch6<TH, BN, 2, false, true, false, true>(d, s);
             case 4: return launch6<TH, BN, 2, true, true, false, true>(d, s);
             default: return launch6<TH, BN, 2, true, true, true, true>(d, s);
+        }
+    }
+    // weights in registers: the TH = 8 forms without the residual segment only (same-box A/B: conv1
+    // 338 -> 356 TF/s; the TH = 16 / BN = 64 form drops to 2 waves/SIMD and loses, 312 -> 292; with
+    // the residual the register sets exceed the 3-wave budget and spill)
+    if (f3 && conv3_wr() && !res && TH == 8) {
+        switch ((pro - 1) * 2 + (res ? 1 : 0)) {
+            case 0: return launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s);
+            case 1: return launch6<TH, BN, 1, true, true, true, false, 0, true>(d, s);
+            case 2: return launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);
+            default: return launch6<TH, BN, 2, true, true, true, false, 0, true>(d, s);
         }
     }
     if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here

@@ -132,7 +132,7 @@ WC_DEVICE int row_dx(int r) {
 // VGPRs; the two-deep residual staging would otherwise take the R16 form to 178 and 2 waves, and
 // 3 waves cost it one spilled VGPR); the other forms run at 2.
 template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP = 0, bool WR = false>
-__global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16)) && !(WR && RES)) ? 3 : 2) void conv3x3_x6_kernel(
+__global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(
     X6Dev p) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
     static_assert(!WR || (F3 && (!RES || R16) && !GL && MAP == 0 && T::TPS == 1),
@@ -458,7 +458,12 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16)) && !(WR && RE
         // writes are the next chunk's halo at the chunk's last tap, so there is ONE barrier per
         // chunk (9 taps x 12 MFMAs) instead of one per tap.  Set parity is compile-time: step
         // s = 9c + mt uses set (c + mt) & 1, and chunks run in pairs.
-        u32x4 wreg[2][2][2];  // [set][nb][piece]
+        // two register sets (the next step's fragments land while this one computes); the residual
+        // forms would use one (loads issued after the step's MFMAs), but even then their centre
+        // staging pushes them past the 3-wave register budget (420 B/lane of spills), so the
+        // dispatcher keeps those on LDS-staged weights
+        constexpr int NS = RES ? 1 : 2;
+        u32x4 wreg[NS][2][2];  // [set][nb][piece]
         const unsigned wlane = (unsigned)(half * T::BPLANE + (wn * 64 + l32) * 16);
         auto load_w = [&](int set, int st) {
             unsigned off;
@@ -500,7 +505,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16)) && !(WR && RE
 #pragma unroll
             for (int mt = 0; mt < 9; ++mt) {
                 const int st = 9 * c + mt;
-                if (st + 1 < S) load_w((mt + 1 + PV) & 1, st + 1);
+                if (NS == 2 && st + 1 < S) load_w((mt + 1 + PV) & (NS - 1), st + 1);
                 if (mt == 7) {
                     if (c + 1 < p.nck0) load_halo0(c + 1);
                     else if constexpr (RES) load_center(I0, 0);
@@ -508,7 +513,8 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16)) && !(WR && RE
                 if constexpr (RES) {
                     if (mt == 8 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
                 }
-                compute_w((mt + PV) & 1, PV, (mt / 3) * HWD + mt % 3);
+                compute_w((mt + PV) & (NS - 1), PV, (mt / 3) * HWD + mt % 3);
+                if (NS == 1 && st + 1 < S) load_w(0, st + 1);
             }
             if (c + 1 < p.nck0) write_halo(PV ^ 1, true);
             else if constexpr (RES) write_center(I0, PV ^ 1);
@@ -527,9 +533,10 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16)) && !(WR && RE
                 constexpr int PV = decltype(P)::value, QV = decltype(Q)::value;
                 const int st = S0w + cc;
                 const bool more = st + 1 < S;
-                if (more) load_w(QV ^ 1, st + 1);
+                if (NS == 2 && more) load_w((QV ^ 1) & (NS - 1), st + 1);
                 if (cc + 2 < p.nck1) load_center(P, cc + 2);
-                compute_w(QV, QV, HWD + 1);  // the halo centre = the output pixel
+                compute_w(QV & (NS - 1), QV, HWD + 1);  // the halo centre = the output pixel
+                if (NS == 1 && more) load_w(0, st + 1);
                 if (more) write_center(std::integral_constant<int, PV ^ 1>{}, QV ^ 1);
                 __syncthreads();
             };
@@ -734,12 +741,10 @@ int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
     // weights in registers: the TH = 8 forms without the residual segment only (same-box A/B: conv1
     // 338 -> 356 TF/s; the TH = 16 / BN = 64 form drops to 2 waves/SIMD and loses, 312 -> 292; with
     // the residual the register sets exceed the 3-wave budget and spill)
-    if (f3 && conv3_wr() && !res && TH == 8) {
-        switch ((pro - 1) * 2 + (res ? 1 : 0)) {
-            case 0: return launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s);
-            case 1: return launch6<TH, BN, 1, true, true, true, false, 0, true>(d, s);
-            case 2: return launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);
-            default: return launch6<TH, BN, 2, true, true, true, false, 0, true>(d, s);
+    if constexpr (TH == 8) {
+        if (f3 && conv3_wr() && !res) {
+            return pro == 1 ? launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s)
+                            : launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);
         }
     }
     if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here

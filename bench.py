@@ -50,7 +50,7 @@ HBM_PEAK_GBS = 8000.0
 GFLOP_PER_IMAGE_STEP_256 = 590.61  # SURVEY.md §8(d) algorithmic FLOPs (probe hook count)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=None,
                     help='GPUs of this node (default: WORLD_SIZE, else 1); N>1 without WORLD_SIZE self-launches')
@@ -71,7 +71,7 @@ def parse():
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--precision', default=None, choices=['f16x3', 'bf16x6', 'fp32'],
                     help='conv/attention arithmetic (default: kernels.default_conv_precision(), i.e. f16x3)')
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def roofline_leg(model, x, t_dev, groups: int = 1):
@@ -285,24 +285,34 @@ def parity_leg(model, dev):
             'case': 'tests/golden/unet_256.npz: reference Unet (config.yaml @256px) forward, x seed 301, t=611, B=1'}
 
 
+def _launch_cmd(gpus: int, argv, port: int):
+    """The torch.distributed.run command line for --gpus N>1 (one rank per GPU, loopback rendezvous)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={gpus}',
+            '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + list(argv)
+
+
 def _self_launch(args) -> int:
     """--gpus N>1 outside torch.distributed.run: start it as a child (nothing here has touched the GPU;
     the parent only waits and passes the exit code on)."""
     with socket.socket() as sk:
         sk.bind(('127.0.0.1', 0))
         port = sk.getsockname()[1]
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
-           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+    return subprocess.call(_launch_cmd(args.gpus, sys.argv[1:], port))
+
+
+def _world(args) -> int:
+    """WORLD_SIZE, checked against --gpus when both are given."""
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+    return world
 
 
 def main():
     args = parse()
     if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
         sys.exit(_self_launch(args))
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    if args.gpus is not None and args.gpus != world:
-        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+    world = _world(args)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:

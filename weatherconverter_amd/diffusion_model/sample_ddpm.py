@@ -157,20 +157,38 @@ def sample_tensor(model: Unet, scheduler: LinearNoiseScheduler, batch: int, im_c
     ts = torch.arange(T, device=dev, dtype=torch.long)
     runner = _GraphStep(model, xt) if graph else None
     nxt = torch.empty_like(xt)
-    for i in reversed(range(T)):
-        t_dev = ts[i:i + 1]
-        eps = runner(xt, t_dev) if runner is not None else model(xt, t_dev)
-        if i == 0:
-            scheduler.step(xt, eps, 0, out=nxt)
-        elif noise == 'torch_cpu':
-            scheduler.step(xt, eps, i, out=nxt, z=cpu_noise())
-        else:
-            scheduler.step(xt, eps, i, out=nxt, noise='philox', seed=seed, sample0=sample0)
-        xt, nxt = nxt, xt
-        if progress is not None:
-            progress(i)
-        if progress_x is not None:  # (t, x_{t-1}) after each step (tests / diagnostics)
-            progress_x(i, xt)
+    # reference-RNG mode: the per-step z draws (the full-batch CPU tensor, in the reference's order)
+    # run one step ahead on a worker thread while the GPU computes the UNet; nothing else draws from
+    # the CPU generator meanwhile, so the stream is exactly the sequential one
+    pool = fut = None
+    if noise == 'torch_cpu' and T > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(1)
+
+        def cpu_draw():
+            return torch.randn(full_shape)[sample0:sample0 + batch].contiguous()
+
+        fut = pool.submit(cpu_draw)
+    try:
+        for i in reversed(range(T)):
+            t_dev = ts[i:i + 1]
+            eps = runner(xt, t_dev) if runner is not None else model(xt, t_dev)
+            if i == 0:
+                scheduler.step(xt, eps, 0, out=nxt)
+            elif noise == 'torch_cpu':
+                z = fut.result()
+                fut = pool.submit(cpu_draw) if i > 1 else None
+                scheduler.step(xt, eps, i, out=nxt, z=z.to(dev))
+            else:
+                scheduler.step(xt, eps, i, out=nxt, noise='philox', seed=seed, sample0=sample0)
+            xt, nxt = nxt, xt
+            if progress is not None:
+                progress(i)
+            if progress_x is not None:  # (t, x_{t-1}) after each step (tests / diagnostics)
+                progress_x(i, xt)
+    finally:
+        if pool is not None:
+            pool.shutdown(wait=True)
     return xt
 
 

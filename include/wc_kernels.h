@@ -355,6 +355,10 @@ typedef struct wc_wgrad_args {
     int B, Hm, Wm;
 } wc_wgrad_args;
 int wc_conv_wgrad(const wc_wgrad_args* args, float* part, int splits, void* stream);
+/* The same weight gradient on bf16x6 split-precision MFMA (both operands split exactly into three
+ * bf16 pieces, the 6 piece products with i + j <= 2; fragments read pixel-contiguous from
+ * [pixel][channel] LDS rows with gfx950's transposing ds_read_b64_tr_b16).  Same arguments. */
+int wc_conv_wgrad_x6(const wc_wgrad_args* args, float* part, int splits, void* stream);
 /* The split count wc_conv_wgrad accepts for (M, Kc, P = B*Hm*Wm) aiming at ~target_blocks workgroups. */
 int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks);
 /* dW = sum_split part: column k < K0 is (tap t = k / C0, channel c = k % C0), written (c < Cw only)

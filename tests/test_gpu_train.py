@@ -23,13 +23,14 @@ def _gen(seed):
 
 
 # ------------------------------------------------------------------ kernels
-@pytest.mark.parametrize('silu,res', [(True, True), (False, False)])
-def test_conv_wgrad_3x3_prologue_residual(silu, res):
+@pytest.mark.parametrize('x6', [False, True])
+@pytest.mark.parametrize('silu,res,M', [(True, True, 96), (False, False, 96), (True, False, 64)])
+def test_conv_wgrad_3x3_prologue_residual(silu, res, M, x6):
     from weatherconverter_amd import kernels as K
     from weatherconverter_amd.kernels import Seg, View
     from weatherconverter_amd.diffusion_model.models.engine import TAPS1, TAPS3
     g = _gen(1)
-    B, H, W, C0, C1, M = 2, 12, 20, 32, 64, 96
+    B, H, W, C0, C1 = 2, 12, 20, 32, 64
     x = torch.randn((B, H, W, C0), generator=g)
     xr = torch.randn((B, H, W, C1), generator=g)
     dy = torch.randn((B, H, W, M), generator=g)
@@ -40,7 +41,7 @@ def test_conv_wgrad_3x3_prologue_residual(silu, res):
     segs = [Seg(View.full(x.cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=silu)]
     if res:
         segs.append(Seg(View.full(xr.cuda()), TAPS1, kbase=9 * C0))
-    K.conv_wgrad(View.full(dy.cuda()), segs, dw, (C0 * 9, 9, 1), dw1=dwr if res else None, s1=C1)
+    K.conv_wgrad(View.full(dy.cuda()), segs, dw, (C0 * 9, 9, 1), dw1=dwr if res else None, s1=C1, x6=x6)
     a = x.double() * sc.double()[:, None, None, :] + sh.double()[:, None, None, :]
     a = F.silu(a) if silu else a
     w = torch.zeros((M, C0, 3, 3), dtype=torch.float64, requires_grad=True)
@@ -52,7 +53,8 @@ def test_conv_wgrad_3x3_prologue_residual(silu, res):
         assert rel_l2(dwr.cpu(), ref) < 1e-5
 
 
-def test_conv_wgrad_4x4_stride2_and_transposed():
+@pytest.mark.parametrize('x6', [False, True])
+def test_conv_wgrad_4x4_stride2_and_transposed(x6):
     from weatherconverter_amd import kernels as K
     from weatherconverter_amd.kernels import Seg, View
     from weatherconverter_amd.diffusion_model.models.engine import TAPS4S2
@@ -61,7 +63,7 @@ def test_conv_wgrad_4x4_stride2_and_transposed():
     x = torch.randn((B, H, W, C), generator=g)
     dy = torch.randn((B, H // 2, W // 2, N), generator=g)
     dw = torch.zeros((N, C, 4, 4), device='cuda')
-    K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS4S2, stride=2)], dw, (C * 16, 16, 1))
+    K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS4S2, stride=2)], dw, (C * 16, 16, 1), x6=x6)
     w = torch.zeros((N, C, 4, 4), dtype=torch.float64, requires_grad=True)
     F.conv2d(x.double().permute(0, 3, 1, 2), w, stride=2, padding=1).backward(dy.double().permute(0, 3, 1, 2))
     assert rel_l2(dw.cpu(), w.grad) < 1e-5
@@ -69,7 +71,7 @@ def test_conv_wgrad_4x4_stride2_and_transposed():
     xt = torch.randn((B, H // 2, W // 2, C), generator=g)
     dyt = torch.randn((B, H, W, N), generator=g)
     dwt = torch.zeros((C, N, 4, 4), device='cuda')
-    K.conv_wgrad(View.full(xt.cuda()), [Seg(View.full(dyt.cuda()), TAPS4S2, stride=2)], dwt, (N * 16, 16, 1))
+    K.conv_wgrad(View.full(xt.cuda()), [Seg(View.full(dyt.cuda()), TAPS4S2, stride=2)], dwt, (N * 16, 16, 1), x6=x6)
     wt = torch.zeros((C, N, 4, 4), dtype=torch.float64, requires_grad=True)
     F.conv_transpose2d(xt.double().permute(0, 3, 1, 2), wt, stride=2, padding=1).backward(
         dyt.double().permute(0, 3, 1, 2))

@@ -18,7 +18,7 @@
 //    same reduction without a normalised input is the per-(b, c) channel sum (bias / temb grads).
 //  * gemm_small / silu / colsum / temb helpers for the time-embedding MLP (B x 128 matrices).
 //  * nchw_to_nhwc: the loss gradient (NCHW, the UNet output layout) into a padded NHWC view.
-#include "wc_common.hpp"
+#include "wc_x6.hpp"
 
 namespace {
 
@@ -62,15 +62,24 @@ struct WgDev {
 };
 
 // PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU (segment 0 only, as the forward prologue).
-template <int BM, int BN, int PRO>
+// X6: bf16x6 (both operands split exactly into 3 bf16 pieces; the 6 piece products with i + j <= 2
+// on v_mfma_f32_32x32x16_bf16).  The pieces stay in LDS as [pixel][channel] rows — the order they
+// arrive in from HBM — and the MFMA fragments, which need 8 consecutive PIXELS per lane, are read
+// with ds_read_b64_tr_b16 (gfx950's transposing LDS read: per 16-lane group a 4-row x 16-column
+// block delivered column-major).  Row bytes = 2*width + 64 (== 64 mod 256): the four rows of a
+// half-wave's read land on disjoint banks.  Else fp32 MFMA 32x32x2 on fp32 rows.
+template <int BM, int BN, int PRO, bool X6>
 __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
-    constexpr int AS = BM + 32, BS = BN + 32;  // LDS row strides: lane halves on disjoint banks
-    constexpr int A_PER_T = WG_KP * BM / 4 / WG_THREADS;
-    constexpr int B_PER_T = WG_KP * BN / 4 / WG_THREADS;
-    constexpr int STAGE = WG_KP * (AS + BS);
-    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+    constexpr int KP = X6 ? 16 : WG_KP;        // pixels per K-step
+    constexpr int AS = BM + 32, BS = BN + 32;  // fp32 LDS row strides: lane halves on disjoint banks
+    constexpr int ASB = BM * 2 + 64, BSB = BN * 2 + 64;  // X6 row bytes
+    constexpr int APL = KP * ASB, BPL = KP * BSB;        // X6 bytes of one piece plane
+    constexpr int A_PER_T = KP * BM / 4 / WG_THREADS;
+    constexpr int B_PER_T = KP * BN / 4 / WG_THREADS;
+    constexpr int STAGE = X6 ? 3 * (APL + BPL) : KP * (AS + BS) * 4;  // bytes
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -87,7 +96,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     const long pbeg = (long)sp * p.pps;
     long pend = pbeg + p.pps;
     if (pend > p.P) pend = p.P;
-    const int nsteps = (int)((pend - pbeg + WG_KP - 1) / WG_KP);
+    const int nsteps = (int)((pend - pbeg + KP - 1) / KP);
     const int HWm = p.Hm * p.Wm;
 
     // fixed per-thread column coordinates
@@ -130,7 +139,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
 
     f32x4 ra[A_PER_T], rb[B_PER_T];
-    // pixel coordinates of each B item, advanced by WG_KP pixels per K-step (no per-step division)
+    // pixel coordinates of each B item, advanced by KP pixels per K-step (no per-step division)
     int bb_[B_PER_T], by_[B_PER_T], bx_[B_PER_T];
 #pragma unroll
     for (int j = 0; j < B_PER_T; ++j) {
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     unsigned binb = 0;  // bit j: B item j is a real (in-image) input value
     f32x4 bsc[PRO ? B_PER_T : 1], bsh[PRO ? B_PER_T : 1];
     auto load = [&](int s) {
-        const int pb0 = (int)pbeg + s * WG_KP;
+        const int pb0 = (int)pbeg + s * KP;
 #pragma unroll
         for (int j = 0; j < A_PER_T; ++j) {
             const int px = pb0 + arow[j];
@@ -179,7 +188,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
                 bsh[j] = bload4(srdsh, pro ? o : OOB);
             }
             // advance to the next K-step's pixel
-            int nx = x + WG_KP, ny = y, nb = b;
+            int nx = x + KP, ny = y, nb = b;
             while (nx >= p.Wm) {
                 nx -= p.Wm;
                 if (++ny == p.Hm) {
@@ -193,10 +202,21 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
         }
     };
     auto store = [&](int buf) {
-        float* a = lds + buf * STAGE;
-        float* bb = a + WG_KP * AS;
+        unsigned char* a = lds + buf * STAGE;
+        unsigned char* bb = a + (X6 ? 3 * APL : KP * AS * 4);
 #pragma unroll
-        for (int j = 0; j < A_PER_T; ++j) *reinterpret_cast<f32x4*>(a + arow[j] * AS + acol[j]) = ra[j];
+        for (int j = 0; j < A_PER_T; ++j) {
+            if constexpr (X6) {
+                wcx6::u32x2 p0, p1, p2;
+                wcx6::split3(ra[j], p0, p1, p2);
+                unsigned char* d = a + arow[j] * ASB + acol[j] * 2;
+                *reinterpret_cast<wcx6::u32x2*>(d) = p0;
+                *reinterpret_cast<wcx6::u32x2*>(d + APL) = p1;
+                *reinterpret_cast<wcx6::u32x2*>(d + 2 * APL) = p2;
+            } else {
+                *reinterpret_cast<f32x4*>(a + (arow[j] * AS + acol[j]) * 4) = ra[j];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < B_PER_T; ++j) {
             f32x4 v = rb[j];
@@ -209,7 +229,16 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
                     if (!((binb >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
                 }
             }
-            *reinterpret_cast<f32x4*>(bb + brow[j] * BS + bcol[j]) = v;
+            if constexpr (X6) {
+                wcx6::u32x2 p0, p1, p2;
+                wcx6::split3(v, p0, p1, p2);
+                unsigned char* d = bb + brow[j] * BSB + bcol[j] * 2;
+                *reinterpret_cast<wcx6::u32x2*>(d) = p0;
+                *reinterpret_cast<wcx6::u32x2*>(d + BPL) = p1;
+                *reinterpret_cast<wcx6::u32x2*>(d + 2 * BPL) = p2;
+            } else {
+                *reinterpret_cast<f32x4*>(bb + (brow[j] * BS + bcol[j]) * 4) = v;
+            }
         }
     };
 
@@ -226,20 +255,64 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
         store(0);
     }
     __syncthreads();
+    // X6 fragment addresses: lane = 16 g + 4 q + p supplies row 8 kh + q (kh = g >> 1), columns
+    // 16 (g & 1) + 4 p .. + 3 of its 32-column block; it receives column (lane & 31), 4 pixels
+    const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+    const int tr_a = (8 * (tg >> 1) + tq) * ASB + (wm * 64 + 16 * (tg & 1) + 4 * tp) * 2;
+    const int tr_b = (8 * (tg >> 1) + tq) * BSB + (wn * 64 + 16 * (tg & 1) + 4 * tp) * 2;
+    auto tr_frag = [&](const unsigned char* q0, int rs) {
+        typedef short v4s __attribute__((ext_vector_type(4)));
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(q0));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(q0 + 4 * rs));
+        const wcx6::u32x2 l2 = __builtin_bit_cast(wcx6::u32x2, lo), h2 = __builtin_bit_cast(wcx6::u32x2, hi);
+        return wcx6::u32x4{l2.x, l2.y, h2.x, h2.y};
+    };
     for (int s = 0; s < nsteps; ++s) {
         const int buf = s & 1;
         if (s + 1 < nsteps) load(s + 1);
-        const float* a = lds + buf * STAGE + wm * 64 + l32;
-        const float* bb = lds + buf * STAGE + WG_KP * AS + wn * 64 + l32;
+        if constexpr (X6) {
+            const unsigned char* a = lds + buf * STAGE + tr_a;
+            const unsigned char* bb = lds + buf * STAGE + 3 * APL + tr_b;
+            wcx6::u32x4 fa[2][3], fb[2][3];
 #pragma unroll
-        for (int kk = 0; kk < WG_KP / 2; ++kk) {
-            const int row = 2 * kk + half;
-            const float a0 = a[row * AS], a1 = a[row * AS + 32];
-            const float b0 = bb[row * BS], b1 = bb[row * BS + 32];
-            acc[0][0] = mfma32(a0, b0, acc[0][0]);
-            acc[0][1] = mfma32(a0, b1, acc[0][1]);
-            acc[1][0] = mfma32(a1, b0, acc[1][0]);
-            acc[1][1] = mfma32(a1, b1, acc[1][1]);
+            for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) fa[mb][pc] = tr_frag(a + pc * APL + mb * 64, ASB);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) fb[nb][pc] = tr_frag(bb + pc * BPL + nb * 64, BSB);
+            }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = wcx6::mfma_bf16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    acc[mb][nb] = wcx6::mfma_bf16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_bf16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    acc[mb][nb] = wcx6::mfma_bf16(fa[mb][0], fb[nb][2], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_bf16(fa[mb][1], fb[nb][1], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_bf16(fa[mb][2], fb[nb][0], acc[mb][nb]);
+                }
+        } else {
+            const float* a = reinterpret_cast<const float*>(lds + buf * STAGE) + wm * 64 + l32;
+            const float* bb = reinterpret_cast<const float*>(lds + buf * STAGE) + KP * AS + wn * 64 + l32;
+#pragma unroll
+            for (int kk = 0; kk < KP / 2; ++kk) {
+                const int row = 2 * kk + half;
+                const float a0 = a[row * AS], a1 = a[row * AS + 32];
+                const float b0 = bb[row * BS], b1 = bb[row * BS + 32];
+                acc[0][0] = mfma32(a0, b0, acc[0][0]);
+                acc[0][1] = mfma32(a0, b1, acc[0][1]);
+                acc[1][0] = mfma32(a1, b0, acc[1][0]);
+                acc[1][1] = mfma32(a1, b1, acc[1][1]);
+            }
         }
         if (s + 1 < nsteps) store(buf ^ 1);
         __syncthreads();
@@ -283,15 +356,36 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     *dst = accumulate ? *dst + s : s;
 }
 
-template <int BM, int BN>
-int wgrad_dispatch(const WgDev& d, int pro, int grid, hipStream_t s) {
-    switch (pro) {
-        case 0: hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 0>), dim3(grid), dim3(WG_THREADS), 0, s, d); break;
-        case 1: hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 1>), dim3(grid), dim3(WG_THREADS), 0, s, d); break;
-        default: hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 2>), dim3(grid), dim3(WG_THREADS), 0, s, d); break;
+template <int BM, int BN, int PRO, bool X6>
+int wgrad_launch(const WgDev& d, int grid, hipStream_t s) {
+    constexpr int KP = X6 ? 16 : WG_KP;
+    constexpr int bytes = 2 * (X6 ? 3 * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
+    static bool attr_set = false;
+    if (!attr_set && bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_kernel<BM, BN, PRO, X6>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
     }
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, PRO, X6>), dim3(grid), dim3(WG_THREADS), bytes, s, d);
     WC_CHECK_LAUNCH();
     return WC_OK;
+}
+
+template <int BM, int BN>
+int wgrad_dispatch(const WgDev& d, int pro, bool x6, int grid, hipStream_t s) {
+    if (x6) {
+        switch (pro) {
+            case 0: return wgrad_launch<BM, BN, 0, true>(d, grid, s);
+            case 1: return wgrad_launch<BM, BN, 1, true>(d, grid, s);
+            default: return wgrad_launch<BM, BN, 2, true>(d, grid, s);
+        }
+    }
+    switch (pro) {
+        case 0: return wgrad_launch<BM, BN, 0, false>(d, grid, s);
+        case 1: return wgrad_launch<BM, BN, 1, false>(d, grid, s);
+        default: return wgrad_launch<BM, BN, 2, false>(d, grid, s);
+    }
 }
 
 // ============================================================================================
@@ -511,7 +605,7 @@ inline unsigned blocks_for(long n, int per) { return (unsigned)((n + per - 1) / 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-extern "C" int wc_conv_wgrad(const wc_wgrad_args* a, float* part, int splits, void* stream) {
+static int conv_wgrad_any(const wc_wgrad_args* a, float* part, int splits, bool x6, void* stream) {
     if (!a || !a->g || !part || a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
     const wc_conv_seg& s0 = a->seg[0];
     if (!s0.src) return WC_E_ARG;
@@ -556,7 +650,15 @@ extern "C" int wc_conv_wgrad(const wc_wgrad_args* a, float* part, int splits, vo
     if (grid > (1L << 30)) return WC_E_SHAPE;
     const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return narrow ? wgrad_dispatch<64, 256>(d, pro, (int)grid, s) : wgrad_dispatch<128, 128>(d, pro, (int)grid, s);
+    return narrow ? wgrad_dispatch<64, 256>(d, pro, x6, (int)grid, s) : wgrad_dispatch<128, 128>(d, pro, x6, (int)grid, s);
+}
+
+extern "C" int wc_conv_wgrad(const wc_wgrad_args* a, float* part, int splits, void* stream) {
+    return conv_wgrad_any(a, part, splits, false, stream);
+}
+
+extern "C" int wc_conv_wgrad_x6(const wc_wgrad_args* a, float* part, int splits, void* stream) {
+    return conv_wgrad_any(a, part, splits, true, stream);
 }
 
 extern "C" int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks) {

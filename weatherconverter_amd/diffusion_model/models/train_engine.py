@@ -309,6 +309,10 @@ class TrainEngine:
         self.keep = []
         return self.pgrads
 
+    def _wgrad(self, g: View, segs, dw0, s0, **kw):
+        """Weight gradient on bf16x6 (precision bf16x6) or fp32 MFMA."""
+        K.conv_wgrad(g, segs, dw0, s0, x6=self.precision == 'bf16x6', **kw)
+
     def _bias_grad(self, g: View, *params):
         sums = K.channel_sums(g)
         for p in params:
@@ -323,7 +327,7 @@ class TrainEngine:
         g32 = K.nchw_to_nhwc(gout, 32)
         g4 = View(g32, 0, 4)
         wtmp = torch.zeros((4, C, 3, 3), dtype=torch.float32, device=self.device)
-        K.conv_wgrad(g4, [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], wtmp, (C * 9, 9, 1))
+        self._wgrad(g4, [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], wtmp, (C * 9, 9, 1))
         self._pgrad(m.conv_out.weight).copy_(wtmp[:NO])
         btmp = torch.zeros(4, dtype=torch.float32, device=self.device)
         K.bsum(K.channel_sums(g4), 0, btmp)
@@ -341,7 +345,7 @@ class TrainEngine:
         gY = self._grad(Y)
         gX = self._grad(X)
         self._bias_grad(gY, rp['conv2'].bias, rp['resc'].bias)
-        K.conv_wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
+        self._wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
                      self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci)
         dz2 = View.full(self._new(B, H, W, co))
         self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
@@ -352,7 +356,7 @@ class TrainEngine:
                       dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False)
         sums = self._bias_grad(dh, rp['conv1'].bias)
         self.dproj[:, rp['off']:rp['off'] + co].copy_(sums[:, :, 0])
-        K.conv_wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
+        self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
                      (ci * 9, 9, 1))
         dz1 = View.full(self._new(B, H, W, ci))
         self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
@@ -367,7 +371,7 @@ class TrainEngine:
         mha, gn = ap['mha'], ap['gn']
         gY = self._grad(Yout)
         self._bias_grad(gY, mha.out_proj.bias)
-        K.conv_wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0))
+        self._wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0))
         do = self._new(B, H, W, C)
         self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W)
         dqkv = self._new(B, H, W, 3 * C)
@@ -375,7 +379,7 @@ class TrainEngine:
                         N, C, ap['heads'])
         gq = View.full(dqkv)
         self._bias_grad(gq, mha.in_proj_bias)
-        K.conv_wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),
+        self._wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),
                      (C, 1, 0))
         da = View.full(self._new(B, H, W, C))
         self._conv([Seg(gq, TAPS1)], ap['pk_inT'], None, da, H, W)
@@ -390,7 +394,7 @@ class TrainEngine:
         gc = self._grad(cur)
         w = dp['mod'].weight
         self._bias_grad(gF, dp['mod'].bias)
-        K.conv_wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1))
+        self._wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1))
         for (py, px), (taps, pk) in zip(_PARITIES, dp['dT']):
             self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=gc)
 
@@ -402,7 +406,7 @@ class TrainEngine:
         self._bias_grad(gD, up['mod'].bias)
         # dW[ci][co][ky][kx] = sum_pixels x[ci] * dY[co] at (2y - 1 + ky, 2x - 1 + kx): the 4x4/s2 tap
         # grid over dY with x in the gradient role
-        K.conv_wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1))
+        self._wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1))
         self._conv([Seg(gD, TAPS4S2, stride=2)], up['dT'], None, gc, cur.H, cur.W, res=gc)
 
     def _bwd_conv_in(self, rec, gout):
@@ -412,7 +416,7 @@ class TrainEngine:
         self._bias_grad(g, m.conv_in.bias)
         xn = K.nchw_to_nhwc(self.x, 4)
         w = m.conv_in.weight
-        K.conv_wgrad(g, [Seg(View.full(xn), TAPS3)], self._pgrad(w), (w.shape[1] * 9, 9, 1), Cw=w.shape[1])
+        self._wgrad(g, [Seg(View.full(xn), TAPS3)], self._pgrad(w), (w.shape[1] * 9, 9, 1), Cw=w.shape[1])
 
     def _temb_bwd(self):
         """t_proj (Linear, SiLU, Linear) and the t_emb_layers (SiLU, Linear) backward (B x 128)."""

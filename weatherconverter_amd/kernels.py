@@ -873,10 +873,10 @@ def _fill_seg(cs, s: Seg, B: int):
 
 
 def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, int, int], *, Cw: Optional[int] = None,
-               dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False):
+               dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False, x6: bool = False):
     """Weight gradient of a conv whose input segments are `segs` (as the forward read them, prologue
-    included) and whose output gradient is the view g (pixel grid = g's H x W): fp32-MFMA GEMM over
-    the pixels, split and reduced in a fixed order.  Column (tap t, channel c < Cw) of segment 0 is
+    included) and whose output gradient is the view g (pixel grid = g's H x W): GEMM over the pixels
+    on fp32 MFMA (or bf16x6 with x6), split and reduced in a fixed order.  Column (tap t, channel c < Cw) of segment 0 is
     written to dw0.flat[m*s0[0] + c*s0[1] + t*s0[2]], segment 1's columns to dw1.flat[m*s1 + c]."""
     g.check()
     _req(1 <= len(segs) <= 2, 'wgrad takes 1 or 2 segments')
@@ -903,7 +903,8 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
     splits = lib.wc_conv_wgrad_splits(g.C, Kc, P, 2048)
     part = torch.empty(splits * g.C * Kc, dtype=torch.float32, device=g.t.device)
     s = _stream()
-    _timed('conv_wgrad_kernel', 'wc_conv_wgrad', 2.0 * P * g.C * Kc, ctypes.byref(a), part.data_ptr(), splits, s)
+    _timed('conv_wgrad_kernel' + ('<x6>' if x6 else ''), 'wc_conv_wgrad_x6' if x6 else 'wc_conv_wgrad',
+           2.0 * P * g.C * Kc, ctypes.byref(a), part.data_ptr(), splits, s)
     _native.call('wc_wgrad_reduce', part.data_ptr(), splits, g.C, Kc, K0, C0, Cw, dw0.data_ptr(), s0[0], s0[1], s0[2],
                  _ptr(dw1), s1, int(accumulate), s)
 

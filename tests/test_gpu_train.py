@@ -171,7 +171,7 @@ def _check(ours, ref, per_tensor=1e-4, overall=1e-5):
     assert worst[0][0] < per_tensor, worst[:4]
 
 
-@pytest.mark.parametrize('precision', ['bf16x6', 'fp32'])
+@pytest.mark.parametrize('precision', ['f16x3', 'bf16x6', 'fp32'])
 def test_unet_grads_tiny_vs_oracle_autograd(precision):
     import json
     import os
@@ -186,7 +186,7 @@ def test_unet_grads_tiny_vs_oracle_autograd(precision):
 
 def test_unet_grads_256_baseline_architecture_vs_oracle_autograd():
     from weatherconverter_amd.diffusion_model.config import model_config
-    ours, ref, lo, lr = _model_grads(model_config(256), 2, 'bf16x6')
+    ours, ref, lo, lr = _model_grads(model_config(256), 2, 'f16x3')
     assert len(ref) == 358
     assert abs(lo - lr) <= 1e-5 * abs(lr)
     _check(ours, ref)

@@ -44,9 +44,11 @@ class TrainEngine:
         K._native.load()
         self.model = model
         self.device = params[0].device
-        p = precision or getattr(model, 'conv_precision', None) or 'bf16x6'
-        # f16x3 needs range bounds that gradients do not have: split-precision training runs bf16x6
+        p = precision or getattr(model, 'conv_precision', None) or K.default_conv_precision()
+        # f16x3 needs range bounds that gradients do not have: the backward runs bf16x6; the forward's
+        # GroupNorm-prologue convs and projections run f16x3 under their static bounds (as inference)
         self.precision = 'fp32' if p == 'fp32' else 'bf16x6'
+        self.f3 = p == 'f16x3'
         self.tape: List[tuple] = []
 
     # ------------------------------------------------------------------ packing (per step)
@@ -71,10 +73,16 @@ class TrainEngine:
         w1, w2, wr = f[2].weight.detach(), s[2].weight.detach(), r.weight.detach()
         ci, co = w1.shape[1], w1.shape[0]
         wr2 = wr.reshape(co, ci)
+        f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
+        w2cat = torch.cat([pack_conv(w2), wr2], 1)
         return dict(
             ci=ci, co=co, gn1=f[0], conv1=f[2], gn2=s[0], conv2=s[2], resc=r, temb=blk.t_emb_layers[i][1],
             pk1=self._pk(pack_conv(w1), ci, 9),
-            pk2=self._pk(torch.cat([pack_conv(w2), wr2], 1), co, 9, ci),
+            pk2=self._pk(w2cat, co, 9, ci),
+            f3_1=K.pack_f16x3(pack_conv(w1).float(), ci) if f3 else None,
+            f3_2=K.pack_f16x3(w2cat.float(), co, ci, res_f16=True) if f3 else None,
+            gb1=(float(f[0].weight.abs().max()), float(f[0].bias.abs().max())),
+            gb2=(float(s[0].weight.abs().max()), float(s[0].bias.abs().max())),
             b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
             pk1T=self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9),
             pk2T=self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9),
@@ -84,8 +92,15 @@ class TrainEngine:
         mha, gn = blk.attentions[i], blk.attention_norms[i]
         C = mha.embed_dim
         w_in, w_out = mha.in_proj_weight.detach(), mha.out_proj.weight.detach()
-        return dict(C=C, heads=mha.num_heads, gn=gn, mha=mha, pk_in=self._pk(w_in, C, 1), pk_out=self._pk(w_out, C, 1),
-                    pk_inT=self._pk(w_in.t(), 3 * C, 1), pk_outT=self._pk(w_out.t(), C, 1))
+        d = dict(C=C, heads=mha.num_heads, gn=gn, mha=mha, pk_in=self._pk(w_in, C, 1), pk_out=self._pk(w_out, C, 1),
+                 pk_inT=self._pk(w_in.t(), 3 * C, 1), pk_outT=self._pk(w_out.t(), C, 1), f3_in=None, f3_out=None)
+        if self.f3 and C % 16 == 0:
+            d['f3_in'] = K.pack_f16x3(w_in.float(), C, ntaps=1, order='natural')
+            d['f3_out'] = K.pack_f16x3(w_out.float(), C, ntaps=1, order='natural')
+            d['qkv_l1'] = w_in.double().abs().sum(1).cpu()
+            d['qkv_babs'] = mha.in_proj_bias.detach().double().abs().cpu()
+            d['gb'] = (float(gn.weight.abs().max()), float(gn.bias.abs().max()))
+        return d
 
     def _pack(self):
         m = self.model
@@ -266,15 +281,26 @@ class TrainEngine:
     def _res_fwd(self, X: View, Y: View, rp, temb: torch.Tensor):
         B, H, W = X.B, X.H, X.W
         g1, g2 = rp['gn1'], rp['gn2']
-        st1 = K.gn_stats_pair(X, g1.weight.detach().float(), g1.bias.detach().float())
-        h = View.full(self._new(B, H, W, rp['co']))
-        self._conv([Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], rp['pk1'],
-                   rp['conv1'].bias.detach().float().contiguous(), h, H, W, temb=temb[:, rp['off']:],
-                   temb_ld=temb.shape[1])
+        co = rp['co']
+        st1 = K.gn_stats_pair(X, g1.weight.detach().float(), g1.bias.detach().float(), bound=True)
+        h = View.full(self._new(B, H, W, co))
+        seg1 = [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)]
+        b1 = rp['conv1'].bias.detach().float().contiguous()
+        if rp['f3_1'] is not None and K.x6_eligible(seg1, co, H, W):
+            K.conv3x3_f16x3(seg1, rp['f3_1'], b1, h, Hm=H, Wm=W,
+                            a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8), temb=temb[:, rp['off']:],
+                            temb_ld=temb.shape[1])
+        else:
+            self._conv(seg1, rp['pk1'], b1, h, H, W, temb=temb[:, rp['off']:], temb_ld=temb.shape[1])
         st2 = K.gn_stats_pair(h, g2.weight.detach().float(), g2.bias.detach().float())
-        self._conv([Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * rp['co'])],
-                   rp['pk2'], rp['b2'], Y, H, W)
-        self.tape.append(('res', X, h, Y, rp, st1, st2))
+        seg2 = [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)]
+        if rp['f3_2'] is not None and K.x6_eligible(seg2, co, H, W):
+            # the residual segment (raw X) in fp16 under GN1's per-image bound of |X|
+            K.conv3x3_f16x3(seg2, rp['f3_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
+                            a_bound=st1[4])
+        else:
+            self._conv(seg2, rp['pk2'], rp['b2'], Y, H, W)
+        self.tape.append(('res', X, h, Y, rp, st1[:4], st2))
 
     def _attn_fwd(self, Ypre: View, Yout: View, ap):
         B, H, W, C = Ypre.B, Ypre.H, Ypre.W, Ypre.C
@@ -282,13 +308,23 @@ class TrainEngine:
         gn, mha = ap['gn'], ap['mha']
         st = K.gn_stats_pair(Ypre, gn.weight.detach().float(), gn.bias.detach().float())
         qkv = self._new(B, H, W, 3 * C)
-        self._conv([Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], ap['pk_in'],
-                   mha.in_proj_bias.detach().float().contiguous(), View.full(qkv), H, W)
+        seg = [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)]
+        b_in = mha.in_proj_bias.detach().float().contiguous()
         o = self._new(B, H, W, C)
         lse = torch.empty((B, ap['heads'], N), dtype=torch.float32, device=self.device)
-        K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'])
-        self._conv([Seg(View.full(o), TAPS1)], ap['pk_out'], mha.out_proj.bias.detach().float().contiguous(), Yout, H,
-                   W, res=Ypre)
+        b_out = mha.out_proj.bias.detach().float().contiguous()
+        if ap['f3_in'] is not None:
+            # in_proj under the GN bound; out_proj: |O| <= max|V| (a convex combination of V rows)
+            ng = N * C // 8
+            K.conv_igemm_f16x3(seg, ap['f3_in'], b_in, View.full(qkv), Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*ap['gb'], ng))
+            K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'])
+            exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], ng)
+            K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], ap['f3_out'], b_out, Yout, Hm=H, Wm=W, a_exp=exps[2],
+                               res=Ypre)
+        else:
+            self._conv(seg, ap['pk_in'], b_in, View.full(qkv), H, W)
+            K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'])
+            self._conv([Seg(View.full(o), TAPS1)], ap['pk_out'], b_out, Yout, H, W, res=Ypre)
         self.tape.append(('attn', Ypre, Yout, qkv, o, lse, st, ap))
 
     # ------------------------------------------------------------------ backward

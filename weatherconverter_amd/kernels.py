@@ -909,9 +909,11 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
                  _ptr(dw1), s1, int(accumulate), s)
 
 
-def gn_stats_pair(v: View, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5, groups: int = 8):
+def gn_stats_pair(v: View, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5, groups: int = 8,
+                  bound: bool = False):
     """GroupNorm statistics of v once, finalized twice: (scale, shift) of the affine GN and
-    (sc0, sh0) = (rstd, -mean*rstd) of the plain normalisation (what the backward needs)."""
+    (sc0, sh0) = (rstd, -mean*rstd) of the plain normalisation (what the backward needs); with
+    bound=True a fifth result, the per-image bound of |v| (wc_gn_finalize_bound)."""
     v.check()
     B, HW, C = v.B, v.H * v.W, v.C
     lib = _native.load()
@@ -920,11 +922,16 @@ def gn_stats_pair(v: View, gamma: torch.Tensor, beta: torch.Tensor, eps: float =
     s = _stream()
     _native.call('wc_gn_stats', v.ptr, B, HW, C, v.ldc, groups, part.data_ptr(), s)
     out = [torch.empty((B, C), dtype=torch.float32, device=v.t.device) for _ in range(4)]
-    _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps, out[0].data_ptr(),
-                 out[1].data_ptr(), s)
+    if bound:
+        bnd = torch.empty((B, ), dtype=torch.float32, device=v.t.device)
+        _native.call('wc_gn_finalize_bound', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps,
+                     out[0].data_ptr(), out[1].data_ptr(), bnd.data_ptr(), s)
+    else:
+        _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, _ptr(gamma), _ptr(beta), eps,
+                     out[0].data_ptr(), out[1].data_ptr(), s)
     _native.call('wc_gn_finalize', part.data_ptr(), B, HW, C, groups, None, None, eps, out[2].data_ptr(),
                  out[3].data_ptr(), s)
-    return tuple(out)
+    return tuple(out) + ((bnd, ) if bound else ())
 
 
 def channel_sums(g: View) -> torch.Tensor:

@@ -89,7 +89,9 @@ struct IgTile {
 // TR (the pre-split qkv epilogue only): accumulate the transposed block (lanes = pixels, rows =
 // channels; the same products, B and A fragments swapped in the MFMA).
 // The pre-split qkv form (TR, BN 128) is held to 3 waves per SIMD (174 -> 168 VGPRs, 5 spilled).
-template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false>
+// P1 (UNIB, f16x3 segment 0 only): a pointwise 1x1 stride-1 conv whose tiles are whole rows of one
+// image (the attention projections): no tap stepping, no bounds or padding logic per element.
+template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false, bool P1 = false>
 __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_kernel(IgDev p) {
     using T = IgTile<BM, BN, F3, NPL>;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
@@ -179,12 +181,35 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
             rb[rs][j] = bload_u4(srdw, live && (j < T::B_FULL || i < items) ? base + (unsigned)i * 16u : OOB);
         }
     };
+    // K-step st = (tap, 16-channel chunk), tap-major; taps row-major over the kh x kw grid.  load0 is
+    // called for st = 0, 1, 2, ... in order, so the (chunk, tap) position advances incrementally: a
+    // division by the runtime chunk / tap counts per step cost ~60 scalar instructions, and the CU's
+    // one scalar unit serves all of its waves (SQ_INSTS_SALU was 7.4 per MFMA on the projections)
+    int nx_c0 = 0, nx_ky = 0, nx_kx = 0;
     auto load0 = [&](int st, auto RS) {
         constexpr int rs = decltype(RS)::value;
-        // K-step st = (tap, 16-channel chunk), tap-major; taps row-major over the kh x kw grid
-        const int tap = st / p.cpt;
-        const int c0 = (st - tap * p.cpt) * BK;
-        const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
+        const int c0 = nx_c0, ky = nx_ky, kx = nx_kx;
+        nx_c0 += BK;
+        if constexpr (P1) {  // every row of the tile is an in-bounds pixel of one image
+            const bool live = st < p.steps;
+#pragma unroll
+            for (int j = 0; j < T::A_PER_T; ++j)
+                ra[rs][j] = bload_f4(srd0, live ? (unsigned)(org0[j] + c0) * 4u : OOB);
+            if constexpr (PRO != 0) {
+                const unsigned o = live ? (unsigned)(b_tile * p.C0 + c0 + q4 * 4) * 4u : OOB;
+                rsc[rs][0] = bload_f4(srdsc, o);
+                rsh[rs][0] = bload_f4(srdsh, o);
+            }
+            load_w(st, RS);
+            return;
+        }
+        if (nx_c0 == p.C0) {
+            nx_c0 = 0;
+            if (++nx_kx == p.kw) {
+                nx_kx = 0;
+                ++nx_ky;
+            }
+        }
         const int dy = p.ty0 + ky * p.tdy, dx = p.tx0 + kx * p.tdx;
         const int tap_off = (dy * p.W0 + dx) * p.ldc0 + c0;
         const bool live = st < p.steps;
@@ -251,7 +276,7 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
                     }
                 }
             }
-            if (!(((rs == 0 ? aval0 : aval1) >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
+            if (!P1 && !(((rs == 0 ? aval0 : aval1) >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
             unsigned char* d = buf + a_wr + j * 64 * 16;
             if constexpr (F3) v = v * ascale;
             if (F3 && pro) {
@@ -581,14 +606,24 @@ int launch(const IgDev& d, hipStream_t stream) {
     const int tiles_m = (p.M + BM - 1) / BM;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(tiles_m * p.ntiles_n);
+    const bool p1 = p.kh == 1 && p.kw == 1 && p.ty0 == 0 && p.tx0 == 0 && p.sy == 1 && p.sx == 1 &&
+                    p.steps == p.steps0 && p.H0 == p.Hm && p.W0 == p.Wm;
     if constexpr (F3 && UNIB && PRO == 1 && ACT == WC_ACT_NONE) {
         if (p.qkv3) {  // pre-split attention projection
-            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true>), grid, dim3(NT), 0, stream, p);
+            if (p1) hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true, true>), grid, dim3(NT), 0, stream, p);
+            else hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true>), grid, dim3(NT), 0, stream, p);
             WC_CHECK_LAUNCH();
             return WC_OK;
         }
     }
     if (p.qkv3) return WC_E_ARG;
+    if constexpr (F3 && UNIB && PRO <= 1 && ACT == WC_ACT_NONE) {
+        if (p1) {  // the projections
+            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, false, true>), grid, dim3(NT), 0, stream, p);
+            WC_CHECK_LAUNCH();
+            return WC_OK;
+        }
+    }
     if (F3 && p.steps == p.steps0)  // f16x3 segment 0 only: 4-plane LDS stages
         hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, F3 ? 4 : 6>), grid, dim3(NT), 0, stream, p);
     else

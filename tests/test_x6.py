@@ -555,6 +555,41 @@ def test_igemm_f16x3_projections_and_head():
     assert rel_l2(out3.cpu().double(), ref3) < 2e-6
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('sw', [4, 8, 16, 32])
+def test_igemm_f16x3_pointwise_vector_epilogue(sw):
+    """The attention out-projection form of the pointwise f16x3 GEMM (transposed accumulators,
+    16-byte residual loads and stores): in-place residual Y += O W^T + b into a channel slice,
+    exact per-image absmax, and GroupNorm tile partials equal to a stats pass, for every sub-slot
+    width; vs float64."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(53)
+    B, H, C, N = 3, 16, 256, 8 * sw if 8 * sw >= 128 else 128
+    o = (torch.rand((B, H, H, C), generator=g) * 14 - 7) * torch.tensor([1.0, 0.01, 1.0])[:, None, None, None]
+    w = torch.randn((N, C), generator=g) / C**0.5
+    b = 0.1 * torch.randn(N, generator=g)
+    big = torch.randn((B, H, H, N + 64), generator=g) * 3
+    ref = o.double() @ w.double().t() + b.double() + big[..., 32:32 + N].double()
+    y = big.cuda()
+    yv = K.View(y, 32, N)
+    gp = K.GnPart.attach(y, sw) if (N + 64) % 32 == 0 and N % (8 * sw) == 0 else None
+    am = torch.zeros(B, device='cuda')
+    K.conv_igemm_f16x3([K.Seg(K.View.full(o.cuda()), [(0, 0)])], K.pack_f16x3(w.cuda(), C, ntaps=1, order='natural'),
+                       b.cuda(), yv, Hm=H, Wm=H, a_exp=K.f16x3_a_exp(0.0, 7.0, 2), res=yv, absmax=am,
+                       gn=gp, a_bound=None)
+    torch.cuda.synchronize()
+    got = y.cpu()
+    assert rel_l2(got[..., 32:32 + N].double(), ref) < 2e-6
+    assert torch.equal(got[..., :32], big[..., :32]) and torch.equal(got[..., 32 + N:], big[..., 32 + N:])
+    assert torch.equal(am.cpu(), got[..., 32:32 + N].reshape(B, -1).abs().amax(1))
+    if gp is not None:
+        gamma, beta = (1 + torch.randn(N, generator=g)).cuda(), torch.randn(N, generator=g).cuda()
+        a1 = K.gn_affine(yv, gamma, beta, bound=True, part=gp)
+        a0 = K.gn_affine(yv, gamma, beta, bound=True)
+        for u, v in zip(a1, a0):
+            assert torch.allclose(u, v, rtol=2e-6, atol=1e-7), (u - v).abs().max()
+
+
 # ---------------------------------------------------------------- producer absmax -> per-image f16x3 scale
 
 def _img_amax(o_bhwc):

@@ -459,6 +459,64 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
                     }
                 }
             }
+            return;
+        }
+        // ---- transposed NHWC epilogue (the pointwise projections, UNIB, identity map, N % 32 == 0):
+        // a lane holds pixel l32 of each 32-row block and channels 8 j + 4 half .. + 3 of each
+        // 32-channel block, so residual loads and output stores are 16-byte vectors (16 per lane
+        // instead of 64 scalar ones); per-channel bias and scale through LDS
+        if constexpr (UNIB) {
+            __syncthreads();  // the last K-step's fragment reads are done
+            float* sbias = reinterpret_cast<float*>(smem);
+            if (tid < BN) {
+                const int n = n0 + tid;
+                sbias[tid] = (n < p.N && p.bias) ? p.bias[n] : 0.f;
+                sbias[BN + tid] = n < p.N ? (F3 ? p.wsinv[n] * ainv : 1.0f) : 0.f;
+            }
+            __syncthreads();
+            const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + (long)b_tile * HWm * p.ldo);
+            const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + (long)b_tile * HWm * p.ldres : p.out);
+            const int prow = m0 - b_tile * HWm + wm * 64 + l32;  // pixel of this lane in block mb = 0
+            const int ncol = wn * 64 + 4 * half;                  // tile channel of j = 0 in block nb = 0
+            const bool nok[2] = {n0 + wn * 64 < p.N, n0 + wn * 64 + 32 < p.N};
+            f32x4 rv[2][2][4];
+            if (p.res) {
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            rv[mb][nb][j] = bload_f4(srd_res, nok[nb] ? (unsigned)((prow + 32 * mb) * p.ldres + n0 + ncol +
+                                                                                  32 * nb + 8 * j) * 4u : OOB);
+            }
+            float vmax = 0.f;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                if (!nok[nb]) continue;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = ncol + 32 * nb + 8 * j;
+                    const f32x4 badd = *reinterpret_cast<const f32x4*>(sbias + c);
+                    const f32x4 bmul = *reinterpret_cast<const f32x4*>(sbias + BN + c);
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb) {
+                        f32x4 v = f32x4{acc[mb][nb][4 * j], acc[mb][nb][4 * j + 1], acc[mb][nb][4 * j + 2],
+                                        acc[mb][nb][4 * j + 3]} * bmul + badd;
+                        if (p.res) v += rv[mb][nb][j];
+                        bstore_f4(srd_out, (unsigned)((prow + 32 * mb) * p.ldo + n0 + c) * 4u, v);
+                        vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * j + e] = v[e];
+                    }
+                }
+            }
+            if (p.absmax) block_absmax_atomic(p.absmax, b_tile, vmax);
+            if (p.gn_part) {
+                GnTile g{p.gn_part, p.gn_ncb, p.gn_sw, (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + wm,
+                         (p.gn_c0 + n0 + wn * 64) / 32};
+                gn_tile_partials_tr(acc, g, nok[1] ? 2 : (nok[0] ? 1 : 0));
+            }
         }
         return;
     }
@@ -617,9 +675,11 @@ int launch(const IgDev& d, hipStream_t stream) {
         }
     }
     if (p.qkv3) return WC_E_ARG;
-    if constexpr (F3 && UNIB && PRO <= 1 && ACT == WC_ACT_NONE) {
-        if (p1) {  // the projections
-            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, false, true>), grid, dim3(NT), 0, stream, p);
+    if constexpr (F3 && UNIB && PRO <= 1 && ACT == WC_ACT_NONE && BN == 128) {
+        if (p1 && p.ident && p.N % 32 == 0 && p.ldo % 4 == 0 && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0 &&
+            (!p.res || (p.ldres % 4 == 0 && (reinterpret_cast<uintptr_t>(p.res) & 15) == 0))) {
+            // the projections: transposed accumulators for the vector epilogue
+            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true, true>), grid, dim3(NT), 0, stream, p);
             WC_CHECK_LAUNCH();
             return WC_OK;
         }

@@ -30,6 +30,10 @@ WC_DEVICE void bstore_f1(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }
 
+WC_DEVICE void bstore_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 WC_DEVICE f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -160,6 +164,79 @@ WC_DEVICE void gn_tile_partials(const f32x16 (&acc)[2][NB], const GnTile& g, int
             const long idx = ((g.pix64 * g.ncb + g.cb0 + nb) * (32 / g.sw) + c / g.sw) * 2;
             g.part[idx] = mean;
             g.part[idx + 1] = m2;
+        }
+    }
+}
+
+// The same partials from the TRANSPOSED accumulators of conv_igemm_x6_kernel<..., TR> (lanes =
+// pixels): acc[mb][nb][4 j + e] is pixel 32 mb + (lane & 31) of the wave's 64, channel
+// 8 j + 4 (lane / 32) + e of column block nb.  A sub-slot of sw channels is the lane's quads
+// (j, half) with (8 j + 4 half) / sw equal, reduced over the 32 pixels of each half (and over the
+// halves for sw >= 8); two passes over the registers, fixed butterfly order.
+template <int NB>
+WC_DEVICE void gn_tile_partials_tr(const f32x16 (&acc)[2][NB], const GnTile& g, int nvalid) {
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const float inv_n = 1.0f / (64.0f * (float)g.sw);
+    const int lsw = __builtin_ctz((unsigned)g.sw);  // sw is a power of two
+    auto red = [&](float v) {
+        for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (g.sw >= 8) v += __shfl_xor(v, 32, 64);
+        return v;
+    };
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+        if (nb >= nvalid) break;
+        // quad sums over e and mb; sub-slot of quad (j, half): (8 j + 4 half) / sw
+        float qs[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float t = 0.f;
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t += acc[mb][nb][4 * j + e];
+            qs[j] = t;
+        }
+        const int nsub = 32 >> lsw;  // sub-slots in the block: 8, 4, 2, 1
+        float mean[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // the lane's part of the sub-slot containing quad j: quads j' with (8 j' + 4 h) / sw equal
+            const int s = (8 * j + 4 * half) >> lsw;
+            float t = 0.f;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                if (((8 * jj + 4 * half) >> lsw) == s) t += qs[jj];
+            mean[j] = red(t) * inv_n;
+        }
+        float q2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float t = 0.f;
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float d = acc[mb][nb][4 * j + e] - mean[j];
+                    t = fmaf(d, d, t);
+                }
+            q2[j] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int s = (8 * j + 4 * half) >> lsw;
+            float t = 0.f;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                if (((8 * jj + 4 * half) >> lsw) == s) t += q2[jj];
+            const float m2 = red(t);
+            // one writer per sub-slot: lane 0 of the half owning its first quad, at its first j
+            const bool first_j = ((8 * j + 4 * half) & (g.sw - 1)) == 0;
+            if ((lane & 31) == 0 && first_j && s < nsub) {
+                const long idx = ((g.pix64 * g.ncb + g.cb0 + nb) * nsub + s) * 2;
+                g.part[idx] = mean[j];
+                g.part[idx + 1] = m2;
+            }
         }
     }
 }

@@ -185,6 +185,24 @@ int wc_convtr4x4s2_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_by
 int wc_conv_igemm_f16x3_qkv(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
                             const float* w_inv_scale, void* qkv3, int C, int heads, const int* exps,
                             void* stream);
+/* The attention projections (unet_base.py:110-116 in_proj / out_proj) on an A operand split
+ * beforehand: wc_split_f16x3_tiled writes, from the rows of an NHWC view (B images x HW pixels,
+ * C channels; HW % 128 == 0, C % 32 == 0, 16-byte aligned, ldc % 4 == 0) optionally through a
+ * GroupNorm affine scale/shift[B][C] (+ SiLU), the values x 2^a_exp as two round-to-nearest fp16
+ * pieces in the GEMM's LDS stage order: a3[B*HW/128][C/16][piece 2][k-half 2][128][8] (4 bytes
+ * per element; a3_bytes = B*HW*C*4).  The caller guarantees |value| * 2^a_exp <= 2^14. */
+int wc_split_f16x3_tiled(const float* src, int ldc, int B, int HW, int C, const float* scale, const float* shift,
+                         int silu, int a_exp, void* a3, int64_t a3_bytes, void* stream);
+/* wc_conv_igemm_f16x3 (1x1, no prologue) whose A operand is a3 from wc_split_f16x3_tiled at the same
+ * a_exp: both operands of every K-step are copied to LDS by LDS-DMA.  args->seg[0] describes the
+ * view a3 was made from (1x1 tap, stride 1); N % 128 == 0; identity output map into a 16-byte
+ * aligned view (ldo % 4 == 0), optional residual view (same), bias, absmax_out, GN partials. */
+int wc_proj_f16x3(const wc_conv_args* args, const void* a3, int64_t a3_bytes, const void* w3, int64_t w3_bytes,
+                  int a_exp, const float* w_inv_scale, void* stream);
+/* wc_conv_igemm_f16x3_qkv on a pre-split A operand (the GroupNorm affine applied by the split). */
+int wc_proj_f16x3_qkv(const wc_conv_args* args, const void* a3, int64_t a3_bytes, const void* w3, int64_t w3_bytes,
+                      int a_exp, const float* w_inv_scale, void* qkv3, int C, int heads, const int* exps,
+                      void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* GroupNorm statistics (replaces nn.GroupNorm(8, C) reductions, unet_base.py:90,104,110,448)  */

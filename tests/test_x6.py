@@ -556,8 +556,9 @@ def test_igemm_f16x3_projections_and_head():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('pa', [False, True])
 @pytest.mark.parametrize('sw', [4, 8, 16, 32])
-def test_igemm_f16x3_pointwise_vector_epilogue(sw):
+def test_igemm_f16x3_pointwise_vector_epilogue(sw, pa):
     """The attention out-projection form of the pointwise f16x3 GEMM (transposed accumulators,
     16-byte residual loads and stores): in-place residual Y += O W^T + b into a channel slice,
     exact per-image absmax, and GroupNorm tile partials equal to a stats pass, for every sub-slot
@@ -574,9 +575,13 @@ def test_igemm_f16x3_pointwise_vector_epilogue(sw):
     yv = K.View(y, 32, N)
     gp = K.GnPart.attach(y, sw) if (N + 64) % 32 == 0 and N % (8 * sw) == 0 else None
     am = torch.zeros(B, device='cuda')
-    K.conv_igemm_f16x3([K.Seg(K.View.full(o.cuda()), [(0, 0)])], K.pack_f16x3(w.cuda(), C, ntaps=1, order='natural'),
-                       b.cuda(), yv, Hm=H, Wm=H, a_exp=K.f16x3_a_exp(0.0, 7.0, 2), res=yv, absmax=am,
-                       gn=gp, a_bound=None)
+    e = K.f16x3_a_exp(0.0, 7.0, 2)
+    w3 = K.pack_f16x3(w.cuda(), C, ntaps=1, order='natural')
+    ov = K.View.full(o.cuda())
+    if pa:  # pre-split A operand (wc_split_f16x3_tiled + wc_proj_f16x3)
+        K.proj_f16x3(ov, K.split_f16x3_tiled(ov, e), w3, b.cuda(), yv, a_exp=e, res=yv, absmax=am, gn=gp)
+    else:
+        K.conv_igemm_f16x3([K.Seg(ov, [(0, 0)])], w3, b.cuda(), yv, Hm=H, Wm=H, a_exp=e, res=yv, absmax=am, gn=gp)
     torch.cuda.synchronize()
     got = y.cpu()
     assert rel_l2(got[..., 32:32 + N].double(), ref) < 2e-6
@@ -588,6 +593,51 @@ def test_igemm_f16x3_pointwise_vector_epilogue(sw):
         a0 = K.gn_affine(yv, gamma, beta, bound=True)
         for u, v in zip(a1, a0):
             assert torch.allclose(u, v, rtol=2e-6, atol=1e-7), (u - v).abs().max()
+
+
+@pytest.mark.gpu
+def test_projections_presplit_bit_identical_to_register_staged(monkeypatch):
+    """The attention projections on a pre-split A operand (GN applied and split once by
+    wc_split_f16x3_tiled, both operands copied by LDS-DMA) compute the same split values in the
+    same MFMA order as the register-staged implicit GEMM: the UNet forward (256-cfg at 64 px, B=2,
+    per-sample t) is bit-identical with WC_PROJ_PA=1 and 0; and the pre-split q/k/v equal too."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.config import model_config
+    from weatherconverter_amd.diffusion_model.models.unet_base import Unet
+    from weatherconverter_amd.synthetic import init_synthetic_
+    mc = model_config(256)
+    mc.im_size = 64
+    net = Unet(mc)
+    init_synthetic_(net, seed=0)
+    net = net.cuda().eval()
+    x = torch.randn((2, 3, 64, 64), generator=torch.Generator().manual_seed(9)).cuda()
+    outs = []
+    for pa in ('1', '0'):
+        monkeypatch.setenv('WC_PROJ_PA', pa)
+        with torch.no_grad():
+            outs.append(net(x, torch.tensor([700, 3]).cuda()).cpu())
+    assert torch.equal(outs[0], outs[1])
+    # the qkv projection alone: GN prologue in the kernel vs GN in the split pass
+    g = torch.Generator().manual_seed(57)
+    B, H, C, heads = 2, 16, 256, 4
+    y = torch.randn((B, C, H, H), generator=g) * 2 + 1
+    gamma, beta = 1 + 0.3 * torch.randn(C, generator=g), 0.3 * torch.randn(C, generator=g)
+    sc, sh = _gn_affine(y, gamma, beta)
+    w = torch.randn((3 * C, C), generator=g) / C**0.5
+    bias = 0.1 * torch.randn(3 * C, generator=g)
+    w3 = K.pack_f16x3(w.cuda(), C, ntaps=1, order='natural')
+    yv = K.View.full(_nhwc(y).cuda())
+    e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * H * C // 8)
+    exps = K.attention_exps_from_norms(w.double().abs().sum(1), bias.double().abs(), float(gamma.abs().max()),
+                                       float(beta.abs().max()), H * H * C // 8)
+    q0 = torch.zeros(B * 6 * C * H * H, dtype=torch.int16, device='cuda')
+    q1 = torch.ones_like(q0)
+    K.conv_igemm_f16x3_qkv(K.Seg(yv, [(0, 0)], scale=sc.float().cuda(), shift=sh.float().cuda()), w3, bias.cuda(), q0,
+                           Hm=H, Wm=H, a_exp=e, C=C, heads=heads, exps=exps)
+    a3 = K.split_f16x3_tiled(yv, e, sc.float().cuda().contiguous(), sh.float().cuda().contiguous())
+    K.proj_f16x3_qkv(yv, a3, w3, bias.cuda(), q1, a_exp=e, C=C, heads=heads, exps=exps)
+    torch.cuda.synchronize()
+    assert torch.equal(q0, q1)
 
 
 # ---------------------------------------------------------------- producer absmax -> per-image f16x3 scale

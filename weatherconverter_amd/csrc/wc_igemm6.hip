@@ -60,6 +60,7 @@ struct IgDev {
     float* gn_part;      // optional GroupNorm tile partials (UNIB only; wcx6::gn_tile_partials)
     int gn_ncb, gn_sw, gn_c0, gn_p64, gn_np64;
     unsigned short* qkv3;  // optional: attention in-projection written pre-split (wc_conv_igemm_f16x3_qkv)
+    const unsigned char* a3;  // PA: segment 0 already scaled and split (wc_split_f16x3_tiled layout)
     int qC, qD;            // C and the head dim of that projection
     float qscale[3];       // 2^exps of q, k, v
 };
@@ -91,10 +92,21 @@ struct IgTile {
 // The pre-split qkv form (TR, BN 128) is held to 3 waves per SIMD (174 -> 168 VGPRs, 5 spilled).
 // P1 (UNIB, f16x3 segment 0 only): a pointwise 1x1 stride-1 conv whose tiles are whole rows of one
 // image (the attention projections): no tap stepping, no bounds or padding logic per element.
-template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false, bool P1 = false>
+// PA (with P1): the A operand arrives pre-scaled and pre-split in the LDS stage order
+// (wc_split_f16x3_tiled), so both operands of a K-step are 16 KiB copied HBM/L2 -> LDS by
+// LDS-DMA (4 wave-instructions per wave, no registers, no VALU) into a 3-stage ring: the copy of
+// step s + 2 is issued while step s computes, one barrier per step.
+template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false, bool P1 = false,
+          bool PA = false>
 __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_kernel(IgDev p) {
     using T = IgTile<BM, BN, F3, NPL>;
+    static_assert(!PA || (P1 && F3 && NPL == 4 && UNIB && PRO == 0), "PA: pre-split pointwise f16x3");
+    // PA: the 3 ring stages are distinct LDS objects, so the compiler sees that a step's fragment
+    // reads cannot alias the LDS-DMA in flight into another stage (one array would make it wait
+    // vmcnt(0) before every read, i.e. for the copy just issued)
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char smem_b[PA ? T::STAGE : 16];
+    __shared__ __attribute__((aligned(16))) unsigned char smem_c[PA ? T::STAGE : 16];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -377,6 +389,63 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
         else compute6(buf);
     };
 
+    if constexpr (PA) {
+        // ---- K loop on pre-split operands: LDS-DMA ring of 3 stages (step s in stage s % 3) ----
+        const unsigned char* asrc = p.a3 + (long)(m0 / BM) * p.steps * 8192 + tid * 16;
+        const unsigned char* bsrc = reinterpret_cast<const unsigned char*>(p.w6) +
+                                    (long)tile_n * p.steps * T::BSTEP0 + tid * 16;
+        static_assert(T::ASTAGE == 8192 && T::BSTEP0 == 8192, "PA: 128 x 16 A and B steps");
+        auto stage = [&](auto S) -> unsigned char* {
+            constexpr int SV = decltype(S)::value;
+            if constexpr (SV == 0) return smem;
+            else if constexpr (SV == 1) return smem_b;
+            else return smem_c;
+        };
+        // The copies are issued as inline assembly, outside the compiler's wait tracking (which
+        // cannot tell the ring's stages apart and waits for every copy in flight before each
+        // step's barrier, shrinking the copy's window from two steps to one); the ring's own
+        // s_waitcnt vmcnt below orders them.  M0 (the LDS base of an LDS-DMA) is written only here.
+        auto dma = [&](int st, unsigned char* buf) {
+            const unsigned dst = __builtin_amdgcn_readfirstlane(
+                (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(buf) + wave * 1024);
+            const unsigned char* a0 = asrc + (long)st * 8192;
+            const unsigned char* b0 = bsrc + (long)st * T::BSTEP0;
+            asm volatile(
+                "s_mov_b32 m0, %4\n\t"
+                "global_load_lds_dwordx4 %0, off\n\t"
+                "s_add_u32 m0, %4, 0x1000\n\t"
+                "global_load_lds_dwordx4 %1, off\n\t"
+                "s_add_u32 m0, %4, 0x2000\n\t"
+                "global_load_lds_dwordx4 %2, off\n\t"
+                "s_add_u32 m0, %4, 0x3000\n\t"
+                "global_load_lds_dwordx4 %3, off"
+                :
+                : "v"(a0), "v"(a0 + 4096), "v"(b0), "v"(b0 + 4096), "s"(dst)
+                : "memory", "m0");
+        };
+        const std::integral_constant<int, 0> S0;
+        const std::integral_constant<int, 1> S1;
+        const std::integral_constant<int, 2> S2;
+        auto kstep = [&](auto S, int step) {
+            constexpr int SV = decltype(S)::value;
+            // this wave's copy of step `step` landed (the younger step + 1 may still fly), then
+            // everyone's; and every wave is done with step - 1, whose stage step + 2 reuses
+            if (step + 1 < p.steps) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            if (step + 2 < p.steps) dma(step + 2, stage(std::integral_constant<int, (SV + 2) % 3>{}));
+            compute3(stage(S));
+        };
+        dma(0, smem);
+        if (p.steps > 1) dma(1, smem_b);
+        int step = 0;
+        for (; step + 3 <= p.steps; step += 3) {
+            kstep(S0, step);
+            kstep(S1, step + 1);
+            kstep(S2, step + 2);
+        }
+        if (step < p.steps) kstep(S0, step);
+        if (step + 1 < p.steps) kstep(S1, step + 1);
+    } else {
     // ---- K loop: one barrier per step, two steps per iteration (register stages 0 / 1) ----
     const std::integral_constant<int, 0> R0;
     const std::integral_constant<int, 1> R1;
@@ -395,6 +464,7 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
         if (step + 2 >= p.steps) break;
         store(smem, step + 2, R0);
         __syncthreads();
+    }
     }
 
     // ---- epilogue: pre-split attention projection (wc_conv_igemm_f16x3_qkv, TR) ----
@@ -666,6 +736,15 @@ int launch(const IgDev& d, hipStream_t stream) {
     dim3 grid(tiles_m * p.ntiles_n);
     const bool p1 = p.kh == 1 && p.kw == 1 && p.ty0 == 0 && p.tx0 == 0 && p.sy == 1 && p.sx == 1 &&
                     p.steps == p.steps0 && p.H0 == p.Hm && p.W0 == p.Wm;
+    if constexpr (F3 && UNIB && PRO == 0 && ACT == WC_ACT_NONE && BM == 128 && BN == 128) {
+        if (p.a3) {  // pre-split A operand: LDS-DMA pipeline, transposed accumulators (both epilogues)
+            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, 0, true, ACT, true, 4, true, true, true>), grid, dim3(NT), 0,
+                               stream, p);
+            WC_CHECK_LAUNCH();
+            return WC_OK;
+        }
+    }
+    if (p.a3) return WC_E_ARG;
     if constexpr (F3 && UNIB && PRO == 1 && ACT == WC_ACT_NONE) {
         if (p.qkv3) {  // pre-split attention projection
             if (p1) hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true, true>), grid, dim3(NT), 0, stream, p);
@@ -864,4 +943,131 @@ extern "C" int wc_conv_igemm_f16x3(const wc_conv_args* a, const void* w3, int64_
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (BN == 64) return dispatch<256, 64>(d, pro, a->act, true, s);
     return dispatch<128, 128>(d, pro, a->act, true, s);
+}
+
+// ---- pointwise projections on a pre-split A operand (PA) ----
+
+namespace {
+
+// a3[mt][ks][piece][k-half][row 128][8 x fp16] from the fp32 rows of an NHWC view: optional GroupNorm
+// affine (+ SiLU), x 2^a_exp, two-piece round-to-nearest fp16 split (wcx6::split2_f16).  A wave owns
+// 64 rows x 32 channels: 128-byte row reads, 1 KiB contiguous stores per (step, piece, k-half).
+__global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restrict__ src, int ldc, int HW, int K,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int silu, float ascale,
+                                                          unsigned char* __restrict__ a3) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int row = blockIdx.x * 64 + lane;
+    const int g32 = blockIdx.y * 4 + wave;
+    if (g32 * 32 >= K) return;
+    const int b = row / HW;
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(src + (long)row * ldc + g32 * 32);
+    f32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = s4[i];
+    if (scale) {
+        const f32x4* sc4 = reinterpret_cast<const f32x4*>(scale + (long)b * K + g32 * 32);
+        const f32x4* sh4 = reinterpret_cast<const f32x4*>(shift + (long)b * K + g32 * 32);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            v[i] = v[i] * sc4[i] + sh4[i];
+            if (silu) {
+                v[i].x = silu_fast(v[i].x); v[i].y = silu_fast(v[i].y);
+                v[i].z = silu_fast(v[i].z); v[i].w = silu_fast(v[i].w);
+            }
+        }
+    }
+    const int mt = row >> 7, r = row & 127, KS = K / 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const long step = (long)mt * KS + 2 * g32 + h;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            u32x2 h0, l0, h1, l1;
+            split2_f16(v[4 * h + 2 * kh] * ascale, h0, l0);
+            split2_f16(v[4 * h + 2 * kh + 1] * ascale, h1, l1);
+            unsigned char* d = a3 + ((step * 2 * 2 + kh) * 128 + r) * 16;
+            *reinterpret_cast<u32x4*>(d) = u32x4{h0.x, h0.y, h1.x, h1.y};
+            *reinterpret_cast<u32x4*>(d + 2 * 128 * 16) = u32x4{l0.x, l0.y, l1.x, l1.y};
+        }
+    }
+}
+
+// shared checks of the two PA entry points: the A operand's view shape in args->seg[0] (1x1,
+// stride 1, no prologue: a3 already carries it), a3 of M x C x 4 bytes
+int prepare_pa(const wc_conv_args* a, const void* a3, int64_t a3_bytes, const void* w3, IgDev& d, long& k) {
+    if (!a3 || (reinterpret_cast<uintptr_t>(a3) & 15)) return WC_E_ARG;
+    if (a->nseg != 1 || a->seg[0].scale || a->act) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (s0.ntaps != 1 || s0.dy[0] || s0.dx[0] || s0.sy != 1 || s0.sx != 1 || s0.H != a->Hm || s0.W != a->Wm)
+        return WC_E_SHAPE;
+    if ((a->Hm * a->Wm) % 128 || s0.C % 32 || a->N % 128) return WC_E_SHAPE;
+    const int st = prepare(a, w3, d, k);
+    if (st != WC_OK) return st;
+    if (a3_bytes != (long)d.M * s0.C * 4) return WC_E_SHAPE;
+    d.a3 = reinterpret_cast<const unsigned char*>(a3);
+    return WC_OK;
+}
+
+}  // namespace
+
+extern "C" int wc_split_f16x3_tiled(const float* src, int ldc, int B, int HW, int C, const float* scale,
+                                    const float* shift, int silu, int a_exp, void* a3, int64_t a3_bytes,
+                                    void* stream) {
+    if (!src || !a3 || (scale == nullptr) != (shift == nullptr)) return WC_E_ARG;
+    if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    if (B <= 0 || HW <= 0 || HW % 128 || C <= 0 || C % 32 || ldc < C || ldc % 4) return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(a3) & 15)) return WC_E_SHAPE;
+    if (scale && ((reinterpret_cast<uintptr_t>(scale) & 15) || (reinterpret_cast<uintptr_t>(shift) & 15)))
+        return WC_E_SHAPE;
+    const long M = (long)B * HW;
+    if (a3_bytes != M * C * 4 || M > (1L << 30)) return WC_E_SHAPE;
+    dim3 grid((unsigned)(M / 64), (unsigned)((C / 32 + 3) / 4));
+    hipLaunchKernelGGL(split_tiled_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), src, ldc, HW, C,
+                       scale, shift, silu, ldexpf(1.0f, a_exp), reinterpret_cast<unsigned char*>(a3));
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_proj_f16x3(const wc_conv_args* a, const void* a3, int64_t a3_bytes, const void* w3,
+                             int64_t w3_bytes, int a_exp, const float* w_inv_scale, void* stream) {
+    if (!a || !w_inv_scale || a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    IgDev d;
+    long k;
+    const int st = prepare_pa(a, a3, a3_bytes, w3, d, k);
+    if (st != WC_OK) return st;
+    if (!d.ident || d.ldo % 4 || (reinterpret_cast<uintptr_t>(d.out) & 15)) return WC_E_SHAPE;
+    if (d.res && (d.ldres % 4 || (reinterpret_cast<uintptr_t>(d.res) & 15))) return WC_E_SHAPE;
+    if (a->temb) return WC_E_ARG;
+    if (w3_bytes != (long)(a->N / 128) * d.steps0 * 128 * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    d.a_exp = a_exp;
+    d.wsinv = w_inv_scale;
+    return launch<128, 128, 0, true, WC_ACT_NONE, true>(d, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int wc_proj_f16x3_qkv(const wc_conv_args* a, const void* a3, int64_t a3_bytes, const void* w3,
+                                 int64_t w3_bytes, int a_exp, const float* w_inv_scale, void* qkv3, int C, int heads,
+                                 const int* exps, void* stream) {
+    if (!a || !qkv3 || !exps || !w_inv_scale || a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    if (C <= 0 || heads <= 0 || C % heads || (C / heads) % 32 || a->N != 3 * C) return WC_E_SHAPE;
+    if (a->res || a->temb || a->absmax_out || a->gn_part || a->out_nchw) return WC_E_ARG;
+    if (reinterpret_cast<uintptr_t>(qkv3) & 15) return WC_E_SHAPE;
+    for (int i = 0; i < 3; ++i)
+        if (exps[i] < -60 || exps[i] > 60) return WC_E_ARG;
+    wc_conv_args aa = *a;
+    aa.out = reinterpret_cast<float*>(qkv3);  // unused by the split epilogue; keeps prepare's checks uniform
+    aa.ldo = a->N;
+    aa.Ho = a->Hm; aa.Wo = a->Wm; aa.osy = aa.osx = 1; aa.ooy = aa.oox = 0;
+    IgDev d;
+    long k;
+    const int st = prepare_pa(&aa, a3, a3_bytes, w3, d, k);
+    if (st != WC_OK) return st;
+    if (w3_bytes != (long)(a->N / 128) * d.steps0 * 128 * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    d.a_exp = a_exp;
+    d.wsinv = w_inv_scale;
+    d.qkv3 = reinterpret_cast<unsigned short*>(qkv3);
+    d.qC = C;
+    d.qD = C / heads;
+    for (int i = 0; i < 3; ++i) d.qscale[i] = ldexpf(1.0f, exps[i]);
+    return launch<128, 128, 0, true, WC_ACT_NONE, true>(d, reinterpret_cast<hipStream_t>(stream));
 }

@@ -367,8 +367,15 @@ class UnetEngine:
                 # the in_proj epilogue writes Q, K, V already scaled and split (fp16 pieces, V
                 # transposed in the PV key order); the attention copies K / V^T tiles by LDS-DMA
                 qkv3 = torch.empty(B * 6 * C * N, dtype=torch.int16, device=self.device)
-                K.conv_igemm_f16x3_qkv(seg, p.w_in_f3, p.b_in, qkv3, Hm=H, Wm=W, a_exp=a_exp, C=C, heads=p.heads,
-                                       exps=exps)
+                if K.proj_pa_enabled() and K.proj_pa_ok(Y, 3 * C):
+                    # GN applied and split once per element (not once per 128-column N tile), then
+                    # both GEMM operands staged by LDS-DMA
+                    a3 = K.split_f16x3_tiled(Y, a_exp, sc, sh)
+                    K.proj_f16x3_qkv(Y, a3, p.w_in_f3, p.b_in, qkv3, a_exp=a_exp, C=C, heads=p.heads, exps=exps)
+                    del a3
+                else:
+                    K.conv_igemm_f16x3_qkv(seg, p.w_in_f3, p.b_in, qkv3, Hm=H, Wm=W, a_exp=a_exp, C=C,
+                                           heads=p.heads, exps=exps)
                 K.attention_presplit(qkv3, o.view(B * N, C), B, N, C, p.heads, exps)
             else:
                 qkv = self._new(B, H, W, 3 * C)
@@ -376,8 +383,18 @@ class UnetEngine:
                 K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
             gp = K.GnPart.of(Y)
             fused = K.gn_conv_ok(Y, gp, p.w_out_f3.N, H, W, 256 if p.w_out_f3.N <= 64 else 128)
-            K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y,
-                               absmax=absmax, gn=gp if fused else None)
+            ov = View.full(o)
+            # (the out-projection stays on the register-staged GEMM: a separate split pass of O costs
+            # more than the pre-split GEMM saves there, 0.27 vs 0.08 ms per 256-px step; WC_PROJ_PA=2
+            # forces it, for measurement)
+            if os.environ.get('WC_PROJ_PA') == '2' and K.proj_pa_ok(ov, C) and K.proj_pa_ok(Y, C):
+                a3 = K.split_f16x3_tiled(ov, exps[2])
+                K.proj_f16x3(ov, a3, p.w_out_f3, p.b_out, Y, a_exp=exps[2], res=Y, absmax=absmax,
+                             gn=gp if fused else None)
+                del a3
+            else:
+                K.conv_igemm_f16x3([Seg(ov, TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y,
+                                   absmax=absmax, gn=gp if fused else None)
             self._gn_fill(Y, fused)
             return absmax is not None
         qkv = self._new(B, H, W, 3 * C)

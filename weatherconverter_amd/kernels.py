@@ -538,6 +538,62 @@ def conv_igemm_f16x3_qkv(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], q
            ctypes.cast(ex, ctypes.c_void_p), _stream())
 
 
+def proj_pa_enabled() -> bool:
+    """Attention projections on a pre-split A operand (wc_split_f16x3_tiled + wc_proj_f16x3[_qkv]);
+    WC_PROJ_PA=0 keeps the register-staged implicit GEMM (for A/B measurement)."""
+    return os.environ.get('WC_PROJ_PA', '1') != '0'
+
+
+def proj_pa_ok(v: View, N: int) -> bool:
+    """Shapes the pre-split projection takes: HW % 128 == 0, C % 32 == 0, N % 128 == 0, aligned view."""
+    return (v.H * v.W) % 128 == 0 and v.C % 32 == 0 and N % 128 == 0 and v.ptr % 16 == 0 and v.ldc % 4 == 0
+
+
+def split_f16x3_tiled(v: View, a_exp: int, scale: Optional[torch.Tensor] = None,
+                      shift: Optional[torch.Tensor] = None, silu: bool = False) -> torch.Tensor:
+    """The rows of v (optionally GN-affine, + SiLU) x 2^a_exp as two fp16 pieces in the projection
+    GEMM's LDS stage order (wc_split_f16x3_tiled); an int16 tensor of 2 * B*H*W*C elements."""
+    v.check()
+    _req(proj_pa_ok(v, 128), 'pre-split rows: HW % 128 == 0, C % 32 == 0, 16-byte aligned view')
+    if scale is not None:
+        _req(scale.shape == (v.B, v.C) and shift.shape == (v.B, v.C) and scale.is_contiguous()
+             and shift.is_contiguous() and scale.dtype == torch.float32, 'GN affine [B][C]')
+    a3 = torch.empty(2 * v.B * v.H * v.W * v.C, dtype=torch.int16, device=v.t.device)
+    _timed('split_tiled_kernel', 'wc_split_f16x3_tiled', 8.0 * v.B * v.H * v.W * v.C if PROFILE is not None else 0.0,
+           v.ptr, v.ldc, v.B, v.H * v.W, v.C, _ptr(scale), _ptr(shift), int(silu), int(a_exp), a3.data_ptr(),
+           a3.numel() * 2, _stream())
+    return a3
+
+
+def proj_f16x3(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[torch.Tensor], out: View, *, a_exp: int,
+               res: Optional[View] = None, absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None):
+    """out = (a3 . W^T) x 2^-(a_exp + sW) + bias (+ res): the 1x1 projection of the view v that a3 was
+    split from (wc_proj_f16x3)."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3n' and w3.C0 == v.C and w3.C1 == 0,
+         'f16x3 projection weight (natural order)')
+    seg = Seg(v, [(0, 0)])
+    a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
+    _timed('conv_igemm_x6_kernel<128, 128, 0, true, 0, true> (pre-split A)', 'wc_proj_f16x3',
+           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
+           a3.numel() * 2, w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
+
+
+def proj_f16x3_qkv(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[torch.Tensor], qkv3: torch.Tensor, *,
+                   a_exp: int, C: int, heads: int, exps: Tuple[int, int, int]):
+    """conv_igemm_f16x3_qkv on the pre-split (GN already applied) A operand a3 (wc_proj_f16x3_qkv)."""
+    _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3n' and w3.N == 3 * C, 'f16x3 qkv weight')
+    B = v.B
+    _req(qkv3.is_cuda and qkv3.dtype == torch.int16 and qkv3.is_contiguous()
+         and qkv3.numel() == B * 6 * C * v.H * v.W, 'pre-split qkv buffer: int16, B * 6 * C * HW elements')
+    seg = Seg(v, [(0, 0)])
+    a = _conv_args([seg], w3.N, bias, None, v.H, v.W, None, 0, None, (1, 1, 0, 0), None, 0, out_dummy=True)
+    ex = (ctypes.c_int * 3)(*[int(e) for e in exps])  # host array, read during the call
+    _timed('conv_igemm_x6_kernel<128, 128, 0, true, 0, true> (qkv pre-split, pre-split A)', 'wc_proj_f16x3_qkv',
+           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
+           a3.numel() * 2, w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(),
+           qkv3.data_ptr(), C, heads, ctypes.cast(ex, ctypes.c_void_p), _stream())
+
+
 def attention_presplit(qkv3: torch.Tensor, out: torch.Tensor, B: int, N: int, C: int, heads: int,
                        exps: Tuple[int, int, int]):
     """f16x3 attention on the pre-split projection of conv_igemm_f16x3_qkv (same exps)."""

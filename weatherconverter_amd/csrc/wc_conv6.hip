@@ -458,11 +458,10 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         // writes are the next chunk's halo at the chunk's last tap, so there is ONE barrier per
         // chunk (9 taps x 12 MFMAs) instead of one per tap.  Set parity is compile-time: step
         // s = 9c + mt uses set (c + mt) & 1, and chunks run in pairs.
-        // two register sets (the next step's fragments land while this one computes); the residual
-        // forms would use one (loads issued after the step's MFMAs), but even then their centre
-        // staging pushes them past the 3-wave register budget (420 B/lane of spills), so the
-        // dispatcher keeps those on LDS-staged weights
-        constexpr int NS = RES ? 1 : 2;
+        // two register sets (the next step's fragments land while this one computes), also for the
+        // residual forms: the last 3x3 chunk is peeled (compile-time), so the residual centres it
+        // stages are not live through the chunk loop
+        constexpr int NS = 2;
         u32x4 wreg[NS][2][2];  // [set][nb][piece]
         const unsigned wlane = (unsigned)(half * T::BPLANE + (wn * 64 + l32) * 16);
         auto load_w = [&](int set, int st) {
@@ -496,62 +495,68 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                     acc[mb][nb] = mfma_f16(fa[mb][1], wreg[set][nb][0], acc[mb][nb]);
                 }
         };
+        // Chunk c uses halo buffer and weight-set parity PV = (nck0 - 1 - c) & 1, counted from the
+        // end, so the peeled last 3x3 chunk always has PV = 0 (two compile-time variants of it
+        // flowing into one epilogue made the register allocator spill hundreds of VGPRs).
+        const int pv0 = (p.nck0 - 1) & 1;
         load_halo0(0);
-        load_w(0, 0);
-        write_halo(0, true);
+        if (pv0) load_w(1, 0);
+        else load_w(0, 0);
+        write_halo(pv0, true);
         __syncthreads();
-        auto chunk = [&](auto P, int c) {
-            constexpr int PV = decltype(P)::value;  // c & 1: the chunk's halo buffer and set parity
+        auto chunk = [&](auto P, auto L, int c) {
+            constexpr int PV = decltype(P)::value;  // the chunk's halo buffer and set parity
+            constexpr bool LAST = decltype(L)::value != 0;  // the last 3x3 chunk (compile-time)
 #pragma unroll
             for (int mt = 0; mt < 9; ++mt) {
                 const int st = 9 * c + mt;
-                if (NS == 2 && st + 1 < S) load_w((mt + 1 + PV) & (NS - 1), st + 1);
+                if (st + 1 < S) load_w((mt + 1 + PV) & 1, st + 1);
                 if (mt == 7) {
-                    if (c + 1 < p.nck0) load_halo0(c + 1);
+                    if constexpr (!LAST) load_halo0(c + 1);
                     else if constexpr (RES) load_center(I0, 0);
                 }
-                if constexpr (RES) {
-                    if (mt == 8 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
+                if constexpr (RES && LAST) {
+                    if (mt == 8 && p.nck1 > 1) load_center(I1, 1);
                 }
-                compute_w((mt + PV) & (NS - 1), PV, (mt / 3) * HWD + mt % 3);
-                if (NS == 1 && st + 1 < S) load_w(0, st + 1);
+                compute_w((mt + PV) & 1, PV, (mt / 3) * HWD + mt % 3);
             }
-            if (c + 1 < p.nck0) write_halo(PV ^ 1, true);
+            if constexpr (!LAST) write_halo(PV ^ 1, true);
             else if constexpr (RES) write_center(I0, PV ^ 1);
             __syncthreads();
         };
-        int c = 0;
-        for (; c + 1 < p.nck0; c += 2) {
-            chunk(I0, c);
-            chunk(I1, c + 1);
-        }
-        if (c < p.nck0) chunk(I0, c);
-        if constexpr (RES) {
-            // residual chunk c: centre register set c & 1, halo buffer and weight set (nck0 + c) & 1
-            const int S0w = 9 * p.nck0;
-            auto rstep = [&](auto P, auto Q, int cc) {
-                constexpr int PV = decltype(P)::value, QV = decltype(Q)::value;
-                const int st = S0w + cc;
-                const bool more = st + 1 < S;
-                if (NS == 2 && more) load_w((QV ^ 1) & (NS - 1), st + 1);
-                if (cc + 2 < p.nck1) load_center(P, cc + 2);
-                compute_w(QV & (NS - 1), QV, HWD + 1);  // the halo centre = the output pixel
-                if (NS == 1 && more) load_w(0, st + 1);
-                if (more) write_center(std::integral_constant<int, PV ^ 1>{}, QV ^ 1);
-                __syncthreads();
-            };
-            auto rloop = [&](auto Q0) {
+        // residual chunk cc: centre register set cc & 1, halo buffer and weight set (nck0 + cc) & 1
+        auto residual = [&](auto Q0) {
+            if constexpr (RES) {
                 constexpr int Q = decltype(Q0)::value;
+                const int S0w = 9 * p.nck0;
+                auto rstep = [&](auto P, auto QQ, int cc) {
+                    constexpr int PV = decltype(P)::value, QV = decltype(QQ)::value;
+                    const int st = S0w + cc;
+                    const bool more = st + 1 < S;
+                    if (more) load_w(QV ^ 1, st + 1);
+                    if (cc + 2 < p.nck1) load_center(P, cc + 2);
+                    compute_w(QV, QV, HWD + 1);  // the halo centre = the output pixel
+                    if (more) write_center(std::integral_constant<int, PV ^ 1>{}, QV ^ 1);
+                    __syncthreads();
+                };
                 int cc = 0;
                 for (; cc + 1 < p.nck1; cc += 2) {
                     rstep(I0, std::integral_constant<int, Q>{}, cc);
                     rstep(I1, std::integral_constant<int, Q ^ 1>{}, cc + 1);
                 }
                 if (cc < p.nck1) rstep(I0, std::integral_constant<int, Q>{}, cc);
-            };
-            if (p.nck0 & 1) rloop(I1);
-            else rloop(I0);
+            }
+        };
+        const std::integral_constant<int, 0> NL;
+        const std::integral_constant<int, 1> LL;
+        int c = 0;
+        if (pv0) chunk(I1, NL, c++);  // nck0 even: the leading odd chunk
+        for (; c + 1 < p.nck0 - 1; c += 2) {
+            chunk(I0, NL, c);
+            chunk(I1, NL, c + 1);
         }
+        chunk(I0, LL, p.nck0 - 1);
+        residual(I1);  // the residual centres follow in halo buffer 1, weight set 1
     } else {
         // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
         load_halo0(0);
@@ -725,6 +730,15 @@ bool conv3_wr() {
     return v != 0;
 }
 
+// the fp16-residual forms on weights in registers too (WC_CONV3_WR_RES=0: LDS-staged, for A/B)
+bool conv3_wr_res() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_WR_RES");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+}
+
 template <int TH, int BN>
 int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
     if (f3 && conv3_glds()) {
@@ -746,6 +760,8 @@ int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
             return pro == 1 ? launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s)
                             : launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);
         }
+        if (f3 && conv3_wr_res() && res && d.abound != nullptr && pro == 2)
+            return launch6<TH, BN, 2, true, true, true, false, 0, true>(d, s);
     }
     if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here
         const bool r16 = res && d.abound != nullptr;

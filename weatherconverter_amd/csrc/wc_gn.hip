@@ -248,23 +248,51 @@ __global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
     const int j = threadIdx.x & 63;
     const float n0 = 64.0f * (float)sw;
     if (g < G) {
-        const int slot0 = (c0 + g * cpg) / sw;  // first global sub-slot of the group
+        // sub-slot (pixel block pp, global slot gs) sits at ((b * np64 + pp) * NS + gs) * 2, and a
+        // group's spg slots are contiguous: stream each slot's np64 partials with a fixed lane
+        // stride, four loads in flight per lane, no index division
+        const int NS = ncb * spb;
+        const long pstride = 2L * NS * 64;  // one lane step (64 pixel blocks)
+        const float* base = part + ((long)b * np64 * NS + (c0 + g * cpg) / sw) * 2 + (long)j * NS * 2;
         const int items = np64 * spg;
-        auto at = [&](int it) -> const float* {
-            const int pp = it / spg;
-            const int gs = slot0 + it % spg;
-            return part + ((((long)b * np64 + pp) * ncb + gs / spb) * spb + gs % spb) * 2;
-        };
         float sm = 0.f;
-        for (int it = j; it < items; it += 64) sm += at(it)[0];
+        for (int s = 0; s < spg; ++s) {
+            const float* ps = base + 2 * s;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            int pp = j;
+            for (; pp + 192 < np64; pp += 256, ps += 4 * pstride) {
+                a0 += ps[0];
+                a1 += ps[pstride];
+                a2 += ps[2 * pstride];
+                a3 += ps[3 * pstride];
+            }
+            for (; pp < np64; pp += 64, ps += pstride) a0 += ps[0];
+            sm += (a0 + a1) + (a2 + a3);
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
         const float mean = sm / (float)items;
         float q = 0.f;
-        for (int it = j; it < items; it += 64) {
-            const float* pr = at(it);
-            const float d = pr[0] - mean;
-            q += fmaf(n0 * d, d, pr[1]);
+        for (int s = 0; s < spg; ++s) {
+            const float* ps = base + 2 * s;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            int pp = j;
+            for (; pp + 192 < np64; pp += 256, ps += 4 * pstride) {
+                float d;
+                d = ps[0] - mean;
+                a0 += fmaf(n0 * d, d, ps[1]);
+                d = ps[pstride] - mean;
+                a1 += fmaf(n0 * d, d, ps[pstride + 1]);
+                d = ps[2 * pstride] - mean;
+                a2 += fmaf(n0 * d, d, ps[2 * pstride + 1]);
+                d = ps[3 * pstride] - mean;
+                a3 += fmaf(n0 * d, d, ps[3 * pstride + 1]);
+            }
+            for (; pp < np64; pp += 64, ps += pstride) {
+                const float d = ps[0] - mean;
+                a0 += fmaf(n0 * d, d, ps[1]);
+            }
+            q += (a0 + a1) + (a2 + a3);
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);

@@ -135,7 +135,7 @@ template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP
 __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(
     X6Dev p) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
-    static_assert(!WR || (F3 && (!RES || R16) && !GL && MAP == 0 && T::TPS == 1),
+    static_assert(!WR || (F3 && (!RES || R16) && !GL && (MAP == 0 || TH == 8) && T::TPS == 1),
                   "WR: the f16x3 3x3 forms with 2-piece weights in every step");
     constexpr bool S2D = MAP == 1, CT = MAP == 2;
     static_assert(!MAP || (!RES && !GL && PRO == 0), "MAP 1, 2: raw single-segment register-staged forms");
@@ -498,9 +498,12 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         // Chunk c uses halo buffer and weight-set parity PV = (nck0 - 1 - c) & 1, counted from the
         // end, so the peeled last 3x3 chunk always has PV = 0 (two compile-time variants of it
         // flowing into one epilogue made the register allocator spill hundreds of VGPRs).
+        // weight set of step mt of a chunk of parity PV: (mt + PV) & 1 for 9 taps (odd: the chunk
+        // parity carries the alternation across chunks), mt & 1 for the 2x2 tap grids
+        constexpr int NTAP = T::NTAP, TODD = NTAP & 1;
         const int pv0 = (p.nck0 - 1) & 1;
         load_halo0(0);
-        if (pv0) load_w(1, 0);
+        if (TODD && pv0) load_w(1, 0);
         else load_w(0, 0);
         write_halo(pv0, true);
         __syncthreads();
@@ -508,17 +511,21 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             constexpr int PV = decltype(P)::value;  // the chunk's halo buffer and set parity
             constexpr bool LAST = decltype(L)::value != 0;  // the last 3x3 chunk (compile-time)
 #pragma unroll
-            for (int mt = 0; mt < 9; ++mt) {
-                const int st = 9 * c + mt;
-                if (st + 1 < S) load_w((mt + 1 + PV) & 1, st + 1);
-                if (mt == 7) {
+            for (int mt = 0; mt < NTAP; ++mt) {
+                const int st = NTAP * c + mt;
+                if (st + 1 < S) load_w((mt + 1 + TODD * PV) & 1, st + 1);
+                if (mt == NTAP - 2) {
                     if constexpr (!LAST) load_halo0(c + 1);
                     else if constexpr (RES) load_center(I0, 0);
                 }
                 if constexpr (RES && LAST) {
                     if (mt == 8 && p.nck1 > 1) load_center(I1, 1);
                 }
-                compute_w((mt + PV) & 1, PV, (mt / 3) * HWD + mt % 3);
+                // tap offset in the halo; CT parity (py, px): tap (i, j) reads input offset (py - i, px - j)
+                const int toff = S2D ? ((mt >> 1) + 1) * HWD + (mt & 1) + 1
+                               : CT  ? ((par >> 1) - (mt >> 1) + 1) * HWD + (par & 1) - (mt & 1) + 1
+                                     : (mt / 3) * HWD + mt % 3;
+                compute_w((mt + TODD * PV) & 1, PV, toff);
             }
             if constexpr (!LAST) write_halo(PV ^ 1, true);
             else if constexpr (RES) write_center(I0, PV ^ 1);
@@ -922,6 +929,7 @@ extern "C" int wc_conv4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64_t
     }
     const long ntn = (a->N + BN - 1) / BN;
     if (w3_bytes != ntn * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
+    if (conv3_wr()) return launch6<8, 128, 0, false, true, false, false, 1, true>(d, reinterpret_cast<hipStream_t>(stream));
     return launch6<8, 128, 0, false, true, false, false, 1>(d, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -965,5 +973,6 @@ extern "C" int wc_convtr4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64
     if (w3_bytes != ntn * 4L * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (BN == 64) return launch6<16, 64, 0, false, true, false, false, 2>(d, st);
+    if (conv3_wr()) return launch6<8, 128, 0, false, true, false, false, 2, true>(d, st);
     return launch6<8, 128, 0, false, true, false, false, 2>(d, st);
 }

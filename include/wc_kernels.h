@@ -185,6 +185,11 @@ int wc_convtr4x4s2_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_by
 int wc_conv_igemm_f16x3_qkv(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
                             const float* w_inv_scale, void* qkv3, int C, int heads, const int* exps,
                             void* stream);
+/* wc_attention_fwd_f16x3_presplit whose output is the out-projection's pre-split A operand: O x
+ * 2^v_exp in the a3 layout of wc_split_f16x3_tiled (C % 32 == 0, N % 128 == 0, a3_bytes =
+ * B*N*C*4), bit for bit that split of the fp32 output, for wc_proj_f16x3 at a_exp = v_exp. */
+int wc_attention_fwd_f16x3_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B, int N, int C, int heads,
+                                       float scale, int q_exp, int k_exp, int v_exp, void* stream);
 /* The attention projections (unet_base.py:110-116 in_proj / out_proj) on an A operand split
  * beforehand: wc_split_f16x3_tiled writes, from the rows of an NHWC view (B images x HW pixels,
  * C channels; HW % 128 == 0, C % 32 == 0, 16-byte aligned, ldc % 4 == 0) optionally through a

@@ -638,6 +638,14 @@ def test_projections_presplit_bit_identical_to_register_staged(monkeypatch):
     K.proj_f16x3_qkv(yv, a3, w3, bias.cuda(), q1, a_exp=e, C=C, heads=heads, exps=exps)
     torch.cuda.synchronize()
     assert torch.equal(q0, q1)
+    # the attention writing its output pre-split == the split pass over its fp32 output
+    N = H * H
+    o = torch.empty((B * N, C), device='cuda')
+    K.attention_presplit(q0, o, B, N, C, heads, exps)
+    a3o = K.attention_presplit_a3(q0, B, N, C, heads, exps)
+    a3s = K.split_f16x3_tiled(K.View(o.view(B, H, H, C), 0, C), exps[2])
+    torch.cuda.synchronize()
+    assert torch.equal(a3o, a3s)
 
 
 # ---------------------------------------------------------------- producer absmax -> per-image f16x3 scale

@@ -106,7 +106,10 @@ WC_DEVICE void mfma_split(f32x16& acc, const u32x4 (&a)[F3 ? 2 : 3], const u32x4
 // runs under the other's MFMAs); the larger forms keep Q and O in 512 registers at one wave.
 // PRE (f16x3 only): qkv is the pre-split projection of wc_conv_igemm_f16x3_qkv (already scaled by
 // 2^exps; qs, ks, vs unused); K and V^T tiles are copied into LDS by LDS-DMA in their final image.
-template <int D, bool F3, bool PRE = false>
+// O3 (PRE only): `out` is the A operand of the out-projection GEMM (wc_proj_f16x3): O x 2^ev split
+// into fp16 pieces in the a3 layout of wc_split_f16x3_tiled (C % 32 == 0, N % 128 == 0), bit for bit
+// what that split pass makes of the fp32 O.
+template <int D, bool F3, bool PRE = false, bool O3 = false>
 __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
                                                              float* __restrict__ out, int ldo, int N,
                                                              int C, float score_mul, float qs, float ks,
@@ -386,6 +389,28 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     }
 
     // ---- epilogue: O[q][dv] = O^T[dv][q] / l ----
+    if constexpr (O3) {
+        if (qrow < N) {
+            const float inv = out_mul / l_run;
+            const long m = (long)b * N + qrow;  // GEMM row (pixel of the batch)
+            const long rowbase = ((m >> 7) * (C / 16)) * 4 * 128 * 16 + (m & 127) * 16 + 8 * half;
+            unsigned char* a3 = reinterpret_cast<unsigned char*>(out);
+#pragma unroll
+            for (int d = 0; d < A::NDB; ++d) {
+#pragma unroll
+                for (int r = 0; r < 16; r += 4) {
+                    const int c = head * D + d * 32 + 8 * (r >> 2) + 4 * half;  // c % 8 == 4 half
+                    const f32x4 v = f32x4{o[d][r] * inv, o[d][r + 1] * inv, o[d][r + 2] * inv, o[d][r + 3] * inv} * vs;
+                    u32x2 ph, pl;
+                    split2_f16(v, ph, pl);
+                    unsigned char* dst = a3 + rowbase + ((long)(c >> 4) * 4 + ((c >> 3) & 1)) * 128 * 16;
+                    *reinterpret_cast<u32x2*>(dst) = ph;                 // piece 0
+                    *reinterpret_cast<u32x2*>(dst + 2 * 128 * 16) = pl;  // piece 1
+                }
+            }
+        }
+        return;
+    }
     if (qrow < N) {
         const float inv = out_mul / l_run;
         float* orow = out + ((long)b * N + qrow) * ldo + head * D;
@@ -401,13 +426,13 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     }
 }
 
-template <int D, bool F3, bool PRE = false>
+template <int D, bool F3, bool PRE = false, bool O3 = false>
 int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
                 float scale, int eq, int ek, int ev, hipStream_t stream) {
     using A = Ax6<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3, PRE>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3, PRE, O3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, A::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -415,7 +440,7 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
     constexpr int EP = F3 ? 14 : 0;  // P scale: keeps small probabilities in the fp16 normal range
     const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
     dim3 grid(((N + 127) / 128) * heads * B);
-    hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
+    hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE, O3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
                        score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), ldexpf(1.f, EP),
                        ldexpf(1.f, -(ev + EP)));
     WC_CHECK_LAUNCH();
@@ -460,7 +485,34 @@ int dispatch_att_presplit(const void* qkv3, float* out, int ld_out, int B, int N
     }
 }
 
+int dispatch_att_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B, int N, int C, int heads,
+                             float scale, int eq, int ek, int ev, hipStream_t s) {
+    if (!qkv3 || !a3) return WC_E_ARG;
+    if (heads <= 0 || C % heads != 0 || C % 32 || N <= 0 || B <= 0 || N % 128) return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(qkv3) & 15) || (reinterpret_cast<uintptr_t>(a3) & 15)) return WC_E_SHAPE;
+    if (a3_bytes != (long)B * N * C * 4) return WC_E_SHAPE;
+    if (eq < -60 || eq > 60 || ek < -60 || ek > 60 || ev < -60 || ev > 60) return WC_E_ARG;
+    const float* q = reinterpret_cast<const float*>(qkv3);
+    float* o = reinterpret_cast<float*>(a3);
+    switch (C / heads) {
+        case 32: return launch_att6<32, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        case 64: return launch_att6<64, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        case 96: return launch_att6<96, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        case 128: return launch_att6<128, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        case 160: return launch_att6<160, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        case 192: return launch_att6<192, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        default: return WC_E_SHAPE;
+    }
+}
+
 }  // namespace
+
+extern "C" int wc_attention_fwd_f16x3_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B, int N, int C,
+                                                  int heads, float scale, int q_exp, int k_exp, int v_exp,
+                                                  void* stream) {
+    return dispatch_att_presplit_a3(qkv3, a3, a3_bytes, B, N, C, heads, scale, q_exp, k_exp, v_exp,
+                                    reinterpret_cast<hipStream_t>(stream));
+}
 
 extern "C" int wc_attention_fwd_f16x3_presplit(const void* qkv3, float* out, int ld_out, int B, int N, int C,
                                                int heads, float scale, int q_exp, int k_exp, int v_exp,

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(TE_THREADS) void temb_kernel(const int64_t* __restr
 // conv_in_kernel (any Cout % 4): thread = (pixel, 4 output channels).
 // Both accumulate bias, then (ci, ky, kx) in order, one fma each (out-of-image taps add 0 * w).
 // --------------------------------------------------------------------------------------------
-template <int COUT>
+template <int COUT, int CIN>
 __global__ __launch_bounds__(256) void conv_in_px_kernel(const float* __restrict__ x, int B, int Cin, int H, int W,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          float* __restrict__ out, int ldo) {
@@ -92,26 +92,26 @@ __global__ __launch_bounds__(256) void conv_in_px_kernel(const float* __restrict
     float acc[COUT];
 #pragma unroll
     for (int c = 0; c < COUT; ++c) acc[c] = bias[c];
-    for (int ci = 0; ci < Cin; ++ci) {
-        const float* plane = x + ((long)b * Cin + ci) * H * W;
-        // one tap per iteration: its COUT weights are consumed before the next tap's are read
-#pragma unroll 1
-        for (int t = 0; t < 9; ++t) {
-            const int ky = t / 3, kx = t - 3 * (t / 3);
-            const int iy = yh + ky - 1;
-            const int ix = xw + kx - 1;
-            {
-                const float v = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? plane[(long)iy * W + ix] : 0.f;
-                const f32x4* wr = reinterpret_cast<const f32x4*>(ws + (ci * 9 + t) * COUT);
+    // the pixel's CIN * 9 inputs first, all loads in flight together, then the taps in order
+    float xin[CIN * 9];
 #pragma unroll
-                for (int q = 0; q < COUT / 4; ++q) {
-                    const f32x4 wv = wr[q];
-                    acc[4 * q + 0] = fmaf(v, wv.x, acc[4 * q + 0]);
-                    acc[4 * q + 1] = fmaf(v, wv.y, acc[4 * q + 1]);
-                    acc[4 * q + 2] = fmaf(v, wv.z, acc[4 * q + 2]);
-                    acc[4 * q + 3] = fmaf(v, wv.w, acc[4 * q + 3]);
-                }
-            }
+    for (int k = 0; k < CIN * 9; ++k) {
+        const int ci = k / 9, t = k % 9;
+        const int iy = yh + t / 3 - 1, ix = xw + t % 3 - 1;
+        xin[k] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? x[(((long)b * CIN + ci) * H + iy) * W + ix]
+                                                                            : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < CIN * 9; ++k) {
+        const float v = xin[k];
+        const f32x4* wr = reinterpret_cast<const f32x4*>(ws + k * COUT);
+#pragma unroll
+        for (int q = 0; q < COUT / 4; ++q) {
+            const f32x4 wv = wr[q];
+            acc[4 * q + 0] = fmaf(v, wv.x, acc[4 * q + 0]);
+            acc[4 * q + 1] = fmaf(v, wv.y, acc[4 * q + 1]);
+            acc[4 * q + 2] = fmaf(v, wv.z, acc[4 * q + 2]);
+            acc[4 * q + 3] = fmaf(v, wv.w, acc[4 * q + 3]);
         }
     }
     f32x4* o = reinterpret_cast<f32x4*>(out + pix * ldo);
@@ -204,17 +204,15 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
         inb |= (ok ? 1u : 0u) << k;
         goff[k] = ok ? ((long)(b * H + gy) * W + gx) * ldx + 4 * (i & 3) : 0;
     }
-    f32x4 ra[HD_PER_T], rs[HD_PER_T], rh[HD_PER_T];
+    // every item of a thread has the same channel quad (256 items apart): one scale / shift each
+    f32x4 ra[HD_PER_T], rs, rh;
     auto load = [&](int c0) {
+        const int c = c0 + 4 * (threadIdx.x & 3);
+        rs = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
+        rh = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
 #pragma unroll
-        for (int k = 0; k < HD_PER_T; ++k) {
-            const int c = c0 + 4 * ((threadIdx.x + 256 * k) & 3);
-            if ((inb >> k) & 1u) {
-                ra[k] = *reinterpret_cast<const f32x4*>(x + goff[k] + c0);
-                rs[k] = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
-                rh[k] = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
-            }
-        }
+        for (int k = 0; k < HD_PER_T; ++k)
+            if ((inb >> k) & 1u) ra[k] = *reinterpret_cast<const f32x4*>(x + goff[k] + c0);
     };
     load(0);
     for (int c0 = 0; c0 < C; c0 += 16) {
@@ -225,7 +223,7 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if ((inb >> k) & 1u) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(ra[k][e], rs[k][e], rh[k][e]));
+                for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(ra[k][e], rs[e], rh[e]));
             }
             halo[threadIdx.x + 256 * k] = v;  // zero padding after the prologue, as the reference pads
         }
@@ -459,9 +457,10 @@ extern "C" int wc_conv_in(const float* x, int B, int Cin, int H, int W, const fl
     if (Cin < 1 || Cin > 16 || Cout % 4 != 0 || ldo % 4 != 0) return WC_E_SHAPE;
     size_t lds = (size_t)Cin * 9 * Cout * sizeof(float);
     if (lds > 64 * 1024) return WC_E_SHAPE;
-    if (Cout == 64 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(b) & 15) == 0) {
+    if (Cout == 64 && Cin == 3 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(b) & 15) == 0) {
         const long npix = (long)B * H * W;
-        hipLaunchKernelGGL(conv_in_px_kernel<64>, dim3((unsigned)((npix + 255) / 256)), dim3(256), lds,
+        hipLaunchKernelGGL((conv_in_px_kernel<64, 3>), dim3((unsigned)((npix + 255) / 256)), dim3(256), lds,
                            reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, out, ldo);
         WC_CHECK_LAUNCH();
         return WC_OK;

@@ -356,7 +356,6 @@ class UnetEngine:
         B, H, W, C = Y.B, Y.H, Y.W, Y.C
         N = H * W
         sc, sh = self._gn(Y, p.g, p.be)
-        o = self._new(B, H, W, C)
         if p.w_in_f3 is not None:
             # in_proj: GN output bound; attention: q/k/v bounds; out_proj: |O| <= max|V| (convex
             # combination of V rows), so the V exponent bounds it
@@ -376,28 +375,33 @@ class UnetEngine:
                 else:
                     K.conv_igemm_f16x3_qkv(seg, p.w_in_f3, p.b_in, qkv3, Hm=H, Wm=W, a_exp=a_exp, C=C,
                                            heads=p.heads, exps=exps)
+                if K.proj_pa_enabled() and K.proj_pa_ok(Y, C) and C % 32 == 0:
+                    # the attention writes O already scaled and split in the out-projection's LDS
+                    # stage order (no fp32 O round trip, no split pass); the GEMM copies it by LDS-DMA
+                    a3o = K.attention_presplit_a3(qkv3, B, N, C, p.heads, exps)
+                    del qkv3
+                    gp = K.GnPart.of(Y)
+                    fused = K.gn_conv_ok(Y, gp, p.w_out_f3.N, H, W, 256 if p.w_out_f3.N <= 64 else 128)
+                    shape = View(a3o.view(torch.float32).view(B, H, W, C), 0, C)  # the operand's view shape
+                    K.proj_f16x3(shape, a3o, p.w_out_f3, p.b_out, Y, a_exp=exps[2], res=Y, absmax=absmax,
+                                 gn=gp if fused else None)
+                    self._gn_fill(Y, fused)
+                    return absmax is not None
+                o = self._new(B, H, W, C)
                 K.attention_presplit(qkv3, o.view(B * N, C), B, N, C, p.heads, exps)
             else:
+                o = self._new(B, H, W, C)
                 qkv = self._new(B, H, W, 3 * C)
                 K.conv_igemm_f16x3([seg], p.w_in_f3, p.b_in, View.full(qkv), Hm=H, Wm=W, a_exp=a_exp)
                 K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, 'f16x3', exps)
             gp = K.GnPart.of(Y)
             fused = K.gn_conv_ok(Y, gp, p.w_out_f3.N, H, W, 256 if p.w_out_f3.N <= 64 else 128)
-            ov = View.full(o)
-            # (the out-projection stays on the register-staged GEMM: a separate split pass of O costs
-            # more than the pre-split GEMM saves there, 0.27 vs 0.08 ms per 256-px step; WC_PROJ_PA=2
-            # forces it, for measurement)
-            if os.environ.get('WC_PROJ_PA') == '2' and K.proj_pa_ok(ov, C) and K.proj_pa_ok(Y, C):
-                a3 = K.split_f16x3_tiled(ov, exps[2])
-                K.proj_f16x3(ov, a3, p.w_out_f3, p.b_out, Y, a_exp=exps[2], res=Y, absmax=absmax,
-                             gn=gp if fused else None)
-                del a3
-            else:
-                K.conv_igemm_f16x3([Seg(ov, TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2], res=Y,
-                                   absmax=absmax, gn=gp if fused else None)
+            K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], p.w_out_f3, p.b_out, Y, Hm=H, Wm=W, a_exp=exps[2],
+                               res=Y, absmax=absmax, gn=gp if fused else None)
             self._gn_fill(Y, fused)
             return absmax is not None
         qkv = self._new(B, H, W, 3 * C)
+        o = self._new(B, H, W, C)
         self.conv([Seg(Y, TAPS1, scale=sc, shift=sh, silu=False)], p.w_in, p.w_in_x6, p.b_in, View.full(qkv), H, W)
         K.attention(qkv.view(B * N, 3 * C), o.view(B * N, C), B, N, C, p.heads, self.precision)
         return self.conv([Seg(View.full(o), TAPS1)], p.w_out, p.w_out_x6, p.b_out, Y, H, W, res=Y, absmax=absmax)[0]

@@ -604,6 +604,20 @@ def attention_presplit(qkv3: torch.Tensor, out: torch.Tensor, B: int, N: int, C:
            qkv3.data_ptr(), out.data_ptr(), C, B, N, C, heads, float(d)**-0.5, *[int(e) for e in exps], _stream())
 
 
+def attention_presplit_a3(qkv3: torch.Tensor, B: int, N: int, C: int, heads: int,
+                          exps: Tuple[int, int, int]) -> torch.Tensor:
+    """attention_presplit writing the out-projection's pre-split A operand (O x 2^exps[2] in the
+    split_f16x3_tiled layout, wc_attention_fwd_f16x3_presplit_a3): an int16 tensor of 2*B*N*C."""
+    _req(qkv3.is_cuda and qkv3.dtype == torch.int16 and qkv3.numel() == B * 6 * C * N, 'pre-split qkv buffer')
+    _req(N % 128 == 0 and C % 32 == 0, 'pre-split attention output: N % 128 == 0, C % 32 == 0')
+    a3 = torch.empty(2 * B * N * C, dtype=torch.int16, device=qkv3.device)
+    d = C // heads
+    _timed(f'attention_x6_kernel<{d}, true> (pre-split)', 'wc_attention_fwd_f16x3_presplit_a3', 4.0 * B * N * N * C,
+           qkv3.data_ptr(), a3.data_ptr(), a3.numel() * 2, B, N, C, heads, float(d)**-0.5, *[int(e) for e in exps],
+           _stream())
+    return a3
+
+
 def x6_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
     """True when wc_conv3x3_x6 accepts this conv (mirrors its host checks; output must be a plain
     NHWC view on the same grid)."""

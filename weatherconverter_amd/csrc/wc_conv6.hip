@@ -87,7 +87,7 @@ struct X6Dev {
 // no weight registers; else register-staged, one tap per K-step.
 // MAP: 0 = 3x3 stride 1; 1 = 4x4/s2 down conv over the space-to-depth input (2x2 taps); 2 = the
 // 4x4/s2 transposed conv, one output parity per workgroup (2x2 taps of the 3x3 frame).
-template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, int MAP = 0, bool WR = false>
+template <int TH, int BN, bool RES, bool F3, bool R16, bool GL = false, int MAP = 0, int WR = 0>
 struct X6Tile {
     static constexpr int BM = TH * 16;
     static constexpr int WAVES_N = BN / 64;
@@ -131,7 +131,7 @@ WC_DEVICE int row_dx(int r) {
 // TH = 8 tiles without a residual or with an fp16 one are held to 3 waves per SIMD (<= 168
 // VGPRs; the two-deep residual staging would otherwise take the R16 form to 178 and 2 waves, and
 // 3 waves cost it one spilled VGPR); the other forms run at 2.
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP = 0, bool WR = false>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16, bool GL, int MAP = 0, int WR = 0>
 __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) void conv3x3_x6_kernel(
     X6Dev p) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
@@ -185,7 +185,9 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     const int q = tid & 3;
     // S2D: halo pixel (hy, hx) is the 2x2 input block (BY, BX) = (y0 - 1 + hy, x0 - 1 + hx) of
     // input pixels (2 BY - 1 + py, 2 BX - 1 + px); its in-bounds bits per phase row / column
-    int hoff0[T::H_PER_T], hlds[T::H_PER_T];
+    int hoff0[T::H_PER_T];
+    // item j's halo pixel is (tid >> 2) + 64 j: one LDS base, item j at + 1024 j (immediate offsets)
+    const int hlds0 = (q >> 1) * T::HPLANE + (tid >> 2) * 16 + (q & 1) * 8;
     unsigned hin = 0, hval = 0, hr0 = 0, hr1 = 0, hc0 = 0, hc1 = 0;
 #pragma unroll
     for (int j = 0; j < T::H_PER_T; ++j) {
@@ -196,7 +198,6 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
         const bool valid = i < T::H_ITEMS;
         hval |= (valid ? 1u : 0u) << j;
-        hlds[j] = (q >> 1) * T::HPLANE + P * 16 + (q & 1) * 8;
         if constexpr (S2D) {
             const int y2 = 2 * iy - 1, x2 = 2 * ix - 1;
             hr0 |= (valid && (unsigned)y2 < (unsigned)p.Hi ? 1u : 0u) << j;
@@ -231,7 +232,14 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     f32x4 rsc = {1.f, 1.f, 1.f, 1.f}, rsh = {0.f, 0.f, 0.f, 0.f};
     u32x4 rb[GL ? 1 : T::B_PER_T];
 
-    auto load_halo0 = [&](int c) {
+    auto load_ss = [&](int c) {  // GroupNorm scale / shift of chunk c
+        if constexpr (PRO != 0) {
+            const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
+            rsc = bload_f4(srdsc, o);
+            rsh = bload_f4(srdsh, o);
+        }
+    };
+    auto load_halo0 = [&](int c, bool ss = true) {
         if constexpr (S2D) {  // chunk c = (phase (py, px), 16 channels): phase-major over 4C channels
             const int ph = c / p.s2d_cpp;
             const int py = ph >> 1, px = ph & 1;
@@ -245,11 +253,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             for (int j = 0; j < T::H_PER_T; ++j)
                 rh[j] = bload_f4(srd0, ((hin >> j) & 1u) ? (unsigned)(hoff0[j] + c * 16) * 4u : OOB);
         }
-        if constexpr (PRO != 0) {
-            const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
-            rsc = bload_f4(srdsc, o);
-            rsh = bload_f4(srdsh, o);
-        }
+        if (ss) load_ss(c);
     };
     // seg0: prologue + (F3: scale, 2 fp16 pieces | 3 bf16 pieces); seg1: (F3: scale) 3 bf16 pieces
     auto write_halo = [&](int hs, bool seg0) {
@@ -272,14 +276,14 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             if ((F3 && seg0) || (R16 && !seg0)) {
                 u32x2 a0, a1;
                 split2_f16(v, a0, a1);
-                *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
-                *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds[j]) = a1;
+                *reinterpret_cast<u32x2*>(base + hlds0 + 1024 * j) = a0;
+                *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds0 + 1024 * j) = a1;
             } else {
                 u32x2 a0, a1, a2;
                 split3(v, a0, a1, a2);
-                *reinterpret_cast<u32x2*>(base + hlds[j]) = a0;
-                *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds[j]) = a1;
-                *reinterpret_cast<u32x2*>(base + 4 * T::HPLANE + hlds[j]) = a2;
+                *reinterpret_cast<u32x2*>(base + hlds0 + 1024 * j) = a0;
+                *reinterpret_cast<u32x2*>(base + 2 * T::HPLANE + hlds0 + 1024 * j) = a1;
+                *reinterpret_cast<u32x2*>(base + 4 * T::HPLANE + hlds0 + 1024 * j) = a2;
             }
         }
     };
@@ -461,7 +465,10 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         // two register sets (the next step's fragments land while this one computes), also for the
         // residual forms: the last 3x3 chunk is peeled (compile-time), so the residual centres it
         // stages are not live through the chunk loop
-        constexpr int NS = 2;
+        // WR 2 (9-tap grids): the last tap's weights go out two taps ahead, into a third set, so the
+        // next chunk's halo loads can be issued before them (three taps of cover, not one)
+        constexpr bool LA2 = WR == 2 && MAP == 0;
+        constexpr int NS = LA2 ? 3 : 2;
         u32x4 wreg[NS][2][2];  // [set][nb][piece]
         const unsigned wlane = (unsigned)(half * T::BPLANE + (wn * 64 + l32) * 16);
         auto load_w = [&](int set, int st) {
@@ -513,10 +520,20 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
 #pragma unroll
             for (int mt = 0; mt < NTAP; ++mt) {
                 const int st = NTAP * c + mt;
-                if (st + 1 < S) load_w((mt + 1 + TODD * PV) & 1, st + 1);
-                if (mt == NTAP - 2) {
-                    if constexpr (!LAST) load_halo0(c + 1);
-                    else if constexpr (RES) load_center(I0, 0);
+                constexpr bool EARLY = LA2 && !LAST;
+                if (EARLY && mt == NTAP - 3) {
+                    load_w((mt + 1 + TODD * PV) & 1, st + 1);
+                    load_w(NS - 1, st + 2);
+                    load_halo0(c + 1, false);  // scale / shift (L2) in the last tap: 8 registers fewer
+                } else if (EARLY && mt == NTAP - 1) {
+                    load_w((mt + 1 + TODD * PV) & 1, st + 1);
+                    load_ss(c + 1);
+                } else if (!(EARLY && mt == NTAP - 2)) {
+                    if (st + 1 < S) load_w((mt + 1 + TODD * PV) & 1, st + 1);
+                    if (mt == NTAP - 2) {
+                        if constexpr (!LAST) load_halo0(c + 1);
+                        else if constexpr (RES) load_center(I0, 0);
+                    }
                 }
                 if constexpr (RES && LAST) {
                     if (mt == 8 && p.nck1 > 1) load_center(I1, 1);
@@ -525,7 +542,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                 const int toff = S2D ? ((mt >> 1) + 1) * HWD + (mt & 1) + 1
                                : CT  ? ((par >> 1) - (mt >> 1) + 1) * HWD + (par & 1) - (mt & 1) + 1
                                      : (mt / 3) * HWD + mt % 3;
-                compute_w((mt + TODD * PV) & 1, PV, toff);
+                compute_w((EARLY && mt == NTAP - 1) ? NS - 1 : (mt + TODD * PV) & 1, PV, toff);
             }
             if constexpr (!LAST) write_halo(PV ^ 1, true);
             else if constexpr (RES) write_center(I0, PV ^ 1);
@@ -697,7 +714,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0, bool WR = false>
+template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0, int WR = 0>
 int launch6(const X6Dev& d, hipStream_t stream) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
@@ -746,6 +763,26 @@ bool conv3_wr_res() {
     return v != 0;
 }
 
+// WC_CONV3_LA2=1 (A/B only): the plain (no residual) GN+SiLU form with the last tap's weights two
+// taps ahead and the next chunk's halo issued before them.  Alone each launch gains (359 -> 368 TF/s
+// at 256^2, 316 -> 332 at 64^2 / 512 channels) but the whole step does not (same box 27.06 / 27.09
+// vs 27.09 / 27.22 ms: the power-capped clock takes the saved cycles back).  =1r: the residual form
+// too, which needs 2 waves/SIMD or spills at 3, and loses (334 -> 297 TF/s).
+bool conv3_la2() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_LA2");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v != 0;
+}
+bool conv3_la2_res() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_LA2");
+        return (e && e[0] == '1' && e[1] == 'r') ? 1 : 0;
+    }();
+    return v != 0;
+}
+
 template <int TH, int BN>
 int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
     if (f3 && conv3_glds()) {
@@ -763,6 +800,9 @@ int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
     // 338 -> 356 TF/s; the TH = 16 / BN = 64 form drops to 2 waves/SIMD and loses, 312 -> 292; with
     // the residual the register sets exceed the 3-wave budget and spill)
     if constexpr (TH == 8) {
+        if (f3 && conv3_la2() && pro == 2 && (!res || (conv3_la2_res() && d.abound != nullptr)))
+            return res ? launch6<TH, BN, 2, true, true, true, false, 0, 2>(d, s)
+                       : launch6<TH, BN, 2, false, true, false, false, 0, 2>(d, s);
         if (f3 && conv3_wr() && !res) {
             return pro == 1 ? launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s)
                             : launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);

@@ -59,6 +59,14 @@ def build(verbose: bool = False, force: bool = False) -> str:
         list(ex.map(run, jobs))
     if jobs or force or _stale(LIB_PATH, objs):
         run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', LIB_PATH] + objs)
+        # A kernel whose body the host pass rejects (a device-only builtin used directly in a
+        # __global__ template) loses its host stub without any diagnostic and the library then
+        # fails to load: refuse to produce such a library.
+        nm = subprocess.run(['nm', '-D', '--undefined-only', LIB_PATH], capture_output=True, text=True)
+        lost = [ln.split()[-1] for ln in nm.stdout.splitlines() if '_GLOBAL__N_' in ln]
+        if lost:
+            os.remove(LIB_PATH)
+            raise RuntimeError(f'{len(lost)} kernel stub(s) missing from the library, e.g. {lost[0]}')
     return LIB_PATH
 
 

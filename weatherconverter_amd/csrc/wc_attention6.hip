@@ -47,6 +47,13 @@ struct Ax6 {
     static constexpr int VPT = (VITEMS + NT - 1) / NT;
 };
 
+// 16-byte buffer load per lane straight into LDS at the wave-uniform base dst (device-only helper:
+// the target builtins must not appear in the kernel body the host pass parses)
+WC_DEVICE void buf_lds16(__amdgpu_buffer_rsrc_t srd, void* dst, unsigned voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
+WC_DEVICE int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // position of key k (0..31) in the permuted K16 order of the PV MFMA (see header)
 WC_DEVICE int key_pos(int k) { return attn_key_pos(k); }
 
@@ -170,28 +177,43 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
     }
     // LDS-DMA of tile t into buf (PRE): D/16 wave-instructions per wave, half K (plane pairs, key
     // slots XOR-swizzled as write_tile does), half V^T (16 dim rows, 16-byte slots swizzled)
-    auto dma_tile = [&](int t, unsigned char* buf) {
-        const int kv0 = t * KT;
-        constexpr int G = D / 8;  // K planes per piece = V^T row groups of 16 per piece x 2
+    // Buffer loads: per-lane 32-bit byte offsets from the image's pre-split base, fixed for the
+    // whole key loop; the tile enters as the scalar offset, the LDS base (M0) is wave-uniform.
+    constexpr int G = D / 8;  // K planes per piece = V^T row groups of 16 per piece x 2
+    const int wv = uniform_int(wave);
+    unsigned kvoff[G / 4], vvoff[G / 4];
+    __amdgpu_buffer_rsrc_t srd3 = make_srd(q3);
+    if constexpr (PRE) {
 #pragma unroll
         for (int j = 0; j < G / 4; ++j) {
             const int i = wave + 4 * j;  // 0 .. G-1: (piece, plane pair)
             const int pc = i / (G / 2), pp = i % (G / 2);
             const int pl = 2 * pp + (lane >> 5), key = (lane & 31) ^ (pl & 15);
-            const unsigned short* src = Kp + pc * hplane + ((long)pl * N + kv0 + key) * 8;
-            unsigned char* dst = buf + (pc * G + 2 * pp) * A::KPLANE;
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            kvoff[j] = (unsigned)((Kp - q3) + pc * hplane + ((long)pl * N + key) * 8) * 2u;
         }
 #pragma unroll
         for (int j = 0; j < G / 4; ++j) {
             const int i = wave + 4 * j;  // 0 .. G-1: (piece, 16-row block)
             const int pc = i / (D / 16), r0 = 16 * (i % (D / 16));
             const int row = r0 + (lane >> 2), slot = (lane & 3) ^ ((row >> 2) & 3);
-            const unsigned short* src = Vp + pc * hplane + (long)row * N + kv0 + slot * 8;
+            vvoff[j] = (unsigned)((Vp - q3) + pc * hplane + (long)row * N + slot * 8) * 2u;
+        }
+    }
+    auto dma_tile = [&](int t, unsigned char* buf) {
+        const int kv0 = t * KT;
+#pragma unroll
+        for (int j = 0; j < G / 4; ++j) {
+            const int i = wv + 4 * j;
+            const int pc = i / (G / 2), pp = i % (G / 2);
+            unsigned char* dst = buf + (pc * G + 2 * pp) * A::KPLANE;
+            buf_lds16(srd3, dst, kvoff[j], kv0 * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < G / 4; ++j) {
+            const int i = wv + 4 * j;
+            const int pc = i / (D / 16), r0 = 16 * (i % (D / 16));
             unsigned char* dst = buf + A::KBYTES + pc * A::VPLANE + r0 * (KT * 2);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            buf_lds16(srd3, dst, vvoff[j], kv0 * 2);
         }
     };
 
@@ -325,32 +347,35 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
         }
 
         // ---- online softmax over keys, per query (lane) ----
+        // The running max is kept in the exp2 domain: max(s) * score_mul = max(s * score_mul)
+        // (score_mul > 0, rounding is monotonic), and each probability is one fma + v_exp_f32:
+        // p = 2^(s * score_mul + EP - m) carries the f16x3 prescale 2^EP of P exactly in the
+        // exponent (l carries it too, and out_mul omits it)
         float mloc = -INFINITY;
-        if (kv0 + KT <= N) {  // full tile (wave-uniform): no key mask
+        if (PRE || kv0 + KT <= N) {  // full tile (wave-uniform; PRE needs N % KT == 0): no key mask
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                s[r] *= score_mul;
-                mloc = fmaxf(mloc, s[r]);
-            }
+            for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, s[r]);
         } else {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                const float v = (key < N) ? s[r] * score_mul : -INFINITY;
-                s[r] = v;
-                mloc = fmaxf(mloc, v);
+                if (key >= N) s[r] = -INFINITY;
+                mloc = fmaxf(mloc, s[r]);
             }
         }
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        const float m_new = fmaxf(m_run, mloc);
+        const float m_new = fmaxf(m_run, mloc * score_mul);
         const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // v_exp_f32 (results < 2^-126 flush: negligible)
-        float lsum = 0.f;
+        const float nb = (F3 ? 14.0f : 0.0f) - m_new;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(s[r] - m_new);
-            s[r] = pv;
-            lsum += pv;
-        }
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(fmaf(s[r], score_mul, nb));
+        // row sum as a packed-add tree (8 instructions, not 16)
+        f32x2 ts[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            ts[i] = f32x2{s[4 * i], s[4 * i + 1]} + f32x2{s[4 * i + 2], s[4 * i + 3]};
+        const f32x2 u = (ts[0] + ts[1]) + (ts[2] + ts[3]);
+        float lsum = u.x + u.y;
         lsum += __shfl_xor(lsum, 32, 64);
         l_run = l_run * alpha + lsum;
         m_run = m_new;
@@ -366,8 +391,8 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             u32x4 pp[NP];
-            pieces8<F3>(f32x4{s[8 * c + 0], s[8 * c + 1], s[8 * c + 2], s[8 * c + 3]} * ps,
-                        f32x4{s[8 * c + 4], s[8 * c + 5], s[8 * c + 6], s[8 * c + 7]} * ps, pp);
+            pieces8<F3>(f32x4{s[8 * c + 0], s[8 * c + 1], s[8 * c + 2], s[8 * c + 3]},
+                        f32x4{s[8 * c + 4], s[8 * c + 5], s[8 * c + 6], s[8 * c + 7]}, pp);
 #pragma unroll
             for (int db = 0; db < A::NDB; ++db) {
                 const int d = db * 32 + l32;
@@ -437,12 +462,12 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
-    constexpr int EP = F3 ? 14 : 0;  // P scale: keeps small probabilities in the fp16 normal range
+    // P carries 2^14 under f16x3 (small probabilities stay in the fp16 normal range); it is added
+    // in the exp2 argument inside the kernel and cancels in O / l
     const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
     dim3 grid(((N + 127) / 128) * heads * B);
     hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE, O3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
-                       score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), ldexpf(1.f, EP),
-                       ldexpf(1.f, -(ev + EP)));
+                       score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), 1.0f, ldexpf(1.f, -ev));
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

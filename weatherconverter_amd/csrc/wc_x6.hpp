@@ -78,11 +78,15 @@ WC_DEVICE void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
 // v_cvt_pk_f16_f32, 2.5 VALU per value, already packed as the MFMA operand wants.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+// l = fp16(v - h) by v_fma_mix (f32 v, f16 h): v - h is exact in fp32 (at most 12 significant bits
+// below h), so rounding the exact fma result to fp16 once is bit for bit the convert-back / subtract /
+// convert sequence, in 3 instructions per pair instead of 5-6
 WC_DEVICE void split2_pair(f32x2 v, unsigned& h, unsigned& l) {
     const f16x2v hh = __builtin_convertvector(v, f16x2v);
-    const f32x2 r = v - __builtin_convertvector(hh, f32x2);
     h = __builtin_bit_cast(unsigned, hh);
-    l = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2v));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(l) : "v"(v.x), "v"(h), "v"(v.y));
 }
 WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
     unsigned h0, l0, h1, l1;

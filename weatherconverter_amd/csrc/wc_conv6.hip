@@ -209,7 +209,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
             hin |= (inb ? 1u : 0u) << j;
             const int pix = (b * p.H + iy) * p.W + ix;
-            hoff0[j] = inb ? pix * p.ldc0 + 4 * q : 0;
+            hoff0[j] = inb ? (pix * p.ldc0 + 4 * q) * 4 : (int)OOB;  // byte offset, chunk 0
         }
     }
     unsigned hinc = hin;  // in-bounds bits of the chunk in the halo registers
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         } else {
 #pragma unroll
             for (int j = 0; j < T::H_PER_T; ++j)
-                rh[j] = bload_f4(srd0, ((hin >> j) & 1u) ? (unsigned)(hoff0[j] + c * 16) * 4u : OOB);
+                rh[j] = bload_f4s(srd0, (unsigned)hoff0[j], c * 64);
         }
         if (ss) load_ss(c);
     };
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         constexpr int PV = decltype(P)::value;
 #pragma unroll
         for (int j = 0; j < T::C_PER_T; ++j)
-            rc[PV][j] = bload_f4(srd1, (coff0 + (unsigned)j * cstep + (unsigned)c * 16u) * 4u);
+            rc[PV][j] = bload_f4s(srd1, coff0 * 4u, (int)(((unsigned)j * cstep + (unsigned)c * 16u) * 4u));
     };
     // segment-1 centre -> halo buffer hs: raw input (F3: scaled), R16: 2 fp16 pieces, else 3 bf16
     auto write_center = [&](auto P, int hs) {
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
             const bool ok = j < T::B_FULL || i < items;
-            rb[j] = bload_u4(srdw, ok ? base + (unsigned)i * 16u : OOB);
+            rb[j] = bload_u4s(srdw, ok ? (unsigned)i * 16u : OOB, (int)base);
         }
     };
     auto write_b = [&](int bs, int s) {
@@ -474,13 +474,12 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         auto load_w = [&](int set, int st) {
             unsigned off;
             int items_unused;
-            step_w(st, off, items_unused);
-            off += wlane;
+            step_w(st, off, items_unused);  // wave-uniform: the scalar offset
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
                 for (int pc = 0; pc < 2; ++pc)
-                    wreg[set][nb][pc] = bload_u4(srdw, off + (unsigned)(nb * 32 * 16 + pc * 2 * T::BPLANE));
+                    wreg[set][nb][pc] = bload_u4s(srdw, wlane + (unsigned)(nb * 32 * 16 + pc * 2 * T::BPLANE), (int)off);
         };
         auto compute_w = [&](int set, int hs, int toff) {
             const unsigned char* ha = smem + hs * T::HSTAGE + toff * 16;

@@ -23,6 +23,15 @@ WC_DEVICE u32x4 bload_u4(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// per-lane offset voff plus a wave-uniform (SGPR) offset soff: loop-invariant lane offsets need no
+// per-load VALU (OOB in voff still reads 0: the range check is on voff + the immediate)
+WC_DEVICE f32x4 bload_f4s(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+WC_DEVICE u32x4 bload_u4s(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
 WC_DEVICE float bload_f1(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }

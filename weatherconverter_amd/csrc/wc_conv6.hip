@@ -287,11 +287,14 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             }
         }
     };
-    auto load_center = [&](auto P, int c) {
+    // live = false: the same loads at an out-of-range offset (zeros, no traffic), so that the
+    // number of loads in flight does not depend on a runtime condition (see load_w below)
+    auto load_center = [&](auto P, int c, bool live = true) {
         constexpr int PV = decltype(P)::value;
+        const unsigned v = live ? coff0 * 4u : OOB;
 #pragma unroll
         for (int j = 0; j < T::C_PER_T; ++j)
-            rc[PV][j] = bload_f4s(srd1, coff0 * 4u, (int)(((unsigned)j * cstep + (unsigned)c * 16u) * 4u));
+            rc[PV][j] = bload_f4s(srd1, v, (int)(((unsigned)j * cstep + (unsigned)c * 16u) * 4u));
     };
     // segment-1 centre -> halo buffer hs: raw input (F3: scaled), R16: 2 fp16 pieces, else 3 bf16
     auto write_center = [&](auto P, int hs) {
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         if constexpr (GL) return;
         unsigned base;
         int items;
-        step_w(s, base, items);
+        step_w(s < S ? s : S - 1, base, items);  // issued unconditionally: see load_w
 #pragma unroll
         for (int j = 0; j < T::B_PER_T; ++j) {
             const int i = tid + NT * j;
@@ -471,10 +474,14 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         constexpr int NS = LA2 ? 3 : 2;
         u32x4 wreg[NS][2][2];  // [set][nb][piece]
         const unsigned wlane = (unsigned)(half * T::BPLANE + (wn * 64 + l32) * 16);
+        // Every weight / centre load is issued unconditionally (a step past the end re-reads the last
+        // one, unused): with a load behind a branch the compiler's vmcnt bookkeeping must assume the
+        // skipped path at the join and waits for ALL loads in flight, i.e. for the next step's
+        // weights in the middle of this step, on every other step.
         auto load_w = [&](int set, int st) {
             unsigned off;
             int items_unused;
-            step_w(st, off, items_unused);  // wave-uniform: the scalar offset
+            step_w(st < S ? st : S - 1, off, items_unused);  // wave-uniform: the scalar offset
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
@@ -528,14 +535,17 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                     load_w((mt + 1 + TODD * PV) & 1, st + 1);
                     load_ss(c + 1);
                 } else if (!(EARLY && mt == NTAP - 2)) {
-                    if (st + 1 < S) load_w((mt + 1 + TODD * PV) & 1, st + 1);
+                    load_w((mt + 1 + TODD * PV) & 1, st + 1);
                     if (mt == NTAP - 2) {
                         if constexpr (!LAST) load_halo0(c + 1);
                         else if constexpr (RES) load_center(I0, 0);
                     }
                 }
+                // keep the next step's loads at the head of this one (the scheduler otherwise sinks
+                // them behind this step's MFMAs, leaving a few hundred cycles for an L2 round trip)
+                __builtin_amdgcn_sched_barrier(0);
                 if constexpr (RES && LAST) {
-                    if (mt == 8 && p.nck1 > 1) load_center(I1, 1);
+                    if (mt == 8) load_center(I1, p.nck1 > 1 ? 1 : 0);
                 }
                 // tap offset in the halo; CT parity (py, px): tap (i, j) reads input offset (py - i, px - j)
                 const int toff = S2D ? ((mt >> 1) + 1) * HWD + (mt & 1) + 1
@@ -556,8 +566,9 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                     constexpr int PV = decltype(P)::value, QV = decltype(QQ)::value;
                     const int st = S0w + cc;
                     const bool more = st + 1 < S;
-                    if (more) load_w(QV ^ 1, st + 1);
-                    if (cc + 2 < p.nck1) load_center(P, cc + 2);
+                    load_w(QV ^ 1, st + 1);
+                    load_center(P, cc + 2 < p.nck1 ? cc + 2 : p.nck1 - 1);
+                    __builtin_amdgcn_sched_barrier(0);
                     compute_w(QV, QV, HWD + 1);  // the halo centre = the output pixel
                     if (more) write_center(std::integral_constant<int, PV ^ 1>{}, QV ^ 1);
                     __syncthreads();
@@ -597,18 +608,22 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                 if constexpr (GL) {
                     if (more) glds_b(s + 1);  // buffer (s+1)&1 was last read in step s-1
                 }
-                if (more) load_b(s + 1);
+                load_b(s + 1);
                 // The next chunk's halo loads go out one K-step before the last, after that step's
                 // weight loads: vmcnt drains in issue order, so a halo load issued earlier would be
                 // waited for by every later step's weight-tile wait (an HBM-latency stall per chunk).
                 // After the last chunk come residual centres 0 (one step early) and 1 (in the last).
+                // Every load is issued in every chunk (the last chunk re-reads its own halo, the
+                // centres of the other chunks go to an out-of-range offset): a load behind a runtime
+                // branch makes the compiler wait for all loads in flight at the next weight wait.
                 if (mt == T::NMT - 2) {
-                    if (c + 1 < p.nck0) load_halo0(c + 1);
-                    else if constexpr (RES) load_center(I0, 0);
+                    load_halo0(c + 1 < p.nck0 ? c + 1 : c);
+                    if constexpr (RES) load_center(I0, 0, c + 1 == p.nck0);
                 }
                 if constexpr (RES) {
-                    if (mt == T::NMT - 1 && c + 1 == p.nck0 && p.nck1 > 1) load_center(I1, 1);
+                    if (mt == T::NMT - 1) load_center(I1, 1, c + 1 == p.nck0 && p.nck1 > 1);
                 }
+                __builtin_amdgcn_sched_barrier(0);
     #pragma unroll
                 for (int tt = 0; tt < T::TPS; ++tt) {
                     const int tp = mt * T::TPS + tt;
@@ -636,11 +651,12 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
                 constexpr int PV = decltype(P)::value;
                 const int hs = (p.nck0 + c) & 1;
                 const bool more = s + 1 < S;
-                if (more) {
-                    if constexpr (GL) glds_b(s + 1);
-                    load_b(s + 1);
+                if constexpr (GL) {
+                    if (more) glds_b(s + 1);
                 }
-                if (c + 2 < p.nck1) load_center(P, c + 2);
+                load_b(s + 1);
+                load_center(P, c + 2, c + 2 < p.nck1);
+                __builtin_amdgcn_sched_barrier(0);
                 if constexpr (R16) compute3(hs, HWD + 1, s & 1, 0);  // the halo centre = the output pixel
                 else compute6(hs, HWD + 1, s & 1);
                 if (more) {

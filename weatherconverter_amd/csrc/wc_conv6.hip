@@ -790,6 +790,13 @@ bool conv3_la2() {
     }();
     return v != 0;
 }
+bool conv3_wr16() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_WR16");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+}
 bool conv3_la2_res() {
     static const int v = [] {
         const char* e = getenv("WC_CONV3_LA2");
@@ -814,6 +821,12 @@ int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
     // weights in registers: the TH = 8 forms without the residual segment only (same-box A/B: conv1
     // 338 -> 356 TF/s; the TH = 16 / BN = 64 form drops to 2 waves/SIMD and loses, 312 -> 292; with
     // the residual the register sets exceed the 3-wave budget and spill)
+    if constexpr (TH == 16) {  // the 64-channel forms on weights in registers too (WC_CONV3_WR16=0: LDS-staged,
+                               // for A/B; same box 27.10 -> 27.00 ms/step)
+        if (f3 && conv3_wr16() && pro == 2 && (!res || d.abound != nullptr))
+            return res ? launch6<TH, BN, 2, true, true, true, false, 0, 1>(d, s)
+                       : launch6<TH, BN, 2, false, true, false, false, 0, 1>(d, s);
+    }
     if constexpr (TH == 8) {
         if (f3 && conv3_la2() && pro == 2 && (!res || (conv3_la2_res() && d.abound != nullptr)))
             return res ? launch6<TH, BN, 2, true, true, true, false, 0, 2>(d, s)

@@ -694,6 +694,51 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         if (ok && p.temb) eadd[nb] += p.temb[b * p.temb_ld + n];
         emul[nb] = (F3 && ok) ? p.wsinv[n] * ainv : 1.0f;
     }
+    // Fast path (no activation, the whole column tile inside N: every UNet 3x3 conv): straight-line
+    // code, per 32 x 32 block 16 residual loads issued together, then 16 stores; row offsets in the
+    // scalar buffer offset.  The general path below branches per element on the activation and per
+    // block on n < N, and the compiler then waits for each residual load right after issuing it.
+    const bool fast = p.act == WC_ACT_NONE && n0 + BN <= p.N;
+    auto epi_fast = [&](auto HR) {
+        constexpr bool HASRES = decltype(HR)::value;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int pix0 = CT ? (2 * (y0 + 4 * wm + 2 * mb) + (par >> 1)) * 2 * p.W + 2 * x0 + (par & 1)
+                                : (y0 + 4 * wm + 2 * mb) * p.W + x0;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int n = n0 + wn * 64 + nb * 32 + l32;
+                const float add = eadd[nb], mul = emul[nb];
+                float rv[16];
+                if constexpr (HASRES) {
+                    const unsigned vres = (unsigned)(pix0 * p.ldres + n) * 4u;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                        const int dpx = CT ? (row_dy(row) ? 4 * p.W : 0) + 2 * row_dx(row)
+                                           : (row_dy(row) ? p.W : 0) + row_dx(row);
+                        rv[r] = bload_f1s(srd_res, vres, dpx * p.ldres * 4);
+                    }
+                }
+                const unsigned vout = (unsigned)(pix0 * p.ldo + n) * 4u;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                    const int dpx = CT ? (row_dy(row) ? 4 * p.W : 0) + 2 * row_dx(row)
+                                       : (row_dy(row) ? p.W : 0) + row_dx(row);
+                    float v = (F3 ? acc[mb][nb][r] * mul : acc[mb][nb][r]) + add;
+                    if constexpr (HASRES) v += rv[r];
+                    bstore_f1s(srd_out, vout, dpx * p.ldo * 4, v);
+                    vmax = fmaxf(vmax, fabsf(v));
+                    acc[mb][nb][r] = v;
+                }
+            }
+        }
+    };
+    if (fast) {
+        if (p.res) epi_fast(std::true_type{});
+        else epi_fast(std::false_type{});
+    } else
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
         // pixel (dy 0, dx 0) of this 32-row block; CT: output pixel (2y + py, 2x + px) of 2H x 2W

@@ -108,8 +108,10 @@ struct X6Tile {
     static constexpr int NMT = (NTAP + TPS - 1) / TPS;    // K-steps per 16-channel chunk
     static constexpr int BSTEPM = TPS * BSTEP0;           // weight bytes of a full segment-0 K-step
     static constexpr int BSTAGE = (RES && BSTEP1 > BSTEPM) ? BSTEP1 : BSTEPM;  // LDS weight buffer
-    // WR: weight fragments go from global (L2) straight into registers, no LDS weight stage
-    static constexpr int LDS = 2 * HSTAGE + (WR ? 0 : 2 * BSTAGE);
+    // WR: weight fragments go from global (L2) straight into registers, no LDS weight stage.
+    // WR 3 (nck1 == nck0): residual chunk c rides in 3x3 chunk c as a tenth step; its TH x 16
+    // centre goes to two more halo-shaped buffers after the halo's own (same A addressing)
+    static constexpr int LDS = 2 * HSTAGE + (WR ? (WR == 3 ? 2 * HSTAGE : 0) : 2 * BSTAGE);
     static constexpr int H_ITEMS = HPIX * 4;             // float4 items of one halo chunk
     static constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
     static constexpr int C_PER_T = TH * 16 * 4 / NT;      // float4 items of one residual centre chunk
@@ -515,10 +517,14 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         // parity carries the alternation across chunks), mt & 1 for the 2x2 tap grids
         constexpr int NTAP = T::NTAP, TODD = NTAP & 1;
         const int pv0 = (p.nck0 - 1) & 1;
+        // WR 3: the centre of a chunk (rc set 0) into centre buffer hs (halo-shaped, after the halo's)
+        auto write_cf = [&](int hs) { write_center(I0, 2 + hs); };
         load_halo0(0);
-        if (TODD && pv0) load_w(1, 0);
+        if constexpr (WR == 3 && RES) load_center(I0, 0);
+        if (TODD && pv0 && WR != 3) load_w(1, 0);
         else load_w(0, 0);
         write_halo(pv0, true);
+        if constexpr (WR == 3 && RES) write_cf(pv0);
         __syncthreads();
         auto chunk = [&](auto P, auto L, int c) {
             constexpr int PV = decltype(P)::value;  // the chunk's halo buffer and set parity
@@ -583,6 +589,56 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         };
         const std::integral_constant<int, 0> NL;
         const std::integral_constant<int, 1> LL;
+        if constexpr (WR == 3 && RES) {
+            // ---- residual interleaved: chunk c = 9 taps of segment 0 + the 1x1 step of segment-1
+            // chunk c (nck1 == nck0). Ten steps per chunk, so the weight set of step mt is mt & 1
+            // for every chunk; the centre of chunk c + 1 is loaded with its halo and written to the
+            // other buffer's centre region at the chunk's end: no separate residual phase, no
+            // barrier per 1x1 step.
+            // weights of step (c, mt): taps in segment 0, mt == 9 the segment-1 step c; past the
+            // end: the last step again (issued unconditionally, unused)
+            auto load_wf = [&](int set, int c, int mt) {
+                if (c >= p.nck0) { c = p.nck0 - 1; mt = 9; }
+                const unsigned off = mt < 9 ? wtile + (unsigned)((9 * c + mt) * T::BSTEP0)
+                                            : wtile + seg0_bytes + (unsigned)(c * T::BSTEP1);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int pc = 0; pc < 2; ++pc)
+                        wreg[set][nb][pc] = bload_u4s(srdw, wlane + (unsigned)(nb * 32 * 16 + pc * 2 * T::BPLANE), (int)off);
+            };
+            auto compute_cf = [&](int set, int hs) { compute_w(set, 2 + hs, HWD + 1); };
+            auto chunk_f = [&](auto P, auto L, int c) {
+                constexpr int PV = decltype(P)::value;
+                constexpr bool LAST = decltype(L)::value != 0;
+#pragma unroll
+                for (int mt = 0; mt < 10; ++mt) {
+                    load_wf((mt + 1) & 1, mt < 9 ? c : c + 1, mt < 9 ? mt + 1 : 0);
+                    if constexpr (!LAST) {  // GN scale / shift (L2) last: 8 registers fewer through taps 7-8
+                        if (mt == 7) load_halo0(c + 1, false);
+                        if (mt == 8) load_center(I0, c + 1);
+                        if (mt == 9) load_ss(c + 1);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (mt < 9) compute_w(mt & 1, PV, (mt / 3) * HWD + mt % 3);
+                    else compute_cf(1, PV);
+                }
+                if constexpr (!LAST) {
+                    write_halo(PV ^ 1, true);
+                    write_cf(PV ^ 1);
+                    __syncthreads();
+                }
+            };
+            // (the prologue above wrote chunk 0's halo and centre into buffer pv0 and loaded step
+            // (0, 0)'s weights into set 0)
+            int c = 0;
+            if (pv0) chunk_f(I1, NL, c++);
+            for (; c + 1 < p.nck0 - 1; c += 2) {
+                chunk_f(I0, NL, c);
+                chunk_f(I1, NL, c + 1);
+            }
+            chunk_f(I0, LL, p.nck0 - 1);
+        } else {
         int c = 0;
         if (pv0) chunk(I1, NL, c++);  // nck0 even: the leading odd chunk
         for (; c + 1 < p.nck0 - 1; c += 2) {
@@ -591,6 +647,7 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         }
         chunk(I0, LL, p.nck0 - 1);
         residual(I1);  // the residual centres follow in halo buffer 1, weight set 1
+        }
     } else {
         // ---- K loop: steps = (chunk, tap) of segment 0, then the chunks of segment 1 ----
         load_halo0(0);
@@ -842,6 +899,15 @@ bool conv3_wr16() {
     }();
     return v != 0;
 }
+// residual 1x1 chunks interleaved with the 3x3 chunks when the two segments have as many chunks
+// (WC_CONV3_FUSE=0: the separate residual phase, one barrier per 1x1 step; for A/B)
+bool conv3_fuse() {
+    static const int v = [] {
+        const char* e = getenv("WC_CONV3_FUSE");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+}
 bool conv3_la2_res() {
     static const int v = [] {
         const char* e = getenv("WC_CONV3_LA2");
@@ -880,8 +946,10 @@ int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
             return pro == 1 ? launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s)
                             : launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);
         }
-        if (f3 && conv3_wr_res() && res && d.abound != nullptr && pro == 2)
+        if (f3 && conv3_wr_res() && res && d.abound != nullptr && pro == 2) {
+            if (d.nck1 == d.nck0 && conv3_fuse()) return launch6<TH, BN, 2, true, true, true, false, 0, 3>(d, s);
             return launch6<TH, BN, 2, true, true, true, false, 0, true>(d, s);
+        }
     }
     if (f3) {  // f16x3 needs the GN prologue (the static bound); pro is 1 or 2 here
         const bool r16 = res && d.abound != nullptr;

@@ -1,0 +1,82 @@
+// Host-side AddressSanitizer check of the C ABI (include/wc_kernels.h).
+//
+// Built by tools/asan/run.sh with `-Xarch_host -fsanitize=address`, so only the host code of every
+// entry point is instrumented (GPU ASan is not available on this pool).  It needs no GPU: every call
+// below is rejected by the argument / shape validation before any launch, or is a host-only sizing
+// helper.  What it proves: the validation code reads nothing outside the caller's structs, and each
+// rejection returns the documented WC_E_* code (the Python layer turns these into RuntimeError).
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "wc_kernels.h"
+
+static int failures = 0;
+
+#define EXPECT(expr, want)                                                                       \
+    do {                                                                                         \
+        const int got_ = (expr);                                                                 \
+        if (got_ != (want)) {                                                                    \
+            std::printf("FAIL %s:%d %s -> %d (want %d)\n", __FILE__, __LINE__, #expr, got_, want); \
+            ++failures;                                                                          \
+        }                                                                                        \
+    } while (0)
+
+int main() {
+    // Host buffers stand in for device pointers: none of them is dereferenced by the host code.
+    std::vector<float> buf(1 << 12, 0.f);
+    float* p = buf.data();
+    wc_conv_args a;
+    std::memset(&a, 0, sizeof(a));
+
+    // Convolution entry points: null struct / weights / output, bad segment count, bad channels.
+    EXPECT(wc_conv_igemm(nullptr, nullptr), WC_E_ARG);
+    EXPECT(wc_conv_igemm(&a, nullptr), WC_E_ARG);
+    a.w = p;
+    a.out = p;
+    a.nseg = 3;
+    EXPECT(wc_conv_igemm(&a, nullptr), WC_E_ARG);
+    a.nseg = 1;
+    EXPECT(wc_conv_igemm(&a, nullptr), WC_E_ARG);  // seg[0].src == NULL
+    a.seg[0].src = p;
+    a.seg[0].C = 30;  // not a multiple of the K tile
+    a.seg[0].ldc = 32;
+    EXPECT(wc_conv_igemm(&a, nullptr), WC_E_SHAPE);
+    EXPECT(wc_conv3x3_x6(nullptr, p, 0, nullptr), WC_E_ARG);
+    EXPECT(wc_conv3x3_f16x3(nullptr, p, 0, 0, p, nullptr, nullptr), WC_E_ARG);
+    a.seg[0].scale = p;  // scale without shift
+    EXPECT(wc_conv3x3_f16x3(&a, p, 0, 0, p, nullptr, nullptr), WC_E_ARG);
+    a.seg[0].scale = nullptr;
+    EXPECT(wc_conv_igemm_x6(nullptr, p, 0, nullptr), WC_E_ARG);
+
+    // Attention: null operands, heads not dividing C, unsupported head width, misaligned strides.
+    EXPECT(wc_attention_fwd(nullptr, 96, p, 32, 1, 64, 32, 4, 1.f, nullptr), WC_E_ARG);
+    EXPECT(wc_attention_fwd(p, 96, p, 32, 1, 64, 30, 4, 1.f, nullptr), WC_E_SHAPE);
+    EXPECT(wc_attention_fwd(p, 96, p, 32, 1, 64, 36, 9, 1.f, nullptr), WC_E_SHAPE);  // D = 4
+    EXPECT(wc_attention_fwd(p, 90, p, 32, 1, 64, 32, 4, 1.f, nullptr), WC_E_SHAPE);
+    EXPECT(wc_attention_fwd_lse(p, 96, p, 32, nullptr, 1, 64, 32, 4, 1.f, nullptr), WC_E_ARG);
+    EXPECT(wc_attention_fwd_f16x3(nullptr, 96, p, 32, 1, 64, 32, 4, 1.f, 0, 0, 0, nullptr), WC_E_ARG);
+
+    // Sampler / training element-wise entry points.
+    EXPECT(wc_ddpm_step(nullptr, p, p, p, nullptr, 1, 16, 0.f, 0.f, 1.f, 0.f, 0, 0, 0, 0, nullptr), WC_E_ARG);
+    EXPECT(wc_ddpm_step(p, p, p, p, nullptr, 1, 15, 0.f, 0.f, 1.f, 0.f, 0, 0, 0, 0, nullptr), WC_E_SHAPE);
+    EXPECT(wc_ddpm_step(p, p, p, p, nullptr, 1, 16, 0.f, 0.f, 1.f, 0.f, 7, 0, 0, 0, nullptr), WC_E_ARG);
+    EXPECT(wc_mse_loss(nullptr, p, 16, nullptr, 1.f, nullptr, p, nullptr), WC_E_ARG);
+    std::vector<double> ws(wc_mse_workspace_doubles());
+    EXPECT(wc_mse_loss(p, p, 0, nullptr, 1.f, ws.data(), p, nullptr), WC_E_SHAPE);
+    EXPECT(wc_mse_loss(p + 1, p, 16, nullptr, 1.f, ws.data(), p, nullptr), WC_E_SHAPE);  // misaligned
+
+    // Host-only sizing helpers must be positive and deterministic.
+    if (wc_conv3x3_x6_tile_n(64) != 64 || wc_conv3x3_x6_tile_n(320) != 128) {
+        std::printf("FAIL wc_conv3x3_x6_tile_n\n");
+        ++failures;
+    }
+    if (wc_gn_num_splits(16, 4096, 320) <= 0 || wc_gn_bwd_splits(16, 4096) <= 0 ||
+        wc_conv_wgrad_splits(320, 2880, 65536, 1024) <= 0 || wc_mse_workspace_doubles() <= 0) {
+        std::printf("FAIL sizing helpers\n");
+        ++failures;
+    }
+
+    std::printf("abi_validation: %d failure(s)\n", failures);
+    return failures == 0 ? 0 : 1;
+}

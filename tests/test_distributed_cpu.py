@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: the N>1 sharding contract (ranges, keyed noise slicing, final gather)."""
+"""CPU, world_size 2/4/8 over gloo: the N>1 sharding contract (ranges, keyed noise slicing, final gather)."""
 import os
 import socket
 
@@ -47,9 +47,9 @@ def _worker(rank, world, port, total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('total', [4, 5])
-def test_gloo_world2_gather_equals_single_rank(total):
-    world = 2
+@pytest.mark.parametrize('world,total', [(2, 4), (2, 5), (4, 7), (8, 5)])
+def test_gloo_gather_equals_single_rank(world, total):
+    """world 8 with 5 samples leaves three ranks with an empty shard (the rehearsal of the driver's N=8 run)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()

@@ -60,7 +60,7 @@ def _worker(rank, world, port, total, noise, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('total,noise', [(4, 'philox'), (5, 'philox'), (4, 'torch_cpu')])
+@pytest.mark.parametrize('total,noise', [(4, 'philox'), (5, 'philox'), (4, 'torch_cpu'), (1, 'philox')])
 def test_sample_sharded_world2_equals_single_rank(total, noise):
     from weatherconverter_amd.diffusion_model.sample_ddpm import sample_tensor
     from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler

@@ -65,6 +65,10 @@ def sample_sharded(model, scheduler, total_batch: int, im_channels: int, im_size
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     start, count = shard_range(total_batch, world, rank)
+    if count == 0:  # more ranks than images: this rank launches nothing and only joins the gather
+        dev = next(model.parameters()).device
+        x = torch.empty((0, im_channels, im_size, im_size), dtype=torch.float32, device=dev)
+        return gather_samples(x, total_batch, group) if gather else x
     x = sample_tensor(model, scheduler, count, im_channels, im_size, noise=noise, seed=seed, sample0=start,
                       total_batch=total_batch, graph=graph)
     if world == 1 or not gather:

@@ -71,6 +71,9 @@ def parse(argv=None):
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--precision', default=None, choices=['f16x3', 'bf16x6', 'fp32'],
                     help='conv/attention arithmetic (default: kernels.default_conv_precision(), i.e. f16x3)')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='process-group backend for N>1: nccl (= RCCL over xGMI, the benched path) or gloo '
+                         '(x0 gather staged through host memory; lets N ranks share one GPU for rehearsal)')
     return ap.parse_args(argv)
 
 
@@ -291,9 +294,27 @@ def _launch_cmd(gpus: int, argv, port: int):
             '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + list(argv)
 
 
+def _profiler_preloaded() -> bool:
+    """True when a profiler library is preloaded into this process (``rocprofv3 -- python bench.py``):
+    it has initialised the GPU before main() runs, so spawning the launcher from here is the
+    fork-after-GPU-init pattern this pool forbids."""
+    if 'rocprof' in os.environ.get('LD_PRELOAD', ''):
+        return True
+    try:
+        with open('/proc/self/maps') as f:
+            # librocprofiler-register ships inside torch itself; the profiler's tool library is the SDK's
+            return 'rocprofiler-sdk' in f.read()
+    except OSError:
+        return False
+
+
 def _self_launch(args) -> int:
     """--gpus N>1 outside torch.distributed.run: start it as a child (nothing here has touched the GPU;
-    the parent only waits and passes the exit code on)."""
+    the parent only waits and passes the exit code on).  Refused under a profiler preload."""
+    if _profiler_preloaded():
+        raise SystemExit('bench.py: --gpus N>1 would start torch.distributed.run from a process whose GPU '
+                         'runtime is already loaded (profiler preload?); run it under torch.distributed.run '
+                         'directly instead')
     with socket.socket() as sk:
         sk.bind(('127.0.0.1', 0))
         port = sk.getsockname()[1]
@@ -308,6 +329,33 @@ def _world(args) -> int:
     return world
 
 
+def _gather_x0(x, world: int, backend: str):
+    """The one collective of the path: all-gather every rank's x0 block into the full batch.  RCCL
+    gathers the device tensors in place over xGMI; gloo cannot gather device tensors, so its blocks are
+    staged through host memory and the result copied back (as distributed.gather_samples does)."""
+    if backend == 'nccl':
+        out = torch.empty((x.shape[0] * world, ) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        dist.all_gather_into_tensor(out, x)
+        return out
+    xs = x.detach().cpu()
+    parts = [torch.empty_like(xs) for _ in range(world)]
+    dist.all_gather(parts, xs)
+    return torch.cat(parts, 0).to(x.device)
+
+
+def _gather_times(vals, world: int, backend: str, dev):
+    """(world, len(vals)) float64 of every rank's timings (for the max-over-ranks rule)."""
+    if backend == 'nccl':
+        tt = torch.tensor(vals, device=dev, dtype=torch.float64)
+        allt = torch.empty((world, len(vals)), device=dev, dtype=torch.float64)
+        dist.all_gather_into_tensor(allt, tt)
+        return allt.cpu()
+    tt = torch.tensor(vals, dtype=torch.float64)
+    parts = [torch.empty_like(tt) for _ in range(world)]
+    dist.all_gather(parts, tt)
+    return torch.stack(parts)
+
+
 def main():
     args = parse()
     if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
@@ -315,11 +363,16 @@ def main():
     world = _world(args)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
+    # one rank per GPU; under gloo more ranks than GPUs may share a card (rehearsal of the N-rank path
+    # on a one-GPU box).  device_count() does not initialise the GPU on this image.
+    ndev = max(1, torch.cuda.device_count())
+    dev = torch.device('cuda', local % ndev if args.backend == 'gloo' else local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
     from weatherconverter_amd import kernels
     from weatherconverter_amd.diffusion_model.config import model_config
@@ -361,10 +414,8 @@ def main():
         del xw
         gathered = None
         gather_sec = 0.0
-        if world > 1:  # RCCL communicator set up outside the timed region
-            warm = torch.empty((B * world, ) + shape[1:], device=dev)
-            dist.all_gather_into_tensor(warm, x)
-            del warm
+        if world > 1:  # communicator set up outside the timed region
+            _gather_x0(x, world, args.backend)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -378,8 +429,7 @@ def main():
         if world > 1:
             torch.cuda.synchronize()
             g0 = time.perf_counter()
-            gathered = torch.empty((B * world, ) + shape[1:], device=dev)
-            dist.all_gather_into_tensor(gathered, x)
+            gathered = _gather_x0(x, world, args.backend)
             torch.cuda.synchronize()
             gather_sec = time.perf_counter() - g0
         torch.cuda.synchronize()
@@ -388,9 +438,7 @@ def main():
         per_rank = [elapsed]
         per_rank_gather = [gather_sec]
         if world > 1:
-            tt = torch.tensor([elapsed, gather_sec], device=dev, dtype=torch.float64)
-            allt = torch.empty((world, 2), device=dev, dtype=torch.float64)
-            dist.all_gather_into_tensor(allt, tt)
+            allt = _gather_times([elapsed, gather_sec], world, args.backend, dev)
             per_rank = [float(v) for v in allt[:, 0].tolist()]
             per_rank_gather = [float(v) for v in allt[:, 1].tolist()]
             elapsed = max(per_rank)
@@ -414,7 +462,9 @@ def main():
                 'higher_is_better': True,
                 'scaling': 'weak',
                 'vs_baseline': None,
-                'dtype': 'f32',
+                'dtype': {'f16x3': 'fp32-class (f16x3: 2-piece fp16 split MFMA, fp32 accumulate)',
+                          'bf16x6': 'fp32-class (bf16x6: 3-piece bf16 split MFMA, fp32 accumulate)',
+                          'fp32': 'f32 (fp32 MFMA)'}[precision],
                 'data': 'synthetic (keyed random-init weights, Philox N(0,1) x_T and per-step noise)',
                 'extrapolated_from_steps': None if K == T else
                 f'{K} of T={T} steps timed; images/s = images x {K}/{T} / elapsed (UNet cost does not depend on t)',
@@ -424,7 +474,11 @@ def main():
                     'global_batch': B * world,
                     'image_size': args.size,
                     'timesteps': T,
-                    'parallelism': f'batch-sharded x{world}, 1 RCCL all-gather of x0' if world > 1 else 'single GPU',
+                    'parallelism': (f'batch-sharded x{world}, 1 all-gather of x0 over '
+                                    + ('RCCL (xGMI)' if args.backend == 'nccl' else 'gloo (host-staged)'))
+                    if world > 1 else 'single GPU',
+                    'backend': args.backend if world > 1 else None,
+                    'devices': torch.cuda.device_count(),
                     'hip_graph': bool(args.graph),
                     'stream_groups': runner.split if runner is not None else 1,
                     'arithmetic': {
@@ -456,6 +510,9 @@ def main():
             result['cpu_baseline'] = None
         print(json.dumps(result), flush=True)
     if world > 1:
+        # ranks 1..N-1 wait here for rank 0's roofline / parity / CPU-baseline legs before tearing the
+        # communicator down
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -35,3 +35,52 @@ def test_cpu_share_probe():
     share = bench._cpu_share()
     assert 1 <= share['usable_cpus'] <= share['host_cpus']
     assert share['usable_cpus'] <= share['affinity_cpus']
+
+
+def _bench_gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        x = torch.full((2, 3, 4, 4), float(rank))
+        g = bench._gather_x0(x, world, 'gloo')
+        t = bench._gather_times([0.5 + rank, 0.01 * rank], world, 'gloo', None)
+        q.put((rank, g.numpy().copy(), t.numpy().copy()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_bench_gloo_collectives(world):
+    """bench.py's gloo branch of the x0 all-gather and of the per-rank timing reduction."""
+    import socket
+
+    import numpy as np
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for _, g, t in res:
+        assert g.shape == (2 * world, 3, 4, 4)
+        for r in range(world):
+            assert np.all(g[2 * r:2 * r + 2] == r)
+        assert t.shape == (world, 2)
+        assert np.allclose(t[:, 0], 0.5 + np.arange(world))
+
+
+def test_self_launch_refused_under_profiler(monkeypatch):
+    monkeypatch.setenv('LD_PRELOAD', '/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so')
+    assert bench._profiler_preloaded()
+    with pytest.raises(SystemExit):
+        bench._self_launch(bench.parse(['--gpus', '2']))

@@ -35,6 +35,19 @@ from .engine import TAPS1, TAPS3, TAPS4S2, pack_conv, pack_convT
 _PARITIES = ((0, 0), (0, 1), (1, 0), (1, 1))
 
 
+class Tape:
+    """Everything one training forward saved for its backward: the layer records (activations, GN
+    statistics, packed weights) plus the inputs and the per-step weight packs the backward reads.  One
+    per forward, owned by that forward's autograd node, consumed by exactly one backward."""
+    _FIELDS = ('records', 'x', 'tt', 'U', 'P', 'head_T', 'tproj', 'temb_w', 'res_rows')
+
+    def __init__(self, engine: 'TrainEngine'):
+        self.records = engine.tape
+        for f in self._FIELDS[1:]:
+            setattr(self, f, getattr(engine, f))
+        self.consumed = False
+
+
 class TrainEngine:
 
     def __init__(self, model, precision: Optional[str] = None):
@@ -50,6 +63,7 @@ class TrainEngine:
         self.precision = 'fp32' if p == 'fp32' else 'bf16x6'
         self.f3 = p == 'f16x3'
         self.tape: List[tuple] = []
+        self.last_tape: Optional[Tape] = None
 
     # ------------------------------------------------------------------ packing (per step)
     def _pk(self, w2d: torch.Tensor, C0: int, ntaps: int, C1: int = 0):
@@ -276,6 +290,8 @@ class TrainEngine:
         self._conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.head_pk,
                    m.conv_out.bias.detach().float().contiguous(), None, S, S2, out_nchw=out)
         self.tape.append(('head', cur, (sc, sh, a0, o0)))
+        self.last_tape = Tape(self)
+        self.tape = []
         return out
 
     def _res_fwd(self, X: View, Y: View, rp, temb: torch.Tensor):
@@ -328,8 +344,21 @@ class TrainEngine:
         self.tape.append(('attn', Ypre, Yout, qkv, o, lse, st, ap))
 
     # ------------------------------------------------------------------ backward
-    def backward(self, gout: torch.Tensor) -> Dict[int, torch.Tensor]:
-        """Gradients of every parameter given d loss / d output (B, C, S, S); returns {id(param): grad}."""
+    def backward(self, gout: torch.Tensor, tape: Optional[Tape] = None) -> Dict[int, torch.Tensor]:
+        """Gradients of every parameter given d loss / d output (B, C, S, S) for the forward that
+        recorded ``tape`` (default: the latest forward); returns {id(param): grad}.  A tape is
+        consumed (its activations freed) by its backward: a second backward through it raises."""
+        tape = tape if tape is not None else self.last_tape
+        if tape is None or tape.consumed:
+            raise RuntimeError('Unet training backward: this forward\'s saved activations were already consumed '
+                               'by an earlier backward (retain_graph / a second backward is not supported)')
+        for f in Tape._FIELDS[1:]:
+            setattr(self, f, getattr(tape, f))
+        records = tape.records
+        tape.consumed = True
+        tape.records = []
+        if self.last_tape is tape:
+            self.last_tape = None
         m = self.model
         self.gmap: Dict[int, Tuple[torch.Tensor, int]] = {}
         self.pgrads: Dict[int, torch.Tensor] = {}
@@ -337,12 +366,14 @@ class TrainEngine:
         B = gout.shape[0]
         self.dproj = torch.zeros((B, self.P), dtype=torch.float32, device=self.device)
         gout = gout.to(self.device, torch.float32).contiguous()
-        for rec in reversed(self.tape):
+        for rec in reversed(records):
             getattr(self, '_bwd_' + rec[0])(rec, gout)
+        del records
         self._temb_bwd()
-        self.tape = []
         self.gmap = {}
         self.keep = []
+        for f in Tape._FIELDS[1:]:  # the tape's tensors die with it, not with the engine
+            setattr(self, f, None)
         return self.pgrads
 
     def _wgrad(self, g: View, segs, dw0, s0, **kw):
@@ -493,13 +524,19 @@ class UnetTrainFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, engine: TrainEngine, x: torch.Tensor, t, *params):
+        if x.requires_grad:
+            raise RuntimeError('Unet training forward: the gradient w.r.t. the input image is not computed; '
+                               'pass a tensor that does not require grad (x.detach())')
         with torch.no_grad():
             out = engine.forward(x, t)
         ctx.engine = engine
+        ctx.tape = engine.last_tape  # this forward's own saved state (gradient accumulation safe)
+        engine.last_tape = None
         ctx.param_ids = [id(p) for p in engine.model.parameters()]
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        grads = ctx.engine.backward(gout)
+        grads = ctx.engine.backward(gout, ctx.tape)
+        ctx.tape = None
         return (None, None, None) + tuple(grads.get(i) for i in ctx.param_ids)

@@ -231,8 +231,12 @@ def _cpu_share() -> dict:
 
 
 def cpu_baseline_leg(args):
-    """The reference UNet step restated op for op in PyTorch-CPU (oracle/, bitwise-equal to the reference
-    import, tests/test_oracle_golden.py), at the timed batch, on every CPU this process may use."""
+    """The reference UNet step restated op for op in PyTorch-CPU (oracle/), at the timed batch, on every
+    CPU this process may use.  The oracle calls the same torch CPU ops as the reference import
+    (including nn.MultiheadAttention's fused fast path): its forwards are bitwise-equal to the
+    reference's at equal thread count (tests/test_oracle_golden.py, 8 threads), and timed side by
+    side with the imported reference in the build container it takes 1.005x the reference's time at
+    256 px B=2 (profiles/r03_cpu_provenance.json, tools/cpu_provenance.py)."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle.unet_oracle import unet_forward, unet_state_dict_keys
     from weatherconverter_amd.diffusion_model.config import model_config
@@ -263,6 +267,8 @@ def cpu_baseline_leg(args):
         'kind': 'port',
         'ms_per_step': round(dt * 1e3, 1),
         'host': share,
+        'provenance': 'profiles/r03_cpu_provenance.json: oracle bitwise-equal to the imported reference, '
+                      '1.005x its CPU time (256 px, B=2, 8 threads, build container)',
         'sample': f'oracle PyTorch-CPU UNet step (reference unet_base.Unet restated op for op), {args.size}px, '
                   f'B={B}, {len(times)} timed step(s) after 1 warmup on {threads} threads (the CPUs this process '
                   f'may use: affinity capped by the cgroup quota), extrapolated x{args.timesteps} (T) -- '

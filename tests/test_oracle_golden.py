@@ -1,7 +1,9 @@
 """CPU: pin the oracle (oracle/) against golden vectors captured from the reference import.
 
-Tolerances: the oracle restates the reference op for op with the same torch CPU kernels except
-nn.MultiheadAttention's fused fast path, so forwards agree to ~1e-7 relative; we assert 1e-6.
+Tolerances: the oracle restates the reference op for op with the same torch CPU kernels, including
+nn.MultiheadAttention's fused fast path (torch._native_multi_head_attention), so at the goldens'
+thread count (8, tests/golden/make_golden.py) its forwards are BITWISE equal to the reference
+import; at another thread count oneDNN may reorder reductions, and we assert 1e-6.
 """
 import json
 import os
@@ -73,17 +75,24 @@ def _forward_case(name, fixture, key, B, t, xseed):
     return rel_l2(y, g[key])
 
 
+GOLDEN_THREADS = 8
+
+
+def _bound():
+    return 0.0 if torch.get_num_threads() == GOLDEN_THREADS else 1e-6
+
+
 def test_oracle_unet_tiny():
-    assert _forward_case('tiny', 'unet_tiny.npz', 'y_shared_t', 2, [7], 101) < 1e-6
-    assert _forward_case('tiny', 'unet_tiny.npz', 'y_batch_t', 2, [3, 900], 102) < 1e-6
+    assert _forward_case('tiny', 'unet_tiny.npz', 'y_shared_t', 2, [7], 101) <= _bound()
+    assert _forward_case('tiny', 'unet_tiny.npz', 'y_batch_t', 2, [3, 900], 102) <= _bound()
 
 
 def test_oracle_unet_64():
-    assert _forward_case('default_64', 'unet_64.npz', 'y', 2, [37], 201) < 1e-6
+    assert _forward_case('default_64', 'unet_64.npz', 'y', 2, [37], 201) <= _bound()
 
 
 def test_oracle_unet_256():
-    assert _forward_case('default_256', 'unet_256.npz', 'y', 1, [611], 301) < 1e-6
+    assert _forward_case('default_256', 'unet_256.npz', 'y', 1, [611], 301) <= _bound()
 
 
 @pytest.mark.slow

@@ -77,11 +77,50 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+KERNEL_DESC = {
+    'conv3x3_x6': 'split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue',
+    'conv_igemm_x6': 'split-precision MFMA implicit-GEMM conv / projection',
+    'attention_x6': 'split-precision MFMA flash attention',
+    'conv_igemm_kernel': 'fp32 MFMA implicit-GEMM conv',
+    'attention_kernel': 'fp32 MFMA flash attention',
+}
+
+
+def _describe(name: str) -> str:
+    """Human description of a kernel instantiation (rocprofv3 name, all template arguments)."""
+    base = name.split('<')[0]
+    targs = name[name.index('<') + 1:name.rindex('>')].split(', ') if '<' in name else []
+    mode = 'f16x3' if _mode_peak(name) == F16X3_PEAK_TFLOPS else ('bf16x6' if _mode_peak(name) == BF16X6_PEAK_TFLOPS
+                                                                   else 'fp32')
+    d = KERNEL_DESC.get(base, base)
+    if base == 'conv3x3_x6_kernel' and len(targs) >= 9:
+        if targs[7] == '1':
+            d = 'split-precision MFMA 4x4/s2 down conv over the space-to-depth input (halo-tiled)'
+        elif targs[7] == '2':
+            d = 'split-precision MFMA ConvTranspose 4x4/s2, four parities per halo'
+        elif targs[3] == 'true':
+            d += ', fused 1x1 residual' + (' interleaved per chunk' if targs[8] == '3' else '') + (
+                ' in f16x3 under the per-image GN bound' if targs[5] == 'true' else ' in bf16x6')
+        if targs[8] != '0':
+            d += ', weights in registers'
+    return f'{mode}: {d}'
+
+
 def roofline_leg(model, x, t_dev, groups: int = 1):
+    """Per-kernel timing of one UNet forward (eager, same kernels and arguments as the graph).
+
+    Every conv / projection / attention launch is re-issued 5x back to back right after itself
+    between one HIP event pair (kernels.replay_timing('*')): per-launch durations without event
+    gaps, as rocprofv3's kernel trace times them.  Launches are keyed by the exact instantiation the
+    library reports (rocprofv3's name), so this table lines up with the trace of the timed graph
+    replays (tools/step_table.py).  The dominant kernel = the instantiation with the most time per
+    forward; achieved = its algorithmic (fp32-equivalent) FLOPs per launch / its mean duration,
+    against its arithmetic mode's ceiling."""
     from weatherconverter_amd import kernels
     with torch.no_grad():
         model(x, t_dev)  # packs / allocations outside the measured forward
     torch.cuda.synchronize()
+    # pass 1: per-launch events around single launches (kept beside the re-issue means)
     prof = kernels.profile_conv(True)
     # Park the GPU first so the host enqueues the whole forward ahead of it: the kernels then run
     # back to back and each event pair brackets one kernel, not a host launch gap.
@@ -90,62 +129,49 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
         model(x, t_dev)
     torch.cuda.synchronize()
     kernels.profile_conv(False)
-    per, hbm = {}, {}
-    for tile, flops, e0, e1 in prof:  # HBM-bound launches (GroupNorm statistics) carry bytes, not FLOPs
-        d = (hbm if tile.startswith('gn_') else per).setdefault(tile, [0, 0.0, 0.0])
+    ev = {}
+    for name, flops, e0, e1 in prof:
+        d = ev.setdefault(name, [0, 0.0])
         d[0] += 1
-        d[1] += flops
-        d[2] += e0.elapsed_time(e1) * 1e-3
-    # dominant kernel = the conv / attention instantiation with the most event time in one UNet forward
-    name = max(per, key=lambda k: per[k][2])
-    n, fl, sec = per[name]
-    mean_events = sec / n
-    # each launch of that kernel re-issued 5x back to back between one event pair (no per-launch
-    # event gaps, as rocprof's kernel trace times it) in a second forward; the per-launch event mean
-    # of the first forward is kept beside it
-    rep = kernels.replay_timing(name, reps=5)
+        d[1] += e0.elapsed_time(e1) * 1e-3
+    # pass 2: every launch re-issued 5x between one event pair
+    rep = kernels.replay_timing('*', reps=5)
     torch.cuda._sleep(1 << 28)
     with torch.no_grad():
         model(x, t_dev)
     torch.cuda.synchronize()
     kernels.replay_timing(None)
-    replay = None
-    if rep['events']:
-        replay = sum(a.elapsed_time(b) for a, b in rep['events']) / (rep['reps'] * len(rep['events']))
-    mean_dur = replay * 1e-3 if replay is not None else mean_events
+    per, hbm = {}, {}
+    for name, flops, r0, r1, reps, nbytes in rep['events']:
+        d = (hbm if name.startswith(('gn_', 'split_')) else per).setdefault(name, [0, 0.0, 0.0, 0.0])
+        d[0] += 1
+        d[1] += flops
+        d[2] += r0.elapsed_time(r1) * 1e-3 / reps
+        d[3] += nbytes
+    name = max(per, key=lambda k: per[k][2])
+    n, fl, sec, abytes = per[name]
+    mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
-    total_conv = sum(v[2] for v in per.values())
+    peak = _mode_peak(name)
+    total_mfma = sum(v[2] for v in per.values())
     # HBM bytes per launch of this kernel from the committed two-pass PMC measurement
     # (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), if present
     traffic, traffic_src = None, None
     for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
                                               '*_hbm_traffic.json')))[-1:]:
         recs = json.load(open(path))
-        # rocprof names carry every template argument; the profile label may omit trailing defaults
-        rec = recs.get(name) or next((v for k, v in recs.items() if k.startswith(name[:-1] + ',')), None)
+        rec = recs.get(name)
         if rec:
             traffic = round(rec['total_bytes'] / 1e9, 4)
             traffic_src = (f'{os.path.relpath(path, os.path.dirname(os.path.abspath(__file__)))}: GB per launch '
                            f'(read {rec["read_bytes"] / 1e9:.3f} + write {rec["write_bytes"] / 1e9:.3f}), '
-                           f'mean over {rec["launches"]} launches')
-    targs = name[name.index('<') + 1:name.rindex('>')].split(', ')
-    f16x3 = ((name.startswith('conv3x3_x6') and len(targs) >= 5 and targs[4] == 'true')
-             or (name.startswith(('conv_igemm_x6', 'attention_x6')) and targs[-1] == 'true'))
-    desc = {'conv3x3_x6': ' (bf16x6 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue)',
-            'conv_igemm_x6': ' (bf16x6 split-precision MFMA implicit-GEMM conv)',
-            'attention_x6': ' (bf16x6 split-precision MFMA flash attention)',
-            'conv_igemm_kernel': ' (fp32 MFMA implicit-GEMM conv)',
-            'attention_kernel': ' (fp32 MFMA flash attention)'}[name.split('<')[0].replace('_kernel', '')
-                                                                   if '_x6' in name else name.split('<')[0]]
-    peak = BF16X6_PEAK_TFLOPS if '_x6' in name else FP32_PEAK_TFLOPS
-    if f16x3:
-        desc = desc.replace('bf16x6', 'f16x3')
-        if name.startswith('conv3x3_x6'):
-            desc = (' (f16x3 split-precision MFMA 3x3 conv, halo-tiled, GN+SiLU prologue, fused 1x1 residual in '
-                    + ('f16x3 under the per-image GN bound)' if targs[5:] == ['true'] else 'bf16x6)'))
-        peak = F16X3_PEAK_TFLOPS
+                           f'mean over {rec["launches"]} launches'
+                           + (f'; algorithmic {rec["algorithmic_bytes"] / 1e9:.3f}' if 'algorithmic_bytes' in rec
+                              else ''))
+    ev_n, ev_sec = ev.get(name, (0, 0.0))
     return {
-        'kernel': name + desc,
+        'kernel': name,
+        'kernel_desc': _describe(name),
         'bound': 'mfma',
         'achieved': round(achieved, 2),
         'peak': peak,
@@ -156,15 +182,18 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
         'launches_per_step': n * groups,
         'images_per_launch': int(x.shape[0]),
         'mean_launch_ms': round(mean_dur * 1e3, 4),
-        'mean_launch_ms_source': 'each launch re-issued 5x back to back between one event pair' if replay is not None else
-                                 'per-launch HIP events',
-        'mean_launch_ms_events': round(mean_events * 1e3, 4),
+        'mean_launch_ms_source': 'each launch re-issued 5x back to back between one HIP event pair',
+        'mean_launch_ms_events': round(ev_sec / ev_n * 1e3, 4) if ev_n else None,
         'gflop_per_launch': round(fl / n / 1e9, 3),
-        'share_of_mfma_event_time': round(sec / max(total_conv, 1e-12), 3),
-        'mfma_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 3), 'tflops': round(v[1] / v[2] / 1e12, 1),
-                             'peak': _mode_peak(k), 'frac': round(v[1] / v[2] / 1e12 / _mode_peak(k), 4)}
+        'algorithmic_gb_per_launch': round(abytes / n / 1e9, 4) if abytes else None,
+        'traffic_over_algorithmic': round(traffic / (abytes / n / 1e9), 3) if (traffic and abytes) else None,
+        'share_of_mfma_time': round(sec / max(total_mfma, 1e-12), 3),
+        'mfma_ms_per_forward': round(total_mfma * 1e3 * groups, 3),
+        'mfma_kernels': {k: {'launches': v[0] * groups, 'ms': round(v[2] * 1e3 * groups, 3),
+                             'tflops': round(v[1] / v[2] / 1e12, 1), 'peak': _mode_peak(k),
+                             'frac': round(v[1] / v[2] / 1e12 / _mode_peak(k), 4), 'desc': _describe(k)}
                          for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])},
-        'hbm_kernels': hbm_leg(hbm),
+        'hbm_kernels': hbm_leg(hbm, groups),
     }
 
 
@@ -177,21 +206,22 @@ def _mode_peak(name: str) -> float:
     if name.startswith('conv3x3_x6'):
         return F16X3_PEAK_TFLOPS if len(targs) >= 5 and targs[4] == 'true' else BF16X6_PEAK_TFLOPS
     if name.startswith('conv_igemm_x6'):
-        return F16X3_PEAK_TFLOPS if targs[-1] == 'true' else BF16X6_PEAK_TFLOPS
+        return F16X3_PEAK_TFLOPS if len(targs) >= 6 and targs[5] == 'true' else BF16X6_PEAK_TFLOPS
     if name.startswith('attention_x6'):
         return F16X3_PEAK_TFLOPS if targs[1] == 'true' else BF16X6_PEAK_TFLOPS
     return FP32_PEAK_TFLOPS
 
 
-def hbm_leg(hbm):
-    """The HBM-bound half of the fused ResBlock: GroupNorm+SiLU are applied in the convs' prologues,
-    so what stays on HBM is the statistics pass (one read of the activation, 4 B/element); its
-    achieved GB/s over every launch of one forward against the 8 TB/s HBM peak."""
+def hbm_leg(hbm, groups: int = 1):
+    """The HBM-bound kernels of the forward: GroupNorm+SiLU are applied in the convs' prologues, so
+    what stays on HBM is the statistics pass (one read of the activation, 4 B/element) and the
+    pre-split of the projection operand (read 4 + write 4 B/element); achieved GB/s over every
+    launch of one forward against the 8 TB/s HBM peak."""
     if not hbm:
         return None
     out = {}
-    for k, (n, by, sec) in hbm.items():
-        out[k] = {'launches': n, 'ms': round(sec * 1e3, 3), 'gbytes': round(by / 1e9, 3),
+    for k, (n, by, sec, _) in hbm.items():
+        out[k] = {'launches': n * groups, 'ms': round(sec * 1e3 * groups, 3), 'gbytes': round(by / 1e9, 3),
                   'achieved': round(by / sec / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                   'frac': round(by / sec / 1e9 / HBM_PEAK_GBS, 4)}
     return out

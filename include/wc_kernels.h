@@ -447,6 +447,13 @@ int wc_dwconv(const float* x, int ldx, float* out, int ldo, const float* w, cons
 /* Library identification (for the CPU load test). */
 const char* wc_version(void);
 
+/* Instrumentation (no reference counterpart): the exact template instantiation of the kernel the
+ * calling host thread launched last through one of the entry points above, in the demangled form
+ * rocprofv3 reports (e.g. "conv3x3_x6_kernel<8, 128, 2, false, true, false, false, 0, 1>"), or ""
+ * when that entry point does not name its kernel.  Reading it clears it.  bench.py keys its
+ * per-launch HIP-event timings by this name so they line up with the rocprofv3 kernel trace. */
+const char* wc_last_kernel_name(void);
+
 #ifdef __cplusplus
 }
 #endif

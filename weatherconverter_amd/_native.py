@@ -24,7 +24,7 @@ EXPORTS = [
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
     'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
-    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc'
+    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
@@ -148,6 +148,8 @@ def load(build_if_missing: bool = True):
         fn.restype = ctypes.c_int
     lib.wc_version.argtypes = []
     lib.wc_version.restype = ctypes.c_char_p
+    lib.wc_last_kernel_name.argtypes = []
+    lib.wc_last_kernel_name.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -160,3 +162,9 @@ def check(status: int, op: str):
 
 def call(name: str, *args):
     check(getattr(load(), name)(*args), name)
+
+
+def last_kernel_name() -> str:
+    """The exact instantiation (rocprofv3's name) of the kernel the last named launcher started on
+    this thread, or '' (wc_last_kernel_name)."""
+    return load().wc_last_kernel_name().decode()

@@ -466,6 +466,7 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
     // in the exp2 argument inside the kernel and cancels in O / l
     const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
     dim3 grid(((N + 127) / 128) * heads * B);
+    WC_SET_NAME("attention_x6_kernel", {WC_TI(D), WC_TB(F3), WC_TB(PRE), WC_TB(O3)});
     hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE, O3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
                        score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), 1.0f, ldexpf(1.f, -ev));
     WC_CHECK_LAUNCH();

@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <initializer_list>
+#include <string>
+
 #include "../../include/wc_kernels.h"
 
 #define WC_DEVICE __device__ __forceinline__
@@ -32,6 +35,35 @@ WC_DEVICE f32x16 mfma32(float a, float b, f32x16 c) {
 }
 
 WC_DEVICE int wc_lane() { return __lane_id(); }
+
+// Instantiation name of the kernel the calling host thread launched last, in the demangled form
+// rocprofv3 prints ("conv3x3_x6_kernel<8, 128, 2, false, true, false, false, 0, 1>"), read once per
+// launch through wc_last_kernel_name() so per-launch timings can be keyed exactly as the profiler
+// keys them.  Templated launchers build their name once (a function-local static string).
+inline thread_local const char* wc_last_kernel = "";
+struct WcTArg {
+    long v;
+    bool is_bool;
+};
+#define WC_TI(x) WcTArg{(long)(x), false}
+#define WC_TB(x) WcTArg{(long)(x), true}
+inline std::string wc_tname(const char* base, std::initializer_list<WcTArg> args) {
+    std::string s(base);
+    s += '<';
+    bool first = true;
+    for (const WcTArg& a : args) {
+        if (!first) s += ", ";
+        first = false;
+        s += a.is_bool ? (a.v ? "true" : "false") : std::to_string(a.v);
+    }
+    s += '>';
+    return s;
+}
+#define WC_SET_NAME(...)                                            \
+    do {                                                            \
+        static const std::string _wc_nm = wc_tname(__VA_ARGS__);    \
+        wc_last_kernel = _wc_nm.c_str();                            \
+    } while (0)
 
 // Wave-level reductions over 64 lanes.
 WC_DEVICE float wave_sum(float v) {

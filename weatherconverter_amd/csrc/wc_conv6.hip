@@ -846,6 +846,8 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n * (MAP == 2 ? 4 : 1));
+    WC_SET_NAME("conv3x3_x6_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES), WC_TB(F3), WC_TB(R16), WC_TB(GL),
+                                      WC_TI(MAP), WC_TI(WR)});
     hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>), grid, dim3(NT), T::LDS, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;

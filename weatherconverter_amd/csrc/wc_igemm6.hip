@@ -738,6 +738,7 @@ int launch(const IgDev& d, hipStream_t stream) {
                     p.steps == p.steps0 && p.H0 == p.Hm && p.W0 == p.Wm;
     if constexpr (F3 && UNIB && PRO == 0 && ACT == WC_ACT_NONE && BM == 128 && BN == 128) {
         if (p.a3) {  // pre-split A operand: LDS-DMA pipeline, transposed accumulators (both epilogues)
+            WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(0), WC_TB(true), WC_TI(ACT), WC_TB(true), WC_TI(4), WC_TB(true), WC_TB(true), WC_TB(true)});
             hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, 0, true, ACT, true, 4, true, true, true>), grid, dim3(NT), 0,
                                stream, p);
             WC_CHECK_LAUNCH();
@@ -747,8 +748,13 @@ int launch(const IgDev& d, hipStream_t stream) {
     if (p.a3) return WC_E_ARG;
     if constexpr (F3 && UNIB && PRO == 1 && ACT == WC_ACT_NONE) {
         if (p.qkv3) {  // pre-split attention projection
-            if (p1) hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true, true>), grid, dim3(NT), 0, stream, p);
-            else hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true>), grid, dim3(NT), 0, stream, p);
+            if (p1) {
+                WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(PRO), WC_TB(UNIB), WC_TI(ACT), WC_TB(F3), WC_TI(4), WC_TB(true), WC_TB(true), WC_TB(false)});
+                hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true, true>), grid, dim3(NT), 0, stream, p);
+            } else {
+                WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(PRO), WC_TB(UNIB), WC_TI(ACT), WC_TB(F3), WC_TI(4), WC_TB(true), WC_TB(false), WC_TB(false)});
+                hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true>), grid, dim3(NT), 0, stream, p);
+            }
             WC_CHECK_LAUNCH();
             return WC_OK;
         }
@@ -758,15 +764,21 @@ int launch(const IgDev& d, hipStream_t stream) {
         if (p1 && p.ident && p.N % 32 == 0 && p.ldo % 4 == 0 && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0 &&
             (!p.res || (p.ldres % 4 == 0 && (reinterpret_cast<uintptr_t>(p.res) & 15) == 0))) {
             // the projections: transposed accumulators for the vector epilogue
+            WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(PRO), WC_TB(UNIB), WC_TI(ACT), WC_TB(F3), WC_TI(4), WC_TB(true), WC_TB(true), WC_TB(false)});
             hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 4, true, true>), grid, dim3(NT), 0, stream, p);
             WC_CHECK_LAUNCH();
             return WC_OK;
         }
     }
-    if (F3 && p.steps == p.steps0)  // f16x3 segment 0 only: 4-plane LDS stages
+    if (F3 && p.steps == p.steps0) {  // f16x3 segment 0 only: 4-plane LDS stages
+        WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(PRO), WC_TB(UNIB), WC_TI(ACT), WC_TB(F3),
+                                             WC_TI(F3 ? 4 : 6), WC_TB(false), WC_TB(false), WC_TB(false)});
         hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, F3 ? 4 : 6>), grid, dim3(NT), 0, stream, p);
-    else
+    } else {
+        WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(PRO), WC_TB(UNIB), WC_TI(ACT), WC_TB(F3), WC_TI(6),
+                                             WC_TB(false), WC_TB(false), WC_TB(false)});
         hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, PRO, UNIB, ACT, F3, 6>), grid, dim3(NT), 0, stream, p);
+    }
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -1023,6 +1035,7 @@ extern "C" int wc_split_f16x3_tiled(const float* src, int ldc, int B, int HW, in
     const long M = (long)B * HW;
     if (a3_bytes != M * C * 4 || M > (1L << 30)) return WC_E_SHAPE;
     dim3 grid((unsigned)(M / 64), (unsigned)((C / 32 + 3) / 4));
+    wc_last_kernel = "split_tiled_kernel";
     hipLaunchKernelGGL(split_tiled_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), src, ldc, HW, C,
                        scale, shift, silu, ldexpf(1.0f, a_exp), reinterpret_cast<unsigned char*>(a3));
     WC_CHECK_LAUNCH();

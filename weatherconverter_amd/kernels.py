@@ -217,28 +217,52 @@ def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: O
     return a
 
 
-def _timed(name: str, fn_name: str, flops: float, *args):
-    if REPLAY is not None and name == REPLAY['name'] and _idempotent(fn_name, args):
-        _native.call(fn_name, *args)
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        r0.record()
-        for _ in range(REPLAY['reps']):
-            _native.call(fn_name, *args)
-        r1.record()
-        REPLAY['events'].append((r0, r1))
-        return
-    if PROFILE is None:
+def _timed(name: str, fn_name: str, flops: float, *args, nbytes: float = 0.0):
+    """Launch; while profiling, record timing under the launched kernel's exact instantiation name
+    (the library reports it, in rocprofv3's form; ``name`` is the fallback for unnamed kernels).
+
+    REPLAY with name '*' (or this instantiation's name): an idempotent launch is re-issued
+    REPLAY['reps'] times back to back right after itself between one event pair and recorded as
+    (name, flops, e0, e1, reps, nbytes) in REPLAY['events'] — per-launch durations free of event
+    gaps; a launch that rewrites its own input runs once between its own events (reps 1).  nbytes =
+    the launch's algorithmic HBM bytes (each input and output element once) where the wrapper
+    states it."""
+    if PROFILE is None and REPLAY is None:
         _native.call(fn_name, *args)
         return
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     _native.call(fn_name, *args)
     e1.record()
-    PROFILE.append((name, flops, e0, e1))
+    exact = _native.last_kernel_name() or name
+    if PROFILE is not None:
+        PROFILE.append((exact, flops, e0, e1))
+    if REPLAY is not None and REPLAY['name'] in ('*', exact):
+        reps = REPLAY['reps'] if _idempotent(fn_name, args) else 0
+        if reps:
+            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            r0.record()
+            for _ in range(reps):
+                _native.call(fn_name, *args)
+            r1.record()
+            _native.last_kernel_name()
+            REPLAY['events'].append((exact, flops, r0, r1, reps, nbytes))
+        else:
+            REPLAY['events'].append((exact, flops, e0, e1, 1, nbytes))
 
 
 def _flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int) -> float:
     return 2.0 * segs[0].view.B * Hm * Wm * N * sum(len(sg.taps) * sg.view.C for sg in segs)
+
+
+def _abytes(segs: Sequence[Seg], N: int, out_pixels: int, res: Optional[View] = None) -> float:
+    """Algorithmic HBM bytes of a conv launch: every input element of every segment, the output and
+    the residual view once (fp32)."""
+    if REPLAY is None:
+        return 0.0
+    b = sum(4.0 * sg.view.B * sg.view.H * sg.view.W * sg.view.C for sg in segs)
+    b += 4.0 * segs[0].view.B * out_pixels * N * (2 if res is not None else 1)
+    return b
 
 
 def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
@@ -257,7 +281,7 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
     _timed(f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}, {act}>', 'wc_conv_igemm',
-           _flops(segs, Hm, Wm, N) if PROFILE is not None else 0.0, ctypes.byref(a), _stream())
+           _flops(segs, Hm, Wm, N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), _stream())
 
 
 # ---- bf16x6 split-precision 3x3 conv (csrc/wc_conv6.hip) ----
@@ -418,8 +442,9 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
     res_seg = 'true' if len(segs) == 2 else 'false'
     r16 = 'true' if a_bound is not None and len(segs) == 2 else 'false'
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, true, {r16}>', 'wc_conv3x3_f16x3',
-           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
-           w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
+           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
+           w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream(),
+           nbytes=_abytes(segs, w3.N, Hm * Wm, res))
 
 
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,
@@ -444,7 +469,7 @@ def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Ten
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == s0.view.B, 'A bound')
         _req(unib == 'true', 'a per-image A bound needs (Hm*Wm) % BM == 0')
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, 0, true>', 'wc_conv_igemm_f16x3',
-           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
 
 
@@ -491,8 +516,9 @@ def convT4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: 
     a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, None, (2, 2, 0, 0), None, 0, None, gn=gn)
     TH, BN = x6_tile(w3.N)
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, 0, false, true, false, false, 2> (ConvT 4x4/s2)', 'wc_convtr4x4s2_f16x3',
-           2.0 * v.B * v.H * v.W * w3.N * 16 * v.C if PROFILE is not None else 0.0, ctypes.byref(a),
-           w3.data.data_ptr(), w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
+           2.0 * v.B * v.H * v.W * w3.N * 16 * v.C if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
+           w3.data.data_ptr(), w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream(),
+           nbytes=_abytes([seg], w3.N, 4 * v.H * v.W))
 
 
 def conv4x4s2_f16x3_ok(seg: Seg, N: int, Hm: int, Wm: int) -> bool:
@@ -511,8 +537,8 @@ def conv4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: V
     _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == seg.view.B, 'A bound')
     a = _conv_args([seg], w3.N, bias, out, Hm, Wm, None, 0, None, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     _timed('conv3x3_x6_kernel<8, 128, 0, false, true, false, false, true> (s2d 4x4/s2)', 'wc_conv4x4s2_f16x3',
-           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
-           w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
+           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream(), nbytes=_abytes([seg], w3.N, Hm * Wm))
 
 
 def qkv_presplit_ok(B: int, N: int, C: int, heads: int) -> bool:
@@ -533,7 +559,7 @@ def conv_igemm_f16x3_qkv(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], q
     ex = (ctypes.c_int * 3)(*[int(e) for e in exps])  # host array, read during the call
     pro = 0 if seg.scale is None else (2 if seg.silu else 1)
     _timed(f'conv_igemm_x6_kernel<128, 128, {pro}, true, 0, true> (qkv pre-split)', 'wc_conv_igemm_f16x3_qkv',
-           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), qkv3.data_ptr(), C, heads,
            ctypes.cast(ex, ctypes.c_void_p), _stream())
 
@@ -559,7 +585,7 @@ def split_f16x3_tiled(v: View, a_exp: int, scale: Optional[torch.Tensor] = None,
         _req(scale.shape == (v.B, v.C) and shift.shape == (v.B, v.C) and scale.is_contiguous()
              and shift.is_contiguous() and scale.dtype == torch.float32, 'GN affine [B][C]')
     a3 = torch.empty(2 * v.B * v.H * v.W * v.C, dtype=torch.int16, device=v.t.device)
-    _timed('split_tiled_kernel', 'wc_split_f16x3_tiled', 8.0 * v.B * v.H * v.W * v.C if PROFILE is not None else 0.0,
+    _timed('split_tiled_kernel', 'wc_split_f16x3_tiled', 8.0 * v.B * v.H * v.W * v.C if PROFILE is not None or REPLAY is not None else 0.0,
            v.ptr, v.ldc, v.B, v.H * v.W, v.C, _ptr(scale), _ptr(shift), int(silu), int(a_exp), a3.data_ptr(),
            a3.numel() * 2, _stream())
     return a3
@@ -574,7 +600,7 @@ def proj_f16x3(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[torch.T
     seg = Seg(v, [(0, 0)])
     a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     _timed('conv_igemm_x6_kernel<128, 128, 0, true, 0, true> (pre-split A)', 'wc_proj_f16x3',
-           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
+           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
            a3.numel() * 2, w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
 
 
@@ -589,7 +615,7 @@ def proj_f16x3_qkv(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[tor
     a = _conv_args([seg], w3.N, bias, None, v.H, v.W, None, 0, None, (1, 1, 0, 0), None, 0, out_dummy=True)
     ex = (ctypes.c_int * 3)(*[int(e) for e in exps])  # host array, read during the call
     _timed('conv_igemm_x6_kernel<128, 128, 0, true, 0, true> (qkv pre-split, pre-split A)', 'wc_proj_f16x3_qkv',
-           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
+           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
            a3.numel() * 2, w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(),
            qkv3.data_ptr(), C, heads, ctypes.cast(ex, ctypes.c_void_p), _stream())
 
@@ -645,7 +671,7 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     res_seg = 'true' if len(segs) == 2 else 'false'
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, false, false>', 'wc_conv3x3_x6',
-           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
+           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 
 
@@ -663,7 +689,7 @@ def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, {act}, false>', 'wc_conv_igemm_x6',
-           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
+           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 
 
@@ -802,7 +828,7 @@ def head_conv(x: View, scale: torch.Tensor, shift: torch.Tensor, w_packed: torch
     B, NO = out.shape[0], out.shape[1]
     _req(out.is_contiguous() and out.shape == (x.B, NO, x.H, x.W) and bias.numel() >= NO, 'head output shape')
     _req(w_packed.shape == (x.C // 16, 9, 16, 4), 'head weight layout')
-    _timed('head_conv_kernel', 'wc_head_conv', 2.0 * x.B * x.H * x.W * NO * 9 * x.C if PROFILE is not None else 0.0,
+    _timed('head_conv_kernel', 'wc_head_conv', 2.0 * x.B * x.H * x.W * NO * 9 * x.C if PROFILE is not None or REPLAY is not None else 0.0,
            x.ptr, x.ldc, scale.data_ptr(), shift.data_ptr(), x.B, x.H, x.W, x.C, w_packed.data_ptr(),
            bias.data_ptr(), NO, out.data_ptr(), _stream())
 

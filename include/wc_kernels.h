@@ -256,6 +256,14 @@ int wc_attention_fwd_x6(const float* qkv, int ld_qkv, float* out, int ld_out, in
  * the scales are removed in the softmax multiplier and the final 1/l. */
 int wc_attention_fwd_f16x3(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C,
                            int heads, float scale, int q_exp, int k_exp, int v_exp, void* stream);
+/* wc_attention_fwd_f16x3 / wc_attention_fwd_x6 also writing the softmax log-sum-exp
+ * lse[(b*heads + h)*N + q] = log2 sum_k 2^(s_qk * scale * log2 e) (float32 [B][heads][N], the
+ * contract of wc_attention_fwd_lse that wc_attention_bwd reads): the training forward
+ * (train_ddpm.py:106-108) on the sampler's split-precision attention. */
+int wc_attention_fwd_f16x3_lse(const float* qkv, int ld_qkv, float* out, int ld_out, float* lse, int B, int N,
+                               int C, int heads, float scale, int q_exp, int k_exp, int v_exp, void* stream);
+int wc_attention_fwd_x6_lse(const float* qkv, int ld_qkv, float* out, int ld_out, float* lse, int B, int N, int C,
+                            int heads, float scale, void* stream);
 /* wc_attention_fwd_f16x3 reading the pre-split projection written by wc_conv_igemm_f16x3_qkv with
  * exponents (q_exp, k_exp, v_exp): the K and V^T tiles are copied into LDS by LDS-DMA (no split
  * or transpose work in the key loop); results are bit-identical to wc_attention_fwd_f16x3 on the

@@ -130,6 +130,35 @@ def test_attention_backward(C, heads, N):
     assert rel_l2(dqkv.cpu(), q_.grad.reshape(B * N, 3 * C)) < 1e-5
 
 
+@pytest.mark.parametrize('precision', ['f16x3', 'bf16x6'])
+@pytest.mark.parametrize('C,heads,N', [(128, 4, 256), (512, 4, 160), (768, 4, 64), (256, 4, 33)])
+def test_split_attention_lse_matches_float64(precision, C, heads, N):
+    """The training forward's split-precision attention (wc_attention_fwd_{f16x3,x6}_lse): output
+    and log-sum-exp against float64, and the backward from its lse against float64 autograd."""
+    from weatherconverter_amd import kernels as K
+    g = _gen(6)
+    B = 2
+    d = C // heads
+    qkv = torch.randn((B * N, 3 * C), generator=g)
+    do = torch.randn((B * N, C), generator=g)
+    o = torch.empty((B * N, C), device='cuda')
+    lse = torch.empty((B, heads, N), device='cuda')
+    exps = (10, 10, 10) if precision == 'f16x3' else None  # |randn| * 2^10 stays far inside fp16
+    K.attention_fwd_lse(qkv.cuda(), o, lse, B, N, C, heads, precision=precision, exps=exps)
+    dqkv = torch.empty((B * N, 3 * C), device='cuda')
+    K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads)
+    q_ = qkv.double().reshape(B, N, 3 * C).requires_grad_(True)
+    q, k, v = q_.split(C, dim=-1)
+    sh = lambda z: z.reshape(B, N, heads, d).transpose(1, 2)  # noqa: E731
+    sc = (sh(q) * d**-0.5) @ sh(k).transpose(-1, -2)
+    ref_lse = torch.logsumexp(sc, -1) / np.log(2.0)  # log2 domain, [B][heads][N]
+    out = (torch.softmax(sc, -1) @ sh(v)).transpose(1, 2).reshape(B, N, C)
+    out.backward(do.double().reshape(B, N, C))
+    assert rel_l2(o.cpu(), out.detach().reshape(B * N, C)) < 1e-5
+    assert float((lse.cpu().double() - ref_lse.detach()).abs().max()) < 1e-5 * float(ref_lse.abs().max()) + 1e-6
+    assert rel_l2(dqkv.cpu(), q_.grad.reshape(B * N, 3 * C)) < 1e-5
+
+
 # ------------------------------------------------------------------ whole model
 def _model_grads(mc, B, precision, seed=0):
     """(our grads, oracle float64 grads, loss ours, loss ref) for one MSE training iteration."""

@@ -24,7 +24,8 @@ EXPORTS = [
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
     'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
-    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name'
+    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name',
+    'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
@@ -90,6 +91,8 @@ _SIGS = {
     'wc_attention_fwd': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_x6': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_fwd_f16x3': [_P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],
+    'wc_attention_fwd_f16x3_lse': [_P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _I, _I, _I, _P],
+    'wc_attention_fwd_x6_lse': [_P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P],
     'wc_temb': [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     'wc_conv_in': [_P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
     'wc_head_conv': [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P],

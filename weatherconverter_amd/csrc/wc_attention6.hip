@@ -120,7 +120,8 @@ template <int D, bool F3, bool PRE = false, bool O3 = false>
 __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
                                                              float* __restrict__ out, int ldo, int N,
                                                              int C, float score_mul, float qs, float ks,
-                                                             float vs, float ps, float out_mul) {
+                                                             float vs, float ps, float out_mul,
+                                                             float* __restrict__ lse) {
     static_assert(!PRE || F3, "pre-split operands are f16x3");
     using A = Ax6<D, F3>;
     constexpr int NP = A::NP;
@@ -436,6 +437,10 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
         }
         return;
     }
+    // log-sum-exp of the scaled scores for the backward (wc_attention_bwd's contract):
+    // lse = log2 sum_k 2^(s_k * scale * log2 e) = m + log2(l) - EP, EP the f16x3 P prescale
+    if (lse != nullptr && half == 0 && qrow < N)
+        lse[((long)b * heads + head) * N + qrow] = m_run + log2f(l_run) - (F3 ? 14.0f : 0.0f);
     if (qrow < N) {
         const float inv = out_mul / l_run;
         float* orow = out + ((long)b * N + qrow) * ldo + head * D;
@@ -453,7 +458,7 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
 
 template <int D, bool F3, bool PRE = false, bool O3 = false>
 int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
-                float scale, int eq, int ek, int ev, hipStream_t stream) {
+                float scale, int eq, int ek, int ev, hipStream_t stream, float* lse = nullptr) {
     using A = Ax6<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -468,14 +473,14 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
     dim3 grid(((N + 127) / 128) * heads * B);
     WC_SET_NAME("attention_x6_kernel", {WC_TI(D), WC_TB(F3), WC_TB(PRE), WC_TB(O3)});
     hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE, O3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
-                       score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), 1.0f, ldexpf(1.f, -ev));
+                       score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), 1.0f, ldexpf(1.f, -ev), lse);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 template <bool F3>
 int dispatch_att6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C, int heads,
-                  float scale, int eq, int ek, int ev, hipStream_t s) {
+                  float scale, int eq, int ek, int ev, hipStream_t s, float* lse = nullptr) {
     if (!qkv || !out) return WC_E_ARG;
     if (heads <= 0 || C % heads != 0 || ld_qkv % 4 != 0 || ld_out % 4 != 0) return WC_E_SHAPE;
     if (ld_qkv < 3 * C || ld_out < C || N <= 0 || B <= 0) return WC_E_SHAPE;
@@ -483,12 +488,12 @@ int dispatch_att6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, i
     if ((long)N * ld_qkv * 4 >= (1L << 31)) return WC_E_SHAPE;  // per-image SRD range
     if (eq < -60 || eq > 60 || ek < -60 || ek > 60 || ev < -60 || ev > 60) return WC_E_ARG;
     switch (C / heads) {
-        case 32: return launch_att6<32, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-        case 64: return launch_att6<64, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-        case 96: return launch_att6<96, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-        case 128: return launch_att6<128, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-        case 160: return launch_att6<160, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-        case 192: return launch_att6<192, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 32: return launch_att6<32, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s, lse);
+        case 64: return launch_att6<64, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s, lse);
+        case 96: return launch_att6<96, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s, lse);
+        case 128: return launch_att6<128, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s, lse);
+        case 160: return launch_att6<160, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s, lse);
+        case 192: return launch_att6<192, F3>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s, lse);
         default: return WC_E_SHAPE;
     }
 }
@@ -558,4 +563,22 @@ extern "C" int wc_attention_fwd_f16x3(const float* qkv, int ld_qkv, float* out, 
                                       void* stream) {
     return dispatch_att6<true>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, q_exp, k_exp, v_exp,
                                reinterpret_cast<hipStream_t>(stream));
+}
+
+// The same split-precision forwards, also writing the softmax log-sum-exp lse[b][head][query]
+// (float32 [B][heads][N], the contract of wc_attention_fwd_lse / wc_attention_bwd): the training
+// forward's attention on the sampler's arithmetic.
+extern "C" int wc_attention_fwd_f16x3_lse(const float* qkv, int ld_qkv, float* out, int ld_out, float* lse, int B,
+                                          int N, int C, int heads, float scale, int q_exp, int k_exp, int v_exp,
+                                          void* stream) {
+    if (!lse) return WC_E_ARG;
+    return dispatch_att6<true>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, q_exp, k_exp, v_exp,
+                               reinterpret_cast<hipStream_t>(stream), lse);
+}
+
+extern "C" int wc_attention_fwd_x6_lse(const float* qkv, int ld_qkv, float* out, int ld_out, float* lse, int B, int N,
+                                       int C, int heads, float scale, void* stream) {
+    if (!lse) return WC_E_ARG;
+    return dispatch_att6<false>(qkv, ld_qkv, out, ld_out, B, N, C, heads, scale, 0, 0, 0,
+                                reinterpret_cast<hipStream_t>(stream), lse);
 }

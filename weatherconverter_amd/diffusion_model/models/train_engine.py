@@ -35,6 +35,11 @@ from .engine import TAPS1, TAPS3, TAPS4S2, pack_conv, pack_convT
 _PARITIES = ((0, 0), (0, 1), (1, 0), (1, 1))
 
 
+class _Slot:
+    """A host value of the packing pass, filled by TrainEngine._resolve."""
+    __slots__ = ('value', )
+
+
 class Tape:
     """Everything one training forward saved for its backward: the layer records (activations, GN
     statistics, packed weights) plus the inputs and the per-step weight packs the backward reads.  One
@@ -95,8 +100,8 @@ class TrainEngine:
             pk2=self._pk(w2cat, co, 9, ci),
             f3_1=K.pack_f16x3(pack_conv(w1).float(), ci) if f3 else None,
             f3_2=K.pack_f16x3(w2cat.float(), co, ci, res_f16=True) if f3 else None,
-            gb1=(float(f[0].weight.abs().max()), float(f[0].bias.abs().max())),
-            gb2=(float(s[0].weight.abs().max()), float(s[0].bias.abs().max())),
+            gb1=self._later(f[0].weight.abs().max(), f[0].bias.abs().max()),
+            gb2=self._later(s[0].weight.abs().max(), s[0].bias.abs().max()),
             b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
             pk1T=self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9),
             pk2T=self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9),
@@ -111,14 +116,43 @@ class TrainEngine:
         if self.f3 and C % 16 == 0:
             d['f3_in'] = K.pack_f16x3(w_in.float(), C, ntaps=1, order='natural')
             d['f3_out'] = K.pack_f16x3(w_out.float(), C, ntaps=1, order='natural')
-            d['qkv_l1'] = w_in.double().abs().sum(1).cpu()
-            d['qkv_babs'] = mha.in_proj_bias.detach().double().abs().cpu()
-            d['gb'] = (float(gn.weight.abs().max()), float(gn.bias.abs().max()))
+            d['qkv_l1'] = self._later(w_in.double().abs().sum(1), vector=True)
+            d['qkv_babs'] = self._later(mha.in_proj_bias.detach().double().abs(), vector=True)
+            d['gb'] = self._later(gn.weight.abs().max(), gn.bias.abs().max())
         return d
+
+    def _later(self, *vals, vector: bool = False):
+        """A host value computed on the device now and copied to the host with every other one of
+        this forward's packing bounds in ONE transfer (_resolve): one host sync per training forward
+        instead of one per GroupNorm / projection bound."""
+        slot = _Slot()
+        self._pending.append((slot, vals, vector))
+        return slot
+
+    def _resolve(self, packs):
+        """Fill every slot _later handed out and replace the slots inside the pack dicts."""
+        if self._pending:
+            flat = torch.cat([v.detach().reshape(-1).double() for _, vals, _ in self._pending for v in vals])
+            host = flat.cpu()
+            i = 0
+            for slot, vals, vector in self._pending:
+                if vector:
+                    n = vals[0].numel()
+                    slot.value = host[i:i + n]
+                    i += n
+                else:
+                    slot.value = tuple(float(host[i + j]) for j in range(len(vals)))
+                    i += len(vals)
+        self._pending = []
+        for d in packs:
+            for k, v in list(d.items()):
+                if isinstance(v, _Slot):
+                    d[k] = v.value
 
     def _pack(self):
         m = self.model
         self.P = 0
+        self._pending = []
 
         def stage(blk, n_res):
             res = []
@@ -159,6 +193,7 @@ class TrainEngine:
             self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
                           tp[2].weight.detach().float().contiguous(), tp[2].bias.detach().float().contiguous()]
             rows = [rp for st in self.downs + self.mids + self.ups for rp in st[0]]
+            self._resolve(rows + [ap for st in self.downs + self.mids + self.ups for ap in st[1]])
             self.temb_w = torch.cat([rp['temb'].weight.detach().float() for rp in rows], 0).contiguous()
             self.temb_b = torch.cat([rp['temb'].bias.detach().float() for rp in rows], 0).contiguous()
             self.res_rows = rows
@@ -330,16 +365,19 @@ class TrainEngine:
         lse = torch.empty((B, ap['heads'], N), dtype=torch.float32, device=self.device)
         b_out = mha.out_proj.bias.detach().float().contiguous()
         if ap['f3_in'] is not None:
-            # in_proj under the GN bound; out_proj: |O| <= max|V| (a convex combination of V rows)
+            # in_proj under the GN bound; attention on f16x3 under the in-projection row-norm bounds
+            # of Q, K, V (as the sampler); out_proj: |O| <= max|V| (a convex combination of V rows)
             ng = N * C // 8
             K.conv_igemm_f16x3(seg, ap['f3_in'], b_in, View.full(qkv), Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*ap['gb'], ng))
-            K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'])
             exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], ng)
+            K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'],
+                                precision='f16x3', exps=exps)
             K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], ap['f3_out'], b_out, Yout, Hm=H, Wm=W, a_exp=exps[2],
                                res=Ypre)
         else:
             self._conv(seg, ap['pk_in'], b_in, View.full(qkv), H, W)
-            K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'])
+            K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'],
+                                precision=self.precision)
             self._conv([Seg(View.full(o), TAPS1)], ap['pk_out'], b_out, Yout, H, W, res=Ypre)
         self.tape.append(('attn', Ypre, Yout, qkv, o, lse, st, ap))
 

@@ -1081,13 +1081,28 @@ def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: 
            int(accumulate), s)
 
 
-def attention_fwd_lse(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, B: int, N: int, C: int, heads: int):
-    """fp32-MFMA attention (wc_attention_fwd) that also writes lse[b][h][q] (log2 domain) for the backward."""
+def attention_fwd_lse(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, B: int, N: int, C: int, heads: int,
+                      precision: str = 'fp32', exps: Optional[Tuple[int, int, int]] = None):
+    """Attention that also writes lse[b][h][q] (log2 domain) for the backward: fp32 MFMA
+    (wc_attention_fwd_lse), or, for head dims % 32 == 0, the sampler's split-precision kernel
+    ('f16x3' with the (q, k, v) exponents of attention_exps_from_norms: wc_attention_fwd_f16x3_lse;
+    'bf16x6': wc_attention_fwd_x6_lse)."""
     _req(qkv.shape == (B * N, 3 * C) and qkv.is_contiguous() and out.shape == (B * N, C) and out.is_contiguous(),
          'attention shapes')
-    _req(lse.is_contiguous() and lse.numel() == B * heads * N, 'lse: B*heads*N floats')
+    _req(lse.is_contiguous() and lse.dtype == torch.float32 and lse.numel() == B * heads * N, 'lse: B*heads*N floats')
+    _req(precision in CONV_PRECISIONS, f'attention precision {precision!r}')
     d = C // heads
-    _timed(f'attention_kernel<{d}> (lse)', 'wc_attention_fwd_lse', 4.0 * B * N * N * C, qkv.data_ptr(), 3 * C,
+    flops = 4.0 * B * N * N * C
+    if precision != 'fp32' and d % 32 == 0:
+        args = (qkv.data_ptr(), 3 * C, out.data_ptr(), C, lse.data_ptr(), B, N, C, heads, float(d)**-0.5)
+        if precision == 'f16x3':
+            _req(exps is not None, 'f16x3 attention needs (q, k, v) exponents')
+            _timed(f'attention_x6_kernel<{d}, true, false, false>', 'wc_attention_fwd_f16x3_lse', flops, *args,
+                   *[int(e) for e in exps], _stream())
+        else:
+            _timed(f'attention_x6_kernel<{d}, false, false, false>', 'wc_attention_fwd_x6_lse', flops, *args, _stream())
+        return
+    _timed(f'attention_kernel<{d}> (lse)', 'wc_attention_fwd_lse', flops, qkv.data_ptr(), 3 * C,
            out.data_ptr(), C, lse.data_ptr(), B, N, C, heads, float(d**-0.5), _stream())
 
 

@@ -392,6 +392,14 @@ int wc_conv_wgrad(const wc_wgrad_args* args, float* part, int splits, void* stre
 int wc_conv_wgrad_x6(const wc_wgrad_args* args, float* part, int splits, void* stream);
 /* The split count wc_conv_wgrad accepts for (M, Kc, P = B*Hm*Wm) aiming at ~target_blocks workgroups. */
 int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks);
+/* Halo-tiled weight gradient of a 3x3 stride-1 pad-1 conv on bf16x6 (the ResBlock convs' backward,
+ * unet_base.py:92-94,106 under train_ddpm.py:110): a->seg[0] the 3x3 tap grid at the gradient's
+ * own grid (optional GN(+SiLU) prologue), a->nseg == 1; M % 64 == 0, C0 % 32 == 0 (% 64 when
+ * M % 128 != 0), Wm % 16 == 0, Hm % 8 == 0 (% 2 when M % 128 != 0).  Writes the same partials as
+ * wc_conv_wgrad ([splits][M][9*C0], column = tap*C0 + c), reduced by wc_wgrad_reduce; splits from
+ * wc_conv_wgrad3_splits. */
+int wc_conv_wgrad3(const wc_wgrad_args* args, float* part, int splits, void* stream);
+int wc_conv_wgrad3_splits(int M, int C0, int B, int H, int W, int target_blocks);
 /* dW = sum_split part: column k < K0 is (tap t = k / C0, channel c = k % C0), written (c < Cw only)
  * to dw0[m*sM0 + c*sC0 + t*sT0]; columns k >= K0 to dw1[m*sM1 + k - K0].  accumulate: += . */
 int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,

@@ -53,6 +53,48 @@ def test_conv_wgrad_3x3_prologue_residual(silu, res, M, x6):
         assert rel_l2(dwr.cpu(), ref) < 1e-5
 
 
+@pytest.mark.parametrize('pro,res,M,C0,B,H,W', [(2, True, 128, 64, 2, 16, 32), (1, False, 256, 32, 1, 8, 16),
+                                                (0, False, 128, 32, 3, 8, 48), (2, True, 64, 64, 2, 6, 16),
+                                                (2, False, 64, 128, 1, 4, 32)])
+def test_conv_wgrad3_halo_kernel(pro, res, M, C0, B, H, W):
+    """The halo-tiled 3x3 weight gradient (wc_conv_wgrad3, bf16x6) against float64 autograd, both
+    tile configurations (128- and 64-channel M tiles), every prologue, image borders, several
+    images per split, and the residual segment through the generic GEMM beside it."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import Seg, View
+    from weatherconverter_amd.diffusion_model.models.engine import TAPS1, TAPS3
+    g = _gen(3)
+    C1 = 32
+    x = torch.randn((B, H, W, C0), generator=g)
+    xr = torch.randn((B, H, W, C1), generator=g)
+    dy = torch.randn((B, H, W, M), generator=g)
+    sc = torch.rand((B, C0), generator=g) + 0.5
+    sh = torch.randn((B, C0), generator=g) * 0.3
+    dw = torch.zeros((M, C0, 3, 3), device='cuda')
+    dwr = torch.zeros((M, C1), device='cuda')
+    segs = [Seg(View.full(x.cuda()), TAPS3, scale=sc.cuda() if pro else None, shift=sh.cuda() if pro else None,
+                silu=pro == 2)]
+    if res:
+        segs.append(Seg(View.full(xr.cuda()), TAPS1, kbase=9 * C0))
+    assert K.wgrad3_ok(View.full(dy.cuda()), segs[0])
+    prof = K.profile_conv(True)
+    K.conv_wgrad(View.full(dy.cuda()), segs, dw, (C0 * 9, 9, 1), dw1=dwr if res else None, s1=C1, x6=True)
+    torch.cuda.synchronize()
+    K.profile_conv(False)
+    assert any(n.startswith('conv_wgrad3_kernel') for n, *_ in prof)
+    a = x.double()
+    if pro:
+        a = a * sc.double()[:, None, None, :] + sh.double()[:, None, None, :]
+    a = F.silu(a) if pro == 2 else a
+    w = torch.zeros((M, C0, 3, 3), dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(a.permute(0, 3, 1, 2), w, padding=1)
+    y.backward(dy.double().permute(0, 3, 1, 2))
+    assert rel_l2(dw.cpu(), w.grad) < 1e-5
+    if res:
+        ref = torch.einsum('bhwm,bhwc->mc', dy.double(), xr.double())
+        assert rel_l2(dwr.cpu(), ref) < 1e-5
+
+
 @pytest.mark.parametrize('x6', [False, True])
 def test_conv_wgrad_4x4_stride2_and_transposed(x6):
     from weatherconverter_amd import kernels as K

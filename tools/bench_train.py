@@ -152,7 +152,7 @@ def train_step(args):
         'ms_forward': round(fwd, 2), 'ms_backward': round(bwd, 2), 'ms_adam_and_host': round(ms - fwd - bwd, 2),
         'images_per_s': round(B * args.steps / el, 2), 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
         'higher_is_better': True,
-        'dtype': 'f32 (fp32-class: f16x3 forward convs, bf16x6 data/weight gradients, fp32-MFMA attention)',
+        'dtype': 'fp32-class (f16x3 forward convs, projections and attention; bf16x6 data and weight gradients; fp32-MFMA attention backward)',
         'data': 'synthetic (keyed random-init weights; images U[-1,1], Philox N(0,1) noise, t ~ U[0,1000))',
         'config': {'workload': 'BASELINE config 3 full training iteration', 'global_batch': B, 'image_size': S,
                    'backward': True, 'optimizer': 'torch.optim.Adam lr 1e-4'},

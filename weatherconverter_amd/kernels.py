@@ -968,6 +968,22 @@ def _fill_seg(cs, s: Seg, B: int):
     cs.kbase = s.kbase
 
 
+def wgrad3_enabled() -> bool:
+    """The halo-tiled 3x3 weight gradient (wc_conv_wgrad3); WC_WGRAD3=0 keeps the generic GEMM (A/B)."""
+    return os.environ.get('WC_WGRAD3', '1') != '0'
+
+
+def wgrad3_ok(g: View, s0: Seg) -> bool:
+    """Shapes wc_conv_wgrad3 takes: segment 0 a 3x3 stride-1 grid at the gradient's own grid, M % 64,
+    C0 % 32 (% 64 when M % 128 != 0), W % 16, H % 8 (H % 2 for the 64-channel tiles)."""
+    v = s0.view
+    if list(s0.taps) != TAPS3 or s0.stride != 1 or v.H != g.H or v.W != g.W or g.C % 64 or g.W % 16:
+        return False
+    wide = g.C % 128 == 0
+    return v.C % (32 if wide else 64) == 0 and g.H % (8 if wide else 2) == 0 and v.ldc % 4 == 0 and g.ldc % 4 == 0 \
+        and v.ptr % 16 == 0 and g.ptr % 16 == 0
+
+
 def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, int, int], *, Cw: Optional[int] = None,
                dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False, x6: bool = False):
     """Weight gradient of a conv whose input segments are `segs` (as the forward read them, prologue
@@ -995,6 +1011,20 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
         _req(dw1 is not None and dw1.is_cuda and dw1.is_contiguous() and (g.C - 1) * s1 + C1 <= dw1.numel(),
              'dw1: the residual segment gradient')
     lib = _native.load()
+    if x6 and wgrad3_ok(g, segs[0]) and wgrad3_enabled():
+        # 3x3 segment on the halo-tiled kernel; the residual 1x1 segment (if any) as its own GEMM
+        P = B * g.H * g.W
+        splits = lib.wc_conv_wgrad3_splits(g.C, C0, B, g.H, g.W, 1024)
+        a.nseg = 1
+        part = torch.empty(splits * g.C * K0, dtype=torch.float32, device=g.t.device)
+        s = _stream()
+        _timed('conv_wgrad3_kernel', 'wc_conv_wgrad3', 2.0 * P * g.C * K0, ctypes.byref(a), part.data_ptr(), splits, s)
+        _native.call('wc_wgrad_reduce', part.data_ptr(), splits, g.C, K0, K0, C0, Cw, dw0.data_ptr(), s0[0], s0[1],
+                     s0[2], None, 0, int(accumulate), s)
+        if C1:
+            r = segs[1]
+            conv_wgrad(g, [Seg(r.view, r.taps, r.stride)], dw1, (s1, 1, 0), accumulate=accumulate, x6=x6)
+        return
     P = B * g.H * g.W
     splits = lib.wc_conv_wgrad_splits(g.C, Kc, P, 2048)
     part = torch.empty(splits * g.C * Kc, dtype=torch.float32, device=g.t.device)

@@ -127,6 +127,9 @@ int wc_conv3x3_x6(const wc_conv_args* args, const void* w6, int64_t w6_bytes, vo
  * w_inv_scale[n] = 2^-sW[n]. */
 int wc_conv3x3_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes, int a_exp,
                      const float* w_inv_scale, const float* a_bound, void* stream);
+/* (wc_conv3x3_f16x3 also takes a raw segment 0 without the GN prologue when a_bound is given and
+ * nseg == 1: s = min(a_exp, 13 - floor(log2 a_bound[b])) per image, e.g. a_exp = 60 and a_bound from
+ * wc_absmax_images — the 3x3 data gradients of the training backward, unet_base.py:92,106.) */
 /* The output-channel tile (BN) wc_conv3x3_x6 and wc_conv_igemm_x6 use for N output channels. */
 int wc_conv3x3_x6_tile_n(int N);
 
@@ -400,6 +403,10 @@ int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks);
  * wc_conv_wgrad3_splits. */
 int wc_conv_wgrad3(const wc_wgrad_args* args, float* part, int splits, void* stream);
 int wc_conv_wgrad3_splits(int M, int C0, int B, int H, int W, int target_blocks);
+/* absmax[b] = max |x| over image b of the NHWC view (x, ldx) with C channels (C % 4 == 0, 16-byte
+ * aligned); absmax [B] float32 zeroed by the caller.  The per-image range bound that lets the training
+ * backward run its data-gradient convs on f16x3 (train_ddpm.py:110). */
+int wc_absmax_images(const float* x, int ldx, int B, int HW, int C, float* absmax, void* stream);
 /* dW = sum_split part: column k < K0 is (tap t = k / C0, channel c = k % C0), written (c < Cw only)
  * to dw0[m*sM0 + c*sC0 + t*sT0]; columns k >= K0 to dw1[m*sM1 + k - K0].  accumulate: += . */
 int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,

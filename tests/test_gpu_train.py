@@ -201,6 +201,27 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     assert rel_l2(dqkv.cpu(), q_.grad.reshape(B * N, 3 * C)) < 1e-5
 
 
+@pytest.mark.parametrize('B,H,W,C,N', [(3, 16, 32, 128, 128), (2, 32, 16, 64, 64), (1, 8, 48, 256, 128)])
+def test_dgrad_f16x3_raw_segment_per_image_bound(B, H, W, C, N):
+    """The training backward's 3x3 data gradient on f16x3: a raw (no GroupNorm) operand whose
+    per-image scale comes from wc_absmax_images; images of very different magnitude in one batch."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import Seg, View
+    from weatherconverter_amd.diffusion_model.models.engine import TAPS3, pack_conv
+    g = _gen(8)
+    x = torch.randn((B, H, W, C), generator=g) * torch.tensor([1e-3, 50.0, 3.0])[:B, None, None, None]
+    w = torch.randn((N, C, 3, 3), generator=g) / (9 * C)**0.5
+    xv = View.full(x.cuda())
+    bnd = K.absmax_images(xv)
+    assert torch.equal(bnd.cpu(), x.abs().amax(dim=(1, 2, 3)))
+    w3 = K.pack_f16x3(pack_conv(w.cuda()).float(), C)
+    out = torch.empty((B, H, W, N), device='cuda')
+    K.conv3x3_f16x3([Seg(xv, TAPS3)], w3, None, View.full(out), Hm=H, Wm=W, a_exp=60, a_bound=bnd)
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), padding=1).permute(0, 2, 3, 1)
+    for b in range(B):  # every image to fp32-class accuracy against its own norm
+        assert rel_l2(out[b].cpu(), ref[b]) < 1e-5
+
+
 # ------------------------------------------------------------------ whole model
 def _model_grads(mc, B, precision, seed=0):
     """(our grads, oracle float64 grads, loss ours, loss ref) for one MSE training iteration."""

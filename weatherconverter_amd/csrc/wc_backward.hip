@@ -602,6 +602,25 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restri
 
 inline unsigned blocks_for(long n, int per) { return (unsigned)((n + per - 1) / per); }
 
+// absmax[b] = max |x| over image b of an NHWC view (C channels at pixel stride ldx); the caller zeroes
+// absmax.  Grid (chunks, B): each workgroup reduces a contiguous pixel range of one image, one atomic
+// per workgroup (|x| >= 0 orders like its unsigned bits, so the max is exact and order-free).
+__global__ __launch_bounds__(256) void absmax_images_kernel(const float* __restrict__ x, int ldx, int HW, int C4,
+                                                           int ppb, float* __restrict__ absmax) {
+    const int b = blockIdx.y;
+    const long p0 = (long)blockIdx.x * ppb;
+    const long p1 = min((long)HW, p0 + ppb);
+    const float* img = x + (long)b * HW * ldx;
+    float m = 0.f;
+    for (long i = p0 * C4 + threadIdx.x; i < p1 * C4; i += 256) {
+        const long px = i / C4;
+        const int c4 = (int)(i - px * C4);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(img + px * ldx + 4 * c4);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    wcx6::block_absmax_atomic(absmax, b, m);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -812,6 +831,19 @@ extern "C" int wc_nchw_to_nhwc(const float* src, int B, int C, int H, int W, flo
     const long total = (long)B * H * W * ldc;
     hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(blocks_for(total, 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), src, C, H * W, total, dst, ldc);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+// Per-image max |x| of an NHWC view (the range bound of a gradient operand on f16x3): see
+// absmax_images_kernel.  absmax must be zeroed by the caller.
+extern "C" int wc_absmax_images(const float* x, int ldx, int B, int HW, int C, float* absmax, void* stream) {
+    if (!x || !absmax) return WC_E_ARG;
+    if (B <= 0 || HW <= 0 || C <= 0 || C % 4 || ldx % 4 || (reinterpret_cast<uintptr_t>(x) & 15)) return WC_E_SHAPE;
+    const int ppb = 512;  // pixels per workgroup
+    const dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)B);
+    hipLaunchKernelGGL(absmax_images_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, ldx, HW, C / 4,
+                       ppb, absmax);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

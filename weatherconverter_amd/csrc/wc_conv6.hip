@@ -1054,7 +1054,10 @@ extern "C" int wc_conv3x3_f16x3(const wc_conv_args* a, const void* w3, int64_t w
     int BN, TH;
     const int st = prepare(a, w3, d, BN, TH);
     if (st != WC_OK) return st;
-    if (!a->seg[0].scale || !w_inv_scale) return WC_E_ARG;  // the static bound needs the GN prologue
+    if (!w_inv_scale) return WC_E_ARG;
+    // segment 0 needs a range bound: the GN prologue's static one, or (a raw single segment, e.g. a
+    // data gradient in the training backward) the per-image bound a_bound
+    if (!a->seg[0].scale && (!a_bound || a->nseg != 1)) return WC_E_ARG;
     if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
     const long ntn = (a->N + BN - 1) / BN;
     const long res_step = a_bound ? 64 : 96;  // segment 1 in fp16 (2 pieces) when bounded, else bf16x6
@@ -1063,8 +1066,12 @@ extern "C" int wc_conv3x3_f16x3(const wc_conv_args* a, const void* w3, int64_t w
     d.a_exp = a_exp;
     d.abound = a_bound;
     d.wsinv = w_inv_scale;
-    const int pro = a->seg[0].silu ? 2 : 1;
+    const int pro = a->seg[0].scale ? (a->seg[0].silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (pro == 0) {  // raw segment under the per-image bound: the weights-in-registers forms
+        if (BN == 64) return launch6<16, 64, 0, false, true, false, false, 0, 1>(d, s);
+        return launch6<8, 128, 0, false, true, false, false, 0, 1>(d, s);
+    }
     if (BN == 64) return dispatch6<16, 64>(d, pro, a->nseg == 2, true, s);
     return dispatch6<8, 128>(d, pro, a->nseg == 2, true, s);
 }

@@ -67,6 +67,8 @@ class TrainEngine:
         # GroupNorm-prologue convs and projections run f16x3 under their static bounds (as inference)
         self.precision = 'fp32' if p == 'fp32' else 'bf16x6'
         self.f3 = p == 'f16x3'
+        # data gradients on f16x3 under per-image absmax bounds of the incoming gradient (mode f16x3)
+        self.f3d = self.f3 and K.dgrad_f16x3_enabled()
         self.tape: List[tuple] = []
         self.last_tape: Optional[Tape] = None
 
@@ -105,7 +107,11 @@ class TrainEngine:
             b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
             pk1T=self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9),
             pk2T=self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9),
-            pkrT=self._pk(wr2.t(), co, 1))
+            pkrT=self._pk(wr2.t(), co, 1),
+            # f16x3 data gradients (raw gradient operand under its per-image absmax bound)
+            f3_1T=K.pack_f16x3(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co) if self.f3d else None,
+            f3_2T=K.pack_f16x3(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co) if self.f3d else None,
+            f3_rT=K.pack_f16x3(wr2.t().contiguous().float(), co, ntaps=1, order='natural') if self.f3d else None)
 
     def _pack_attn(self, blk, i: int):
         mha, gn = blk.attentions[i], blk.attention_norms[i]
@@ -414,6 +420,12 @@ class TrainEngine:
             setattr(self, f, None)
         return self.pgrads
 
+    @staticmethod
+    def _dgrad3_ok(g: View, n_out: int) -> bool:
+        """The 3x3 data gradient of g (n_out output channels) fits the halo f16x3 kernel."""
+        return K.x6_eligible([Seg(g, TAPS3)], n_out, g.H, g.W) and g.C % 4 == 0 and g.ldc % 4 == 0 \
+            and g.ptr % 16 == 0
+
     def _wgrad(self, g: View, segs, dw0, s0, **kw):
         """Weight gradient on bf16x6 (precision bf16x6) or fp32 MFMA."""
         K.conv_wgrad(g, segs, dw0, s0, x6=self.precision == 'bf16x6', **kw)
@@ -453,8 +465,16 @@ class TrainEngine:
         self._wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
                      self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci)
         dz2 = View.full(self._new(B, H, W, co))
-        self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
-        self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX)
+        if rp['f3_2T'] is not None and self._dgrad3_ok(gY, co):
+            bY = K.absmax_images(gY)
+            K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
+            if (H * W) % (256 if ci <= 64 else 128) == 0 and co % 16 == 0:  # one-image M tiles (per-image bound)
+                K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=gX)
+            else:
+                self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX)
+        else:
+            self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
+            self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX)
         g2 = rp['gn2']
         dh = View.full(self._new(B, H, W, co))
         K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
@@ -464,7 +484,11 @@ class TrainEngine:
         self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
                      (ci * 9, 9, 1))
         dz1 = View.full(self._new(B, H, W, ci))
-        self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
+        if rp['f3_1T'] is not None and self._dgrad3_ok(dh, ci):
+            K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60,
+                            a_bound=K.absmax_images(dh))
+        else:
+            self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
         g1 = rp['gn1']
         K.gn_backward(dz1, X, st1[2], st1[3], g1.weight.detach().float(), g1.bias.detach().float(), True, gX,
                       dgamma=self._pgrad(g1.weight), dbeta=self._pgrad(g1.bias), accumulate=True)

@@ -5,11 +5,13 @@ One training iteration of the reference (``train_ddpm.py:94-114``) is
     noisy_im = scheduler.add_noise(images, noise, t)        # :105
     noise_pred = model(noisy_im, t)                         # :106
     loss = criterion(noise_pred, noise)                     # :108, criterion = nn.MSELoss() (:177)
-followed by ``loss.backward()`` and ``optimizer.step()``.  Here the forward half runs on the HIP
-engine: ``wc_add_noise`` (per-sample coefficients), the UNet forward with per-sample timesteps, and
-``wc_mse_loss`` (fp64-accumulated, deterministic mean, fused with d loss / d noise_pred).
-``training_loss`` is that forward; ``TrainForward`` is the same captured into a HIP graph for the
-config-3 measurement.  Checkpoints keep the reference format (``:56-68``):
+followed by ``loss.backward()`` and ``optimizer.step()``.  All of it runs on HIP kernels except the
+Adam update (torch's ``optim.Adam`` on the device): ``wc_add_noise`` (per-sample coefficients), the
+UNet forward with per-sample timesteps recording its tape, ``wc_mse_loss`` (fp64-accumulated,
+deterministic mean, fused with d loss / d noise_pred), and ``loss.backward()`` through
+``UnetTrainFunction`` (models/train_engine.py: data and weight gradients, GroupNorm, attention and
+time-embedding backward kernels).  ``training_loss`` is the forward; ``TrainForward`` is the same
+captured into a HIP graph for the forward-only line.  Checkpoints keep the reference format (``:56-68``):
 ``{'model_state_dict', 'optimizer_state_dict', 'epoch'}`` saved as ``f'{epoch}-checkpoint.ckpt'``.
 """
 import os

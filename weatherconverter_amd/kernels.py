@@ -435,7 +435,8 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
     if a_bound is not None:
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     _req(w3.C0 == segs[0].view.C and w3.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'f16x3 weight segments')
-    _req(segs[0].scale is not None, 'f16x3 needs the GroupNorm prologue')
+    _req(segs[0].scale is not None or (a_bound is not None and len(segs) == 1),
+         'f16x3 needs the GroupNorm prologue or (one raw segment) a per-image A bound')
     a = _conv_args(segs, w3.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, act, absmax, gn=gn)
     TH, BN = x6_tile(w3.N)
     pro = 2 if segs[0].silu else 1
@@ -966,6 +967,20 @@ def _fill_seg(cs, s: Seg, B: int):
         cs.scale, cs.shift = s.scale.data_ptr(), s.shift.data_ptr()
     cs.silu = int(s.silu)
     cs.kbase = s.kbase
+
+
+def absmax_images(v: View) -> torch.Tensor:
+    """float32[B]: max |x| over each image of the view (wc_absmax_images)."""
+    v.check()
+    _req(v.C % 4 == 0 and v.ldc % 4 == 0 and v.ptr % 16 == 0, 'absmax view: C % 4, 16-byte aligned')
+    out = torch.zeros((v.B, ), dtype=torch.float32, device=v.t.device)
+    _timed('absmax_images_kernel', 'wc_absmax_images', 0.0, v.ptr, v.ldc, v.B, v.H * v.W, v.C, out.data_ptr(), _stream())
+    return out
+
+
+def dgrad_f16x3_enabled() -> bool:
+    """Training data gradients on f16x3 under per-image absmax bounds; WC_DGRAD_F16X3=0 keeps bf16x6."""
+    return os.environ.get('WC_DGRAD_F16X3', '1') != '0'
 
 
 def wgrad3_enabled() -> bool:

@@ -443,6 +443,15 @@ int wc_attention_fwd_lse(const float* qkv, int ld_qkv, float* out, int ld_out, f
 int wc_attention_bwd(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout, int ld_dout,
                      const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C, int heads,
                      float scale, void* stream);
+/* The same backward on bf16x6 split-precision MFMA (exact 3-piece bf16 split of Q, K, V, dO and the
+ * recomputed P and dS; six products per block, fp32 accumulation); head dim C/heads in {32, 64, 128};
+ * qkv, dout, dqkv 16-byte aligned. */
+int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout, int ld_dout,
+                      const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C, int heads,
+                      float scale, void* stream);
+/* Its first step alone: dv_work[(b*heads + h)*N + q] = sum_d dout[b, q, h*D + d] * out[b, q, h*D + d]. */
+int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N, int heads,
+                          int D, float* dv_work, void* stream);
 
 /* Small dense helpers for the time-embedding MLP backward (t_proj, t_emb_layers: B x 128):
  * C[m][n] = alpha*sum_k A[m*sam + k*sak]*B[k*sbk + n*sbn] + beta*C[m][n] (beta 0: C not read);

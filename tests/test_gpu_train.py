@@ -173,7 +173,7 @@ def test_attention_backward(C, heads, N):
 
 
 @pytest.mark.parametrize('precision', ['f16x3', 'bf16x6'])
-@pytest.mark.parametrize('C,heads,N', [(128, 4, 256), (512, 4, 160), (768, 4, 64), (256, 4, 33)])
+@pytest.mark.parametrize('C,heads,N', [(128, 4, 256), (512, 4, 160), (768, 4, 64), (256, 4, 33), (128, 2, 1000)])
 def test_split_attention_lse_matches_float64(precision, C, heads, N):
     """The training forward's split-precision attention (wc_attention_fwd_{f16x3,x6}_lse): output
     and log-sum-exp against float64, and the backward from its lse against float64 autograd."""
@@ -188,7 +188,12 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     exps = (10, 10, 10) if precision == 'f16x3' else None  # |randn| * 2^10 stays far inside fp16
     K.attention_fwd_lse(qkv.cuda(), o, lse, B, N, C, heads, precision=precision, exps=exps)
     dqkv = torch.empty((B * N, 3 * C), device='cuda')
-    K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads)
+    prof = K.profile_conv(True)
+    K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads, precision=precision)
+    torch.cuda.synchronize()
+    K.profile_conv(False)
+    if C // heads in (32, 64, 128):  # the split-precision backward ran (D = 192 stays fp32 MFMA)
+        assert any(n.startswith('attn_bwd6_dq_kernel') for n, *_ in prof)
     q_ = qkv.double().reshape(B, N, 3 * C).requires_grad_(True)
     q, k, v = q_.split(C, dim=-1)
     sh = lambda z: z.reshape(B, N, heads, d).transpose(1, 2)  # noqa: E731

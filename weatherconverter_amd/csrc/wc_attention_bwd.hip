@@ -322,3 +322,16 @@ extern "C" int wc_attention_bwd(const float* qkv, int ld_qkv, const float* out, 
         default: return WC_E_SHAPE;
     }
 }
+
+// Dv = rowsum(dO o O) per (image, head, query) only (the first step of the backward; used by the
+// split-precision backward wc_attention_bwd6).
+extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N,
+                                     int heads, int D, float* dv_work, void* stream) {
+    if (!out || !dout || !dv_work) return WC_E_ARG;
+    if (B <= 0 || N <= 0 || heads <= 0 || D <= 0 || D % 4 || ld_out % 4 || ld_dout % 4) return WC_E_SHAPE;
+    const long n = (long)B * heads * N;
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), out, ld_out, dout, ld_dout, B, N, heads, D, dv_work);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}

@@ -1,0 +1,385 @@
+// Self-attention backward on bf16x6 split-precision MFMA for gfx950 (head dims D % 32 == 0): the same
+// contract and algorithm as wc_attention_bwd (wc_attention_bwd.hip) — the training backward of the
+// softmax(QK^T*s)V core of nn.MultiheadAttention (reference unet_base.py:115,159 under
+// train_ddpm.py:110) — with every product on v_mfma_f32_32x32x16_bf16 instead of fp32 MFMA.
+//
+// Arithmetic: each fp32 operand (Q, K, V, dO and the recomputed P and dS) is split exactly into three
+// bf16 pieces (wcx6::split3, v = v0 + v1 + v2); the six products with i + j <= 2 accumulate in fp32.
+// The dropped terms are < 3*2^-24 relative per product: fp32-class, no range bound needed (dO and dS
+// have none).  A 32x32x16 block costs 6 x 32 cycles here against 8 x 64 on fp32 MFMA.
+//
+//   attn_bwd6_dkdv_kernel  a wave owns 32 keys (K, V rows in registers as bf16 pieces; D <= 128 — at
+//       D = 192 the accumulators and rows spill, and that width stays on fp32 MFMA); 32-query tiles of Q and dO are staged once per tile as
+//       pieces in LDS ([piece][query][dim], shared by the 4 waves).
+//         S = Q K^T, dP = dO V^T     rows = queries (A: ds_read_b128 from the tile), cols = keys (B: regs)
+//         P, dS in the accumulator registers (lane = key, register r = query (r&3)+8(r>>2)+4 half)
+//         dV^T += dO^T P, dK^T += Q^T dS   A: the tile read transposed (ds_read_b64_tr_b16) in the
+//             query order the accumulator registers hold (per lane half: queries 4h+0..3, 8+4h+0..3 of
+//             each 16-query chunk), B: the P / dS registers split in place.
+//   attn_bwd6_dq_kernel    a wave owns 32 queries; 32-key tiles of K and V staged as pieces; S^T,
+//       dP^T with lane = query, dQ^T += K^T dS^T.
+// No atomics, fixed reduction order: deterministic.
+#include "wc_x6.hpp"
+
+namespace {
+
+using namespace wcx6;
+
+template <int D>
+struct B6Cfg {
+    static_assert(D % 32 == 0, "bf16x6 attention backward: D % 32 == 0");
+    static constexpr int NCH = D / 16;      // 16-dim K-steps of S / dP
+    static constexpr int NDB = D / 32;      // 32-dim output blocks
+    static constexpr int RSB = 2 * D + 80;  // tile row bytes (odd multiple of 16: conflict-free b128 reads)
+    static constexpr int PLANE = 32 * RSB;  // one piece of one 32-row tile
+    static constexpr int TILE = 3 * PLANE;  // the three pieces
+    static constexpr int LDS = 2 * TILE + 2 * 32 * 4;  // two tiles (Q, dO or K, V) + lse / Dv
+    static constexpr bool PRESPLIT = D <= 128;   // own rows kept as pieces (else fp32, split per use)
+};
+
+// Three bf16 pieces of 8 consecutive values as MFMA operands.
+WC_DEVICE void pieces8x3(const float* v, u32x4 (&out)[3]) {
+    u32x2 a0, a1, a2, b0, b1, b2;
+    split3(f32x4{v[0], v[1], v[2], v[3]}, a0, a1, a2);
+    split3(f32x4{v[4], v[5], v[6], v[7]}, b0, b1, b2);
+    out[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+    out[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+    out[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+}
+
+// ... of accumulator registers off .. off + 7 (off a compile-time multiple of 8 after unrolling)
+WC_DEVICE void pieces8x3(const f32x16& v, int off, u32x4 (&out)[3]) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = v[off + j];
+    pieces8x3(t, out);
+}
+
+WC_DEVICE void mfma6(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {
+    acc = mfma_bf16(a[0], b[0], acc);
+    acc = mfma_bf16(a[0], b[1], acc);
+    acc = mfma_bf16(a[1], b[0], acc);
+    acc = mfma_bf16(a[0], b[2], acc);
+    acc = mfma_bf16(a[1], b[1], acc);
+    acc = mfma_bf16(a[2], b[0], acc);
+}
+
+// A wave's own 32 rows (lane = row l32) of a [rows][D] fp32 matrix, the dims its lane half feeds:
+// for K-step ch the lane holds dims 16 ch + 8 half .. + 7.  Kept either as bf16 pieces (PRESPLIT) or as
+// fp32 values split per use.
+template <int D>
+struct OwnRows {
+    using Cf = B6Cfg<D>;
+    u32x4 pc[Cf::PRESPLIT ? Cf::NCH : 1][3];
+    float fv[Cf::PRESPLIT ? 1 : Cf::NCH * 8];
+    WC_DEVICE void load(const float* row, bool ok, int half) {
+#pragma unroll
+        for (int ch = 0; ch < Cf::NCH; ++ch) {
+            float v[8];
+            f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+            if (ok) {
+                a = *reinterpret_cast<const f32x4*>(row + 16 * ch + 8 * half);
+                b = *reinterpret_cast<const f32x4*>(row + 16 * ch + 8 * half + 4);
+            }
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+            if constexpr (Cf::PRESPLIT) {
+                pieces8x3(v, pc[ch]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fv[8 * ch + j] = v[j];
+            }
+        }
+    }
+    WC_DEVICE void get(int ch, u32x4 (&out)[3]) const {
+        if constexpr (Cf::PRESPLIT) {
+            out[0] = pc[ch][0]; out[1] = pc[ch][1]; out[2] = pc[ch][2];
+        } else {
+            pieces8x3(fv + 8 * ch, out);
+        }
+    }
+};
+
+// Stage a 32-row x D tile (rows r0.., fp32 NHWC rows at `base` with pitch ld, columns col..) into LDS
+// as three bf16 piece planes [piece][row][dim] (row pitch RSB bytes); rows >= N are zero.
+template <int D>
+WC_DEVICE void stage_tile(unsigned char* dst, const float* base, long ld, int col, int r0, int N, int tid) {
+    using Cf = B6Cfg<D>;
+    for (int i = tid; i < 32 * (D / 4); i += 256) {
+        const int r = i / (D / 4), c4 = i % (D / 4);
+        const int row = r0 + r;
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (row < N) v = *reinterpret_cast<const f32x4*>(base + (long)row * ld + col + 4 * c4);
+        u32x2 p0, p1, p2;
+        split3(v, p0, p1, p2);
+        unsigned char* d = dst + r * Cf::RSB + c4 * 8;
+        *reinterpret_cast<u32x2*>(d) = p0;
+        *reinterpret_cast<u32x2*>(d + Cf::PLANE) = p1;
+        *reinterpret_cast<u32x2*>(d + 2 * Cf::PLANE) = p2;
+    }
+}
+
+// A operand rows = tile rows (lane = row l32), K-step ch: 8 dims per lane half (ds_read_b128).
+template <int D>
+WC_DEVICE void tile_rows(const unsigned char* tile, int l32, int half, int ch, u32x4 (&out)[3]) {
+    using Cf = B6Cfg<D>;
+    const unsigned char* p = tile + l32 * Cf::RSB + (16 * ch + 8 * half) * 2;
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) out[pc] = *reinterpret_cast<const u32x4*>(p + pc * Cf::PLANE);
+}
+
+// A operand = tile^T (rows = the 32 dims of block db, K = 16 tile rows of chunk c) in the row order
+// of the accumulator registers: lane half h gets rows 16c + 4h + 0..3 and 16c + 8 + 4h + 0..3
+// (ds_read_b64_tr_b16: lane 16g + 4q + p supplies row base + q, dims 16(g & 1) + 4p .. + 3; the lane
+// receives dim l32 of the 4 rows its 16-lane group supplied).
+template <int D>
+WC_DEVICE void tile_cols(const unsigned char* tile, int lane, int db, int c, u32x4 (&out)[3]) {
+    using Cf = B6Cfg<D>;
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int row = 16 * c + 4 * (g >> 1) + q;
+    const unsigned char* base = tile + row * Cf::RSB + (32 * db + 16 * (g & 1) + 4 * p) * 2;
+    typedef short v4s __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        const unsigned char* a = base + pc * Cf::PLANE;
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a + 8 * Cf::RSB));
+        const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        out[pc] = u32x4{l2.x, l2.y, h2.x, h2.y};
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
+    const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
+    using Cf = B6Cfg<D>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* Qs = smem;
+    unsigned char* Os = smem + Cf::TILE;
+    float* Ls = reinterpret_cast<float*>(smem + 2 * Cf::TILE);  // [32] lse, [32] Dv
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, half = lane >> 5;
+    const int head = blockIdx.y, b = blockIdx.z, H = gridDim.y;
+    const float* base = qkv + (long)b * N * ldq;
+    const float* dob = dO + (long)b * N * lddo;
+    const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
+    const int key = blockIdx.x * 128 + wave * 32 + l32;
+
+    OwnRows<D> kr, vr;
+    kr.load(base + (long)key * ldq + kcol, key < N, half);
+    vr.load(base + (long)key * ldq + vcol, key < N, half);
+
+    f32x16 dvT[Cf::NDB], dkT[Cf::NDB];
+#pragma unroll
+    for (int d = 0; d < Cf::NDB; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dvT[d][r] = 0.f; dkT[d][r] = 0.f; }
+
+    const int ntiles = (N + 31) / 32;
+    for (int t = 0; t < ntiles; ++t) {
+        const int q0 = t * 32;
+        __syncthreads();  // previous tile consumed
+        stage_tile<D>(Qs, base, ldq, qcol, q0, N, tid);
+        stage_tile<D>(Os, dob, lddo, head * D, q0, N, tid);
+        if (tid < 32) {
+            const int q = q0 + tid;
+            Ls[tid] = q < N ? lse[((long)b * H + head) * N + q] : INFINITY;  // P = 0 for padding queries
+            Ls[32 + tid] = q < N ? Dv[((long)b * H + head) * N + q] : 0.f;
+        }
+        __syncthreads();
+
+        // S = Q K^T, dP = dO V^T: rows = queries, lane = key
+        f32x16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+        for (int ch = 0; ch < Cf::NCH; ++ch) {
+            u32x4 a[3], bk[3];
+            tile_rows<D>(Qs, l32, half, ch, a);
+            kr.get(ch, bk);
+            mfma6(s, a, bk);
+            tile_rows<D>(Os, l32, half, ch, a);
+            vr.get(ch, bk);
+            mfma6(dp, a, bk);
+        }
+        // P and dS in place (register r <-> query (r&3) + 8(r>>2) + 4 half of the tile)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int qi = (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float pr = exp2f(s[r] * scale_log2 - Ls[qi]);
+            s[r] = pr;
+            dp[r] = pr * (dp[r] - Ls[32 + qi]);
+        }
+        // dV^T += dO^T P, dK^T += Q^T dS over the two 16-query chunks
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            u32x4 pp[3], ds[3];
+            pieces8x3(s, 8 * c, pp);
+            pieces8x3(dp, 8 * c, ds);
+#pragma unroll
+            for (int db = 0; db < Cf::NDB; ++db) {
+                u32x4 a[3];
+                tile_cols<D>(Os, lane, db, c, a);
+                mfma6(dvT[db], a, pp);
+                tile_cols<D>(Qs, lane, db, c, a);
+                mfma6(dkT[db], a, ds);
+            }
+        }
+    }
+
+    if (key < N) {
+        float* row = dqkv + ((long)b * N + key) * lddq;
+#pragma unroll
+        for (int d = 0; d < Cf::NDB; ++d) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 4) {
+                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                *reinterpret_cast<f32x4*>(row + kcol + dv) =
+                    f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * scale;
+                *reinterpret_cast<f32x4*>(row + vcol + dv) = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
+            }
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
+    const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
+    using Cf = B6Cfg<D>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* Ks = smem;
+    unsigned char* Vs = smem + Cf::TILE;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, half = lane >> 5;
+    const int head = blockIdx.y, b = blockIdx.z, H = gridDim.y;
+    const float* base = qkv + (long)b * N * ldq;
+    const float* dob = dO + (long)b * N * lddo;
+    const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
+    const int qme = blockIdx.x * 128 + wave * 32 + l32;
+
+    OwnRows<D> qr, orr;
+    qr.load(base + (long)qme * ldq + qcol, qme < N, half);
+    orr.load(dob + (long)qme * lddo + head * D, qme < N, half);
+    const float lq = qme < N ? lse[((long)b * H + head) * N + qme] : INFINITY;
+    const float dq = qme < N ? Dv[((long)b * H + head) * N + qme] : 0.f;
+
+    f32x16 dqT[Cf::NDB];
+#pragma unroll
+    for (int d = 0; d < Cf::NDB; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dqT[d][r] = 0.f;
+
+    const int ntiles = (N + 31) / 32;
+    for (int t = 0; t < ntiles; ++t) {
+        const int k0 = t * 32;
+        __syncthreads();
+        stage_tile<D>(Ks, base, ldq, kcol, k0, N, tid);
+        stage_tile<D>(Vs, base, ldq, vcol, k0, N, tid);
+        __syncthreads();
+
+        // S^T = K Q^T, dP^T = V dO^T: rows = keys, lane = query
+        f32x16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+        for (int ch = 0; ch < Cf::NCH; ++ch) {
+            u32x4 a[3], bq[3];
+            tile_rows<D>(Ks, l32, half, ch, a);
+            qr.get(ch, bq);
+            mfma6(s, a, bq);
+            tile_rows<D>(Vs, l32, half, ch, a);
+            orr.get(ch, bq);
+            mfma6(dp, a, bq);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float pr = key < N ? exp2f(s[r] * scale_log2 - lq) : 0.f;
+            dp[r] = pr * (dp[r] - dq);
+        }
+        // dQ^T += K^T dS^T
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            u32x4 ds[3];
+            pieces8x3(dp, 8 * c, ds);
+#pragma unroll
+            for (int db = 0; db < Cf::NDB; ++db) {
+                u32x4 a[3];
+                tile_cols<D>(Ks, lane, db, c, a);
+                mfma6(dqT[db], a, ds);
+            }
+        }
+    }
+
+    if (qme < N) {
+        float* row = dqkv + ((long)b * N + qme) * lddq + qcol;
+#pragma unroll
+        for (int d = 0; d < Cf::NDB; ++d) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 4) {
+                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                *reinterpret_cast<f32x4*>(row + dv) = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * scale;
+            }
+        }
+    }
+}
+
+template <int D>
+int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
+                int lddq, int B, int N, int C, int heads, float scale, hipStream_t s) {
+    using Cf = B6Cfg<D>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dkdv_kernel<D>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+        if (e != hipSuccess) return (int)e;
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<D>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    const dim3 grid((N + 127) / 128, heads, B);
+    const float scale_log2 = scale * 1.4426950408889634f;
+    WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D)});
+    hipLaunchKernelGGL(attn_bwd6_dkdv_kernel<D>, grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq,
+                       N, C, scale_log2, scale);
+    WC_CHECK_LAUNCH();
+    WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D)});
+    hipLaunchKernelGGL(attn_bwd6_dq_kernel<D>, grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N,
+                       C, scale_log2, scale);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+}  // namespace
+
+// Dv[b][h][q] = sum_d dO O over the head (wc_attention_bwd's prep step) must already be in dv_work
+// (wc_attention_bwd6 runs it itself through wc_attention_bwd_prep).
+extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N,
+                                     int heads, int D, float* dv_work, void* stream);
+
+extern "C" int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
+                                 int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
+                                 int C, int heads, float scale, void* stream) {
+    if (!qkv || !out || !dout || !lse || !dv_work || !dqkv) return WC_E_ARG;
+    if (heads <= 0 || C % heads || B <= 0 || N <= 0) return WC_E_SHAPE;
+    if (ld_qkv % 4 || ld_out % 4 || ld_dout % 4 || ld_dqkv % 4 || ld_qkv < 3 * C || ld_dqkv < 3 * C || ld_out < C ||
+        ld_dout < C)
+        return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dqkv)) & 15)
+        return WC_E_SHAPE;
+    const int D = C / heads;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int st = wc_attention_bwd_prep(out, ld_out, dout, ld_dout, B, N, heads, D, dv_work, stream);
+    if (st != WC_OK) return st;
+    switch (D) {
+        case 32: return launch_bwd6<32>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 64: return launch_bwd6<64>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        case 128:
+            return launch_bwd6<128>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
+        default: return WC_E_SHAPE;  // D = 192 would spill (wc_attention_bwd keeps it on fp32 MFMA)
+    }
+}

@@ -119,6 +119,9 @@ class TrainEngine:
         w_in, w_out = mha.in_proj_weight.detach(), mha.out_proj.weight.detach()
         d = dict(C=C, heads=mha.num_heads, gn=gn, mha=mha, pk_in=self._pk(w_in, C, 1), pk_out=self._pk(w_out, C, 1),
                  pk_inT=self._pk(w_in.t(), 3 * C, 1), pk_outT=self._pk(w_out.t(), C, 1), f3_in=None, f3_out=None)
+        if self.f3d and C % 16 == 0:  # projection data gradients on f16x3 (per-image absmax bounds)
+            d['f3_inT'] = K.pack_f16x3(w_in.t().contiguous().float(), 3 * C, ntaps=1, order='natural')
+            d['f3_outT'] = K.pack_f16x3(w_out.t().contiguous().float(), C, ntaps=1, order='natural')
         if self.f3 and C % 16 == 0:
             d['f3_in'] = K.pack_f16x3(w_in.float(), C, ntaps=1, order='natural')
             d['f3_out'] = K.pack_f16x3(w_out.float(), C, ntaps=1, order='natural')
@@ -502,16 +505,25 @@ class TrainEngine:
         self._bias_grad(gY, mha.out_proj.bias)
         self._wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0))
         do = self._new(B, H, W, C)
-        self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W)
+        f3p = 'f3_outT' in ap and (H * W) % (256 if C <= 64 else 128) == 0
+        if f3p:
+            K.conv_igemm_f16x3([Seg(gY, TAPS1)], ap['f3_outT'], None, View.full(do), Hm=H, Wm=W, a_exp=60,
+                               a_bound=K.absmax_images(gY))
+        else:
+            self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W)
         dqkv = self._new(B, H, W, 3 * C)
         K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C), B,
-                        N, C, ap['heads'])
+                        N, C, ap['heads'], precision=self.precision)
         gq = View.full(dqkv)
         self._bias_grad(gq, mha.in_proj_bias)
         self._wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),
                      (C, 1, 0))
         da = View.full(self._new(B, H, W, C))
-        self._conv([Seg(gq, TAPS1)], ap['pk_inT'], None, da, H, W)
+        if f3p:
+            K.conv_igemm_f16x3([Seg(gq, TAPS1)], ap['f3_inT'], None, da, Hm=H, Wm=W, a_exp=60,
+                               a_bound=K.absmax_images(gq))
+        else:
+            self._conv([Seg(gq, TAPS1)], ap['pk_inT'], None, da, H, W)
         # Yout = Ypre + out_proj(...): Ypre's gradient is Yout's plus the GroupNorm path
         self._alias_grad(Ypre.t, Yout)
         K.gn_backward(da, Ypre, st[2], st[3], gn.weight.detach().float(), gn.bias.detach().float(), False,

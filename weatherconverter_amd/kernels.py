@@ -1151,15 +1151,26 @@ def attention_fwd_lse(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, B
            out.data_ptr(), C, lse.data_ptr(), B, N, C, heads, float(d**-0.5), _stream())
 
 
+def attention_bwd6_enabled() -> bool:
+    """The bf16x6 attention backward (wc_attention_bwd6); WC_ATTN_BWD6=0 keeps fp32 MFMA (A/B)."""
+    return os.environ.get('WC_ATTN_BWD6', '1') != '0'
+
+
 def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, dqkv: torch.Tensor,
-                  B: int, N: int, C: int, heads: int):
-    """d qkv (same [q | k | v] rows as qkv) of softmax(Q K^T / sqrt(d)) V from the forward's output and lse."""
+                  B: int, N: int, C: int, heads: int, precision: str = 'fp32'):
+    """d qkv (same [q | k | v] rows as qkv) of softmax(Q K^T / sqrt(d)) V from the forward's output and lse:
+    fp32 MFMA (wc_attention_bwd), or with precision 'bf16x6' / 'f16x3' and a head dim in {32, 64, 128}
+    the bf16x6 split-precision kernels (wc_attention_bwd6; the gradients have no range bound, so
+    f16x3 requests run bf16x6 here)."""
     for t_, w in ((qkv, 3 * C), (out, C), (dout, C), (dqkv, 3 * C)):
         _req(t_.is_cuda and t_.dtype == torch.float32 and t_.is_contiguous() and t_.numel() == B * N * w,
              'attention backward operands')
     d = C // heads
     dv = torch.empty(B * heads * N, dtype=torch.float32, device=qkv.device)
-    _timed(f'attention_bwd<{d}>', 'wc_attention_bwd', 10.0 * B * N * N * C, qkv.data_ptr(), 3 * C, out.data_ptr(), C,
+    fn = 'wc_attention_bwd'
+    if precision != 'fp32' and d in (32, 64, 128) and attention_bwd6_enabled():
+        fn = 'wc_attention_bwd6'
+    _timed(f'attention_bwd<{d}>', fn, 10.0 * B * N * N * C, qkv.data_ptr(), 3 * C, out.data_ptr(), C,
            dout.data_ptr(), C, lse.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), 3 * C, B, N, C, heads, float(d**-0.5),
            _stream())
 

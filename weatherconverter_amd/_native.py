@@ -113,7 +113,9 @@ _SIGS = {
     'wc_conv_wgrad_splits': [_I, _I, _L, _I],
     'wc_conv_wgrad3': [ctypes.POINTER(WgradArgs), _P, _I, _P],
     'wc_conv_wgrad3_splits': [_I, _I, _I, _I, _I, _I],
-    'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_prep': [_P, _I, _I, _I, _I, _P, _P],
+    'wc_absmax_images': [_P, _I, _I, _I, _I, _P, _P],
+    'wc_attention_bwd6': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
+    'wc_attention_bwd_prep': [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P],
     'wc_wgrad_reduce': [_P, _I, _I, _I, _I, _I, _I, _P, _L, _L, _L, _P, _L, _I, _P],
     'wc_gn_bwd_splits': [_I, _I],
     'wc_gn_bwd_reduce': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P],

@@ -33,7 +33,9 @@ struct B6Cfg {
     static constexpr int RSB = 2 * D + 80;  // tile row bytes (odd multiple of 16: conflict-free b128 reads)
     static constexpr int PLANE = 32 * RSB;  // one piece of one 32-row tile
     static constexpr int TILE = 3 * PLANE;  // the three pieces
-    static constexpr int LDS = 2 * TILE + 2 * 32 * 4;  // two tiles (Q, dO or K, V) + lse / Dv
+    static constexpr int STAGE = 2 * TILE + 2 * 32 * 4;  // two tiles (Q, dO or K, V) + lse / Dv
+    static constexpr int LDS = 2 * STAGE;                // double-buffered: tile t + 1 staged under tile t
+    static constexpr int IPT = D / 32;                   // float4 items per thread of one 32 x D tile
     static constexpr bool PRESPLIT = D <= 128;   // own rows kept as pieces (else fp32, split per use)
 };
 
@@ -99,24 +101,37 @@ struct OwnRows {
     }
 };
 
-// Stage a 32-row x D tile (rows r0.., fp32 NHWC rows at `base` with pitch ld, columns col..) into LDS
-// as three bf16 piece planes [piece][row][dim] (row pitch RSB bytes); rows >= N are zero.
+// A 32-row x D tile (rows r0.., fp32 rows at `base` with pitch ld, columns col..) staged into LDS as
+// three bf16 piece planes [piece][row][dim] (row pitch RSB bytes); rows >= N are zero.  Split in two
+// halves so the next tile's global loads are in flight while the current tile computes.
 template <int D>
-WC_DEVICE void stage_tile(unsigned char* dst, const float* base, long ld, int col, int r0, int N, int tid) {
+struct TileStage {
     using Cf = B6Cfg<D>;
-    for (int i = tid; i < 32 * (D / 4); i += 256) {
-        const int r = i / (D / 4), c4 = i % (D / 4);
-        const int row = r0 + r;
-        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (row < N) v = *reinterpret_cast<const f32x4*>(base + (long)row * ld + col + 4 * c4);
-        u32x2 p0, p1, p2;
-        split3(v, p0, p1, p2);
-        unsigned char* d = dst + r * Cf::RSB + c4 * 8;
-        *reinterpret_cast<u32x2*>(d) = p0;
-        *reinterpret_cast<u32x2*>(d + Cf::PLANE) = p1;
-        *reinterpret_cast<u32x2*>(d + 2 * Cf::PLANE) = p2;
+    f32x4 v[Cf::IPT];
+    WC_DEVICE void load(const float* base, long ld, int col, int r0, int N, int tid) {
+#pragma unroll
+        for (int j = 0; j < Cf::IPT; ++j) {
+            const int i = tid + 256 * j;
+            const int r = i / (D / 4), c4 = i % (D / 4);
+            const int row = r0 + r;
+            v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (row < N) v[j] = *reinterpret_cast<const f32x4*>(base + (long)row * ld + col + 4 * c4);
+        }
     }
-}
+    WC_DEVICE void store(unsigned char* dst, int tid) const {
+#pragma unroll
+        for (int j = 0; j < Cf::IPT; ++j) {
+            const int i = tid + 256 * j;
+            const int r = i / (D / 4), c4 = i % (D / 4);
+            u32x2 p0, p1, p2;
+            split3(v[j], p0, p1, p2);
+            unsigned char* d = dst + r * Cf::RSB + c4 * 8;
+            *reinterpret_cast<u32x2*>(d) = p0;
+            *reinterpret_cast<u32x2*>(d + Cf::PLANE) = p1;
+            *reinterpret_cast<u32x2*>(d + 2 * Cf::PLANE) = p2;
+        }
+    }
+};
 
 // A operand rows = tile rows (lane = row l32), K-step ch: 8 dims per lane half (ds_read_b128).
 template <int D>
@@ -153,10 +168,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
     using Cf = B6Cfg<D>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* Qs = smem;
-    unsigned char* Os = smem + Cf::TILE;
-    float* Ls = reinterpret_cast<float*>(smem + 2 * Cf::TILE);  // [32] lse, [32] Dv
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages: Q, dO tiles, lse, Dv
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l32 = lane & 31, half = lane >> 5;
@@ -177,18 +189,36 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
         for (int r = 0; r < 16; ++r) { dvT[d][r] = 0.f; dkT[d][r] = 0.f; }
 
     const int ntiles = (N + 31) / 32;
-    for (int t = 0; t < ntiles; ++t) {
+    TileStage<D> sq, so;
+    float rl = INFINITY, rdv = 0.f;
+    auto gload = [&](int t) {
         const int q0 = t * 32;
-        __syncthreads();  // previous tile consumed
-        stage_tile<D>(Qs, base, ldq, qcol, q0, N, tid);
-        stage_tile<D>(Os, dob, lddo, head * D, q0, N, tid);
+        sq.load(base, ldq, qcol, q0, N, tid);
+        so.load(dob, lddo, head * D, q0, N, tid);
         if (tid < 32) {
             const int q = q0 + tid;
-            Ls[tid] = q < N ? lse[((long)b * H + head) * N + q] : INFINITY;  // P = 0 for padding queries
-            Ls[32 + tid] = q < N ? Dv[((long)b * H + head) * N + q] : 0.f;
+            rl = q < N ? lse[((long)b * H + head) * N + q] : INFINITY;  // P = 0 for padding queries
+            rdv = q < N ? Dv[((long)b * H + head) * N + q] : 0.f;
         }
-        __syncthreads();
-
+    };
+    auto swrite = [&](int buf) {
+        unsigned char* st = smem + buf * Cf::STAGE;
+        sq.store(st, tid);
+        so.store(st + Cf::TILE, tid);
+        if (tid < 32) {
+            float* l = reinterpret_cast<float*>(st + 2 * Cf::TILE);
+            l[tid] = rl;
+            l[32 + tid] = rdv;
+        }
+    };
+    gload(0);
+    swrite(0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        unsigned char* Qs = smem + (t & 1) * Cf::STAGE;
+        unsigned char* Os = Qs + Cf::TILE;
+        const float* Ls = reinterpret_cast<const float*>(Qs + 2 * Cf::TILE);
+        if (t + 1 < ntiles) gload(t + 1);  // in flight under this tile's MFMAs
         // S = Q K^T, dP = dO V^T: rows = queries, lane = key
         f32x16 s, dp;
 #pragma unroll
@@ -226,6 +256,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
                 mfma6(dkT[db], a, ds);
             }
         }
+        if (t + 1 < ntiles) swrite((t + 1) & 1);  // the other stage: last read in tile t - 1
+        __syncthreads();
     }
 
     if (key < N) {
@@ -248,9 +280,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
     using Cf = B6Cfg<D>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* Ks = smem;
-    unsigned char* Vs = smem + Cf::TILE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages: K, V tiles
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l32 = lane & 31, half = lane >> 5;
@@ -273,13 +303,24 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
         for (int r = 0; r < 16; ++r) dqT[d][r] = 0.f;
 
     const int ntiles = (N + 31) / 32;
+    TileStage<D> sk, sv;
+    auto gload = [&](int t) {
+        sk.load(base, ldq, kcol, t * 32, N, tid);
+        sv.load(base, ldq, vcol, t * 32, N, tid);
+    };
+    auto swrite = [&](int buf) {
+        unsigned char* st = smem + buf * Cf::STAGE;
+        sk.store(st, tid);
+        sv.store(st + Cf::TILE, tid);
+    };
+    gload(0);
+    swrite(0);
+    __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const int k0 = t * 32;
-        __syncthreads();
-        stage_tile<D>(Ks, base, ldq, kcol, k0, N, tid);
-        stage_tile<D>(Vs, base, ldq, vcol, k0, N, tid);
-        __syncthreads();
-
+        unsigned char* Ks = smem + (t & 1) * Cf::STAGE;
+        unsigned char* Vs = Ks + Cf::TILE;
+        if (t + 1 < ntiles) gload(t + 1);  // in flight under this tile's MFMAs
         // S^T = K Q^T, dP^T = V dO^T: rows = keys, lane = query
         f32x16 s, dp;
 #pragma unroll
@@ -312,6 +353,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
                 mfma6(dqT[db], a, ds);
             }
         }
+        if (t + 1 < ntiles) swrite((t + 1) & 1);
+        __syncthreads();
     }
 
     if (qme < N) {

@@ -35,6 +35,27 @@ from .engine import TAPS1, TAPS3, TAPS4S2, pack_conv, pack_convT
 _PARITIES = ((0, 0), (0, 1), (1, 0), (1, 1))
 
 
+class _Pack(dict):
+    """A layer's packing record whose weight packs are built on first use: a value wrapped in
+    _Pack.lazy(fn) is computed by fn() when read, then cached.  Each training step packs only the
+    forms its arithmetic actually launches (e.g. the f16x3 data-gradient packs, not also the bf16x6
+    ones) — the packing is host-launched torch work on every step."""
+
+    class lazy:
+        __slots__ = ('fn', )
+
+        def __init__(self, fn):
+            self.fn = fn
+
+    def __getitem__(self, k):
+        v = dict.__getitem__(self, k)
+        if isinstance(v, _Pack.lazy):
+            with torch.no_grad():
+                v = v.fn()
+            dict.__setitem__(self, k, v)
+        return v
+
+
 class _Slot:
     """A host value of the packing pass, filled by TrainEngine._resolve."""
     __slots__ = ('value', )
@@ -96,32 +117,36 @@ class TrainEngine:
         wr2 = wr.reshape(co, ci)
         f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
         w2cat = torch.cat([pack_conv(w2), wr2], 1)
-        return dict(
+        L = _Pack.lazy
+        return _Pack(
             ci=ci, co=co, gn1=f[0], conv1=f[2], gn2=s[0], conv2=s[2], resc=r, temb=blk.t_emb_layers[i][1],
-            pk1=self._pk(pack_conv(w1), ci, 9),
-            pk2=self._pk(w2cat, co, 9, ci),
+            pk1=L(lambda: self._pk(pack_conv(w1), ci, 9)),
+            pk2=L(lambda: self._pk(w2cat, co, 9, ci)),
             f3_1=K.pack_f16x3(pack_conv(w1).float(), ci) if f3 else None,
             f3_2=K.pack_f16x3(w2cat.float(), co, ci, res_f16=True) if f3 else None,
             gb1=self._later(f[0].weight.abs().max(), f[0].bias.abs().max()),
             gb2=self._later(s[0].weight.abs().max(), s[0].bias.abs().max()),
             b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
-            pk1T=self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9),
-            pk2T=self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9),
-            pkrT=self._pk(wr2.t(), co, 1),
+            pk1T=L(lambda: self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9)),
+            pk2T=L(lambda: self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9)),
+            pkrT=L(lambda: self._pk(wr2.t(), co, 1)),
             # f16x3 data gradients (raw gradient operand under its per-image absmax bound)
-            f3_1T=K.pack_f16x3(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co) if self.f3d else None,
-            f3_2T=K.pack_f16x3(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co) if self.f3d else None,
-            f3_rT=K.pack_f16x3(wr2.t().contiguous().float(), co, ntaps=1, order='natural') if self.f3d else None)
+            f3_1T=L(lambda: K.pack_f16x3(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co)) if self.f3d else None,
+            f3_2T=L(lambda: K.pack_f16x3(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co)) if self.f3d else None,
+            f3_rT=L(lambda: K.pack_f16x3(wr2.t().contiguous().float(), co, ntaps=1, order='natural'))
+            if self.f3d else None)
 
     def _pack_attn(self, blk, i: int):
         mha, gn = blk.attentions[i], blk.attention_norms[i]
         C = mha.embed_dim
         w_in, w_out = mha.in_proj_weight.detach(), mha.out_proj.weight.detach()
-        d = dict(C=C, heads=mha.num_heads, gn=gn, mha=mha, pk_in=self._pk(w_in, C, 1), pk_out=self._pk(w_out, C, 1),
-                 pk_inT=self._pk(w_in.t(), 3 * C, 1), pk_outT=self._pk(w_out.t(), C, 1), f3_in=None, f3_out=None)
+        L = _Pack.lazy
+        d = _Pack(C=C, heads=mha.num_heads, gn=gn, mha=mha, pk_in=L(lambda: self._pk(w_in, C, 1)),
+                  pk_out=L(lambda: self._pk(w_out, C, 1)), pk_inT=L(lambda: self._pk(w_in.t(), 3 * C, 1)),
+                  pk_outT=L(lambda: self._pk(w_out.t(), C, 1)), f3_in=None, f3_out=None)
         if self.f3d and C % 16 == 0:  # projection data gradients on f16x3 (per-image absmax bounds)
-            d['f3_inT'] = K.pack_f16x3(w_in.t().contiguous().float(), 3 * C, ntaps=1, order='natural')
-            d['f3_outT'] = K.pack_f16x3(w_out.t().contiguous().float(), C, ntaps=1, order='natural')
+            d['f3_inT'] = L(lambda: K.pack_f16x3(w_in.t().contiguous().float(), 3 * C, ntaps=1, order='natural'))
+            d['f3_outT'] = L(lambda: K.pack_f16x3(w_out.t().contiguous().float(), C, ntaps=1, order='natural'))
         if self.f3 and C % 16 == 0:
             d['f3_in'] = K.pack_f16x3(w_in.float(), C, ntaps=1, order='natural')
             d['f3_out'] = K.pack_f16x3(w_out.float(), C, ntaps=1, order='natural')

@@ -407,6 +407,16 @@ int wc_conv_wgrad3_splits(int M, int C0, int B, int H, int W, int target_blocks)
  * aligned); absmax [B] float32 zeroed by the caller.  The per-image range bound that lets the training
  * backward run its data-gradient convs on f16x3 (train_ddpm.py:110). */
 int wc_absmax_images(const float* x, int ldx, int B, int HW, int C, float* absmax, void* stream);
+
+/* Weight re-pack for the split-precision kernels in one launch (the layouts of kernels.pack_x6 /
+ * pack_f16x3, see wc_pack.hip): w [N][ldw] fp32 with K = ntaps*C0 + C1 columns; order 0 'halo'
+ * (16-channel chunk, tap) steps or 1 'natural' K/16 steps; mode 0 bf16x6 (3 truncated bf16 pieces),
+ * mode 1 f16x3 (per-row power-of-two scale, wsinv[n] = 2^-sW[n], segment 0 as 2 fp16 pieces, segment 1
+ * as 2 fp16 pieces with res_f16 else 3 bf16); BN the output-channel tile (64 or 128); out_bytes the
+ * exact packed size.  Replaces the per-step host-side packing of every weight in the training step
+ * (train_ddpm.py:110-111 re-runs the forward on updated weights). */
+int wc_pack_split(const float* w, int ldw, int N, int C0, int ntaps, int C1, int order, int mode, int res_f16,
+                  int BN, void* out, int64_t out_bytes, float* wsinv, void* stream);
 /* dW = sum_split part: column k < K0 is (tap t = k / C0, channel c = k % C0), written (c < Cw only)
  * to dw0[m*sM0 + c*sC0 + t*sT0]; columns k >= K0 to dw1[m*sM1 + k - K0].  accumulate: += . */
 int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,

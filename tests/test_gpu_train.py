@@ -227,6 +227,32 @@ def test_dgrad_f16x3_raw_segment_per_image_bound(B, H, W, C, N):
         assert rel_l2(out[b].cpu(), ref[b]) < 1e-5
 
 
+@pytest.mark.parametrize('N,C0,C1,ntaps,order,res_f16', [
+    (128, 64, 0, 9, 'halo', False), (256, 128, 64, 9, 'halo', True), (256, 128, 64, 9, 'halo', False),
+    (64, 32, 32, 9, 'halo', True), (96, 48, 0, 9, 'halo', False), (384, 128, 0, 1, 'natural', False),
+    (512, 1536, 0, 1, 'natural', False), (130, 64, 0, 4, 'halo', False), (64, 256, 0, 1, 'natural', False)])
+def test_device_pack_equals_torch_pack(N, C0, C1, ntaps, order, res_f16):
+    """wc_pack_split (one launch per weight) is bit for bit the torch-op definitions pack_f16x3 /
+    pack_x6, including row scales (an all-zero row, a power-of-two maximum), tile padding and the
+    residual segment in both encodings."""
+    from weatherconverter_amd import kernels as K
+    g = _gen(12)
+    w = torch.randn((N, ntaps * C0 + C1), generator=g) * torch.exp(torch.randn((N, 1), generator=g) * 3)
+    w[0] = 0.0
+    w[1, 0] = 2.0 * float(w[1].abs().max()) if w.shape[0] > 1 else 0.0
+    if N > 2:
+        w[2] = w[2] / w[2].abs().max() * 0.25  # maximum exactly 2^-2
+    w = w.cuda()
+    a = K.pack_f16x3(w, C0, C1, ntaps=ntaps, order=order, res_f16=res_f16, device=True)
+    b = K.pack_f16x3(w, C0, C1, ntaps=ntaps, order=order, res_f16=res_f16, device=False)
+    assert a.data.shape == b.data.shape and torch.equal(a.data, b.data)
+    assert torch.equal(a.wsinv, b.wsinv) and (a.order, a.BN, a.res_f16) == (b.order, b.BN, b.res_f16)
+    if order == 'natural' or ntaps == 9:
+        a6 = K.pack_x6(w, C0, C1, ntaps=ntaps, order=order, device=True)
+        b6 = K.pack_x6(w, C0, C1, ntaps=ntaps, order=order, device=False)
+        assert torch.equal(a6.data, b6.data)
+
+
 # ------------------------------------------------------------------ whole model
 def _model_grads(mc, B, precision, seed=0):
     """(our grads, oracle float64 grads, loss ours, loss ref) for one MSE training iteration."""

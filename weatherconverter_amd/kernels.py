@@ -335,11 +335,42 @@ def split3_bits(x: torch.Tensor) -> torch.Tensor:
     return (torch.stack([u0, u1, u2]) >> 16).to(torch.int16)
 
 
-def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo') -> X6Weight:
+def _pack_dev(w: torch.Tensor, C0: int, C1: int, ntaps: int, order: str, mode: int, res_f16: bool):
+    """One-launch device re-pack (wc_pack_split) of a [N][ntaps*C0 + C1] fp32 CUDA weight: (data, wsinv)
+    in exactly the layout of the torch definitions below (tests/test_gpu_train.py compares them bit
+    for bit)."""
+    N, K = w.shape
+    _, BN = x6_tile(N)
+    Np = -(-N // BN) * BN
+    P0, P1 = (2, 2 if res_f16 else 3) if mode == 1 else (3, 3)
+    row = (ntaps * C0 // 16 * P0 + C1 // 16 * P1) * 2 * BN * 8
+    w = w.float().contiguous()
+    data = torch.empty((Np // BN, row), dtype=torch.int16, device=w.device)
+    wsinv = torch.empty(Np, dtype=torch.float32, device=w.device) if mode == 1 else None
+    _timed('pack_split_kernel', 'wc_pack_split', 0.0, w.data_ptr(), K, N, C0, ntaps, C1,
+           0 if order == 'halo' else 1, mode, int(res_f16), BN, data.data_ptr(), data.numel() * 2, _ptr(wsinv),
+           _stream())
+    return data, wsinv
+
+
+def pack_device_enabled() -> bool:
+    """Weight packs built by the one-launch device kernel for CUDA weights; WC_PACK_DEVICE=0 keeps the
+    torch-op definitions (A/B, and the reference the kernel is tested against)."""
+    return os.environ.get('WC_PACK_DEVICE', '1') != '0'
+
+
+def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo',
+            device: Optional[bool] = None) -> X6Weight:
     """Re-pack a [N][ntaps*C0 + C1] conv weight (K = (tap, c) then the 1x1 residual columns, as
     engine.pack_conv) for the bf16x6 kernels.  order 'halo' (wc_conv3x3_x6, ntaps 9): steps are
-    (16-channel chunk, tap) then the residual chunks; 'natural' (wc_conv_igemm_x6): K/16 in order."""
+    (16-channel chunk, tap) then the residual chunks; 'natural' (wc_conv_igemm_x6): K/16 in order.
+    A CUDA weight is packed by the device kernel (device=None: unless WC_PACK_DEVICE=0)."""
     N, K = w.shape
+    if (device if device is not None else pack_device_enabled()) and w.is_cuda:
+        _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
+        _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
+        data, _ = _pack_dev(w, C0, C1, ntaps, order, 0, False)
+        return X6Weight(data, N, x6_tile(N)[1], C0, C1, order)
     _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
     _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
     _, BN = x6_tile(N)
@@ -360,7 +391,7 @@ def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str
 
 
 def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str = 'halo',
-               res_f16: bool = False, amax: Optional[torch.Tensor] = None) -> X6Weight:
+               res_f16: bool = False, amax: Optional[torch.Tensor] = None, device: Optional[bool] = None) -> X6Weight:
     """Re-pack a [N][ntaps*C0 + C1] conv (+ 1x1 residual) weight for the f16x3 kernels: per output
     channel n a power-of-two scale 2^sW[n] with max_k |w[n, k]| * 2^sW[n] <= 2^14 over the fp16-packed
     columns (segment 0, and the residual with res_f16); segment 0
@@ -371,6 +402,10 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     N, K = w.shape
     _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'f16x3 weight shape')
     _req(order == 'natural' or ntaps in (9, 4), "order 'halo' is for 3x3 (or s2d 2x2) weights")
+    if (device if device is not None else pack_device_enabled()) and w.is_cuda and amax is None:
+        data, wsinv = _pack_dev(w, C0, C1, ntaps, order, 1, res_f16)
+        order_tag = ('f16x3' if ntaps == 9 else 'f16x3s') if order == 'halo' else 'f16x3n'
+        return X6Weight(data, N, x6_tile(N)[1], C0, C1, order_tag, wsinv, res_f16)
     _, BN = x6_tile(N)
     Np = -(-N // BN) * BN
     T = Np // BN

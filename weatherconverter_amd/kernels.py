@@ -337,8 +337,10 @@ def split3_bits(x: torch.Tensor) -> torch.Tensor:
 
 def _pack_dev(w: torch.Tensor, C0: int, C1: int, ntaps: int, order: str, mode: int, res_f16: bool):
     """One-launch device re-pack (wc_pack_split) of a [N][ntaps*C0 + C1] fp32 CUDA weight: (data, wsinv)
-    in exactly the layout of the torch definitions below (tests/test_gpu_train.py compares them bit
-    for bit)."""
+    in exactly the layout of the torch definitions below, evaluated with IEEE fp32 arithmetic and
+    round-to-nearest-even conversions — bit for bit the definitions run on the CPU
+    (tests/test_gpu_train.py).  (The same torch ops run on the GPU are not: their fp16 / power-of-two
+    scaling ops differ in the last bit of some pieces, which the split tolerates.)"""
     N, K = w.shape
     _, BN = x6_tile(N)
     Np = -(-N // BN) * BN
@@ -370,7 +372,9 @@ def pack_x6(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: str
         _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
         _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
         data, _ = _pack_dev(w, C0, C1, ntaps, order, 0, False)
-        return X6Weight(data, N, x6_tile(N)[1], C0, C1, order)
+        BN = x6_tile(N)[1]
+        S = (ntaps * C0 + C1) // 16
+        return X6Weight(data.view(data.shape[0], S, 3, 2, BN, 8), N, BN, C0, C1, order)
     _req(K == ntaps * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'x6 weight shape')
     _req(order == 'natural' or ntaps == 9, "order 'halo' is for 3x3 weights")
     _, BN = x6_tile(N)

@@ -1068,7 +1068,7 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
     if x6 and wgrad3_ok(g, segs[0]) and wgrad3_enabled():
         # 3x3 segment on the halo-tiled kernel; the residual 1x1 segment (if any) as its own GEMM
         P = B * g.H * g.W
-        splits = lib.wc_conv_wgrad3_splits(g.C, C0, B, g.H, g.W, 1024)
+        splits = lib.wc_conv_wgrad3_splits(g.C, C0, B, g.H, g.W, 512)
         a.nseg = 1
         part = torch.empty(splits * g.C * K0, dtype=torch.float32, device=g.t.device)
         s = _stream()

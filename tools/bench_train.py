@@ -6,9 +6,11 @@ mode 'step' (default): the reference's whole training iteration (train_ddpm.py:9
     opt.zero_grad(); noisy = scheduler.add_noise(images, noise, t); pred = model(noisy, t);
     loss = MSELoss()(pred, noise); loss.backward(); opt.step()
   with the HIP forward-with-tape and HIP backward (models/train_engine.py) and torch Adam, timed per
-  phase with events.  Arithmetic (the model's conv precision, f16x3 by default): forward convs /
-  projections f16x3 under static GroupNorm range bounds, data-gradient convs bf16x6, weight gradients
-  bf16x6 MFMA, attention fp32 MFMA; all fp32-class and checked against float64 autograd.
+  phase with events.  Arithmetic (the model's conv precision, f16x3 by default): forward convs,
+  projections and attention f16x3 under static range bounds (GroupNorm, in-projection row norms),
+  data-gradient convs f16x3 under per-image absmax bounds of the gradient, weight gradients and the
+  attention backward bf16x6 (fp32 MFMA at head dim 192); all fp32-class and checked against float64
+  autograd.
 mode 'forward': the training-loss forward only (add_noise + UNet fwd + MSE), HIP-graph replay (the
   round-1 line).
 """
@@ -152,7 +154,8 @@ def train_step(args):
         'ms_forward': round(fwd, 2), 'ms_backward': round(bwd, 2), 'ms_adam_and_host': round(ms - fwd - bwd, 2),
         'images_per_s': round(B * args.steps / el, 2), 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
         'higher_is_better': True,
-        'dtype': 'fp32-class (f16x3 forward convs, projections and attention; bf16x6 data and weight gradients; fp32-MFMA attention backward)',
+        'dtype': 'fp32-class (f16x3: forward convs, projections, attention, and the data gradients under per-image '
+                 'absmax bounds; bf16x6: weight gradients, attention backward (fp32 MFMA at head dim 192))',
         'data': 'synthetic (keyed random-init weights; images U[-1,1], Philox N(0,1) noise, t ~ U[0,1000))',
         'config': {'workload': 'BASELINE config 3 full training iteration', 'global_batch': B, 'image_size': S,
                    'backward': True, 'optimizer': 'torch.optim.Adam lr 1e-4'},

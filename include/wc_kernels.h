@@ -402,6 +402,13 @@ int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks);
  * wc_conv_wgrad ([splits][M][9*C0], column = tap*C0 + c), reduced by wc_wgrad_reduce; splits from
  * wc_conv_wgrad3_splits. */
 int wc_conv_wgrad3(const wc_wgrad_args* args, float* part, int splits, void* stream);
+/* The same halo-tiled weight gradient on f16x3: segment 0's operand (a GroupNorm(+SiLU) output) scaled
+ * by 2^x_exp, the forward conv's exponent for it (|X~| * 2^x_exp <= 2^14, Samuelson bound), and G by
+ * 2^sg with sg = 13 - floor(log2 max_b gbound[b]); gbound[B] = per-image max |G| (wc_absmax_images,
+ * device memory).  Two fp16 pieces per operand, products h*h + h*l + l*h, the common power-of-two
+ * factor removed in the epilogue.  Same partials and reduce as wc_conv_wgrad3. */
+int wc_conv_wgrad3_f16x3(const wc_wgrad_args* args, float* part, int splits, int x_exp, const float* gbound,
+                         void* stream);
 int wc_conv_wgrad3_splits(int M, int C0, int B, int H, int W, int target_blocks);
 /* absmax[b] = max |x| over image b of the NHWC view (x, ldx) with C channels (C % 4 == 0, 16-byte
  * aligned); absmax [B] float32 zeroed by the caller.  The per-image range bound that lets the training
@@ -418,8 +425,10 @@ int wc_absmax_images(const float* x, int ldx, int B, int HW, int C, float* absma
 int wc_pack_split(const float* w, int ldw, int N, int C0, int ntaps, int C1, int order, int mode, int res_f16,
                   int BN, void* out, int64_t out_bytes, float* wsinv, void* stream);
 /* dW = sum_split part: column k < K0 is (tap t = k / C0, channel c = k % C0), written (c < Cw only)
- * to dw0[m*sM0 + c*sC0 + t*sT0]; columns k >= K0 to dw1[m*sM1 + k - K0].  accumulate: += . */
-int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,
+ * to dw0[m*sM0 + c*sC0 + t*sT0]; columns k >= K0 to dw1[m*sM1 + k - K0].  accumulate: += .
+ * part is scratch: with more than 32 splits the sums of each group of 32 slabs (in a fixed order)
+ * overwrite the group's first slab, and the groups are then added in order. */
+int wc_wgrad_reduce(float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,
                     int64_t sM0, int64_t sC0, int64_t sT0, float* dw1, int64_t sM1, int accumulate,
                     void* stream);
 
@@ -459,6 +468,14 @@ int wc_attention_bwd(const float* qkv, int ld_qkv, const float* out, int ld_out,
 int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout, int ld_dout,
                       const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C, int heads,
                       float scale, void* stream);
+/* The same backward on f16x3 (two round-to-nearest fp16 pieces per operand, three products per block):
+ * Q, K, V scaled by 2^eq, 2^ek, 2^ev — the training forward's exponents from the in-projection bounds
+ * (|Q| 2^eq <= 2^14 ...); dO by 2^edo from dobound[b] = per-image max |dO| (device, wc_absmax_images);
+ * P by 2^14; dS by 2^eds with the bound |dS| <= 2 d max|dO| max|V|.  Head dim in {32, 64, 128}. */
+int wc_attention_bwd_f16x3(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
+                           int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
+                           int C, int heads, float scale, int eq, int ek, int ev, const float* dobound,
+                           void* stream);
 /* Its first step alone: dv_work[(b*heads + h)*N + q] = sum_d dout[b, q, h*D + d] * out[b, q, h*D + d]. */
 int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N, int heads,
                           int D, float* dv_work, void* stream);

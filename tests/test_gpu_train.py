@@ -95,6 +95,63 @@ def test_conv_wgrad3_halo_kernel(pro, res, M, C0, B, H, W):
         assert rel_l2(dwr.cpu(), ref) < 1e-5
 
 
+@pytest.mark.parametrize('pro,M,C0,B,H,W', [(2, 128, 64, 2, 16, 32), (1, 256, 32, 1, 8, 16), (2, 64, 128, 3, 4, 32)])
+def test_conv_wgrad3_f16x3_vs_float64(pro, M, C0, B, H, W):
+    """The halo-tiled 3x3 weight gradient on f16x3 (wc_conv_wgrad3_f16x3): X~ under its own
+    exponent, G under the batch's max of the per-image absmax (wc_absmax_images), images whose
+    gradients differ by 10^3 in scale; against float64 autograd at rel-L2 <= 1e-5."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import Seg, View
+    from weatherconverter_amd.diffusion_model.models.engine import TAPS3
+    g = _gen(5)
+    x = torch.randn((B, H, W, C0), generator=g)
+    dy = torch.randn((B, H, W, M), generator=g)
+    dy[0] *= 1e-3
+    sc = torch.rand((B, C0), generator=g) + 0.5
+    sh = torch.randn((B, C0), generator=g) * 0.3
+    a = x.double() * sc.double()[:, None, None, :] + sh.double()[:, None, None, :]
+    a = F.silu(a) if pro == 2 else a
+    x_exp = 13 - int(np.floor(np.log2(float(a.abs().max()))))
+    dyc = dy.cuda()
+    gb = K.absmax_images(View.full(dyc))
+    assert torch.allclose(gb.cpu(), dy.abs().amax((1, 2, 3)))
+    dw = torch.zeros((M, C0, 3, 3), device='cuda')
+    seg = Seg(View.full(x.cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=pro == 2)
+    prof = K.profile_conv(True)
+    K.conv_wgrad(View.full(dyc), [seg], dw, (C0 * 9, 9, 1), x6=True, f3=(x_exp, gb))
+    torch.cuda.synchronize()
+    K.profile_conv(False)
+    assert any(n.startswith('conv_wgrad3_kernel') and n.endswith('true>') for n, *_ in prof), [n for n, *_ in prof]
+    w = torch.zeros((M, C0, 3, 3), dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(a.permute(0, 3, 1, 2), w, padding=1)
+    y.backward(dy.double().permute(0, 3, 1, 2))
+    assert rel_l2(dw.cpu(), w.grad) < 1e-5
+
+
+def test_wgrad_reduce_many_splits_two_level():
+    """More than 32 pixel splits: the split sums go through the two-level fixed-order reduction
+    (groups of 32 slabs in place, then the groups in order); 1x1 weight gradient against float64,
+    accumulate into an existing gradient, and bit-identical on a second run."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd._native import load
+    from weatherconverter_amd.kernels import Seg, View
+    from weatherconverter_amd.diffusion_model.models.engine import TAPS1
+    g = _gen(6)
+    B, H, W, C, M = 4, 64, 64, 128, 128
+    assert load().wc_conv_wgrad_splits(M, C, B * H * W, 2048) > 32
+    x = torch.randn((B, H, W, C), generator=g)
+    dy = torch.randn((B, H, W, M), generator=g)
+    base = torch.randn((M, C), generator=g)
+    outs = []
+    for _ in range(2):
+        dw = base.clone().cuda()
+        K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS1)], dw, (C, 1, 0), accumulate=True, x6=True)
+        outs.append(dw.cpu())
+    ref = base.double() + torch.einsum('bhwm,bhwc->mc', dy.double(), x.double())
+    assert rel_l2(outs[0], ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize('x6', [False, True])
 def test_conv_wgrad_4x4_stride2_and_transposed(x6):
     from weatherconverter_amd import kernels as K
@@ -183,17 +240,21 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     d = C // heads
     qkv = torch.randn((B * N, 3 * C), generator=g)
     do = torch.randn((B * N, C), generator=g)
+    do[:N] *= 1e-3  # images whose output gradients differ in scale (per-image dO exponent)
     o = torch.empty((B * N, C), device='cuda')
     lse = torch.empty((B, heads, N), device='cuda')
     exps = (10, 10, 10) if precision == 'f16x3' else None  # |randn| * 2^10 stays far inside fp16
     K.attention_fwd_lse(qkv.cuda(), o, lse, B, N, C, heads, precision=precision, exps=exps)
     dqkv = torch.empty((B * N, 3 * C), device='cuda')
+    dob = do.abs().reshape(B, -1).amax(1).cuda() if precision == 'f16x3' else None
     prof = K.profile_conv(True)
-    K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads, precision=precision)
+    K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads, precision=precision, exps=exps,
+                    dout_bound=dob)
     torch.cuda.synchronize()
     K.profile_conv(False)
     if C // heads in (32, 64, 128):  # the split-precision backward ran (D = 192 stays fp32 MFMA)
-        assert any(n.startswith('attn_bwd6_dq_kernel') for n, *_ in prof)
+        tag = 'true>' if precision == 'f16x3' else 'false>'
+        assert any(n.startswith('attn_bwd6_dq_kernel') and n.endswith(tag) for n, *_ in prof), [n for n, *_ in prof]
     q_ = qkv.double().reshape(B, N, 3 * C).requires_grad_(True)
     q, k, v = q_.split(C, dim=-1)
     sh = lambda z: z.reshape(B, N, heads, d).transpose(1, 2)  # noqa: E731
@@ -204,6 +265,8 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     assert rel_l2(o.cpu(), out.detach().reshape(B * N, C)) < 1e-5
     assert float((lse.cpu().double() - ref_lse.detach()).abs().max()) < 1e-5 * float(ref_lse.abs().max()) + 1e-6
     assert rel_l2(dqkv.cpu(), q_.grad.reshape(B * N, 3 * C)) < 1e-5
+    # the small-gradient image on its own (its dO exponent is its own)
+    assert rel_l2(dqkv.cpu()[:N], q_.grad.reshape(B * N, 3 * C)[:N]) < 1e-5
 
 
 @pytest.mark.parametrize('B,H,W,C,N', [(3, 16, 32, 128, 128), (2, 32, 16, 64, 64), (1, 8, 48, 256, 128)])

@@ -19,28 +19,51 @@
 //   attn_bwd6_dq_kernel    a wave owns 32 queries; 32-key tiles of K and V staged as pieces; S^T,
 //       dP^T with lane = query, dQ^T += K^T dS^T.
 // No atomics, fixed reduction order: deterministic.
+//
+// F3 = true (wc_attention_bwd_f16x3): the same kernels on f16x3 — every operand scaled by a power of
+// two and split into two round-to-nearest fp16 pieces, products h*h + h*l + l*h on
+// v_mfma_f32_32x32x16_f16 (3 MFMAs per block instead of 6).  The exponents come from range bounds:
+// Q, K, V from the forward's in-projection bounds (eq, ek, ev: |Q| 2^eq <= 2^14 ...); dO from its
+// per-image absmax (dobound[b], |dO| 2^edo < 2^14); P in [0, 1] at 2^14; dS = P (dP - D) with
+// |dP_ij| = |dO_i . V_j| <= d max|dO| max|V| and |D_i| = |dO_i . O_i| <= d max|dO| max|V| (O is a
+// convex combination of V rows), so |dS| < 2^(e_do + 2 + log2 d + 14 - ev) and
+// eds = ev - e_do - 2 - log2 d puts it below 2^14 (e_do = floor(log2 max|dO|)).  Accumulators carry
+// the products' power-of-two factors, removed exactly before use / in the epilogue.
 #include "wc_x6.hpp"
 
 namespace {
 
 using namespace wcx6;
 
-template <int D>
+template <int D, bool F3 = false>
 struct B6Cfg {
-    static_assert(D % 32 == 0, "bf16x6 attention backward: D % 32 == 0");
+    static_assert(D % 32 == 0, "split-precision attention backward: D % 32 == 0");
+    static constexpr int NP = F3 ? 2 : 3;   // operand pieces
     static constexpr int NCH = D / 16;      // 16-dim K-steps of S / dP
     static constexpr int NDB = D / 32;      // 32-dim output blocks
     static constexpr int RSB = 2 * D + 80;  // tile row bytes (odd multiple of 16: conflict-free b128 reads)
     static constexpr int PLANE = 32 * RSB;  // one piece of one 32-row tile
-    static constexpr int TILE = 3 * PLANE;  // the three pieces
+    static constexpr int TILE = NP * PLANE; // the pieces
     static constexpr int STAGE = 2 * TILE + 2 * 32 * 4;  // two tiles (Q, dO or K, V) + lse / Dv
     static constexpr int LDS = 2 * STAGE;                // double-buffered: tile t + 1 staged under tile t
     static constexpr int IPT = D / 32;                   // float4 items per thread of one 32 x D tile
     static constexpr bool PRESPLIT = D <= 128;   // own rows kept as pieces (else fp32, split per use)
 };
 
-// Three bf16 pieces of 8 consecutive values as MFMA operands.
-WC_DEVICE void pieces8x3(const float* v, u32x4 (&out)[3]) {
+// Split-precision pieces of 8 consecutive values as MFMA operands: three exact bf16 pieces, or (F3)
+// two fp16 pieces of v * sc.
+template <bool F3>
+WC_DEVICE void pieces8(const float* v, float sc, u32x4 (&out)[F3 ? 2 : 3]);
+template <>
+WC_DEVICE void pieces8<true>(const float* v, float sc, u32x4 (&out)[2]) {
+    u32x2 a0, a1, b0, b1;
+    split2_f16(f32x4{v[0], v[1], v[2], v[3]} * sc, a0, a1);
+    split2_f16(f32x4{v[4], v[5], v[6], v[7]} * sc, b0, b1);
+    out[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+    out[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+}
+template <>
+WC_DEVICE void pieces8<false>(const float* v, float, u32x4 (&out)[3]) {
     u32x2 a0, a1, a2, b0, b1, b2;
     split3(f32x4{v[0], v[1], v[2], v[3]}, a0, a1, a2);
     split3(f32x4{v[4], v[5], v[6], v[7]}, b0, b1, b2);
@@ -48,16 +71,20 @@ WC_DEVICE void pieces8x3(const float* v, u32x4 (&out)[3]) {
     out[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
     out[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
 }
-
-// ... of accumulator registers off .. off + 7 (off a compile-time multiple of 8 after unrolling)
-WC_DEVICE void pieces8x3(const f32x16& v, int off, u32x4 (&out)[3]) {
+template <bool F3>
+WC_DEVICE void pieces8(const f32x16& v, int off, float sc, u32x4 (&out)[F3 ? 2 : 3]) {
     float t[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) t[j] = v[off + j];
-    pieces8x3(t, out);
+    pieces8<F3>(t, sc, out);
+}
+WC_DEVICE void mfmaP(f32x16& acc, const u32x4 (&a)[2], const u32x4 (&b)[2]) {
+    acc = mfma_f16(a[0], b[0], acc);
+    acc = mfma_f16(a[0], b[1], acc);
+    acc = mfma_f16(a[1], b[0], acc);
 }
 
-WC_DEVICE void mfma6(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {
+WC_DEVICE void mfmaP(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {
     acc = mfma_bf16(a[0], b[0], acc);
     acc = mfma_bf16(a[0], b[1], acc);
     acc = mfma_bf16(a[1], b[0], acc);
@@ -69,12 +96,14 @@ WC_DEVICE void mfma6(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {
 // A wave's own 32 rows (lane = row l32) of a [rows][D] fp32 matrix, the dims its lane half feeds:
 // for K-step ch the lane holds dims 16 ch + 8 half .. + 7.  Kept either as bf16 pieces (PRESPLIT) or as
 // fp32 values split per use.
-template <int D>
+template <int D, bool F3>
 struct OwnRows {
-    using Cf = B6Cfg<D>;
-    u32x4 pc[Cf::PRESPLIT ? Cf::NCH : 1][3];
+    using Cf = B6Cfg<D, F3>;
+    u32x4 pc[Cf::PRESPLIT ? Cf::NCH : 1][Cf::NP];
     float fv[Cf::PRESPLIT ? 1 : Cf::NCH * 8];
-    WC_DEVICE void load(const float* row, bool ok, int half) {
+    float sc = 1.f;
+    WC_DEVICE void load(const float* row, bool ok, int half, float scale) {
+        sc = scale;
 #pragma unroll
         for (int ch = 0; ch < Cf::NCH; ++ch) {
             float v[8];
@@ -85,18 +114,19 @@ struct OwnRows {
             }
             v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
             if constexpr (Cf::PRESPLIT) {
-                pieces8x3(v, pc[ch]);
+                pieces8<F3>(v, sc, pc[ch]);
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) fv[8 * ch + j] = v[j];
             }
         }
     }
-    WC_DEVICE void get(int ch, u32x4 (&out)[3]) const {
+    WC_DEVICE void get(int ch, u32x4 (&out)[Cf::NP]) const {
         if constexpr (Cf::PRESPLIT) {
-            out[0] = pc[ch][0]; out[1] = pc[ch][1]; out[2] = pc[ch][2];
+#pragma unroll
+            for (int pp = 0; pp < Cf::NP; ++pp) out[pp] = pc[ch][pp];
         } else {
-            pieces8x3(fv + 8 * ch, out);
+            pieces8<F3>(fv + 8 * ch, sc, out);
         }
     }
 };
@@ -104,9 +134,9 @@ struct OwnRows {
 // A 32-row x D tile (rows r0.., fp32 rows at `base` with pitch ld, columns col..) staged into LDS as
 // three bf16 piece planes [piece][row][dim] (row pitch RSB bytes); rows >= N are zero.  Split in two
 // halves so the next tile's global loads are in flight while the current tile computes.
-template <int D>
+template <int D, bool F3>
 struct TileStage {
-    using Cf = B6Cfg<D>;
+    using Cf = B6Cfg<D, F3>;
     f32x4 v[Cf::IPT];
     WC_DEVICE void load(const float* base, long ld, int col, int r0, int N, int tid) {
 #pragma unroll
@@ -118,43 +148,50 @@ struct TileStage {
             if (row < N) v[j] = *reinterpret_cast<const f32x4*>(base + (long)row * ld + col + 4 * c4);
         }
     }
-    WC_DEVICE void store(unsigned char* dst, int tid) const {
+    WC_DEVICE void store(unsigned char* dst, int tid, float sc) const {
 #pragma unroll
         for (int j = 0; j < Cf::IPT; ++j) {
             const int i = tid + 256 * j;
             const int r = i / (D / 4), c4 = i % (D / 4);
-            u32x2 p0, p1, p2;
-            split3(v[j], p0, p1, p2);
             unsigned char* d = dst + r * Cf::RSB + c4 * 8;
-            *reinterpret_cast<u32x2*>(d) = p0;
-            *reinterpret_cast<u32x2*>(d + Cf::PLANE) = p1;
-            *reinterpret_cast<u32x2*>(d + 2 * Cf::PLANE) = p2;
+            if constexpr (F3) {
+                u32x2 h, l;
+                split2_f16(v[j] * sc, h, l);
+                *reinterpret_cast<u32x2*>(d) = h;
+                *reinterpret_cast<u32x2*>(d + Cf::PLANE) = l;
+            } else {
+                u32x2 p0, p1, p2;
+                split3(v[j], p0, p1, p2);
+                *reinterpret_cast<u32x2*>(d) = p0;
+                *reinterpret_cast<u32x2*>(d + Cf::PLANE) = p1;
+                *reinterpret_cast<u32x2*>(d + 2 * Cf::PLANE) = p2;
+            }
         }
     }
 };
 
 // A operand rows = tile rows (lane = row l32), K-step ch: 8 dims per lane half (ds_read_b128).
-template <int D>
-WC_DEVICE void tile_rows(const unsigned char* tile, int l32, int half, int ch, u32x4 (&out)[3]) {
-    using Cf = B6Cfg<D>;
+template <int D, bool F3>
+WC_DEVICE void tile_rows(const unsigned char* tile, int l32, int half, int ch, u32x4 (&out)[F3 ? 2 : 3]) {
+    using Cf = B6Cfg<D, F3>;
     const unsigned char* p = tile + l32 * Cf::RSB + (16 * ch + 8 * half) * 2;
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc) out[pc] = *reinterpret_cast<const u32x4*>(p + pc * Cf::PLANE);
+    for (int pc = 0; pc < Cf::NP; ++pc) out[pc] = *reinterpret_cast<const u32x4*>(p + pc * Cf::PLANE);
 }
 
 // A operand = tile^T (rows = the 32 dims of block db, K = 16 tile rows of chunk c) in the row order
 // of the accumulator registers: lane half h gets rows 16c + 4h + 0..3 and 16c + 8 + 4h + 0..3
 // (ds_read_b64_tr_b16: lane 16g + 4q + p supplies row base + q, dims 16(g & 1) + 4p .. + 3; the lane
 // receives dim l32 of the 4 rows its 16-lane group supplied).
-template <int D>
-WC_DEVICE void tile_cols(const unsigned char* tile, int lane, int db, int c, u32x4 (&out)[3]) {
-    using Cf = B6Cfg<D>;
+template <int D, bool F3>
+WC_DEVICE void tile_cols(const unsigned char* tile, int lane, int db, int c, u32x4 (&out)[F3 ? 2 : 3]) {
+    using Cf = B6Cfg<D, F3>;
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
     const int row = 16 * c + 4 * (g >> 1) + q;
     const unsigned char* base = tile + row * Cf::RSB + (32 * db + 16 * (g & 1) + 4 * p) * 2;
     typedef short v4s __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc) {
+    for (int pc = 0; pc < Cf::NP; ++pc) {
         const unsigned char* a = base + pc * Cf::PLANE;
         const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a));
         const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a + 8 * Cf::RSB));
@@ -163,11 +200,37 @@ WC_DEVICE void tile_cols(const unsigned char* tile, int lane, int db, int c, u32
     }
 }
 
-template <int D>
+// Per-image power-of-two factors of the F3 operands (all 1 for bf16x6).
+struct BwdScales {
+    float sq = 1.f, sk = 1.f, sv = 1.f, sdo = 1.f, sds = 1.f, sp = 1.f;
+    int eq = 0, ek = 0, ev = 0, edo = 0, eds = 0, ep = 0;
+};
+template <int D, bool F3>
+WC_DEVICE BwdScales bwd_scales(int eq, int ek, int ev, const float* dobound, int b) {
+    BwdScales r;
+    if constexpr (F3) {
+        constexpr int LOGD = D == 32 ? 5 : D == 64 ? 6 : D == 128 ? 7 : 8;
+        const float m = dobound[b];
+        int edo = 60, eds = 60;
+        if (m > 0.f) {
+            const int e = (int)((__float_as_uint(m) >> 23) & 0xffu) - 127;  // floor(log2 max|dO|)
+            edo = min(60, 13 - e);
+            eds = min(60, ev - e - 2 - LOGD);
+        }
+        r.eq = eq; r.ek = ek; r.ev = ev; r.edo = max(edo, -100); r.eds = max(eds, -100); r.ep = 14;
+        r.sq = ldexpf(1.f, eq); r.sk = ldexpf(1.f, ek); r.sv = ldexpf(1.f, ev);
+        r.sdo = ldexpf(1.f, r.edo); r.sds = ldexpf(1.f, r.eds); r.sp = 16384.f;
+    }
+    return r;
+}
+
+template <int D, bool F3>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
-    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
-    using Cf = B6Cfg<D>;
+    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
+    int eq, int ek, int ev, const float* __restrict__ dobound) {
+    using Cf = B6Cfg<D, F3>;
+    constexpr int NP = Cf::NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages: Q, dO tiles, lse, Dv
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -177,10 +240,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* dob = dO + (long)b * N * lddo;
     const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
     const int key = blockIdx.x * 128 + wave * 32 + l32;
+    const BwdScales sc = bwd_scales<D, F3>(eq, ek, ev, dobound, b);
+    const float s_log2 = scale_log2 * ldexpf(1.f, -(sc.eq + sc.ek));  // S carries 2^(eq + ek)
+    const float dp_un = ldexpf(1.f, -(sc.edo + sc.ev));               // dP carries 2^(edo + ev)
 
-    OwnRows<D> kr, vr;
-    kr.load(base + (long)key * ldq + kcol, key < N, half);
-    vr.load(base + (long)key * ldq + vcol, key < N, half);
+    OwnRows<D, F3> kr, vr;
+    kr.load(base + (long)key * ldq + kcol, key < N, half, sc.sk);
+    vr.load(base + (long)key * ldq + vcol, key < N, half, sc.sv);
 
     f32x16 dvT[Cf::NDB], dkT[Cf::NDB];
 #pragma unroll
@@ -189,7 +255,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
         for (int r = 0; r < 16; ++r) { dvT[d][r] = 0.f; dkT[d][r] = 0.f; }
 
     const int ntiles = (N + 31) / 32;
-    TileStage<D> sq, so;
+    TileStage<D, F3> sq, so;
     float rl = INFINITY, rdv = 0.f;
     auto gload = [&](int t) {
         const int q0 = t * 32;
@@ -203,8 +269,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     };
     auto swrite = [&](int buf) {
         unsigned char* st = smem + buf * Cf::STAGE;
-        sq.store(st, tid);
-        so.store(st + Cf::TILE, tid);
+        sq.store(st, tid, sc.sq);
+        so.store(st + Cf::TILE, tid, sc.sdo);
         if (tid < 32) {
             float* l = reinterpret_cast<float*>(st + 2 * Cf::TILE);
             l[tid] = rl;
@@ -225,35 +291,35 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
         for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
 #pragma unroll
         for (int ch = 0; ch < Cf::NCH; ++ch) {
-            u32x4 a[3], bk[3];
-            tile_rows<D>(Qs, l32, half, ch, a);
+            u32x4 a[NP], bk[NP];
+            tile_rows<D, F3>(Qs, l32, half, ch, a);
             kr.get(ch, bk);
-            mfma6(s, a, bk);
-            tile_rows<D>(Os, l32, half, ch, a);
+            mfmaP(s, a, bk);
+            tile_rows<D, F3>(Os, l32, half, ch, a);
             vr.get(ch, bk);
-            mfma6(dp, a, bk);
+            mfmaP(dp, a, bk);
         }
         // P and dS in place (register r <-> query (r&3) + 8(r>>2) + 4 half of the tile)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int qi = (r & 3) + 8 * (r >> 2) + 4 * half;
-            const float pr = exp2f(s[r] * scale_log2 - Ls[qi]);
+            const float pr = exp2f(s[r] * s_log2 - Ls[qi]);
             s[r] = pr;
-            dp[r] = pr * (dp[r] - Ls[32 + qi]);
+            dp[r] = pr * (F3 ? dp[r] * dp_un - Ls[32 + qi] : dp[r] - Ls[32 + qi]);
         }
         // dV^T += dO^T P, dK^T += Q^T dS over the two 16-query chunks
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            u32x4 pp[3], ds[3];
-            pieces8x3(s, 8 * c, pp);
-            pieces8x3(dp, 8 * c, ds);
+            u32x4 pp[NP], ds[NP];
+            pieces8<F3>(s, 8 * c, sc.sp, pp);
+            pieces8<F3>(dp, 8 * c, sc.sds, ds);
 #pragma unroll
             for (int db = 0; db < Cf::NDB; ++db) {
-                u32x4 a[3];
-                tile_cols<D>(Os, lane, db, c, a);
-                mfma6(dvT[db], a, pp);
-                tile_cols<D>(Qs, lane, db, c, a);
-                mfma6(dkT[db], a, ds);
+                u32x4 a[NP];
+                tile_cols<D, F3>(Os, lane, db, c, a);
+                mfmaP(dvT[db], a, pp);
+                tile_cols<D, F3>(Qs, lane, db, c, a);
+                mfmaP(dkT[db], a, ds);
             }
         }
         if (t + 1 < ntiles) swrite((t + 1) & 1);  // the other stage: last read in tile t - 1
@@ -261,6 +327,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     }
 
     if (key < N) {
+        const float kun = scale * ldexpf(1.f, -(sc.eq + sc.eds)), vun = ldexpf(1.f, -(sc.edo + sc.ep));
         float* row = dqkv + ((long)b * N + key) * lddq;
 #pragma unroll
         for (int d = 0; d < Cf::NDB; ++d) {
@@ -268,18 +335,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
             for (int r = 0; r < 16; r += 4) {
                 const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
                 *reinterpret_cast<f32x4*>(row + kcol + dv) =
-                    f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * scale;
-                *reinterpret_cast<f32x4*>(row + vcol + dv) = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
+                    f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * kun;
+                const f32x4 vv = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
+                *reinterpret_cast<f32x4*>(row + vcol + dv) = F3 ? vv * vun : vv;
             }
         }
     }
 }
 
-template <int D>
+template <int D, bool F3>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
-    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale) {
-    using Cf = B6Cfg<D>;
+    const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
+    int eq, int ek, int ev, const float* __restrict__ dobound) {
+    using Cf = B6Cfg<D, F3>;
+    constexpr int NP = Cf::NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages: K, V tiles
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -289,10 +359,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float* dob = dO + (long)b * N * lddo;
     const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
     const int qme = blockIdx.x * 128 + wave * 32 + l32;
+    const BwdScales sc = bwd_scales<D, F3>(eq, ek, ev, dobound, b);
+    const float s_log2 = scale_log2 * ldexpf(1.f, -(sc.eq + sc.ek));
+    const float dp_un = ldexpf(1.f, -(sc.edo + sc.ev));
 
-    OwnRows<D> qr, orr;
-    qr.load(base + (long)qme * ldq + qcol, qme < N, half);
-    orr.load(dob + (long)qme * lddo + head * D, qme < N, half);
+    OwnRows<D, F3> qr, orr;
+    qr.load(base + (long)qme * ldq + qcol, qme < N, half, sc.sq);
+    orr.load(dob + (long)qme * lddo + head * D, qme < N, half, sc.sdo);
     const float lq = qme < N ? lse[((long)b * H + head) * N + qme] : INFINITY;
     const float dq = qme < N ? Dv[((long)b * H + head) * N + qme] : 0.f;
 
@@ -303,15 +376,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
         for (int r = 0; r < 16; ++r) dqT[d][r] = 0.f;
 
     const int ntiles = (N + 31) / 32;
-    TileStage<D> sk, sv;
+    TileStage<D, F3> sk, sv;
     auto gload = [&](int t) {
         sk.load(base, ldq, kcol, t * 32, N, tid);
         sv.load(base, ldq, vcol, t * 32, N, tid);
     };
     auto swrite = [&](int buf) {
         unsigned char* st = smem + buf * Cf::STAGE;
-        sk.store(st, tid);
-        sv.store(st + Cf::TILE, tid);
+        sk.store(st, tid, sc.sk);
+        sv.store(st + Cf::TILE, tid, sc.sv);
     };
     gload(0);
     swrite(0);
@@ -327,30 +400,30 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
         for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
 #pragma unroll
         for (int ch = 0; ch < Cf::NCH; ++ch) {
-            u32x4 a[3], bq[3];
-            tile_rows<D>(Ks, l32, half, ch, a);
+            u32x4 a[NP], bq[NP];
+            tile_rows<D, F3>(Ks, l32, half, ch, a);
             qr.get(ch, bq);
-            mfma6(s, a, bq);
-            tile_rows<D>(Vs, l32, half, ch, a);
+            mfmaP(s, a, bq);
+            tile_rows<D, F3>(Vs, l32, half, ch, a);
             orr.get(ch, bq);
-            mfma6(dp, a, bq);
+            mfmaP(dp, a, bq);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            const float pr = key < N ? exp2f(s[r] * scale_log2 - lq) : 0.f;
-            dp[r] = pr * (dp[r] - dq);
+            const float pr = key < N ? exp2f(s[r] * s_log2 - lq) : 0.f;
+            dp[r] = pr * (F3 ? dp[r] * dp_un - dq : dp[r] - dq);
         }
         // dQ^T += K^T dS^T
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            u32x4 ds[3];
-            pieces8x3(dp, 8 * c, ds);
+            u32x4 ds[NP];
+            pieces8<F3>(dp, 8 * c, sc.sds, ds);
 #pragma unroll
             for (int db = 0; db < Cf::NDB; ++db) {
-                u32x4 a[3];
-                tile_cols<D>(Ks, lane, db, c, a);
-                mfma6(dqT[db], a, ds);
+                u32x4 a[NP];
+                tile_cols<D, F3>(Ks, lane, db, c, a);
+                mfmaP(dqT[db], a, ds);
             }
         }
         if (t + 1 < ntiles) swrite((t + 1) & 1);
@@ -358,41 +431,43 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     }
 
     if (qme < N) {
+        const float qun = scale * ldexpf(1.f, -(sc.ek + sc.eds));
         float* row = dqkv + ((long)b * N + qme) * lddq + qcol;
 #pragma unroll
         for (int d = 0; d < Cf::NDB; ++d) {
 #pragma unroll
             for (int r = 0; r < 16; r += 4) {
                 const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
-                *reinterpret_cast<f32x4*>(row + dv) = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * scale;
+                *reinterpret_cast<f32x4*>(row + dv) = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * qun;
             }
         }
     }
 }
 
-template <int D>
+template <int D, bool F3>
 int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
-                int lddq, int B, int N, int C, int heads, float scale, hipStream_t s) {
-    using Cf = B6Cfg<D>;
+                int lddq, int B, int N, int C, int heads, float scale, int eq, int ek, int ev, const float* dobound,
+                hipStream_t s) {
+    using Cf = B6Cfg<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dkdv_kernel<D>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dkdv_kernel<D, F3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
         if (e != hipSuccess) return (int)e;
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<D>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<D, F3>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
     const dim3 grid((N + 127) / 128, heads, B);
     const float scale_log2 = scale * 1.4426950408889634f;
-    WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D)});
-    hipLaunchKernelGGL(attn_bwd6_dkdv_kernel<D>, grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq,
-                       N, C, scale_log2, scale);
+    WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D), WC_TB(F3)});
+    hipLaunchKernelGGL((attn_bwd6_dkdv_kernel<D, F3>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
+                       lddq, N, C, scale_log2, scale, eq, ek, ev, dobound);
     WC_CHECK_LAUNCH();
-    WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D)});
-    hipLaunchKernelGGL(attn_bwd6_dq_kernel<D>, grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N,
-                       C, scale_log2, scale);
+    WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D), WC_TB(F3)});
+    hipLaunchKernelGGL((attn_bwd6_dq_kernel<D, F3>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
+                       lddq, N, C, scale_log2, scale, eq, ek, ev, dobound);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -404,25 +479,49 @@ int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const floa
 extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N,
                                      int heads, int D, float* dv_work, void* stream);
 
-extern "C" int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
-                                 int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
-                                 int C, int heads, float scale, void* stream) {
-    if (!qkv || !out || !dout || !lse || !dv_work || !dqkv) return WC_E_ARG;
+static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
+                               int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
+                               int C, int heads, float scale, bool f3, int eq, int ek, int ev, const float* dobound,
+                               void* stream) {
+    if (!qkv || !out || !dout || !lse || !dv_work || !dqkv || (f3 && !dobound)) return WC_E_ARG;
     if (heads <= 0 || C % heads || B <= 0 || N <= 0) return WC_E_SHAPE;
     if (ld_qkv % 4 || ld_out % 4 || ld_dout % 4 || ld_dqkv % 4 || ld_qkv < 3 * C || ld_dqkv < 3 * C || ld_out < C ||
         ld_dout < C)
         return WC_E_SHAPE;
     if ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dqkv)) & 15)
         return WC_E_SHAPE;
+    if (f3 && (eq < -60 || eq > 60 || ek < -60 || ek > 60 || ev < -60 || ev > 60)) return WC_E_ARG;
     const int D = C / heads;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int st = wc_attention_bwd_prep(out, ld_out, dout, ld_dout, B, N, heads, D, dv_work, stream);
     if (st != WC_OK) return st;
+#define WC_BWD6(DD)                                                                                                    \
+    (f3 ? launch_bwd6<DD, true>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, eq, ek, \
+                                ev, dobound, s)                                                                        \
+        : launch_bwd6<DD, false>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, 0, 0, \
+                                 0, nullptr, s))
     switch (D) {
-        case 32: return launch_bwd6<32>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
-        case 64: return launch_bwd6<64>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
-        case 128:
-            return launch_bwd6<128>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, s);
-        default: return WC_E_SHAPE;  // D = 192 would spill (wc_attention_bwd keeps it on fp32 MFMA)
+        case 32: return WC_BWD6(32);
+        case 64: return WC_BWD6(64);
+        case 128: return WC_BWD6(128);
+        default: return WC_E_SHAPE;  // D = 192 spills in both forms (wc_attention_bwd keeps it on fp32 MFMA)
     }
+#undef WC_BWD6
+}
+
+extern "C" int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
+                                 int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
+                                 int C, int heads, float scale, void* stream) {
+    return attention_bwd_split(qkv, ld_qkv, out, ld_out, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
+                               scale, false, 0, 0, 0, nullptr, stream);
+}
+
+// f16x3 form: eq / ek / ev the forward's exponents of Q, K, V (|Q| 2^eq <= 2^14 ...), dobound[B] the
+// per-image max |dO| (device memory).
+extern "C" int wc_attention_bwd_f16x3(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
+                                      int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B,
+                                      int N, int C, int heads, float scale, int eq, int ek, int ev,
+                                      const float* dobound, void* stream) {
+    return attention_bwd_split(qkv, ld_qkv, out, ld_out, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
+                               scale, true, eq, ek, ev, dobound, stream);
 }

@@ -333,15 +333,15 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
         }
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int M, int Kc,
-                                                           int K0, int C0, int Cw, float* __restrict__ dw0, long sM0,
-                                                           long sC0, long sT0, float* __restrict__ dw1, long sM1,
-                                                           int accumulate) {
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int step,
+                                                           int M, int Kc, int K0, int C0, int Cw, float* __restrict__ dw0,
+                                                           long sM0, long sC0, long sT0, float* __restrict__ dw1,
+                                                           long sM1, int accumulate) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     const long n = (long)M * Kc;
     if (i >= n) return;
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += part[(long)sp * n + i];
+    for (int sp = 0; sp < splits; sp += step) s += part[(long)sp * n + i];
     const int m = (int)(i / Kc);
     const int k = (int)(i - (long)m * Kc);
     float* dst;
@@ -356,6 +356,27 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     *dst = accumulate ? *dst + s : s;
 }
 
+// First level of the split reduction when there are many splits: workgroup (chunk, grp) sums slabs
+// [grp * RG, grp * RG + RG) of 256 consecutive elements (4 waves, wave w takes slabs w, w + 4, ...,
+// float4 per lane; the wave sums meet in LDS in wave order) and writes the result over slab grp * RG
+// in place.  The second level (wgrad_reduce_kernel, step RG) adds the groups' slabs in order: a fixed
+// summation tree, so results stay deterministic, with the partial slabs read by
+// (n / 256) x (splits / RG) workgroups instead of one serial loop per element.
+constexpr int RG = 32;
+__global__ __launch_bounds__(256) void wgrad_reduce_groups_kernel(float* __restrict__ part, int splits, long n4) {
+    __shared__ f32x4 red[3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long e = (long)blockIdx.x * 64 + lane;  // float4 index
+    const int g0 = blockIdx.y * RG, g1 = min(splits, g0 + RG);
+    f32x4* p4 = reinterpret_cast<f32x4*>(part);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (e < n4)
+#pragma unroll 4
+        for (int sp = g0 + w; sp < g1; sp += 4) s += p4[(long)sp * n4 + e];
+    if (w) red[w - 1][lane] = s;
+    __syncthreads();
+    if (w == 0 && e < n4) p4[(long)g0 * n4 + e] = ((s + red[0][lane]) + red[1][lane]) + red[2][lane];
+}
 template <int BM, int BN, int PRO, bool X6>
 int wgrad_launch(const WgDev& d, int grid, hipStream_t s) {
     constexpr int KP = X6 ? 16 : WG_KP;
@@ -693,14 +714,26 @@ extern "C" int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks)
     return (int)((P + pps - 1) / pps);
 }
 
-extern "C" int wc_wgrad_reduce(const float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,
+extern "C" int wc_wgrad_reduce(float* part, int splits, int M, int Kc, int K0, int C0, int Cw, float* dw0,
                                int64_t sM0, int64_t sC0, int64_t sT0, float* dw1, int64_t sM1, int accumulate,
                                void* stream) {
     if (!part || !dw0 || splits < 1 || M <= 0 || Kc <= 0 || K0 <= 0 || C0 <= 0 || K0 % C0 || K0 > Kc) return WC_E_ARG;
     if (Kc > K0 && !dw1) return WC_E_ARG;
     const long n = (long)M * Kc;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       part, splits, M, Kc, K0, C0, Cw, dw0, (long)sM0, (long)sC0, (long)sT0, dw1, (long)sM1, accumulate);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int step = 1;
+    if (splits > RG && n % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0) {
+        // part is scratch: the group sums overwrite the first slab of each group
+        const long n4 = n / 4;
+        const int ng = (splits + RG - 1) / RG;
+        hipLaunchKernelGGL(wgrad_reduce_groups_kernel, dim3((unsigned)((n4 + 63) / 64), (unsigned)ng), dim3(256), 0, s,
+                           part, splits, n4);
+        WC_CHECK_LAUNCH();
+        step = RG;
+    }
+    wc_last_kernel = "wgrad_reduce_kernel";
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, part, splits, step, M, Kc, K0,
+                       C0, Cw, dw0, (long)sM0, (long)sC0, (long)sT0, dw1, (long)sM1, accumulate);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

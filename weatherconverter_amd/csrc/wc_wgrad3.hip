@@ -17,10 +17,16 @@
 // channel per lane) go straight from L2 into registers one K-step ahead and are reused by all nine
 // taps: 54 MFMAs per wave per K-step (9 taps x 6 piece products), one barrier per block.
 //
-// Arithmetic: both operands split exactly into three bf16 pieces (wcx6::split3), the six products
-// with i + j <= 2 accumulated in fp32 (as wc_conv_wgrad_x6) — G has no static range bound, so no
-// f16x3.  Results: partial sums per pixel split [split][M][9*C0] (column = tap*C0 + c, the layout
-// of wc_conv_wgrad), reduced in a fixed order by wc_wgrad_reduce: deterministic run to run.
+// Arithmetic (F3 = false, bf16x6): both operands split exactly into three bf16 pieces
+// (wcx6::split3), the six products with i + j <= 2 accumulated in fp32 (as wc_conv_wgrad_x6).
+// F3 = true (f16x3): X~ * 2^x_exp (the forward's static exponent of the GroupNorm(+SiLU) output,
+// Samuelson bound) and G * 2^sg split into two round-to-nearest fp16 pieces, products h*h + h*l +
+// l*h (27 MFMAs per wave per K-step); sg = 13 - floor(log2 max_b gbound[b]) from the per-image absmax
+// of G that the f16x3 data gradient already measured, so |G| * 2^sg < 2^14.  One exponent for the
+// whole batch: a pixel split may cross images, and every product carries the same factor, which the
+// epilogue removes exactly (power of two).  Results: partial sums per pixel split [split][M][9*C0]
+// (column = tap*C0 + c, the layout of wc_conv_wgrad), reduced in a fixed order by wc_wgrad_reduce:
+// deterministic run to run.
 #include "wc_x6.hpp"
 
 namespace {
@@ -42,27 +48,30 @@ struct W3Dev {
     int Kc;          // partial row length: 9 * C0
     int nblk, bps;   // TH x 16 blocks in the batch; blocks per split
     int nmt, nct;    // m tiles, c tiles
+    int x_exp;              // F3: exponent of X~
+    const float* gbound;    // F3: per-image max |G| [B]
 };
 
 // WM waves along M (32 output channels each), 4 / WM along C (32 input channels each); TH rows per
 // block.  PRO: 0 raw input, 1 GN affine, 2 GN affine + SiLU.
-template <int WM, int TH, int PRO>
+template <int WM, int TH, int PRO, bool F3 = false>
 struct W3Cfg {
+    static constexpr int NPC = F3 ? 2 : 3;                         // operand pieces
     static constexpr int WC = 4 / WM;
     static constexpr int BM = 32 * WM, BC = 32 * WC, CPL = WC;    // c planes of 32 channels
     static constexpr int HP = (TH + 2) * W3_HW;                     // halo pixels
     static constexpr int ROW = 64;                                  // bytes of one pixel row of one plane
     static constexpr int PLANE = HP * ROW;                          // one (piece, c-plane) plane
-    static constexpr int BUF = 3 * CPL * PLANE;                     // one halo buffer
+    static constexpr int BUF = NPC * CPL * PLANE;                   // one halo buffer
     static constexpr int LDS = 2 * BUF;
     static constexpr int ITEMS = HP * CPL * 8;                      // float4 items of one halo
     static constexpr int HJ = (ITEMS + W3_NT - 1) / W3_NT;
     static_assert(W3_NT % (8 * CPL) == 0, "each thread keeps its channel quad and plane");
 };
 
-template <int WM, int TH, int PRO>
+template <int WM, int TH, int PRO, bool F3>
 __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
-    using Cf = W3Cfg<WM, TH, PRO>;
+    using Cf = W3Cfg<WM, TH, PRO, F3>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -86,6 +95,18 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
     const int k0 = sp * p.bps;
     const int k1 = min(p.nblk, k0 + p.bps);
     const int bx_n = p.W / 16, by_n = p.H / TH;
+    // F3 scales: X~ by its static exponent, G by the batch's absmax bound
+    float xsc = 1.f, gsc = 1.f, unscale = 1.f;
+    if constexpr (F3) {
+        float gm = 0.f;
+        for (int b = 0; b < p.B; ++b) gm = fmaxf(gm, p.gbound[b]);
+        int sg = 60;
+        if (gm > 0.f) sg = min(60, 13 - ((int)((__float_as_uint(gm) >> 23) & 0xffu) - 127));
+        sg = max(sg, -100);
+        xsc = ldexpf(1.f, p.x_exp);
+        gsc = ldexpf(1.f, sg);
+        unscale = ldexpf(1.f, -(sg + p.x_exp));
+    }
 
     const __amdgpu_buffer_rsrc_t srdg = make_srd(p.g);
     const __amdgpu_buffer_rsrc_t srdx = make_srd(p.x);
@@ -142,12 +163,19 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
                 }
             }
             if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // zero padding after the prologue
-            u32x2 a0, a1, a2;
-            split3(v, a0, a1, a2);
             unsigned char* d = base + hp * Cf::ROW;
-            *reinterpret_cast<u32x2*>(d) = a0;
-            *reinterpret_cast<u32x2*>(d + Cf::CPL * Cf::PLANE) = a1;
-            *reinterpret_cast<u32x2*>(d + 2 * Cf::CPL * Cf::PLANE) = a2;
+            if constexpr (F3) {
+                u32x2 h, l;
+                split2_f16(v * xsc, h, l);
+                *reinterpret_cast<u32x2*>(d) = h;
+                *reinterpret_cast<u32x2*>(d + Cf::CPL * Cf::PLANE) = l;
+            } else {
+                u32x2 a0, a1, a2;
+                split3(v, a0, a1, a2);
+                *reinterpret_cast<u32x2*>(d) = a0;
+                *reinterpret_cast<u32x2*>(d + Cf::CPL * Cf::PLANE) = a1;
+                *reinterpret_cast<u32x2*>(d + 2 * Cf::CPL * Cf::PLANE) = a2;
+            }
         }
     };
 
@@ -194,14 +222,20 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
 #pragma unroll
             for (int r = 0; r < TH; ++r) {
                 // this K-step's A pieces (loaded one step ahead), then the next step's loads
-                u32x4 af[3];
-                {
+                u32x4 af[Cf::NPC];
+                if constexpr (F3) {
+                    u32x2 a0, a1, b0, b1;
+                    split2_f16(f32x4{gr[0], gr[1], gr[2], gr[3]} * gsc, a0, a1);
+                    split2_f16(f32x4{gr[4], gr[5], gr[6], gr[7]} * gsc, b0, b1);
+                    af[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+                    af[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+                } else {
                     u32x2 a0, a1, a2, b0, b1, b2;
                     split3(f32x4{gr[0], gr[1], gr[2], gr[3]}, a0, a1, a2);
                     split3(f32x4{gr[4], gr[5], gr[6], gr[7]}, b0, b1, b2);
                     af[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
                     af[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
-                    af[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+                    af[Cf::NPC - 1] = u32x4{a2.x, a2.y, b2.x, b2.y};
                 }
                 if (r + 1 < TH) load_g(k, r + 1);
                 else load_g(k + 1, 0);
@@ -213,15 +247,21 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
                 for (int tap = 0; tap < 9; ++tap) {
                     const int dy = tap / 3, dx = tap % 3;  // halo offset of the tap's first pixel
                     const unsigned char* q0 = hb + ((r + dy) * W3_HW + dx) * Cf::ROW;
-                    u32x4 bf[3];
+                    u32x4 bf[Cf::NPC];
 #pragma unroll
-                    for (int pc = 0; pc < 3; ++pc) bf[pc] = tr_frag(q0 + pc * Cf::CPL * Cf::PLANE);
-                    acc[tap] = mfma_bf16(af[0], bf[0], acc[tap]);
-                    acc[tap] = mfma_bf16(af[0], bf[1], acc[tap]);
-                    acc[tap] = mfma_bf16(af[1], bf[0], acc[tap]);
-                    acc[tap] = mfma_bf16(af[0], bf[2], acc[tap]);
-                    acc[tap] = mfma_bf16(af[1], bf[1], acc[tap]);
-                    acc[tap] = mfma_bf16(af[2], bf[0], acc[tap]);
+                    for (int pc = 0; pc < Cf::NPC; ++pc) bf[pc] = tr_frag(q0 + pc * Cf::CPL * Cf::PLANE);
+                    if constexpr (F3) {
+                        acc[tap] = mfma_f16(af[0], bf[0], acc[tap]);
+                        acc[tap] = mfma_f16(af[0], bf[1], acc[tap]);
+                        acc[tap] = mfma_f16(af[1], bf[0], acc[tap]);
+                    } else {
+                        acc[tap] = mfma_bf16(af[0], bf[0], acc[tap]);
+                        acc[tap] = mfma_bf16(af[0], bf[1], acc[tap]);
+                        acc[tap] = mfma_bf16(af[1], bf[0], acc[tap]);
+                        acc[tap] = mfma_bf16(af[0], bf[Cf::NPC - 1], acc[tap]);
+                        acc[tap] = mfma_bf16(af[1], bf[1], acc[tap]);
+                        acc[tap] = mfma_bf16(af[Cf::NPC - 1], bf[0], acc[tap]);
+                    }
                 }
             }
             write_halo(buf ^ 1);  // (past the last block: an unused write of zeros)
@@ -237,23 +277,23 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            out[(long)m * p.Kc + tap * p.C0 + c] = acc[tap][r];
+            out[(long)m * p.Kc + tap * p.C0 + c] = F3 ? acc[tap][r] * unscale : acc[tap][r];
         }
     }
 }
 
-template <int WM, int TH, int PRO>
+template <int WM, int TH, int PRO, bool F3>
 int launch_w3(const W3Dev& d, int grid, hipStream_t s) {
-    using Cf = W3Cfg<WM, TH, PRO>;
+    using Cf = W3Cfg<WM, TH, PRO, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad3_kernel<WM, TH, PRO>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad3_kernel<WM, TH, PRO, F3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
-    WC_SET_NAME("conv_wgrad3_kernel", {WC_TI(WM), WC_TI(TH), WC_TI(PRO)});
-    hipLaunchKernelGGL((conv_wgrad3_kernel<WM, TH, PRO>), dim3(grid), dim3(W3_NT), Cf::LDS, s, d);
+    WC_SET_NAME("conv_wgrad3_kernel", {WC_TI(WM), WC_TI(TH), WC_TI(PRO), WC_TB(F3)});
+    hipLaunchKernelGGL((conv_wgrad3_kernel<WM, TH, PRO, F3>), dim3(grid), dim3(W3_NT), Cf::LDS, s, d);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -289,8 +329,26 @@ extern "C" int wc_conv_wgrad3_splits(int M, int C0, int B, int H, int W, int tar
 // 1x1 segment goes through wc_conv_wgrad).  part: [splits][M][9*C0] floats, splits from
 // wc_conv_wgrad3_splits; then wc_wgrad_reduce(part, splits, M, 9*C0, 9*C0, C0, ...) as for
 // wc_conv_wgrad.
-extern "C" int wc_conv_wgrad3(const wc_wgrad_args* a, float* part, int splits, void* stream) {
+template <bool F3>
+int launch_w3_any(int WM, int pro, const W3Dev& d, int grid, hipStream_t s) {
+    if (WM == 4) {
+        switch (pro) {
+            case 0: return launch_w3<4, 8, 0, F3>(d, grid, s);
+            case 1: return launch_w3<4, 8, 1, F3>(d, grid, s);
+            default: return launch_w3<4, 8, 2, F3>(d, grid, s);
+        }
+    }
+    switch (pro) {
+        case 0: return launch_w3<2, 2, 0, F3>(d, grid, s);
+        case 1: return launch_w3<2, 2, 1, F3>(d, grid, s);
+        default: return launch_w3<2, 2, 2, F3>(d, grid, s);
+    }
+}
+
+static int conv_wgrad3_any(const wc_wgrad_args* a, float* part, int splits, bool f3, int x_exp, const float* gbound,
+                           void* stream) {
     if (!a || !a->g || !part || a->nseg != 1) return WC_E_ARG;
+    if (f3 && (!gbound || x_exp < -100 || x_exp > 60)) return WC_E_ARG;
     const wc_conv_seg& s0 = a->seg[0];
     if (!s0.src || (s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
     if (s0.ntaps != 9 || s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
@@ -318,17 +376,19 @@ extern "C" int wc_conv_wgrad3(const wc_wgrad_args* a, float* part, int splits, v
     const long grid = (long)splits * d.nct * d.nmt;
     if (grid > (1L << 30)) return WC_E_SHAPE;
     const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
+    d.x_exp = x_exp;
+    d.gbound = gbound;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (WM == 4) {
-        switch (pro) {
-            case 0: return launch_w3<4, 8, 0>(d, (int)grid, s);
-            case 1: return launch_w3<4, 8, 1>(d, (int)grid, s);
-            default: return launch_w3<4, 8, 2>(d, (int)grid, s);
-        }
-    }
-    switch (pro) {
-        case 0: return launch_w3<2, 2, 0>(d, (int)grid, s);
-        case 1: return launch_w3<2, 2, 1>(d, (int)grid, s);
-        default: return launch_w3<2, 2, 2>(d, (int)grid, s);
-    }
+    return f3 ? launch_w3_any<true>(WM, pro, d, (int)grid, s) : launch_w3_any<false>(WM, pro, d, (int)grid, s);
+}
+
+extern "C" int wc_conv_wgrad3(const wc_wgrad_args* a, float* part, int splits, void* stream) {
+    return conv_wgrad3_any(a, part, splits, false, 0, nullptr, stream);
+}
+
+// f16x3 form: x_exp = the forward's exponent of segment 0's (GroupNorm-bounded) operand, gbound[B] =
+// per-image max |G| (wc_absmax_images); same partial layout and reduce.
+extern "C" int wc_conv_wgrad3_f16x3(const wc_wgrad_args* a, float* part, int splits, int x_exp, const float* gbound,
+                                    void* stream) {
+    return conv_wgrad3_any(a, part, splits, true, x_exp, gbound, stream);
 }

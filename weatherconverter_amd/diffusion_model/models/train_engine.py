@@ -454,9 +454,10 @@ class TrainEngine:
         return K.x6_eligible([Seg(g, TAPS3)], n_out, g.H, g.W) and g.C % 4 == 0 and g.ldc % 4 == 0 \
             and g.ptr % 16 == 0
 
-    def _wgrad(self, g: View, segs, dw0, s0, **kw):
-        """Weight gradient on bf16x6 (precision bf16x6) or fp32 MFMA."""
-        K.conv_wgrad(g, segs, dw0, s0, x6=self.precision == 'bf16x6', **kw)
+    def _wgrad(self, g: View, segs, dw0, s0, f3=None, **kw):
+        """Weight gradient on bf16x6 (precision bf16x6) or fp32 MFMA; f3 = (x_exp, per-image max |g|):
+        the 3x3 halo kernel on f16x3 (mode f16x3)."""
+        K.conv_wgrad(g, segs, dw0, s0, x6=self.precision == 'bf16x6', f3=f3 if self.f3d else None, **kw)
 
     def _bias_grad(self, g: View, *params):
         sums = K.channel_sums(g)
@@ -490,11 +491,14 @@ class TrainEngine:
         gY = self._grad(Y)
         gX = self._grad(X)
         self._bias_grad(gY, rp['conv2'].bias, rp['resc'].bias)
+        # per-image max |gY|: the range bound of the f16x3 data gradients and weight gradient
+        f3Y = rp['f3_2T'] is not None and self._dgrad3_ok(gY, co)
+        bY = K.absmax_images(gY) if f3Y else None
         self._wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
-                     self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci)
+                    self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci,
+                    f3=(K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), bY) if f3Y else None)
         dz2 = View.full(self._new(B, H, W, co))
-        if rp['f3_2T'] is not None and self._dgrad3_ok(gY, co):
-            bY = K.absmax_images(gY)
+        if f3Y:
             K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
             if (H * W) % (256 if ci <= 64 else 128) == 0 and co % 16 == 0:  # one-image M tiles (per-image bound)
                 K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=gX)
@@ -509,12 +513,13 @@ class TrainEngine:
                       dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False)
         sums = self._bias_grad(dh, rp['conv1'].bias)
         self.dproj[:, rp['off']:rp['off'] + co].copy_(sums[:, :, 0])
+        f3h = rp['f3_1T'] is not None and self._dgrad3_ok(dh, ci)
+        bh = K.absmax_images(dh) if f3h else None
         self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
-                     (ci * 9, 9, 1))
+                    (ci * 9, 9, 1), f3=(K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8), bh) if f3h else None)
         dz1 = View.full(self._new(B, H, W, ci))
-        if rp['f3_1T'] is not None and self._dgrad3_ok(dh, ci):
-            K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60,
-                            a_bound=K.absmax_images(dh))
+        if f3h:
+            K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
         else:
             self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
         g1 = rp['gn1']
@@ -537,8 +542,14 @@ class TrainEngine:
         else:
             self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W)
         dqkv = self._new(B, H, W, 3 * C)
-        K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C), B,
-                        N, C, ap['heads'], precision=self.precision)
+        if self.f3d and ap['f3_in'] is not None:
+            # f16x3 under the forward's Q / K / V exponents and the per-image max |dO|
+            exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], N * C // 8)
+            K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
+                            B, N, C, ap['heads'], precision='f16x3', exps=exps, dout_bound=K.absmax_images(View.full(do)))
+        else:
+            K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
+                            B, N, C, ap['heads'], precision=self.precision)
         gq = View.full(dqkv)
         self._bias_grad(gq, mha.in_proj_bias)
         self._wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),

@@ -1038,12 +1038,21 @@ def wgrad3_ok(g: View, s0: Seg) -> bool:
         and v.ptr % 16 == 0 and g.ptr % 16 == 0
 
 
+def wgrad3_f16x3_enabled() -> bool:
+    """The halo 3x3 weight gradient on f16x3 when the caller supplies the bounds (WC_WGRAD3_F16X3=0:
+    bf16x6, for A/B)."""
+    return os.environ.get('WC_WGRAD3_F16X3', '1') != '0'
+
+
 def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, int, int], *, Cw: Optional[int] = None,
-               dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False, x6: bool = False):
+               dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False, x6: bool = False,
+               f3: Optional[Tuple[int, torch.Tensor]] = None):
     """Weight gradient of a conv whose input segments are `segs` (as the forward read them, prologue
     included) and whose output gradient is the view g (pixel grid = g's H x W): GEMM over the pixels
     on fp32 MFMA (or bf16x6 with x6), split and reduced in a fixed order.  Column (tap t, channel c < Cw) of segment 0 is
-    written to dw0.flat[m*s0[0] + c*s0[1] + t*s0[2]], segment 1's columns to dw1.flat[m*s1 + c]."""
+    written to dw0.flat[m*s0[0] + c*s0[1] + t*s0[2]], segment 1's columns to dw1.flat[m*s1 + c].
+    f3 = (x_exp, gbound): segment 0's f16x3 exponent (the forward's, for its GroupNorm-bounded operand)
+    and the per-image max |g| [B] on the device; the 3x3 halo kernel then runs f16x3."""
     g.check()
     _req(1 <= len(segs) <= 2, 'wgrad takes 1 or 2 segments')
     _req(dw0.is_cuda and dw0.dtype == torch.float32 and dw0.is_contiguous(), 'dw0: contiguous fp32 device tensor')
@@ -1072,7 +1081,14 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
         a.nseg = 1
         part = torch.empty(splits * g.C * K0, dtype=torch.float32, device=g.t.device)
         s = _stream()
-        _timed('conv_wgrad3_kernel', 'wc_conv_wgrad3', 2.0 * P * g.C * K0, ctypes.byref(a), part.data_ptr(), splits, s)
+        if f3 is not None and segs[0].scale is not None and wgrad3_f16x3_enabled():
+            gb = f3[1]
+            _req(gb.is_cuda and gb.dtype == torch.float32 and gb.numel() >= B, 'f3 bound: float32 [B] on the device')
+            _timed('conv_wgrad3_kernel', 'wc_conv_wgrad3_f16x3', 2.0 * P * g.C * K0, ctypes.byref(a), part.data_ptr(),
+                   splits, int(f3[0]), gb.data_ptr(), s)
+        else:
+            _timed('conv_wgrad3_kernel', 'wc_conv_wgrad3', 2.0 * P * g.C * K0, ctypes.byref(a), part.data_ptr(), splits,
+                   s)
         _native.call('wc_wgrad_reduce', part.data_ptr(), splits, g.C, K0, K0, C0, Cw, dw0.data_ptr(), s0[0], s0[1],
                      s0[2], None, 0, int(accumulate), s)
         if C1:
@@ -1195,23 +1211,36 @@ def attention_bwd6_enabled() -> bool:
     return os.environ.get('WC_ATTN_BWD6', '1') != '0'
 
 
+def attention_bwd_f16x3_enabled() -> bool:
+    """The f16x3 attention backward when the caller supplies the bounds (WC_ATTN_BWD_F16X3=0: bf16x6, A/B)."""
+    return os.environ.get('WC_ATTN_BWD_F16X3', '1') != '0'
+
+
 def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, dqkv: torch.Tensor,
-                  B: int, N: int, C: int, heads: int, precision: str = 'fp32'):
+                  B: int, N: int, C: int, heads: int, precision: str = 'fp32', exps: Optional[Tuple[int, int, int]] = None,
+                  dout_bound: Optional[torch.Tensor] = None):
     """d qkv (same [q | k | v] rows as qkv) of softmax(Q K^T / sqrt(d)) V from the forward's output and lse:
     fp32 MFMA (wc_attention_bwd), or with precision 'bf16x6' / 'f16x3' and a head dim in {32, 64, 128}
-    the bf16x6 split-precision kernels (wc_attention_bwd6; the gradients have no range bound, so
-    f16x3 requests run bf16x6 here)."""
+    the split-precision kernels: f16x3 (wc_attention_bwd_f16x3) when the Q / K / V exponents of the
+    forward (exps) and the per-image max |dout| (dout_bound, device float32 [B]) are given, else
+    bf16x6 (wc_attention_bwd6)."""
     for t_, w in ((qkv, 3 * C), (out, C), (dout, C), (dqkv, 3 * C)):
         _req(t_.is_cuda and t_.dtype == torch.float32 and t_.is_contiguous() and t_.numel() == B * N * w,
              'attention backward operands')
     d = C // heads
     dv = torch.empty(B * heads * N, dtype=torch.float32, device=qkv.device)
-    fn = 'wc_attention_bwd'
+    args = (qkv.data_ptr(), 3 * C, out.data_ptr(), C, dout.data_ptr(), C, lse.data_ptr(), dv.data_ptr(),
+            dqkv.data_ptr(), 3 * C, B, N, C, heads, float(d**-0.5))
     if precision != 'fp32' and d in (32, 64, 128) and attention_bwd6_enabled():
-        fn = 'wc_attention_bwd6'
-    _timed(f'attention_bwd<{d}>', fn, 10.0 * B * N * N * C, qkv.data_ptr(), 3 * C, out.data_ptr(), C,
-           dout.data_ptr(), C, lse.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), 3 * C, B, N, C, heads, float(d**-0.5),
-           _stream())
+        if precision == 'f16x3' and exps is not None and dout_bound is not None and attention_bwd_f16x3_enabled():
+            _req(dout_bound.is_cuda and dout_bound.dtype == torch.float32 and dout_bound.numel() >= B,
+                 'dout_bound: float32 [B] on the device')
+            _timed(f'attention_bwd<{d}>', 'wc_attention_bwd_f16x3', 10.0 * B * N * N * C, *args, int(exps[0]),
+                   int(exps[1]), int(exps[2]), dout_bound.data_ptr(), _stream())
+            return
+        _timed(f'attention_bwd<{d}>', 'wc_attention_bwd6', 10.0 * B * N * N * C, *args, _stream())
+        return
+    _timed(f'attention_bwd<{d}>', 'wc_attention_bwd', 10.0 * B * N * N * C, *args, _stream())
 
 
 def gemm_small(M: int, N: int, K: int, A: torch.Tensor, sa: Tuple[int, int], Bm: torch.Tensor, sb: Tuple[int, int],

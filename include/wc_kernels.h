@@ -440,7 +440,9 @@ int wc_wgrad_reduce(float* part, int splits, int M, int Kc, int K0, int C0, int 
  * finalize: sums[B][C][2] in a fixed order; with coef: coef[B][C][4] = (rstd*gamma, -rstd*A/n,
  *         -rstd*Bs/n, 0), A / Bs the group sums of gamma*sum dy / gamma*sum dy*xhat.
  * bsum: out[c] (+)= sum_b sums[b][c][idx]  (idx 0: dbeta / bias grad, 1: dgamma).
- * apply: dx (+)= coef0*dy + coef1 + coef2*xhat.  C % 4 == 0, 16-byte aligned views. */
+ * apply: dx (+)= coef0*dy + coef1 + coef2*xhat.  C % 4 == 0, 16-byte aligned views.  absmax (optional,
+ *         [B], caller-zeroed or carried over): raised to the max |dx| written per image, so that over
+ *         every writer of a gradient tensor it bounds the tensor (the f16x3 backward's range bound). */
 int wc_gn_bwd_splits(int B, int HW);
 int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
                      const float* gamma, const float* beta, int silu, int B, int HW, int C, int splits,
@@ -450,7 +452,7 @@ int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, 
 int wc_bsum(const float* sums, int B, int C, int idx, float* out, int accumulate, void* stream);
 int wc_gn_bwd_apply(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
                     const float* gamma, const float* beta, int silu, const float* coef, int B, int HW, int C,
-                    float* dx, int lddx, int accumulate, void* stream);
+                    float* dx, int lddx, int accumulate, float* absmax, void* stream);
 
 /* Attention forward that also writes lse[b][h][q] = log2 sum_k exp2(s_qk * scale * log2 e) (fp32
  * MFMA kernel of wc_attention_fwd), and its backward: dqkv (same [q | k | v] column layout as

@@ -364,7 +364,9 @@ def _check(ours, ref, per_tensor=1e-4, overall=1e-5):
 
 
 @pytest.mark.parametrize('precision', ['f16x3', 'bf16x6', 'fp32'])
-def test_unet_grads_tiny_vs_oracle_autograd(precision):
+def test_unet_grads_tiny_vs_oracle_autograd(precision, monkeypatch):
+    # f16x3: every tracked gradient range bound is checked against a fresh absmax of its tensor
+    monkeypatch.setenv('WC_CHECK_GBOUND', '1')
     import json
     import os
     from conftest import GOLDEN
@@ -376,7 +378,8 @@ def test_unet_grads_tiny_vs_oracle_autograd(precision):
     _check(ours, ref)
 
 
-def test_unet_grads_256_baseline_architecture_vs_oracle_autograd():
+def test_unet_grads_256_baseline_architecture_vs_oracle_autograd(monkeypatch):
+    monkeypatch.setenv('WC_CHECK_GBOUND', '1')
     from weatherconverter_amd.diffusion_model.config import model_config
     ours, ref, lo, lr = _model_grads(model_config(256), 2, 'f16x3')
     assert len(ref) == 358

@@ -127,6 +127,25 @@ def test_sharded_sampling_equals_single_rank():
     assert rel_l2(fc[2:], pc) < 1e-6
 
 
+def test_reference_rng_stream_isolated_from_callbacks():
+    """noise='torch_cpu': a progress callback drawing from the global CPU generator leaves the sample
+    unchanged, and the global generator ends where the reference's sequential loop leaves it
+    (x_T + T - 1 full-batch draws)."""
+    from weatherconverter_amd.diffusion_model.sample_ddpm import sample_tensor
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    mc, net = _model('tiny')
+    T = 6
+    s = LinearNoiseScheduler(T, 0.0001, 0.02)
+    a = sample_tensor(net, s, 2, 3, 32, noise='torch_cpu', seed=23)
+    after = torch.randn(3)
+    b = sample_tensor(net, s, 2, 3, 32, noise='torch_cpu', seed=23, progress=lambda i: torch.rand(7))
+    assert torch.equal(a, b)
+    torch.manual_seed(23)
+    for _ in range(T):  # x_T and the T - 1 z draws of the reference loop
+        torch.randn((2, 3, 32, 32))
+    assert torch.equal(torch.randn(3), after)
+
+
 def test_unet_256_batch_above_descriptor_limit_chunks():
     """B=64 at 256 px puts the level-0 skip buffer at 2 GiB (past one buffer descriptor's 32-bit range):
     the engine runs it as chunks of max_batch (63) images; rows equal singleton runs bit for bit."""

@@ -881,6 +881,50 @@ def test_convT4x4s2_one_launch_vs_float64(B, H, W, Ci, Co):
         assert rel_l2(outs['one'][i], outs['parities'][i]) < 1e-5
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('form', ['convT', 's2d'])
+def test_halo_resample_residual_and_absmax(form):
+    """The training data gradients of the down / up convs: the one-launch ConvT and the
+    space-to-depth down conv with the epilogue residual (out = conv + res, the gradient accumulating)
+    and the per-image absmax of the values written, against float64; into a wider buffer whose
+    other channels stay untouched."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(21)
+    B, Ci, Co = 2, 64, 128
+    H, W = (8, 16) if form == 'convT' else (16, 32)
+    x = torch.randn((B, Ci, H, W), generator=g) * torch.tensor([2.0, 1e-2])[:, None, None, None]
+    xin = _nhwc(x).cuda()
+    am = _img_amax(_nhwc(x)).cuda()
+    if form == 'convT':
+        wt = torch.randn((Ci, Co, 4, 4), generator=g) / (4 * Ci)**0.5
+        ref = F.conv_transpose2d(x.double(), wt.double(), None, stride=2, padding=1)
+        Ho, Wo = 2 * H, 2 * W
+    else:
+        w = torch.randn((Co, Ci, 4, 4), generator=g) / (16 * Ci)**0.5
+        ref = F.conv2d(x.double(), w.double(), None, stride=2, padding=1)
+        Ho, Wo = H // 2, W // 2
+    r0 = torch.randn((B, Ho, Wo, 2 * Co), generator=g)
+    buf = r0.clone().cuda()
+    dst = K.View(buf, 0, Co)
+    amx = torch.zeros(B, device='cuda')
+    seg = K.Seg(K.View.full(xin), [(0, 0)]) if form == 'convT' else K.Seg(K.View.full(xin), TAPS4S2, stride=2)
+    if form == 'convT':
+        assert K.convT4x4s2_f16x3_ok(seg, Co)
+        K.convT4x4s2_f16x3(seg, K.pack_f16x3_convT(wt.cuda()), None, dst, a_bound=am, res=dst, absmax=amx)
+    else:
+        assert K.conv4x4s2_f16x3_ok(seg, Co, Ho, Wo)
+        K.conv4x4s2_f16x3(seg, K.pack_f16x3_s2d(_pack(w).cuda(), Ci), None, dst, Hm=Ho, Wm=Wo, a_bound=am, res=dst,
+                          absmax=amx)
+    torch.cuda.synchronize()
+    bc = buf.cpu()
+    assert torch.equal(bc[..., Co:], r0[..., Co:])
+    want = ref + _nchw(r0[..., :Co]).double()
+    got = _nchw(bc[..., :Co]).double()
+    for i in range(B):
+        assert rel_l2(got[i], want[i]) < 1e-5, (i, rel_l2(got[i], want[i]))
+    assert torch.equal(amx.cpu(), bc[..., :Co].abs().amax((1, 2, 3)))
+
+
 # ---------------------------------------------------------------- GroupNorm tile partials (epilogue-fused statistics)
 
 @pytest.mark.gpu

@@ -124,7 +124,7 @@ _SIGS = {
     'wc_gn_bwd_reduce': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P],
     'wc_gn_bwd_finalize': [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     'wc_bsum': [_P, _I, _I, _I, _P, _I, _P],
-    'wc_gn_bwd_apply': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P],
+    'wc_gn_bwd_apply': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P],
     'wc_attention_fwd_lse': [_P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P],
     'wc_attention_bwd': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_gemm_small': [_I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _F, _F, _P],

@@ -18,6 +18,8 @@
 //    same reduction without a normalised input is the per-(b, c) channel sum (bias / temb grads).
 //  * gemm_small / silu / colsum / temb helpers for the time-embedding MLP (B x 128 matrices).
 //  * nchw_to_nhwc: the loss gradient (NCHW, the UNet output layout) into a padded NHWC view.
+#include <algorithm>
+
 #include "wc_x6.hpp"
 
 namespace {
@@ -531,17 +533,15 @@ __global__ __launch_bounds__(256) void bsum_kernel(const float* __restrict__ sum
 
 // dx (+)= coef0*dy + coef1 + coef2*xhat, elementwise over (b, pixel, 4 channels)
 template <bool SILU, bool ACC>
-__global__ __launch_bounds__(256) void gnb_apply_kernel(const float* __restrict__ dz, int ldz, const float* __restrict__ x,
-                                                        int ldx, const float* __restrict__ sc0,
-                                                        const float* __restrict__ sh0, const float* __restrict__ gamma,
-                                                        const float* __restrict__ beta, const float* __restrict__ coef,
-                                                        float* __restrict__ dx, int lddx, long n4, int HW, int C) {
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n4) return;
+WC_DEVICE f32x4 gnb_apply_one(const float* __restrict__ dz, int ldz, const float* __restrict__ x, int ldx,
+                              const float* __restrict__ sc0, const float* __restrict__ sh0,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              const float* __restrict__ coef, float* __restrict__ dx, int lddx, long i, int HW, int C,
+                              int& b) {
     const int C4 = C / 4;
     const long pix = i / C4;
     const int c = (int)(i - pix * C4) * 4;
-    const int b = (int)(pix / HW);
+    b = (int)(pix / HW);
     const long bc = (long)b * C + c;
     f32x4 d = *reinterpret_cast<const f32x4*>(dz + pix * ldz + c);
     const f32x4 xh = *reinterpret_cast<const f32x4*>(x + pix * ldx + c) * *reinterpret_cast<const f32x4*>(sc0 + bc) +
@@ -561,6 +561,68 @@ __global__ __launch_bounds__(256) void gnb_apply_kernel(const float* __restrict_
     f32x4* o = reinterpret_cast<f32x4*>(dx + pix * lddx + c);
     if constexpr (ACC) res += *o;
     *o = res;
+    return res;
+}
+
+template <bool SILU, bool ACC>
+__global__ __launch_bounds__(256) void gnb_apply_kernel(const float* __restrict__ dz, int ldz, const float* __restrict__ x,
+                                                        int ldx, const float* __restrict__ sc0,
+                                                        const float* __restrict__ sh0, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float* __restrict__ coef,
+                                                        float* __restrict__ dx, int lddx, long n4, int HW, int C) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    int b;
+    gnb_apply_one<SILU, ACC>(dz, ldz, x, ldx, sc0, sh0, gamma, beta, coef, dx, lddx, i, HW, C, b);
+}
+
+// The same, also raising absmax[b] to the max |dx| WRITTEN per image (after the accumulate: the
+// final value of every element it writes, so absmax over all writers of a tensor bounds the tensor).
+// Workgroup k walks the float4 range [k per, (k + 1) per) (per a multiple of 1024), four elements in
+// flight per thread; the maxima go out once per workgroup when the range lies in one image (the usual
+// case: all B slots share one L2 line, so the atomics are kept few), per wave or per lane otherwise.
+template <bool SILU, bool ACC>
+__global__ __launch_bounds__(256) void gnb_apply_absmax_kernel(
+    const float* __restrict__ dz, int ldz, const float* __restrict__ x, int ldx, const float* __restrict__ sc0,
+    const float* __restrict__ sh0, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ coef, float* __restrict__ dx, int lddx, long n4, int HW, int C, long per,
+    float* __restrict__ absmax) {
+    __shared__ float wm[4];
+    const long i0 = (long)blockIdx.x * per;
+    const long i1 = min(n4, i0 + per);
+    const long per_img = (long)HW * (C / 4);
+    const int bfirst = (int)(i0 / per_img), blast = (int)((i1 - 1) / per_img);
+    float m = 0.f;
+    int bc = bfirst;
+    for (long base = i0 + threadIdx.x; base < i1; base += 1024) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long i = base + 256 * u;
+            if (i < i1) {
+                int b;
+                const f32x4 r =
+                    gnb_apply_one<SILU, ACC>(dz, ldz, x, ldx, sc0, sh0, gamma, beta, coef, dx, lddx, i, HW, C, b);
+                const float v = fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w)));
+                if (bfirst != blast && b != bc) {  // a range crossing images: flush the lane's maximum
+                    atomicMax(reinterpret_cast<unsigned*>(absmax) + bc, __float_as_uint(m));
+                    bc = b;
+                    m = 0.f;
+                }
+                m = fmaxf(m, v);
+            }
+        }
+    }
+    if (bfirst == blast) {  // one image: one atomic for the workgroup
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<unsigned*>(absmax) + bfirst,
+                      __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+    } else {
+        atomicMax(reinterpret_cast<unsigned*>(absmax) + bc, __float_as_uint(m));
+    }
 }
 
 // ============================================================================================
@@ -800,13 +862,29 @@ extern "C" int wc_bsum(const float* sums, int B, int C, int idx, float* out, int
 
 extern "C" int wc_gn_bwd_apply(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
                                const float* gamma, const float* beta, int silu, const float* coef, int B, int HW, int C,
-                               float* dx, int lddx, int accumulate, void* stream) {
+                               float* dx, int lddx, int accumulate, float* absmax, void* stream) {
     if (!dz || !x || !sc0 || !sh0 || !coef || !dx) return WC_E_ARG;
     if (C % 4 || ldz % 4 || ldx % 4 || lddx % 4) return WC_E_SHAPE;
     if (((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx)) & 15) != 0)
         return WC_E_SHAPE;
     const long n4 = (long)B * HW * (C / 4);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (absmax) {
+        const long nb = std::min<long>(blocks_for(n4, 1024), 2048);
+        const long per = ((n4 + nb - 1) / nb + 1023) / 1024 * 1024;
+        const dim3 g((unsigned)((n4 + per - 1) / per));
+#define WC_GNB_APPLY(S, A)                                                                                       \
+    hipLaunchKernelGGL((gnb_apply_absmax_kernel<S, A>), g, dim3(256), 0, s, dz, ldz, x, ldx, sc0, sh0, gamma, beta, \
+                       coef, dx, lddx, n4, HW, C, per, absmax)
+        if (silu) {
+            if (accumulate) WC_GNB_APPLY(true, true); else WC_GNB_APPLY(true, false);
+        } else {
+            if (accumulate) WC_GNB_APPLY(false, true); else WC_GNB_APPLY(false, false);
+        }
+#undef WC_GNB_APPLY
+        WC_CHECK_LAUNCH();
+        return WC_OK;
+    }
     const dim3 g(blocks_for(n4, 256));
 #define WC_GNB_APPLY(S, A) \
     hipLaunchKernelGGL((gnb_apply_kernel<S, A>), g, dim3(256), 0, s, dz, ldz, x, ldx, sc0, sh0, gamma, beta, coef, dx, lddx, n4, HW, C)

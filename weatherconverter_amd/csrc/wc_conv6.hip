@@ -1097,10 +1097,12 @@ extern "C" int wc_conv4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64_t
     if (a->B <= 0 || a->Hm % 8 || a->Wm % 16 || s0.H != 2 * a->Hm || s0.W != 2 * a->Wm) return WC_E_SHAPE;
     if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
     if (reinterpret_cast<uintptr_t>(w3) & 15) return WC_E_SHAPE;
-    if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox || a->res)
+    if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox)
         return WC_E_SHAPE;
-    if ((long)a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;
+    if ((long)a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;  // per image: offsets from its base
+    if (a->res && ((long)a->Hm * a->Wm * a->ldres * 4 >= (1L << 31) || a->ldres % 4)) return WC_E_SHAPE;
     X6Dev d{};
+    d.res = a->res; d.ldres = a->ldres;  // epilogue: out = conv + res (the training data gradient accumulates)
     d.src0 = s0.src; d.C0 = 4 * s0.C; d.ldc0 = s0.ldc;
     d.nck0 = 4 * s0.C / 16;
     d.s2d_cpp = s0.C / 16; d.Hi = s0.H; d.Wi = s0.W;
@@ -1141,10 +1143,12 @@ extern "C" int wc_convtr4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64
     if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
     if (reinterpret_cast<uintptr_t>(w3) & 15) return WC_E_SHAPE;
     if (a->out_nchw || a->Ho != 2 * a->Hm || a->Wo != 2 * a->Wm || a->osy != 2 || a->osx != 2 || a->ooy || a->oox ||
-        a->res || a->temb)
+        a->temb)
         return WC_E_SHAPE;
-    if (4L * a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;
+    if (4L * a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;  // per image: offsets from its base
+    if (a->res && (4L * a->Hm * a->Wm * a->ldres * 4 >= (1L << 31) || a->ldres % 4)) return WC_E_SHAPE;
     X6Dev d{};
+    d.res = a->res; d.ldres = a->ldres;  // epilogue: out = conv + res, at the parity's output pixel
     d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.nck0 = s0.C / 16;
     d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
     d.w6 = w3; d.bias = a->bias;

@@ -9,21 +9,26 @@ pre-residual input, q/k/v, its output and the softmax log-sum-exp.
 
 Backward, per layer type (reference modules of unet_base.py):
   Conv2d 3x3 / 1x1 / 4x4-s2, ConvTranspose2d 4x4-s2, in/out projections
-      data gradient   the forward implicit-GEMM kernels on re-packed weights: a 3x3 conv's is the
-                      3x3 conv of dY with W flipped and transposed; a 4x4/s2 conv's is the
-                      transposed conv of dY (four parity sub-convs); a transposed conv's is the
-                      4x4/s2 conv of dY with its own weight; a linear layer's is dY W.
-      weight gradient wc_conv_wgrad (fp32-MFMA GEMM over the pixels, input re-read through the
-                      forward's taps and GN prologue), scattered into the parameter's layout.
+      data gradient   the forward kernels on re-packed weights: a 3x3 conv's is the 3x3 conv of dY
+                      with W flipped and transposed (halo kernel); a 4x4/s2 conv's is the transposed
+                      conv of dY (four parity sub-convs); a transposed conv's is the 4x4/s2 conv of
+                      dY with its own weight; a linear layer's is dY W.
+      weight gradient wc_conv_wgrad3 (3x3: halo-tiled) or wc_conv_wgrad (GEMM over the pixels), the
+                      input re-read through the forward's taps and GN prologue; split partials
+                      reduced in a fixed order and scattered into the parameter's layout.
       bias            per-(b, c) pixel sums, summed over b in a fixed order.
   GroupNorm(+SiLU)    wc_gn_bwd_* (dx, dgamma, dbeta).
-  attention core      wc_attention_bwd (dq, dk, dv from lse; no N x N matrix).
+  attention core      wc_attention_bwd_f16x3 / _bwd6 / _bwd (dq, dk, dv from lse; no N x N matrix).
   time embedding MLP  small GEMM / SiLU kernels (B x 128).
-Arithmetic: the forward and data-gradient convs on bf16x6 (exact 3-piece bf16 split, fp32
-accumulation) where channels allow (else fp32 MFMA), weight gradients and attention on fp32 MFMA:
-fp32-class gradients, checked against PyTorch autograd of the reference restatement.
-Every gradient buffer is written in a fixed order: results are deterministic run to run.
+Arithmetic (precision f16x3, the default): forward convs, projections and attention on f16x3 under
+the sampler's static bounds; 3x3 and projection data gradients, the 3x3 weight gradients and the
+attention backward on f16x3 under per-image range bounds of the gradients, which every kernel
+writing a gradient tensor raises as it writes (_gb); the rest on bf16x6 (exact 3-piece bf16 split).
+Precision bf16x6 / fp32: bf16x6 / fp32 MFMA throughout.  fp32-class gradients, checked against
+PyTorch autograd of the reference restatement in float64.  Every gradient buffer is written in a
+fixed order: results are deterministic run to run.
 """
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -105,6 +110,8 @@ class TrainEngine:
 
     def _conv(self, segs, pk, bias, out: Optional[View], H: int, W: int, **kw):
         w, x6 = pk
+        if kw.get('absmax', 0) is None:  # no bound tracked (outside the f16x3 backward)
+            del kw['absmax']
         if x6 is not None:
             K.conv_igemm_x6(segs, x6, bias, out, Hm=H, Wm=W, **kw)
         else:
@@ -208,8 +215,15 @@ class TrainEngine:
                     w = blk.down_sample_conv.weight.detach()
                     ci = w.shape[1]
                     parts = [pack_convT(w, py, px) for py, px in _PARITIES]  # dgrad: ConvT of dY (in = Co)
-                    self.down_pk.append(dict(mod=blk.down_sample_conv, pk=self._pk(pack_conv(w), ci, 16),
-                                             dT=[(taps, self._pk(wp, w.shape[0], len(taps))) for taps, wp in parts]))
+                    L = _Pack.lazy
+                    f3 = self.f3 and ci % 16 == 0 and w.shape[0] % 16 == 0 and K.x6_tile(w.shape[0])[1] == 128
+                    self.down_pk.append(_Pack(
+                        mod=blk.down_sample_conv, pk=L(lambda w=w, ci=ci: self._pk(pack_conv(w), ci, 16)),
+                        dT=L(lambda parts=parts, w=w: [(taps, self._pk(wp, w.shape[0], len(taps))) for taps, wp in parts]),
+                        # f16x3 halo forms: the forward on the space-to-depth kernel, the data gradient (the
+                        # ConvT of dY with the same weight) on the one-launch ConvT kernel
+                        f3=L(lambda w=w, ci=ci: K.pack_f16x3_s2d(pack_conv(w).float(), ci)) if f3 else None,
+                        f3T=L(lambda w=w: K.pack_f16x3_convT(w.float())) if self.f3d and f3 else None))
                 else:
                     self.down_pk.append(None)
             self.up_pk = []
@@ -218,9 +232,16 @@ class TrainEngine:
                     wt = blk.up_sample_conv.weight.detach()  # [Cin][Cout][4][4]
                     ci = wt.shape[0]
                     parts = [pack_convT(wt, py, px) for py, px in _PARITIES]
-                    self.up_pk.append(dict(mod=blk.up_sample_conv,
-                                           fw=[(taps, self._pk(wp, ci, len(taps))) for taps, wp in parts],
-                                           dT=self._pk(pack_conv(wt), wt.shape[1], 16)))
+                    L = _Pack.lazy
+                    co = wt.shape[1]
+                    f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
+                    self.up_pk.append(_Pack(
+                        mod=blk.up_sample_conv, fw=L(lambda parts=parts, ci=ci: [(taps, self._pk(wp, ci, len(taps)))
+                                                                                 for taps, wp in parts]),
+                        dT=L(lambda wt=wt, co=co: self._pk(pack_conv(wt), co, 16)),
+                        f3=L(lambda wt=wt: K.pack_f16x3_convT(wt.float())) if f3 else None,
+                        f3T=L(lambda wt=wt, co=co: K.pack_f16x3_s2d(pack_conv(wt).float(), co))
+                        if self.f3d and f3 and K.x6_tile(ci)[1] == 128 else None))
                 else:
                     self.up_pk.append(None)
             tp = m.t_proj
@@ -256,6 +277,30 @@ class TrainEngine:
         g = self._grad(v)
         self.gmap[id(t)] = (g.t, g.c0)
         self.keep.append(t)
+
+    def _gb(self, v: View) -> Optional[torch.Tensor]:
+        """The range bound of v's gradient tensor for the f16x3 backward: float32[B], raised by EVERY
+        kernel that writes into that tensor to the max |value| it wrote per image (so it bounds the
+        final values), zero while nothing has; None outside the f16x3 backward."""
+        if not self.f3d:
+            return None
+        g = self._grad(v)
+        t = self.gbnd.get(id(g.t))
+        if t is None:
+            t = torch.zeros((v.B, ), dtype=torch.float32, device=self.device)
+            self.gbnd[id(g.t)] = t
+        return t
+
+    def _bound(self, v: View, tracked: Optional[torch.Tensor]) -> torch.Tensor:
+        """The per-image bound a consumer uses: the writers' tracked bound (WC_CHECK_GBOUND=1: checked
+        against a fresh absmax of the view, which it must not be below)."""
+        if tracked is None:
+            return K.absmax_images(v)
+        if os.environ.get('WC_CHECK_GBOUND', '0') == '1':
+            real = K.absmax_images(v)
+            if bool((real > tracked).any()):
+                raise RuntimeError(f'gradient range bound below the values: {tracked.tolist()} < {real.tolist()}')
+        return tracked
 
     def _pgrad(self, p: torch.nn.Parameter) -> torch.Tensor:
         g = self.pgrads.get(id(p))
@@ -312,8 +357,13 @@ class TrainEngine:
                 cur = block(cur, tgt, rp, att[li] if att else None)
             if self.down_pk[i] is not None:
                 dp = self.down_pk[i]
-                self._conv([Seg(cur, TAPS4S2, stride=2)], dp['pk'], dp['mod'].bias.detach().float().contiguous(), final,
-                           sizes[i + 1][0], sizes[i + 1][1])
+                seg = Seg(cur, TAPS4S2, stride=2)
+                bd = dp['mod'].bias.detach().float().contiguous()
+                Hm, Wm = sizes[i + 1]
+                if dp['f3'] is not None and K.conv4x4s2_f16x3_ok(seg, final.C, Hm, Wm):
+                    K.conv4x4s2_f16x3(seg, dp['f3'], bd, final, Hm=Hm, Wm=Wm, a_bound=K.absmax_images(cur))
+                else:
+                    self._conv([seg], dp['pk'], bd, final, Hm, Wm)
                 self.tape.append(('down', cur, final, dp))
                 cur = final
 
@@ -339,8 +389,11 @@ class TrainEngine:
                 up = self.up_pk[k]
                 dst = View(U[i], 0, dc[i])
                 b = up['mod'].bias.detach().float().contiguous()
-                for (py, px), (taps, pk) in zip(_PARITIES, up['fw']):
-                    self._conv([Seg(cur, taps)], pk, b, dst, cur.H, cur.W, out_map=(2, 2, py, px))
+                if up['f3'] is not None and K.convT4x4s2_f16x3_ok(Seg(cur, [(0, 0)]), dst.C):
+                    K.convT4x4s2_f16x3(Seg(cur, [(0, 0)]), up['f3'], b, dst, a_bound=K.absmax_images(cur))
+                else:
+                    for (py, px), (taps, pk) in zip(_PARITIES, up['fw']):
+                        self._conv([Seg(cur, taps)], pk, b, dst, cur.H, cur.W, out_map=(2, 2, py, px))
                 self.tape.append(('up', cur, dst, up))
             else:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
@@ -433,6 +486,7 @@ class TrainEngine:
             self.last_tape = None
         m = self.model
         self.gmap: Dict[int, Tuple[torch.Tensor, int]] = {}
+        self.gbnd: Dict[int, torch.Tensor] = {}
         self.pgrads: Dict[int, torch.Tensor] = {}
         self.keep = []
         B = gout.shape[0]
@@ -443,6 +497,7 @@ class TrainEngine:
         del records
         self._temb_bwd()
         self.gmap = {}
+        self.gbnd = {}
         self.keep = []
         for f in Tape._FIELDS[1:]:  # the tape's tensors die with it, not with the engine
             setattr(self, f, None)
@@ -482,7 +537,7 @@ class TrainEngine:
         self._conv([Seg(View.full(g32), TAPS3)], self.head_T, None, dz, S, S2)
         gn = m.norm_out
         K.gn_backward(dz, cur, a0, o0, gn.weight.detach().float(), gn.bias.detach().float(), True, self._grad(cur),
-                      dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias))
+                      dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), absmax=self._gb(cur))
 
     def _bwd_res(self, rec, gout):
         _, X, h, Y, rp, st1, st2 = rec
@@ -493,7 +548,8 @@ class TrainEngine:
         self._bias_grad(gY, rp['conv2'].bias, rp['resc'].bias)
         # per-image max |gY|: the range bound of the f16x3 data gradients and weight gradient
         f3Y = rp['f3_2T'] is not None and self._dgrad3_ok(gY, co)
-        bY = K.absmax_images(gY) if f3Y else None
+        bY = self._bound(gY, self._gb(Y)) if f3Y else None
+        bX = self._gb(X)
         self._wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
                     self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci,
                     f3=(K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), bY) if f3Y else None)
@@ -501,20 +557,22 @@ class TrainEngine:
         if f3Y:
             K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
             if (H * W) % (256 if ci <= 64 else 128) == 0 and co % 16 == 0:  # one-image M tiles (per-image bound)
-                K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=gX)
+                K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=gX,
+                                   absmax=bX)
             else:
-                self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX)
+                self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX, absmax=bX)
         else:
             self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
-            self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX)
+            self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX, absmax=bX)
         g2 = rp['gn2']
         dh = View.full(self._new(B, H, W, co))
+        bdh = torch.zeros((B, ), dtype=torch.float32, device=self.device) if self.f3d else None
         K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
-                      dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False)
+                      dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh)
         sums = self._bias_grad(dh, rp['conv1'].bias)
         self.dproj[:, rp['off']:rp['off'] + co].copy_(sums[:, :, 0])
         f3h = rp['f3_1T'] is not None and self._dgrad3_ok(dh, ci)
-        bh = K.absmax_images(dh) if f3h else None
+        bh = self._bound(dh, bdh) if f3h else None
         self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
                     (ci * 9, 9, 1), f3=(K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8), bh) if f3h else None)
         dz1 = View.full(self._new(B, H, W, ci))
@@ -524,7 +582,7 @@ class TrainEngine:
             self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
         g1 = rp['gn1']
         K.gn_backward(dz1, X, st1[2], st1[3], g1.weight.detach().float(), g1.bias.detach().float(), True, gX,
-                      dgamma=self._pgrad(g1.weight), dbeta=self._pgrad(g1.bias), accumulate=True)
+                      dgamma=self._pgrad(g1.weight), dbeta=self._pgrad(g1.bias), accumulate=True, absmax=bX)
 
     def _bwd_attn(self, rec, gout):
         _, Ypre, Yout, qkv, o, lse, st, ap = rec
@@ -535,18 +593,20 @@ class TrainEngine:
         self._bias_grad(gY, mha.out_proj.bias)
         self._wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0))
         do = self._new(B, H, W, C)
+        bdo = torch.zeros((B, ), dtype=torch.float32, device=self.device) if self.f3d else None
         f3p = 'f3_outT' in ap and (H * W) % (256 if C <= 64 else 128) == 0
         if f3p:
             K.conv_igemm_f16x3([Seg(gY, TAPS1)], ap['f3_outT'], None, View.full(do), Hm=H, Wm=W, a_exp=60,
-                               a_bound=K.absmax_images(gY))
+                               a_bound=self._bound(gY, self._gb(Yout)), absmax=bdo)
         else:
-            self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W)
+            self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W, absmax=bdo)
         dqkv = self._new(B, H, W, 3 * C)
         if self.f3d and ap['f3_in'] is not None:
             # f16x3 under the forward's Q / K / V exponents and the per-image max |dO|
             exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], N * C // 8)
             K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
-                            B, N, C, ap['heads'], precision='f16x3', exps=exps, dout_bound=K.absmax_images(View.full(do)))
+                            B, N, C, ap['heads'], precision='f16x3', exps=exps,
+                            dout_bound=self._bound(View.full(do), bdo))
         else:
             K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
                             B, N, C, ap['heads'], precision=self.precision)
@@ -563,7 +623,8 @@ class TrainEngine:
         # Yout = Ypre + out_proj(...): Ypre's gradient is Yout's plus the GroupNorm path
         self._alias_grad(Ypre.t, Yout)
         K.gn_backward(da, Ypre, st[2], st[3], gn.weight.detach().float(), gn.bias.detach().float(), False,
-                      self._grad(Ypre), dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), accumulate=True)
+                      self._grad(Ypre), dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), accumulate=True,
+                      absmax=self._gb(Ypre))
 
     def _bwd_down(self, rec, gout):
         _, cur, final, dp = rec
@@ -572,8 +633,13 @@ class TrainEngine:
         w = dp['mod'].weight
         self._bias_grad(gF, dp['mod'].bias)
         self._wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1))
+        if dp['f3T'] is not None and K.convT4x4s2_f16x3_ok(Seg(gF, [(0, 0)]), gc.C) and gF.ptr % 16 == 0:
+            # the ConvT of dY (same weight) in one launch on f16x3 under dY's tracked bound
+            K.convT4x4s2_f16x3(Seg(gF, [(0, 0)]), dp['f3T'], None, gc, a_bound=self._bound(gF, self._gb(final)),
+                               res=gc, absmax=self._gb(cur))
+            return
         for (py, px), (taps, pk) in zip(_PARITIES, dp['dT']):
-            self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=gc)
+            self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=gc, absmax=self._gb(cur))
 
     def _bwd_up(self, rec, gout):
         _, cur, dst, up = rec
@@ -584,7 +650,13 @@ class TrainEngine:
         # dW[ci][co][ky][kx] = sum_pixels x[ci] * dY[co] at (2y - 1 + ky, 2x - 1 + kx): the 4x4/s2 tap
         # grid over dY with x in the gradient role
         self._wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1))
-        self._conv([Seg(gD, TAPS4S2, stride=2)], up['dT'], None, gc, cur.H, cur.W, res=gc)
+        seg = Seg(gD, TAPS4S2, stride=2)
+        if up['f3T'] is not None and K.conv4x4s2_f16x3_ok(seg, gc.C, cur.H, cur.W) and gD.ptr % 16 == 0:
+            # the 4x4/s2 conv of dY on the space-to-depth halo kernel, f16x3 under dY's tracked bound
+            K.conv4x4s2_f16x3(seg, up['f3T'], None, gc, Hm=cur.H, Wm=cur.W, a_bound=self._bound(gD, self._gb(dst)),
+                              res=gc, absmax=self._gb(cur))
+            return
+        self._conv([seg], up['dT'], None, gc, cur.H, cur.W, res=gc, absmax=self._gb(cur))
 
     def _bwd_conv_in(self, rec, gout):
         m = self.model

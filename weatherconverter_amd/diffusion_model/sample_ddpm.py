@@ -158,15 +158,19 @@ def sample_tensor(model: Unet, scheduler: LinearNoiseScheduler, batch: int, im_c
     runner = _GraphStep(model, xt) if graph else None
     nxt = torch.empty_like(xt)
     # reference-RNG mode: the per-step z draws (the full-batch CPU tensor, in the reference's order)
-    # run one step ahead on a worker thread while the GPU computes the UNet; nothing else draws from
-    # the CPU generator meanwhile, so the stream is exactly the sequential one
-    pool = fut = None
+    # run one step ahead on a worker thread while the GPU computes the UNet.  They come from a private
+    # generator that continues the global CPU generator's state, and the global state is set to the
+    # private one's at the end: the stream is exactly the reference's sequential one, and a callback
+    # (progress / progress_x) drawing from the global generator meanwhile cannot interleave with it.
+    pool = fut = gen = None
     if noise == 'torch_cpu' and T > 1:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(1)
+        gen = torch.Generator()
+        gen.set_state(torch.get_rng_state())
 
         def cpu_draw():
-            return torch.randn(full_shape)[sample0:sample0 + batch].contiguous()
+            return torch.randn(full_shape, generator=gen)[sample0:sample0 + batch].contiguous()
 
         fut = pool.submit(cpu_draw)
     try:
@@ -189,6 +193,8 @@ def sample_tensor(model: Unet, scheduler: LinearNoiseScheduler, batch: int, im_c
     finally:
         if pool is not None:
             pool.shutdown(wait=True)
+        if gen is not None:
+            torch.set_rng_state(gen.get_state())
     return xt
 
 

@@ -546,14 +546,15 @@ def convT4x4s2_f16x3_ok(seg: Seg, N: int) -> bool:
 
 
 def convT4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, a_bound: torch.Tensor,
-                     gn: Optional[GnPart] = None):
+                     gn: Optional[GnPart] = None, res: Optional[View] = None, absmax: Optional[torch.Tensor] = None):
     """Up-sampling 4x4 / stride-2 / pad-1 transposed conv of a raw input on f16x3 in one launch
-    (wc_convtr4x4s2_f16x3); out is the 2H x 2W view; a_bound = per-image max |x|."""
+    (wc_convtr4x4s2_f16x3); out is the 2H x 2W view (+ res, same grid); a_bound = per-image max |x|;
+    absmax: optional float32[B] raised to the max |out| written per image."""
     _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3t', 'f16x3 ConvT weight')
     v = seg.view
     _req(w3.C0 == v.C and out.H == 2 * v.H and out.W == 2 * v.W, 'ConvT shapes')
     _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == v.B, 'A bound')
-    a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, None, (2, 2, 0, 0), None, 0, None, gn=gn)
+    a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, res, (2, 2, 0, 0), None, 0, absmax, gn=gn)
     TH, BN = x6_tile(w3.N)
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, 0, false, true, false, false, 2> (ConvT 4x4/s2)', 'wc_convtr4x4s2_f16x3',
            2.0 * v.B * v.H * v.W * w3.N * 16 * v.C if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
@@ -569,13 +570,15 @@ def conv4x4s2_f16x3_ok(seg: Seg, N: int, Hm: int, Wm: int) -> bool:
 
 
 def conv4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
-                    a_bound: torch.Tensor, absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None):
+                    a_bound: torch.Tensor, absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None,
+                    res: Optional[View] = None):
     """Down-sampling 4x4 / stride-2 / pad-1 conv of a raw input on f16x3 (wc_conv4x4s2_f16x3): the
-    halo-tiled kernel over the space-to-depth view; a_bound = per-image max |x| (the producer's absmax)."""
+    halo-tiled kernel over the space-to-depth view; a_bound = per-image max |x| (the producer's absmax);
+    res: optional view added in the epilogue."""
     _req(w3.data.is_cuda and w3.data.is_contiguous() and w3.order == 'f16x3s', 'f16x3 s2d weight')
     _req(w3.C0 == 4 * seg.view.C and w3.C1 == 0, 'f16x3 s2d weight channels')
     _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == seg.view.B, 'A bound')
-    a = _conv_args([seg], w3.N, bias, out, Hm, Wm, None, 0, None, (1, 1, 0, 0), None, 0, absmax, gn=gn)
+    a = _conv_args([seg], w3.N, bias, out, Hm, Wm, None, 0, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     _timed('conv3x3_x6_kernel<8, 128, 0, false, true, false, false, true> (s2d 4x4/s2)', 'wc_conv4x4s2_f16x3',
            _flops([seg], Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream(), nbytes=_abytes([seg], w3.N, Hm * Wm))
@@ -1154,9 +1157,10 @@ def bsum(sums: torch.Tensor, idx: int, out: torch.Tensor, accumulate: bool = Fal
 
 def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
                 silu: bool, dx: View, *, dgamma: Optional[torch.Tensor] = None, dbeta: Optional[torch.Tensor] = None,
-                accumulate: bool = True, groups: int = 8):
+                accumulate: bool = True, groups: int = 8, absmax: Optional[torch.Tensor] = None):
     """Backward of SiLU(GroupNorm(x)) (silu) or GroupNorm(x): dx (+)= d/dx given dz = d/d output;
-    dgamma / dbeta (+)= their gradients."""
+    dgamma / dbeta (+)= their gradients.  absmax: optional float32[B] raised to the max |dx| written
+    per image."""
     for v in (dz, x, dx):
         v.check()
     B, HW, C = x.B, x.H * x.W, x.C
@@ -1178,7 +1182,7 @@ def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: 
         bsum(sums, 1, dgamma, accumulate=True)
     _timed('gnb_apply_kernel', 'wc_gn_bwd_apply', 16.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc, sc0.data_ptr(),
            sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), coef.data_ptr(), B, HW, C, dx.ptr, dx.ldc,
-           int(accumulate), s)
+           int(accumulate), _ptr(absmax), s)
 
 
 def attention_fwd_lse(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, B: int, N: int, C: int, heads: int,

@@ -393,6 +393,12 @@ int wc_conv_wgrad(const wc_wgrad_args* args, float* part, int splits, void* stre
  * bf16 pieces, the 6 piece products with i + j <= 2; fragments read pixel-contiguous from
  * [pixel][channel] LDS rows with gfx950's transposing ds_read_b64_tr_b16).  Same arguments. */
 int wc_conv_wgrad_x6(const wc_wgrad_args* args, float* part, int splits, void* stream);
+/* The same weight gradient on f16x3 (two fp16 pieces per operand, products h*h + h*l + l*h):
+ * gbound[B] = per-image max |g|; segment 0 scaled by 2^min(x_exp0, 13 - floor(log2 max xbound0)) (xbound0
+ * may be NULL: the static exponent x_exp0 of a GroupNorm-bounded operand, |x| 2^x_exp0 <= 2^14);
+ * segment 1 (if any) by its per-image bound xbound1[B].  Device arrays; same partials and reduce. */
+int wc_conv_wgrad_f16x3(const wc_wgrad_args* args, float* part, int splits, const float* gbound, int x_exp0,
+                        const float* xbound0, const float* xbound1, void* stream);
 /* The split count wc_conv_wgrad accepts for (M, Kc, P = B*Hm*Wm) aiming at ~target_blocks workgroups. */
 int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks);
 /* Halo-tiled weight gradient of a 3x3 stride-1 pad-1 conv on bf16x6 (the ResBlock convs' backward,

@@ -118,13 +118,63 @@ def test_conv_wgrad3_f16x3_vs_float64(pro, M, C0, B, H, W):
     dw = torch.zeros((M, C0, 3, 3), device='cuda')
     seg = Seg(View.full(x.cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=pro == 2)
     prof = K.profile_conv(True)
-    K.conv_wgrad(View.full(dyc), [seg], dw, (C0 * 9, 9, 1), x6=True, f3=(x_exp, gb))
+    K.conv_wgrad(View.full(dyc), [seg], dw, (C0 * 9, 9, 1), x6=True, f3=K.F3Bounds(gb, x_exp))
     torch.cuda.synchronize()
     K.profile_conv(False)
     assert any(n.startswith('conv_wgrad3_kernel') and n.endswith('true>') for n, *_ in prof), [n for n, *_ in prof]
     w = torch.zeros((M, C0, 3, 3), dtype=torch.float64, requires_grad=True)
     y = F.conv2d(a.permute(0, 3, 1, 2), w, padding=1)
     y.backward(dy.double().permute(0, 3, 1, 2))
+    assert rel_l2(dw.cpu(), w.grad) < 1e-5
+
+
+@pytest.mark.parametrize('form', ['3x3_gn_res', '4x4s2_raw', '1x1_raw'])
+def test_conv_wgrad_generic_f16x3_vs_float64(form):
+    """The generic weight-gradient GEMM on f16x3 (wc_conv_wgrad_f16x3): a GroupNorm+SiLU 3x3 segment at
+    its static exponent with a raw 1x1 residual segment under its per-image bound (a grid the halo
+    kernel does not take), a raw 4x4/s2 conv and a raw 1x1 under per-image bounds; gradients whose
+    images differ by 10^3 in scale; against float64 at rel-L2 <= 1e-5."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import Seg, View
+    from weatherconverter_amd.diffusion_model.models.engine import TAPS1, TAPS3, TAPS4S2
+    g = _gen(8)
+    B, C0, C1, M = 2, 64, 32, 128
+    H, W = (12, 20) if form != '4x4s2_raw' else (16, 32)
+    Hm, Wm = (H // 2, W // 2) if form == '4x4s2_raw' else (H, W)
+    x = torch.randn((B, H, W, C0), generator=g) * torch.tensor([1.0, 30.0])[:, None, None, None]
+    xr = torch.randn((B, H, W, C1), generator=g)
+    dy = torch.randn((B, Hm, Wm, M), generator=g)
+    dy[1] *= 1e-3
+    gb = dy.abs().amax((1, 2, 3)).cuda()
+    dwr = torch.zeros((M, C1), device='cuda')
+    if form == '3x3_gn_res':
+        sc = torch.rand((B, C0), generator=g) + 0.5
+        sh = torch.randn((B, C0), generator=g) * 0.3
+        a = F.silu(x.double() * sc.double()[:, None, None, :] + sh.double()[:, None, None, :])
+        x_exp = 13 - int(np.floor(np.log2(float(a.abs().max()))))
+        segs = [Seg(View.full(x.cuda()), TAPS3, scale=sc.cuda(), shift=sh.cuda(), silu=True),
+                Seg(View.full(xr.cuda()), TAPS1, kbase=9 * C0)]
+        assert not K.wgrad3_ok(View.full(dy.cuda()), segs[0])
+        f3 = K.F3Bounds(gb, x_exp, None, xr.abs().amax((1, 2, 3)).cuda())
+        dw = torch.zeros((M, C0, 3, 3), device='cuda')
+        K.conv_wgrad(View.full(dy.cuda()), segs, dw, (C0 * 9, 9, 1), dw1=dwr, s1=C1, x6=True, f3=f3)
+        w = torch.zeros((M, C0, 3, 3), dtype=torch.float64, requires_grad=True)
+        F.conv2d(a.permute(0, 3, 1, 2), w, padding=1).backward(dy.double().permute(0, 3, 1, 2))
+        ref = torch.einsum('bhwm,bhwc->mc', dy.double(), xr.double())
+        assert rel_l2(dwr.cpu(), ref) < 1e-5
+    elif form == '4x4s2_raw':
+        f3 = K.F3Bounds(gb, 60, x.abs().amax((1, 2, 3)).cuda())
+        dw = torch.zeros((M, C0, 4, 4), device='cuda')
+        K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS4S2, stride=2)], dw, (C0 * 16, 16, 1),
+                     x6=True, f3=f3)
+        w = torch.zeros((M, C0, 4, 4), dtype=torch.float64, requires_grad=True)
+        F.conv2d(x.double().permute(0, 3, 1, 2), w, stride=2, padding=1).backward(dy.double().permute(0, 3, 1, 2))
+    else:
+        f3 = K.F3Bounds(gb, 60, x.abs().amax((1, 2, 3)).cuda())
+        dw = torch.zeros((M, C0), device='cuda')
+        K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS1)], dw, (C0, 1, 0), x6=True, f3=f3)
+        w = torch.zeros((M, C0), dtype=torch.float64, requires_grad=True)
+        (torch.einsum('bhwc,mc->bhwm', x.double(), w) * dy.double()).sum().backward()
     assert rel_l2(dw.cpu(), w.grad) < 1e-5
 
 

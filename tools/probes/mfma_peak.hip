@@ -79,7 +79,7 @@ int run(const u32x4* ops, float* out, int grid, int wps, const char* name, doubl
     const int iters = (MODE == 2 ? 20000 : MODE == 3 ? 200000 : 100000) * 8 / wps;  // ~0.1 s per launch
     hipLaunchKernelGGL(mfma_stream<MODE>, dim3(grid), dim3(256), 0, 0, ops, out, iters / 10);  // warm-up
     CK(hipDeviceSynchronize());
-    for (int rep = 0; rep < 5; ++rep) {
+    for (int rep = 0; rep < 3; ++rep) {
         CK(hipEventRecord(e0));
         hipLaunchKernelGGL(mfma_stream<MODE>, dim3(grid), dim3(256), 0, 0, ops, out, iters);
         CK(hipEventRecord(e1));
@@ -111,9 +111,11 @@ int main() {
     CK(hipMalloc(&ops, h.size() * 4));
     CK(hipMalloc(&out, (size_t)grid8 * 256 * 4));
     CK(hipMemcpy(ops, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    for (int wps : {8, 1}) {  // waves per SIMD: 8, or one (grid = one 4-wave workgroup per CU)
+    const char* only = getenv("MFMA_PEAK_ONLY");  // "f16": the 32x32x16 f16 sweep over waves per SIMD only
+    for (int wps : {8, 4, 3, 2, 1}) {  // waves per SIMD (grid = wps 4-wave workgroups per CU)
         const int grid = ncu * wps;
         if (run<0>(ops, out, grid, wps, "f32_32x32x16_f16", 32768.0, 2516.6)) return 1;
+        if (only) continue;
         if (run<3>(ops, out, grid, wps, "f32_16x16x32_f16", 16384.0, 2516.6)) return 1;
         if (run<1>(ops, out, grid, wps, "f32_32x32x16_bf16", 32768.0, 2516.6)) return 1;
         if (run<2>(ops, out, grid, wps, "f32_32x32x2_f32", 4096.0, 157.3)) return 1;

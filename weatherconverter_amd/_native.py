@@ -22,7 +22,7 @@ EXPORTS = [
     'wc_temb', 'wc_conv_in', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
-    'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
+    'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_f16x3', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
     'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name',
     'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse',
@@ -110,6 +110,7 @@ _SIGS = {
     'wc_dwconv': [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
     'wc_conv_wgrad': [ctypes.POINTER(WgradArgs), _P, _I, _P],
     'wc_conv_wgrad_x6': [ctypes.POINTER(WgradArgs), _P, _I, _P],
+    'wc_conv_wgrad_f16x3': [ctypes.POINTER(WgradArgs), _P, _I, _P, _I, _P, _P, _P],
     'wc_conv_wgrad_splits': [_I, _I, _L, _I],
     'wc_conv_wgrad3': [ctypes.POINTER(WgradArgs), _P, _I, _P],
     'wc_conv_wgrad3_f16x3': [ctypes.POINTER(WgradArgs), _P, _I, _I, _P, _P],

@@ -224,7 +224,9 @@ WC_DEVICE BwdScales bwd_scales(int eq, int ek, int ev, const float* dobound, int
     return r;
 }
 
-template <int D, bool F3>
+// DS: the output dims split over DS workgroups (each computes S and dP in full, and dK / dV — or dQ —
+// for D / DS of the dims): at D = 192 the whole width does not fit one wave's registers.
+template <int D, bool F3, int DS = 1>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
@@ -239,7 +241,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* base = qkv + (long)b * N * ldq;
     const float* dob = dO + (long)b * N * lddo;
     const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
-    const int key = blockIdx.x * 128 + wave * 32 + l32;
+    constexpr int NDBP = Cf::NDB / DS;  // output blocks of this workgroup
+    static_assert(Cf::NDB % DS == 0, "DS divides the 32-dim output blocks");
+    const int db0 = (int)(blockIdx.x % DS) * NDBP;
+    const int key = (int)(blockIdx.x / DS) * 128 + wave * 32 + l32;
     const BwdScales sc = bwd_scales<D, F3>(eq, ek, ev, dobound, b);
     const float s_log2 = scale_log2 * ldexpf(1.f, -(sc.eq + sc.ek));  // S carries 2^(eq + ek)
     const float dp_un = ldexpf(1.f, -(sc.edo + sc.ev));               // dP carries 2^(edo + ev)
@@ -248,9 +253,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     kr.load(base + (long)key * ldq + kcol, key < N, half, sc.sk);
     vr.load(base + (long)key * ldq + vcol, key < N, half, sc.sv);
 
-    f32x16 dvT[Cf::NDB], dkT[Cf::NDB];
+    f32x16 dvT[NDBP], dkT[NDBP];
 #pragma unroll
-    for (int d = 0; d < Cf::NDB; ++d)
+    for (int d = 0; d < NDBP; ++d)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { dvT[d][r] = 0.f; dkT[d][r] = 0.f; }
 
@@ -314,11 +319,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
             pieces8<F3>(s, 8 * c, sc.sp, pp);
             pieces8<F3>(dp, 8 * c, sc.sds, ds);
 #pragma unroll
-            for (int db = 0; db < Cf::NDB; ++db) {
+            for (int db = 0; db < NDBP; ++db) {
                 u32x4 a[NP];
-                tile_cols<D, F3>(Os, lane, db, c, a);
+                tile_cols<D, F3>(Os, lane, db0 + db, c, a);
                 mfmaP(dvT[db], a, pp);
-                tile_cols<D, F3>(Qs, lane, db, c, a);
+                tile_cols<D, F3>(Qs, lane, db0 + db, c, a);
                 mfmaP(dkT[db], a, ds);
             }
         }
@@ -330,10 +335,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
         const float kun = scale * ldexpf(1.f, -(sc.eq + sc.eds)), vun = ldexpf(1.f, -(sc.edo + sc.ep));
         float* row = dqkv + ((long)b * N + key) * lddq;
 #pragma unroll
-        for (int d = 0; d < Cf::NDB; ++d) {
+        for (int d = 0; d < NDBP; ++d) {
 #pragma unroll
             for (int r = 0; r < 16; r += 4) {
-                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                const int dv = (db0 + d) * 32 + 8 * (r >> 2) + 4 * half;
                 *reinterpret_cast<f32x4*>(row + kcol + dv) =
                     f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * kun;
                 const f32x4 vv = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     }
 }
 
-template <int D, bool F3>
+template <int D, bool F3, int DS = 1>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
@@ -358,7 +363,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float* base = qkv + (long)b * N * ldq;
     const float* dob = dO + (long)b * N * lddo;
     const int qcol = head * D, kcol = C + head * D, vcol = 2 * C + head * D;
-    const int qme = blockIdx.x * 128 + wave * 32 + l32;
+    constexpr int NDBP = Cf::NDB / DS;
+    static_assert(Cf::NDB % DS == 0, "DS divides the 32-dim output blocks");
+    const int db0 = (int)(blockIdx.x % DS) * NDBP;
+    const int qme = (int)(blockIdx.x / DS) * 128 + wave * 32 + l32;
     const BwdScales sc = bwd_scales<D, F3>(eq, ek, ev, dobound, b);
     const float s_log2 = scale_log2 * ldexpf(1.f, -(sc.eq + sc.ek));
     const float dp_un = ldexpf(1.f, -(sc.edo + sc.ev));
@@ -369,9 +377,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float lq = qme < N ? lse[((long)b * H + head) * N + qme] : INFINITY;
     const float dq = qme < N ? Dv[((long)b * H + head) * N + qme] : 0.f;
 
-    f32x16 dqT[Cf::NDB];
+    f32x16 dqT[NDBP];
 #pragma unroll
-    for (int d = 0; d < Cf::NDB; ++d)
+    for (int d = 0; d < NDBP; ++d)
 #pragma unroll
         for (int r = 0; r < 16; ++r) dqT[d][r] = 0.f;
 
@@ -420,9 +428,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
             u32x4 ds[NP];
             pieces8<F3>(dp, 8 * c, sc.sds, ds);
 #pragma unroll
-            for (int db = 0; db < Cf::NDB; ++db) {
+            for (int db = 0; db < NDBP; ++db) {
                 u32x4 a[NP];
-                tile_cols<D, F3>(Ks, lane, db, c, a);
+                tile_cols<D, F3>(Ks, lane, db0 + db, c, a);
                 mfmaP(dqT[db], a, ds);
             }
         }
@@ -434,39 +442,39 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
         const float qun = scale * ldexpf(1.f, -(sc.ek + sc.eds));
         float* row = dqkv + ((long)b * N + qme) * lddq + qcol;
 #pragma unroll
-        for (int d = 0; d < Cf::NDB; ++d) {
+        for (int d = 0; d < NDBP; ++d) {
 #pragma unroll
             for (int r = 0; r < 16; r += 4) {
-                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                const int dv = (db0 + d) * 32 + 8 * (r >> 2) + 4 * half;
                 *reinterpret_cast<f32x4*>(row + dv) = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * qun;
             }
         }
     }
 }
 
-template <int D, bool F3>
+template <int D, bool F3, int DS = 1>
 int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
                 int lddq, int B, int N, int C, int heads, float scale, int eq, int ek, int ev, const float* dobound,
                 hipStream_t s) {
     using Cf = B6Cfg<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dkdv_kernel<D, F3>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dkdv_kernel<D, F3, DS>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
         if (e != hipSuccess) return (int)e;
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<D, F3>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<D, F3, DS>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
-    const dim3 grid((N + 127) / 128, heads, B);
+    const dim3 grid((N + 127) / 128 * DS, heads, B);
     const float scale_log2 = scale * 1.4426950408889634f;
     WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D), WC_TB(F3)});
-    hipLaunchKernelGGL((attn_bwd6_dkdv_kernel<D, F3>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
+    hipLaunchKernelGGL((attn_bwd6_dkdv_kernel<D, F3, DS>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
                        lddq, N, C, scale_log2, scale, eq, ek, ev, dobound);
     WC_CHECK_LAUNCH();
     WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D), WC_TB(F3)});
-    hipLaunchKernelGGL((attn_bwd6_dq_kernel<D, F3>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
+    hipLaunchKernelGGL((attn_bwd6_dq_kernel<D, F3, DS>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
                        lddq, N, C, scale_log2, scale, eq, ek, ev, dobound);
     WC_CHECK_LAUNCH();
     return WC_OK;
@@ -504,7 +512,7 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
         case 32: return WC_BWD6(32);
         case 64: return WC_BWD6(64);
         case 128: return WC_BWD6(128);
-        default: return WC_E_SHAPE;  // D = 192 spills in both forms (wc_attention_bwd keeps it on fp32 MFMA)
+        default: return WC_E_SHAPE;  // D = 192: the own K / V rows spill even with the output dims split (DS)
     }
 #undef WC_BWD6
 }

@@ -61,6 +61,11 @@ struct WgDev {
     float* part;
     long pps;   // pixels per split (multiple of WG_KP)
     int ntm, ntn;
+    // F3: per-image bounds (device [B]) of G, segment 0 and segment 1; xe0 = segment 0's static exponent
+    const float* gb;
+    const float* xb0;
+    const float* xb1;
+    int xe0, B;
 };
 
 // PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU (segment 0 only, as the forward prologue).
@@ -70,8 +75,13 @@ struct WgDev {
 // with ds_read_b64_tr_b16 (gfx950's transposing LDS read: per 16-lane group a 4-row x 16-column
 // block delivered column-major).  Row bytes = 2*width + 64 (== 64 mod 256): the four rows of a
 // half-wave's read land on disjoint banks.  Else fp32 MFMA 32x32x2 on fp32 rows.
-template <int BM, int BN, int PRO, bool X6>
+// F3 (with X6): f16x3 instead — G x 2^sg, segment 0 x 2^sx0, segment 1 x 2^sx1 split into two fp16
+// pieces (products h*h + h*l + l*h), s = 13 - floor(log2 bound) from the batch max of the per-image
+// bounds (segment 0: at most its static exponent xe0); the epilogue removes 2^-(sg + sx) per column.
+template <int BM, int BN, int PRO, bool X6, bool F3 = false>
 __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
+    static_assert(!F3 || X6, "F3 runs the X6 structure");
+    constexpr int NP = F3 ? 2 : 3;
     constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
     constexpr int KP = X6 ? 16 : WG_KP;        // pixels per K-step
@@ -80,7 +90,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     constexpr int APL = KP * ASB, BPL = KP * BSB;        // X6 bytes of one piece plane
     constexpr int A_PER_T = KP * BM / 4 / WG_THREADS;
     constexpr int B_PER_T = KP * BN / 4 / WG_THREADS;
-    constexpr int STAGE = X6 ? 3 * (APL + BPL) : KP * (AS + BS) * 4;  // bytes
+    constexpr int STAGE = X6 ? NP * (APL + BPL) : KP * (AS + BS) * 4;  // bytes
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
     const int tid = threadIdx.x;
@@ -100,6 +110,20 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     if (pend > p.P) pend = p.P;
     const int nsteps = (int)((pend - pbeg + KP - 1) / KP);
     const int HWm = p.Hm * p.Wm;
+    int sg = 0, sx0 = 0, sx1 = 0;
+    if constexpr (F3) {
+        auto exp_of = [&](const float* bnd, int cap) {
+            float m = 0.f;
+            for (int b = 0; b < p.B; ++b) m = fmaxf(m, bnd[b]);
+            int e = cap;
+            if (m > 0.f) e = min(cap, 13 - ((int)((__float_as_uint(m) >> 23) & 0xffu) - 127));
+            return max(e, -100);
+        };
+        sg = exp_of(p.gb, 60);
+        sx0 = p.xb0 ? exp_of(p.xb0, p.xe0) : p.xe0;
+        sx1 = p.xb1 ? exp_of(p.xb1, 60) : 0;
+    }
+    const float gsc = ldexpf(1.f, sg), xsc0 = ldexpf(1.f, sx0), xsc1 = ldexpf(1.f, sx1);
 
     // fixed per-thread column coordinates
     int arow[A_PER_T], acol[A_PER_T];
@@ -205,10 +229,16 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     };
     auto store = [&](int buf) {
         unsigned char* a = lds + buf * STAGE;
-        unsigned char* bb = a + (X6 ? 3 * APL : KP * AS * 4);
+        unsigned char* bb = a + (X6 ? NP * APL : KP * AS * 4);
 #pragma unroll
         for (int j = 0; j < A_PER_T; ++j) {
-            if constexpr (X6) {
+            if constexpr (F3) {
+                wcx6::u32x2 h, l;
+                wcx6::split2_f16(ra[j] * gsc, h, l);
+                unsigned char* d = a + arow[j] * ASB + acol[j] * 2;
+                *reinterpret_cast<wcx6::u32x2*>(d) = h;
+                *reinterpret_cast<wcx6::u32x2*>(d + APL) = l;
+            } else if constexpr (X6) {
                 wcx6::u32x2 p0, p1, p2;
                 wcx6::split3(ra[j], p0, p1, p2);
                 unsigned char* d = a + arow[j] * ASB + acol[j] * 2;
@@ -231,7 +261,13 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
                     if (!((binb >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
                 }
             }
-            if constexpr (X6) {
+            if constexpr (F3) {
+                wcx6::u32x2 h, l;
+                wcx6::split2_f16(v * (bseg[j] == 1 ? xsc1 : xsc0), h, l);
+                unsigned char* d = bb + brow[j] * BSB + bcol[j] * 2;
+                *reinterpret_cast<wcx6::u32x2*>(d) = h;
+                *reinterpret_cast<wcx6::u32x2*>(d + BPL) = l;
+            } else if constexpr (X6) {
                 wcx6::u32x2 p0, p1, p2;
                 wcx6::split3(v, p0, p1, p2);
                 unsigned char* d = bb + brow[j] * BSB + bcol[j] * 2;
@@ -272,7 +308,26 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     for (int s = 0; s < nsteps; ++s) {
         const int buf = s & 1;
         if (s + 1 < nsteps) load(s + 1);
-        if constexpr (X6) {
+        if constexpr (F3) {
+            const unsigned char* a = lds + buf * STAGE + tr_a;
+            const unsigned char* bb = lds + buf * STAGE + 2 * APL + tr_b;
+            wcx6::u32x4 fa[2][2], fb[2][2];
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc) {
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) fa[mb][pc] = tr_frag(a + pc * APL + mb * 64, ASB);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) fb[nb][pc] = tr_frag(bb + pc * BPL + nb * 64, BSB);
+            }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    acc[mb][nb] = wcx6::mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                }
+        } else if constexpr (X6) {
             const unsigned char* a = lds + buf * STAGE + tr_a;
             const unsigned char* bb = lds + buf * STAGE + 3 * APL + tr_b;
             wcx6::u32x4 fa[2][3], fb[2][3];
@@ -327,10 +382,11 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             const int k = n0 + wn * 64 + nb * 32 + l32;
+            const float un = F3 ? ldexpf(1.f, -(sg + (k < p.K0 ? sx0 : sx1))) : 1.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm * 64 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                if (m < p.M && k < p.Kc) out[(long)m * p.Kc + k] = acc[mb][nb][r];
+                if (m < p.M && k < p.Kc) out[(long)m * p.Kc + k] = F3 ? acc[mb][nb][r] * un : acc[mb][nb][r];
             }
         }
 }
@@ -379,25 +435,34 @@ __global__ __launch_bounds__(256) void wgrad_reduce_groups_kernel(float* __restr
     __syncthreads();
     if (w == 0 && e < n4) p4[(long)g0 * n4 + e] = ((s + red[0][lane]) + red[1][lane]) + red[2][lane];
 }
-template <int BM, int BN, int PRO, bool X6>
+template <int BM, int BN, int PRO, bool X6, bool F3 = false>
 int wgrad_launch(const WgDev& d, int grid, hipStream_t s) {
     constexpr int KP = X6 ? 16 : WG_KP;
-    constexpr int bytes = 2 * (X6 ? 3 * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
+    constexpr int bytes =
+        2 * (X6 ? (F3 ? 2 : 3) * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
     static bool attr_set = false;
     if (!attr_set && bytes > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_kernel<BM, BN, PRO, X6>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_kernel<BM, BN, PRO, X6, F3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, PRO, X6>), dim3(grid), dim3(WG_THREADS), bytes, s, d);
+    WC_SET_NAME("conv_wgrad_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(PRO), WC_TB(X6), WC_TB(F3)});
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, PRO, X6, F3>), dim3(grid), dim3(WG_THREADS), bytes, s, d);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 template <int BM, int BN>
-int wgrad_dispatch(const WgDev& d, int pro, bool x6, int grid, hipStream_t s) {
-    if (x6) {
+int wgrad_dispatch(const WgDev& d, int pro, int mode, int grid, hipStream_t s) {  // mode 0 fp32, 1 x6, 2 f16x3
+    if (mode == 2) {
+        switch (pro) {
+            case 0: return wgrad_launch<BM, BN, 0, true, true>(d, grid, s);
+            case 1: return wgrad_launch<BM, BN, 1, true, true>(d, grid, s);
+            default: return wgrad_launch<BM, BN, 2, true, true>(d, grid, s);
+        }
+    }
+    if (mode == 1) {
         switch (pro) {
             case 0: return wgrad_launch<BM, BN, 0, true>(d, grid, s);
             case 1: return wgrad_launch<BM, BN, 1, true>(d, grid, s);
@@ -578,9 +643,11 @@ __global__ __launch_bounds__(256) void gnb_apply_kernel(const float* __restrict_
 
 // The same, also raising absmax[b] to the max |dx| WRITTEN per image (after the accumulate: the
 // final value of every element it writes, so absmax over all writers of a tensor bounds the tensor).
-// Workgroup k walks the float4 range [k per, (k + 1) per) (per a multiple of 1024), four elements in
-// flight per thread; the maxima go out once per workgroup when the range lies in one image (the usual
-// case: all B slots share one L2 line, so the atomics are kept few), per wave or per lane otherwise.
+// Workgroup k walks the float4 range [k per, (k + 1) per) (per a multiple of 1024), four elements per
+// thread per round with every load of the round issued before its first store (vmcnt counts stores:
+// a load after a store would wait for the store); the maxima go out once per workgroup when the range
+// lies in one image (the usual case: all B slots share one L2 line, so the atomics are kept few), per
+// lane otherwise.
 template <bool SILU, bool ACC>
 __global__ __launch_bounds__(256) void gnb_apply_absmax_kernel(
     const float* __restrict__ dz, int ldz, const float* __restrict__ x, int ldx, const float* __restrict__ sc0,
@@ -590,26 +657,57 @@ __global__ __launch_bounds__(256) void gnb_apply_absmax_kernel(
     __shared__ float wm[4];
     const long i0 = (long)blockIdx.x * per;
     const long i1 = min(n4, i0 + per);
-    const long per_img = (long)HW * (C / 4);
+    const int C4 = C / 4;
+    const long per_img = (long)HW * C4;
     const int bfirst = (int)(i0 / per_img), blast = (int)((i1 - 1) / per_img);
     float m = 0.f;
     int bc = bfirst;
     for (long base = i0 + threadIdx.x; base < i1; base += 1024) {
+        f32x4 d[4], xv[4], o[4];
+        long pofs[4];
+        int bb[4], cc[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const long i = base + 256 * u;
-            if (i < i1) {
-                int b;
-                const f32x4 r =
-                    gnb_apply_one<SILU, ACC>(dz, ldz, x, ldx, sc0, sh0, gamma, beta, coef, dx, lddx, i, HW, C, b);
-                const float v = fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w)));
-                if (bfirst != blast && b != bc) {  // a range crossing images: flush the lane's maximum
-                    atomicMax(reinterpret_cast<unsigned*>(absmax) + bc, __float_as_uint(m));
-                    bc = b;
-                    m = 0.f;
-                }
-                m = fmaxf(m, v);
+            const long i = min(base + 256 * u, i1 - 1);  // past the range: a repeat of the last element, not stored
+            const long pix = i / C4;
+            cc[u] = (int)(i - pix * C4) * 4;
+            bb[u] = (int)(pix / HW);
+            pofs[u] = pix;
+            d[u] = *reinterpret_cast<const f32x4*>(dz + pix * ldz + cc[u]);
+            xv[u] = *reinterpret_cast<const f32x4*>(x + pix * ldx + cc[u]);
+            if constexpr (ACC) o[u] = *reinterpret_cast<const f32x4*>(dx + pix * lddx + cc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long bc4 = (long)bb[u] * C + cc[u];
+            const f32x4 xh = xv[u] * *reinterpret_cast<const f32x4*>(sc0 + bc4) + *reinterpret_cast<const f32x4*>(sh0 + bc4);
+            f32x4 dd = d[u];
+            if constexpr (SILU) {
+                const f32x4 g = gamma ? *reinterpret_cast<const f32x4*>(gamma + cc[u]) : f32x4{1.f, 1.f, 1.f, 1.f};
+                const f32x4 be = beta ? *reinterpret_cast<const f32x4*>(beta + cc[u]) : f32x4{0.f, 0.f, 0.f, 0.f};
+                const f32x4 y = g * xh + be;
+                dd.x *= silu_grad(y.x); dd.y *= silu_grad(y.y); dd.z *= silu_grad(y.z); dd.w *= silu_grad(y.w);
             }
+            f32x4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const f32x4 cf = *reinterpret_cast<const f32x4*>(coef + (bc4 + e) * 4);
+                r[e] = cf.x * dd[e] + cf.y + cf.z * xh[e];
+            }
+            if constexpr (ACC) r += o[u];
+            o[u] = r;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (base + 256 * u >= i1) continue;
+            *reinterpret_cast<f32x4*>(dx + pofs[u] * lddx + cc[u]) = o[u];
+            const float v = fmaxf(fmaxf(fabsf(o[u].x), fabsf(o[u].y)), fmaxf(fabsf(o[u].z), fabsf(o[u].w)));
+            if (bfirst != blast && bb[u] != bc) {  // a range crossing images: flush the lane's maximum
+                atomicMax(reinterpret_cast<unsigned*>(absmax) + bc, __float_as_uint(m));
+                bc = bb[u];
+                m = 0.f;
+            }
+            m = fmaxf(m, v);
         }
     }
     if (bfirst == blast) {  // one image: one atomic for the workgroup
@@ -707,8 +805,10 @@ __global__ __launch_bounds__(256) void absmax_images_kernel(const float* __restr
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-static int conv_wgrad_any(const wc_wgrad_args* a, float* part, int splits, bool x6, void* stream) {
+static int conv_wgrad_any(const wc_wgrad_args* a, float* part, int splits, int mode, const float* gb, int xe0,
+                          const float* xb0, const float* xb1, void* stream) {
     if (!a || !a->g || !part || a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
+    if (mode == 2 && (!gb || (a->nseg == 2 && !xb1) || xe0 < -100 || xe0 > 60)) return WC_E_ARG;
     const wc_conv_seg& s0 = a->seg[0];
     if (!s0.src) return WC_E_ARG;
     if (a->M <= 0 || a->M % 4 || a->ldg % 4 || s0.C <= 0 || s0.C % 4 || s0.ldc % 4) return WC_E_SHAPE;
@@ -748,19 +848,25 @@ static int conv_wgrad_any(const wc_wgrad_args* a, float* part, int splits, bool 
     const long nsp = (P + d.pps - 1) / d.pps;
     if (nsp != splits) return WC_E_SHAPE;  // the caller sizes part by wc_conv_wgrad_splits
     d.part = part;
+    d.gb = gb; d.xb0 = xb0; d.xb1 = xb1; d.xe0 = xe0; d.B = a->B;
     const long grid = (long)d.ntm * d.ntn * splits;
     if (grid > (1L << 30)) return WC_E_SHAPE;
     const int pro = s0.scale ? (s0.silu ? 2 : 1) : 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return narrow ? wgrad_dispatch<64, 256>(d, pro, x6, (int)grid, s) : wgrad_dispatch<128, 128>(d, pro, x6, (int)grid, s);
+    return narrow ? wgrad_dispatch<64, 256>(d, pro, mode, (int)grid, s) : wgrad_dispatch<128, 128>(d, pro, mode, (int)grid, s);
 }
 
 extern "C" int wc_conv_wgrad(const wc_wgrad_args* a, float* part, int splits, void* stream) {
-    return conv_wgrad_any(a, part, splits, false, stream);
+    return conv_wgrad_any(a, part, splits, 0, nullptr, 0, nullptr, nullptr, stream);
 }
 
 extern "C" int wc_conv_wgrad_x6(const wc_wgrad_args* a, float* part, int splits, void* stream) {
-    return conv_wgrad_any(a, part, splits, true, stream);
+    return conv_wgrad_any(a, part, splits, 1, nullptr, 0, nullptr, nullptr, stream);
+}
+
+extern "C" int wc_conv_wgrad_f16x3(const wc_wgrad_args* a, float* part, int splits, const float* gbound, int x_exp0,
+                                   const float* xbound0, const float* xbound1, void* stream) {
+    return conv_wgrad_any(a, part, splits, 2, gbound, x_exp0, xbound0, xbound1, stream);
 }
 
 extern "C" int wc_conv_wgrad_splits(int M, int Kc, int64_t P, int target_blocks) {

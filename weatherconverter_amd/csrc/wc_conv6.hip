@@ -831,13 +831,26 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     }
 }
 
+// A/B knob (WC_CONV3_WGS_PER_CU=n, 1..2): pad each workgroup's dynamic LDS so that at most n
+// workgroups (n waves per SIMD) share a CU; 0 = the kernel's own occupancy.
+int conv3_lds_for(int lds) {
+    static const int n = [] {
+        const char* e = getenv("WC_CONV3_WGS_PER_CU");
+        return e ? atoi(e) : 0;
+    }();
+    if (n < 1 || n > 2) return lds;
+    const int need = (160 * 1024) / (n + 1) + 1024;  // more than 1 / (n + 1) of the CU's 160 KiB
+    return lds > need ? lds : need;
+}
+
 template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0, int WR = 0>
 int launch6(const X6Dev& d, hipStream_t stream) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
+    static const int lds = conv3_lds_for(T::LDS);
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
@@ -848,7 +861,7 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n * (MAP == 2 ? 4 : 1));
     WC_SET_NAME("conv3x3_x6_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES), WC_TB(F3), WC_TB(R16), WC_TB(GL),
                                       WC_TI(MAP), WC_TI(WR)});
-    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>), grid, dim3(NT), T::LDS, stream, p);
+    hipLaunchKernelGGL((conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>), grid, dim3(NT), lds, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

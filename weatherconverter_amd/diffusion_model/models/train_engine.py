@@ -360,11 +360,13 @@ class TrainEngine:
                 seg = Seg(cur, TAPS4S2, stride=2)
                 bd = dp['mod'].bias.detach().float().contiguous()
                 Hm, Wm = sizes[i + 1]
-                if dp['f3'] is not None and K.conv4x4s2_f16x3_ok(seg, final.C, Hm, Wm):
-                    K.conv4x4s2_f16x3(seg, dp['f3'], bd, final, Hm=Hm, Wm=Wm, a_bound=K.absmax_images(cur))
+                f3 = dp['f3'] is not None and K.conv4x4s2_f16x3_ok(seg, final.C, Hm, Wm)
+                bcur = K.absmax_images(cur) if (f3 or self.f3d) else None  # also the weight gradient's bound
+                if f3:
+                    K.conv4x4s2_f16x3(seg, dp['f3'], bd, final, Hm=Hm, Wm=Wm, a_bound=bcur)
                 else:
                     self._conv([seg], dp['pk'], bd, final, Hm, Wm)
-                self.tape.append(('down', cur, final, dp))
+                self.tape.append(('down', cur, final, dp, bcur))
                 cur = final
 
         for j, (res, att) in enumerate(self.mids):
@@ -389,12 +391,14 @@ class TrainEngine:
                 up = self.up_pk[k]
                 dst = View(U[i], 0, dc[i])
                 b = up['mod'].bias.detach().float().contiguous()
-                if up['f3'] is not None and K.convT4x4s2_f16x3_ok(Seg(cur, [(0, 0)]), dst.C):
-                    K.convT4x4s2_f16x3(Seg(cur, [(0, 0)]), up['f3'], b, dst, a_bound=K.absmax_images(cur))
+                f3 = up['f3'] is not None and K.convT4x4s2_f16x3_ok(Seg(cur, [(0, 0)]), dst.C)
+                bcur = K.absmax_images(cur) if (f3 or self.f3d) else None
+                if f3:
+                    K.convT4x4s2_f16x3(Seg(cur, [(0, 0)]), up['f3'], b, dst, a_bound=bcur)
                 else:
                     for (py, px), (taps, pk) in zip(_PARITIES, up['fw']):
                         self._conv([Seg(cur, taps)], pk, b, dst, cur.H, cur.W, out_map=(2, 2, py, px))
-                self.tape.append(('up', cur, dst, up))
+                self.tape.append(('up', cur, dst, up, bcur))
             else:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
             cur = View.full(U[i])
@@ -438,7 +442,7 @@ class TrainEngine:
                             a_bound=st1[4])
         else:
             self._conv(seg2, rp['pk2'], rp['b2'], Y, H, W)
-        self.tape.append(('res', X, h, Y, rp, st1[:4], st2))
+        self.tape.append(('res', X, h, Y, rp, st1[:4], st2, st1[4]))
 
     def _attn_fwd(self, Ypre: View, Yout: View, ap):
         B, H, W, C = Ypre.B, Ypre.H, Ypre.W, Ypre.C
@@ -540,7 +544,7 @@ class TrainEngine:
                       dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), absmax=self._gb(cur))
 
     def _bwd_res(self, rec, gout):
-        _, X, h, Y, rp, st1, st2 = rec
+        _, X, h, Y, rp, st1, st2, bXf = rec  # bXf: GN1's per-image bound of |X| (the forward's)
         B, H, W = X.B, X.H, X.W
         ci, co = rp['ci'], rp['co']
         gY = self._grad(Y)
@@ -552,7 +556,7 @@ class TrainEngine:
         bX = self._gb(X)
         self._wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
                     self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci,
-                    f3=(K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), bY) if f3Y else None)
+                    f3=K.F3Bounds(bY, K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), None, bXf) if f3Y else None)
         dz2 = View.full(self._new(B, H, W, co))
         if f3Y:
             K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
@@ -574,7 +578,7 @@ class TrainEngine:
         f3h = rp['f3_1T'] is not None and self._dgrad3_ok(dh, ci)
         bh = self._bound(dh, bdh) if f3h else None
         self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
-                    (ci * 9, 9, 1), f3=(K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8), bh) if f3h else None)
+                    (ci * 9, 9, 1), f3=K.F3Bounds(bh, K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8)) if f3h else None)
         dz1 = View.full(self._new(B, H, W, ci))
         if f3h:
             K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
@@ -591,19 +595,24 @@ class TrainEngine:
         mha, gn = ap['mha'], ap['gn']
         gY = self._grad(Yout)
         self._bias_grad(gY, mha.out_proj.bias)
-        self._wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0))
+        f3a = self.f3d and ap['f3_in'] is not None
+        # the forward's Q / K / V exponents (|O| <= max|V|: O shares V's)
+        exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], N * C // 8) \
+            if f3a else None
+        bgY = self._bound(gY, self._gb(Yout)) if self.f3d else None
+        self._wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0),
+                    f3=K.F3Bounds(bgY, exps[2]) if f3a else None)
         do = self._new(B, H, W, C)
         bdo = torch.zeros((B, ), dtype=torch.float32, device=self.device) if self.f3d else None
         f3p = 'f3_outT' in ap and (H * W) % (256 if C <= 64 else 128) == 0
         if f3p:
             K.conv_igemm_f16x3([Seg(gY, TAPS1)], ap['f3_outT'], None, View.full(do), Hm=H, Wm=W, a_exp=60,
-                               a_bound=self._bound(gY, self._gb(Yout)), absmax=bdo)
+                               a_bound=bgY, absmax=bdo)
         else:
             self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W, absmax=bdo)
         dqkv = self._new(B, H, W, 3 * C)
-        if self.f3d and ap['f3_in'] is not None:
+        if f3a:
             # f16x3 under the forward's Q / K / V exponents and the per-image max |dO|
-            exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], N * C // 8)
             K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
                             B, N, C, ap['heads'], precision='f16x3', exps=exps,
                             dout_bound=self._bound(View.full(do), bdo))
@@ -612,12 +621,12 @@ class TrainEngine:
                             B, N, C, ap['heads'], precision=self.precision)
         gq = View.full(dqkv)
         self._bias_grad(gq, mha.in_proj_bias)
+        bgq = K.absmax_images(gq) if (f3a or f3p) else None
         self._wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),
-                     (C, 1, 0))
+                    (C, 1, 0), f3=K.F3Bounds(bgq, K.f16x3_a_exp(*ap['gb'], N * C // 8)) if f3a else None)
         da = View.full(self._new(B, H, W, C))
         if f3p:
-            K.conv_igemm_f16x3([Seg(gq, TAPS1)], ap['f3_inT'], None, da, Hm=H, Wm=W, a_exp=60,
-                               a_bound=K.absmax_images(gq))
+            K.conv_igemm_f16x3([Seg(gq, TAPS1)], ap['f3_inT'], None, da, Hm=H, Wm=W, a_exp=60, a_bound=bgq)
         else:
             self._conv([Seg(gq, TAPS1)], ap['pk_inT'], None, da, H, W)
         # Yout = Ypre + out_proj(...): Ypre's gradient is Yout's plus the GroupNorm path
@@ -627,34 +636,36 @@ class TrainEngine:
                       absmax=self._gb(Ypre))
 
     def _bwd_down(self, rec, gout):
-        _, cur, final, dp = rec
+        _, cur, final, dp, bcur = rec  # bcur: the forward's per-image max |cur|
         gF = self._grad(final)
         gc = self._grad(cur)
         w = dp['mod'].weight
         self._bias_grad(gF, dp['mod'].bias)
-        self._wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1))
+        bgF = self._bound(gF, self._gb(final)) if self.f3d else None
+        self._wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1),
+                    f3=K.F3Bounds(bgF, 60, bcur) if bgF is not None and bcur is not None else None)
         if dp['f3T'] is not None and K.convT4x4s2_f16x3_ok(Seg(gF, [(0, 0)]), gc.C) and gF.ptr % 16 == 0:
             # the ConvT of dY (same weight) in one launch on f16x3 under dY's tracked bound
-            K.convT4x4s2_f16x3(Seg(gF, [(0, 0)]), dp['f3T'], None, gc, a_bound=self._bound(gF, self._gb(final)),
-                               res=gc, absmax=self._gb(cur))
+            K.convT4x4s2_f16x3(Seg(gF, [(0, 0)]), dp['f3T'], None, gc, a_bound=bgF, res=gc, absmax=self._gb(cur))
             return
         for (py, px), (taps, pk) in zip(_PARITIES, dp['dT']):
             self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=gc, absmax=self._gb(cur))
 
     def _bwd_up(self, rec, gout):
-        _, cur, dst, up = rec
+        _, cur, dst, up, bcur = rec
         gD = self._grad(dst)
         gc = self._grad(cur)
         wt = up['mod'].weight  # [Cin][Cout][4][4]
         self._bias_grad(gD, up['mod'].bias)
         # dW[ci][co][ky][kx] = sum_pixels x[ci] * dY[co] at (2y - 1 + ky, 2x - 1 + kx): the 4x4/s2 tap
         # grid over dY with x in the gradient role
-        self._wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1))
+        bgD = self._bound(gD, self._gb(dst)) if self.f3d else None
+        self._wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1),
+                    f3=K.F3Bounds(bcur, 60, bgD) if bgD is not None and bcur is not None else None)
         seg = Seg(gD, TAPS4S2, stride=2)
         if up['f3T'] is not None and K.conv4x4s2_f16x3_ok(seg, gc.C, cur.H, cur.W) and gD.ptr % 16 == 0:
             # the 4x4/s2 conv of dY on the space-to-depth halo kernel, f16x3 under dY's tracked bound
-            K.conv4x4s2_f16x3(seg, up['f3T'], None, gc, Hm=cur.H, Wm=cur.W, a_bound=self._bound(gD, self._gb(dst)),
-                              res=gc, absmax=self._gb(cur))
+            K.conv4x4s2_f16x3(seg, up['f3T'], None, gc, Hm=cur.H, Wm=cur.W, a_bound=bgD, res=gc, absmax=self._gb(cur))
             return
         self._conv([seg], up['dT'], None, gc, cur.H, cur.W, res=gc, absmax=self._gb(cur))
 

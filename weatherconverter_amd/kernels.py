@@ -9,7 +9,7 @@ import ctypes
 import functools
 import os
 from dataclasses import dataclass
-from typing import Optional, Sequence, Tuple
+from typing import NamedTuple, Optional, Sequence, Tuple
 
 import torch
 
@@ -1041,6 +1041,25 @@ def wgrad3_ok(g: View, s0: Seg) -> bool:
         and v.ptr % 16 == 0 and g.ptr % 16 == 0
 
 
+class F3Bounds(NamedTuple):
+    """Range bounds for an f16x3 weight gradient: g = per-image max |gradient| (device float32 [B]);
+    segment 0 at the static exponent x_exp0 (a GroupNorm-bounded operand: |x| 2^x_exp0 <= 2^14) or,
+    raw, under x0 = its per-image max |x|; segment 1 (raw) under x1."""
+    g: torch.Tensor
+    x_exp0: int = 60
+    x0: Optional[torch.Tensor] = None
+    x1: Optional[torch.Tensor] = None
+
+
+def _bound_ok(t: torch.Tensor, B: int) -> bool:
+    return t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= B
+
+
+def wgrad_f16x3_enabled() -> bool:
+    """The generic weight gradient on f16x3 when the caller supplies bounds (WC_WGRAD_F16X3=0: bf16x6)."""
+    return os.environ.get('WC_WGRAD_F16X3', '1') != '0'
+
+
 def wgrad3_f16x3_enabled() -> bool:
     """The halo 3x3 weight gradient on f16x3 when the caller supplies the bounds (WC_WGRAD3_F16X3=0:
     bf16x6, for A/B)."""
@@ -1049,13 +1068,13 @@ def wgrad3_f16x3_enabled() -> bool:
 
 def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, int, int], *, Cw: Optional[int] = None,
                dw1: Optional[torch.Tensor] = None, s1: int = 0, accumulate: bool = False, x6: bool = False,
-               f3: Optional[Tuple[int, torch.Tensor]] = None):
+               f3: Optional[F3Bounds] = None):
     """Weight gradient of a conv whose input segments are `segs` (as the forward read them, prologue
     included) and whose output gradient is the view g (pixel grid = g's H x W): GEMM over the pixels
     on fp32 MFMA (or bf16x6 with x6), split and reduced in a fixed order.  Column (tap t, channel c < Cw) of segment 0 is
     written to dw0.flat[m*s0[0] + c*s0[1] + t*s0[2]], segment 1's columns to dw1.flat[m*s1 + c].
-    f3 = (x_exp, gbound): segment 0's f16x3 exponent (the forward's, for its GroupNorm-bounded operand)
-    and the per-image max |g| [B] on the device; the 3x3 halo kernel then runs f16x3."""
+    f3: the f16x3 range bounds (F3Bounds); with x6, the 3x3 halo kernel (segment 0 GroupNorm-bounded)
+    and the generic GEMM then run f16x3."""
     g.check()
     _req(1 <= len(segs) <= 2, 'wgrad takes 1 or 2 segments')
     _req(dw0.is_cuda and dw0.dtype == torch.float32 and dw0.is_contiguous(), 'dw0: contiguous fp32 device tensor')
@@ -1084,11 +1103,10 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
         a.nseg = 1
         part = torch.empty(splits * g.C * K0, dtype=torch.float32, device=g.t.device)
         s = _stream()
-        if f3 is not None and segs[0].scale is not None and wgrad3_f16x3_enabled():
-            gb = f3[1]
-            _req(gb.is_cuda and gb.dtype == torch.float32 and gb.numel() >= B, 'f3 bound: float32 [B] on the device')
+        if f3 is not None and segs[0].scale is not None and f3.x0 is None and wgrad3_f16x3_enabled():
+            _req(_bound_ok(f3.g, B), 'f3 bound: float32 [B] on the device')
             _timed('conv_wgrad3_kernel', 'wc_conv_wgrad3_f16x3', 2.0 * P * g.C * K0, ctypes.byref(a), part.data_ptr(),
-                   splits, int(f3[0]), gb.data_ptr(), s)
+                   splits, int(f3.x_exp0), f3.g.data_ptr(), s)
         else:
             _timed('conv_wgrad3_kernel', 'wc_conv_wgrad3', 2.0 * P * g.C * K0, ctypes.byref(a), part.data_ptr(), splits,
                    s)
@@ -1096,14 +1114,22 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
                      s0[2], None, 0, int(accumulate), s)
         if C1:
             r = segs[1]
-            conv_wgrad(g, [Seg(r.view, r.taps, r.stride)], dw1, (s1, 1, 0), accumulate=accumulate, x6=x6)
+            f31 = F3Bounds(f3.g, 60, f3.x1) if f3 is not None and f3.x1 is not None else None
+            conv_wgrad(g, [Seg(r.view, r.taps, r.stride)], dw1, (s1, 1, 0), accumulate=accumulate, x6=x6, f3=f31)
         return
     P = B * g.H * g.W
     splits = lib.wc_conv_wgrad_splits(g.C, Kc, P, 2048)
     part = torch.empty(splits * g.C * Kc, dtype=torch.float32, device=g.t.device)
     s = _stream()
-    _timed('conv_wgrad_kernel' + ('<x6>' if x6 else ''), 'wc_conv_wgrad_x6' if x6 else 'wc_conv_wgrad',
-           2.0 * P * g.C * Kc, ctypes.byref(a), part.data_ptr(), splits, s)
+    if (x6 and f3 is not None and wgrad_f16x3_enabled() and (C1 == 0 or f3.x1 is not None)
+            and (f3.x0 is not None or f3.x_exp0 < 60)):
+        for t_ in (f3.g, f3.x0, f3.x1):
+            _req(t_ is None or _bound_ok(t_, B), 'f3 bounds: float32 [B] on the device')
+        _timed('conv_wgrad_kernel', 'wc_conv_wgrad_f16x3', 2.0 * P * g.C * Kc, ctypes.byref(a), part.data_ptr(), splits,
+               f3.g.data_ptr(), int(f3.x_exp0), _ptr(f3.x0), _ptr(f3.x1), s)
+    else:
+        _timed('conv_wgrad_kernel' + ('<x6>' if x6 else ''), 'wc_conv_wgrad_x6' if x6 else 'wc_conv_wgrad',
+               2.0 * P * g.C * Kc, ctypes.byref(a), part.data_ptr(), splits, s)
     _native.call('wc_wgrad_reduce', part.data_ptr(), splits, g.C, Kc, K0, C0, Cw, dw0.data_ptr(), s0[0], s0[1], s0[2],
                  _ptr(dw1), s1, int(accumulate), s)
 

@@ -479,11 +479,12 @@ int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out
 /* The same backward on f16x3 (two round-to-nearest fp16 pieces per operand, three products per block):
  * Q, K, V scaled by 2^eq, 2^ek, 2^ev — the training forward's exponents from the in-projection bounds
  * (|Q| 2^eq <= 2^14 ...); dO by 2^edo from dobound[b] = per-image max |dO| (device, wc_absmax_images);
- * P by 2^14; dS by 2^eds with the bound |dS| <= 2 d max|dO| max|V|.  Head dim in {32, 64, 128}. */
+ * P by 2^14; dS by 2^eds with the bound |dS| <= 2 d max|dO| max|V|.  Head dim in {32, 64, 128}.
+ * dqkv_absmax (optional, [B], caller-zeroed): raised to the max |dqkv| written per image. */
 int wc_attention_bwd_f16x3(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
                            int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
                            int C, int heads, float scale, int eq, int ek, int ev, const float* dobound,
-                           void* stream);
+                           float* dqkv_absmax, void* stream);
 /* Its first step alone: dv_work[(b*heads + h)*N + q] = sum_d dout[b, q, h*D + d] * out[b, q, h*D + d]. */
 int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N, int heads,
                           int D, float* dv_work, void* stream);

@@ -297,9 +297,12 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     K.attention_fwd_lse(qkv.cuda(), o, lse, B, N, C, heads, precision=precision, exps=exps)
     dqkv = torch.empty((B * N, 3 * C), device='cuda')
     dob = do.abs().reshape(B, -1).amax(1).cuda() if precision == 'f16x3' else None
+    amx = torch.zeros(B, device='cuda')
     prof = K.profile_conv(True)
-    K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads, precision=precision, exps=exps,
-                    dout_bound=dob)
+    raised = K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads, precision=precision, exps=exps,
+                             dout_bound=dob, dqkv_absmax=amx)
+    if raised:  # the epilogue's per-image max |dqkv| equals a pass over what it wrote
+        assert torch.equal(amx.cpu(), dqkv.cpu().abs().reshape(B, -1).amax(1))
     torch.cuda.synchronize()
     K.profile_conv(False)
     if C // heads in (32, 64, 128):  # the split-precision backward ran (D = 192 stays fp32 MFMA)

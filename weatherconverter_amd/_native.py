@@ -117,7 +117,7 @@ _SIGS = {
     'wc_conv_wgrad3_splits': [_I, _I, _I, _I, _I, _I],
     'wc_absmax_images': [_P, _I, _I, _I, _I, _P, _P],
     'wc_attention_bwd6': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
-    'wc_attention_bwd_f16x3': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P, _P],
+    'wc_attention_bwd_f16x3': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P, _P, _P],
     'wc_attention_bwd_prep': [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P],
     'wc_pack_split': [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _P],
     'wc_wgrad_reduce': [_P, _I, _I, _I, _I, _I, _I, _P, _L, _L, _L, _P, _L, _I, _P],

@@ -230,7 +230,7 @@ template <int D, bool F3, int DS = 1>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
-    int eq, int ek, int ev, const float* __restrict__ dobound) {
+    int eq, int ek, int ev, const float* __restrict__ dobound, float* __restrict__ amx) {
     using Cf = B6Cfg<D, F3>;
     constexpr int NP = Cf::NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages: Q, dO tiles, lse, Dv
@@ -331,6 +331,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
         __syncthreads();
     }
 
+    float vmax = 0.f;
     if (key < N) {
         const float kun = scale * ldexpf(1.f, -(sc.eq + sc.eds)), vun = ldexpf(1.f, -(sc.edo + sc.ep));
         float* row = dqkv + ((long)b * N + key) * lddq;
@@ -339,20 +340,24 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r += 4) {
                 const int dv = (db0 + d) * 32 + 8 * (r >> 2) + 4 * half;
-                *reinterpret_cast<f32x4*>(row + kcol + dv) =
-                    f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * kun;
-                const f32x4 vv = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
-                *reinterpret_cast<f32x4*>(row + vcol + dv) = F3 ? vv * vun : vv;
+                const f32x4 kk = f32x4{dkT[d][r], dkT[d][r + 1], dkT[d][r + 2], dkT[d][r + 3]} * kun;
+                const f32x4 vv0 = f32x4{dvT[d][r], dvT[d][r + 1], dvT[d][r + 2], dvT[d][r + 3]};
+                const f32x4 vv = F3 ? vv0 * vun : vv0;
+                *reinterpret_cast<f32x4*>(row + kcol + dv) = kk;
+                *reinterpret_cast<f32x4*>(row + vcol + dv) = vv;
+                vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(fabsf(kk.x), fabsf(kk.y)), fmaxf(fabsf(kk.z), fabsf(kk.w))),
+                                         fmaxf(fmaxf(fabsf(vv.x), fabsf(vv.y)), fmaxf(fabsf(vv.z), fabsf(vv.w)))));
             }
         }
     }
+    if (amx) block_absmax_atomic(amx, b, vmax);  // the workgroup is one image
 }
 
 template <int D, bool F3, int DS = 1>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
-    int eq, int ek, int ev, const float* __restrict__ dobound) {
+    int eq, int ek, int ev, const float* __restrict__ dobound, float* __restrict__ amx) {
     using Cf = B6Cfg<D, F3>;
     constexpr int NP = Cf::NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // 2 stages: K, V tiles
@@ -438,6 +443,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
         __syncthreads();
     }
 
+    float vmax = 0.f;
     if (qme < N) {
         const float qun = scale * ldexpf(1.f, -(sc.ek + sc.eds));
         float* row = dqkv + ((long)b * N + qme) * lddq + qcol;
@@ -446,16 +452,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r += 4) {
                 const int dv = (db0 + d) * 32 + 8 * (r >> 2) + 4 * half;
-                *reinterpret_cast<f32x4*>(row + dv) = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * qun;
+                const f32x4 qq = f32x4{dqT[d][r], dqT[d][r + 1], dqT[d][r + 2], dqT[d][r + 3]} * qun;
+                *reinterpret_cast<f32x4*>(row + dv) = qq;
+                vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(qq.x), fabsf(qq.y)), fmaxf(fabsf(qq.z), fabsf(qq.w))));
             }
         }
     }
+    if (amx) block_absmax_atomic(amx, b, vmax);
 }
 
 template <int D, bool F3, int DS = 1>
 int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
                 int lddq, int B, int N, int C, int heads, float scale, int eq, int ek, int ev, const float* dobound,
-                hipStream_t s) {
+                float* amx, hipStream_t s) {
     using Cf = B6Cfg<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -471,11 +480,11 @@ int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const floa
     const float scale_log2 = scale * 1.4426950408889634f;
     WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D), WC_TB(F3)});
     hipLaunchKernelGGL((attn_bwd6_dkdv_kernel<D, F3, DS>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
-                       lddq, N, C, scale_log2, scale, eq, ek, ev, dobound);
+                       lddq, N, C, scale_log2, scale, eq, ek, ev, dobound, amx);
     WC_CHECK_LAUNCH();
     WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D), WC_TB(F3)});
     hipLaunchKernelGGL((attn_bwd6_dq_kernel<D, F3, DS>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
-                       lddq, N, C, scale_log2, scale, eq, ek, ev, dobound);
+                       lddq, N, C, scale_log2, scale, eq, ek, ev, dobound, amx);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -490,7 +499,7 @@ extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* 
 static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
                                int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
                                int C, int heads, float scale, bool f3, int eq, int ek, int ev, const float* dobound,
-                               void* stream) {
+                               float* amx, void* stream) {
     if (!qkv || !out || !dout || !lse || !dv_work || !dqkv || (f3 && !dobound)) return WC_E_ARG;
     if (heads <= 0 || C % heads || B <= 0 || N <= 0) return WC_E_SHAPE;
     if (ld_qkv % 4 || ld_out % 4 || ld_dout % 4 || ld_dqkv % 4 || ld_qkv < 3 * C || ld_dqkv < 3 * C || ld_out < C ||
@@ -505,9 +514,9 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
     if (st != WC_OK) return st;
 #define WC_BWD6(DD)                                                                                                    \
     (f3 ? launch_bwd6<DD, true>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, eq, ek, \
-                                ev, dobound, s)                                                                        \
+                                ev, dobound, amx, s)                                                                   \
         : launch_bwd6<DD, false>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, 0, 0, \
-                                 0, nullptr, s))
+                                 0, nullptr, amx, s))
     switch (D) {
         case 32: return WC_BWD6(32);
         case 64: return WC_BWD6(64);
@@ -521,15 +530,15 @@ extern "C" int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out,
                                  int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
                                  int C, int heads, float scale, void* stream) {
     return attention_bwd_split(qkv, ld_qkv, out, ld_out, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
-                               scale, false, 0, 0, 0, nullptr, stream);
+                               scale, false, 0, 0, 0, nullptr, nullptr, stream);
 }
 
 // f16x3 form: eq / ek / ev the forward's exponents of Q, K, V (|Q| 2^eq <= 2^14 ...), dobound[B] the
-// per-image max |dO| (device memory).
+// per-image max |dO| (device memory); dqkv_absmax (optional, [B]) raised to the max |dqkv| written.
 extern "C" int wc_attention_bwd_f16x3(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
                                       int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B,
                                       int N, int C, int heads, float scale, int eq, int ek, int ev,
-                                      const float* dobound, void* stream) {
+                                      const float* dobound, float* dqkv_absmax, void* stream) {
     return attention_bwd_split(qkv, ld_qkv, out, ld_out, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
-                               scale, true, eq, ek, ev, dobound, stream);
+                               scale, true, eq, ek, ev, dobound, dqkv_absmax, stream);
 }

@@ -323,6 +323,7 @@ class TrainEngine:
         if tt.numel() != B:
             raise RuntimeError(f'timestep tensor has {tt.numel()} entries for a batch of {B}')
         self.tt = tt
+        self._raised: Dict[int, bool] = {}
         temb = K.temb(tt, *self.tproj, self.temb_w, self.temb_b)  # (B, P)
         self.x = x
         dc = m.down_channels
@@ -337,31 +338,43 @@ class TrainEngine:
         K.conv_in(x, m.conv_in.weight.detach().float().contiguous(), m.conv_in.bias.detach().float().contiguous(), cur)
         self.tape.append(('conv_in', cur))
 
-        def block(X: View, tgt: View, rp, att) -> View:
+        def block(X: View, tgt: View, rp, att, amx=None) -> View:
+            """amx: float32[B] the final writer of tgt raises to its per-image max |value| (the bound a
+            following down / up conv needs); left zero when that writer is not an f16x3 kernel."""
             if att is None:
-                self._res_fwd(X, tgt, rp, temb)
+                self._res_fwd(X, tgt, rp, temb, amx)
             else:
                 ypre = View.full(self._new(B, X.H, X.W, rp['co']))
                 self._res_fwd(X, ypre, rp, temb)
-                self._attn_fwd(ypre, tgt, att)
+                self._attn_fwd(ypre, tgt, att, amx)
             return tgt
+
+        def new_amx():
+            return torch.zeros((B, ), dtype=torch.float32, device=self.device) if (self.f3 or self.f3d) else None
+
+        def bound_of(v: View, amx):
+            """The producer-raised bound when it was raised (nonzero), else a pass over v."""
+            if amx is None:
+                return None
+            return amx if self._raised.pop(id(amx), False) else K.absmax_images(v)
 
         for i in range(L):
             res, att = self.downs[i]
             H, W = sizes[i]
             final = View(U[i + 1], dc[i + 1], dc[i + 1]) if i < L - 1 else View.full(
                 self._new(B, sizes[i + 1][0], sizes[i + 1][1], dc[i + 1]))
+            amx = new_amx() if self.down_pk[i] is not None else None
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
                 tgt = final if (last and self.down_pk[i] is None) else View.full(self._new(B, H, W, rp['co']))
-                cur = block(cur, tgt, rp, att[li] if att else None)
+                cur = block(cur, tgt, rp, att[li] if att else None, amx if last else None)
             if self.down_pk[i] is not None:
                 dp = self.down_pk[i]
                 seg = Seg(cur, TAPS4S2, stride=2)
                 bd = dp['mod'].bias.detach().float().contiguous()
                 Hm, Wm = sizes[i + 1]
                 f3 = dp['f3'] is not None and K.conv4x4s2_f16x3_ok(seg, final.C, Hm, Wm)
-                bcur = K.absmax_images(cur) if (f3 or self.f3d) else None  # also the weight gradient's bound
+                bcur = bound_of(cur, amx)  # the conv's A bound and the weight gradient's
                 if f3:
                     K.conv4x4s2_f16x3(seg, dp['f3'], bd, final, Hm=Hm, Wm=Wm, a_bound=bcur)
                 else:
@@ -369,19 +382,23 @@ class TrainEngine:
                 self.tape.append(('down', cur, final, dp, bcur))
                 cur = final
 
+        amx = None
         for j, (res, att) in enumerate(self.mids):
             last_mid = j == len(self.mids) - 1
             H, W = cur.H, cur.W
             for li, rp in enumerate(res):
-                if last_mid and li == len(res) - 1 and self.up_pk[0] is None:
+                last = last_mid and li == len(res) - 1
+                if last and self.up_pk[0] is None:
                     tgt = View(U[L - 1], 0, dc[L - 1])
                 else:
                     tgt = View.full(self._new(B, H, W, rp['co']))
-                self._res_fwd(cur, tgt, rp, temb)
+                if last and self.up_pk[0] is not None:
+                    amx = new_amx()
+                self._res_fwd(cur, tgt, rp, temb, amx if last and li >= len(att) else None)
                 cur = tgt
                 if li < len(att):
                     nxt = View.full(self._new(B, H, W, rp['co']))
-                    self._attn_fwd(cur, nxt, att[li])
+                    self._attn_fwd(cur, nxt, att[li], amx if last else None)
                     cur = nxt
 
         for k, (res, att) in enumerate(self.ups):
@@ -392,7 +409,7 @@ class TrainEngine:
                 dst = View(U[i], 0, dc[i])
                 b = up['mod'].bias.detach().float().contiguous()
                 f3 = up['f3'] is not None and K.convT4x4s2_f16x3_ok(Seg(cur, [(0, 0)]), dst.C)
-                bcur = K.absmax_images(cur) if (f3 or self.f3d) else None
+                bcur = bound_of(cur, amx)
                 if f3:
                     K.convT4x4s2_f16x3(Seg(cur, [(0, 0)]), up['f3'], b, dst, a_bound=bcur)
                 else:
@@ -403,11 +420,12 @@ class TrainEngine:
                 assert cur.t is U[i] and cur.c0 == 0, 'non-upsampling level must have been written in place'
             cur = View.full(U[i])
             next_in_place = i > 0 and self.up_pk[k + 1] is None
+            amx = new_amx() if k + 1 < len(self.ups) and self.up_pk[k + 1] is not None else None
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
                 tgt = View(U[i - 1], 0, dc[i - 1]) if (last and next_in_place) else View.full(
                     self._new(B, H, W, rp['co']))
-                cur = block(cur, tgt, rp, att[li] if att else None)
+                cur = block(cur, tgt, rp, att[li] if att else None, amx if last else None)
 
         # head: GN -> SiLU -> conv_out, NCHW output
         gn = m.norm_out
@@ -420,7 +438,7 @@ class TrainEngine:
         self.tape = []
         return out
 
-    def _res_fwd(self, X: View, Y: View, rp, temb: torch.Tensor):
+    def _res_fwd(self, X: View, Y: View, rp, temb: torch.Tensor, amx: Optional[torch.Tensor] = None):
         B, H, W = X.B, X.H, X.W
         g1, g2 = rp['gn1'], rp['gn2']
         co = rp['co']
@@ -439,12 +457,14 @@ class TrainEngine:
         if rp['f3_2'] is not None and K.x6_eligible(seg2, co, H, W):
             # the residual segment (raw X) in fp16 under GN1's per-image bound of |X|
             K.conv3x3_f16x3(seg2, rp['f3_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
-                            a_bound=st1[4])
+                            a_bound=st1[4], absmax=amx)
+            if amx is not None:
+                self._raised[id(amx)] = True
         else:
             self._conv(seg2, rp['pk2'], rp['b2'], Y, H, W)
         self.tape.append(('res', X, h, Y, rp, st1[:4], st2, st1[4]))
 
-    def _attn_fwd(self, Ypre: View, Yout: View, ap):
+    def _attn_fwd(self, Ypre: View, Yout: View, ap, amx: Optional[torch.Tensor] = None):
         B, H, W, C = Ypre.B, Ypre.H, Ypre.W, Ypre.C
         N = H * W
         gn, mha = ap['gn'], ap['mha']
@@ -464,7 +484,9 @@ class TrainEngine:
             K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'],
                                 precision='f16x3', exps=exps)
             K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], ap['f3_out'], b_out, Yout, Hm=H, Wm=W, a_exp=exps[2],
-                               res=Ypre)
+                               res=Ypre, absmax=amx)
+            if amx is not None:
+                self._raised[id(amx)] = True
         else:
             self._conv(seg, ap['pk_in'], b_in, View.full(qkv), H, W)
             K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'],
@@ -611,17 +633,22 @@ class TrainEngine:
         else:
             self._conv([Seg(gY, TAPS1)], ap['pk_outT'], None, View.full(do), H, W, absmax=bdo)
         dqkv = self._new(B, H, W, 3 * C)
+        bgq = None
         if f3a:
-            # f16x3 under the forward's Q / K / V exponents and the per-image max |dO|
-            K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
-                            B, N, C, ap['heads'], precision='f16x3', exps=exps,
-                            dout_bound=self._bound(View.full(do), bdo))
+            # f16x3 under the forward's Q / K / V exponents and the per-image max |dO|; the kernels raise
+            # the per-image max |dqkv| as they write it (head dims 32 / 64 / 128)
+            bgq = torch.zeros((B, ), dtype=torch.float32, device=self.device)
+            if not K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse,
+                                   dqkv.view(B * N, 3 * C), B, N, C, ap['heads'], precision='f16x3', exps=exps,
+                                   dout_bound=self._bound(View.full(do), bdo), dqkv_absmax=bgq):
+                bgq = None
         else:
             K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse, dqkv.view(B * N, 3 * C),
                             B, N, C, ap['heads'], precision=self.precision)
         gq = View.full(dqkv)
         self._bias_grad(gq, mha.in_proj_bias)
-        bgq = K.absmax_images(gq) if (f3a or f3p) else None
+        if f3a or f3p:
+            bgq = self._bound(gq, bgq) if bgq is not None else K.absmax_images(gq)
         self._wgrad(gq, [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)], self._pgrad(mha.in_proj_weight),
                     (C, 1, 0), f3=K.F3Bounds(bgq, K.f16x3_a_exp(*ap['gb'], N * C // 8)) if f3a else None)
         da = View.full(self._new(B, H, W, C))

@@ -1248,12 +1248,13 @@ def attention_bwd_f16x3_enabled() -> bool:
 
 def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, dqkv: torch.Tensor,
                   B: int, N: int, C: int, heads: int, precision: str = 'fp32', exps: Optional[Tuple[int, int, int]] = None,
-                  dout_bound: Optional[torch.Tensor] = None):
+                  dout_bound: Optional[torch.Tensor] = None, dqkv_absmax: Optional[torch.Tensor] = None) -> bool:
     """d qkv (same [q | k | v] rows as qkv) of softmax(Q K^T / sqrt(d)) V from the forward's output and lse:
     fp32 MFMA (wc_attention_bwd), or with precision 'bf16x6' / 'f16x3' and a head dim in {32, 64, 128}
     the split-precision kernels: f16x3 (wc_attention_bwd_f16x3) when the Q / K / V exponents of the
     forward (exps) and the per-image max |dout| (dout_bound, device float32 [B]) are given, else
-    bf16x6 (wc_attention_bwd6)."""
+    bf16x6 (wc_attention_bwd6).  dqkv_absmax: float32 [B] raised to the max |dqkv| written per image
+    by the f16x3 kernels; returns whether it was (else the caller measures the bound itself)."""
     for t_, w in ((qkv, 3 * C), (out, C), (dout, C), (dqkv, 3 * C)):
         _req(t_.is_cuda and t_.dtype == torch.float32 and t_.is_contiguous() and t_.numel() == B * N * w,
              'attention backward operands')
@@ -1265,12 +1266,15 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
         if precision == 'f16x3' and exps is not None and dout_bound is not None and attention_bwd_f16x3_enabled():
             _req(dout_bound.is_cuda and dout_bound.dtype == torch.float32 and dout_bound.numel() >= B,
                  'dout_bound: float32 [B] on the device')
+            if dqkv_absmax is not None:
+                _req(_bound_ok(dqkv_absmax, B), 'dqkv_absmax: float32 [B] on the device')
             _timed(f'attention_bwd<{d}>', 'wc_attention_bwd_f16x3', 10.0 * B * N * N * C, *args, int(exps[0]),
-                   int(exps[1]), int(exps[2]), dout_bound.data_ptr(), _stream())
-            return
+                   int(exps[1]), int(exps[2]), dout_bound.data_ptr(), _ptr(dqkv_absmax), _stream())
+            return dqkv_absmax is not None
         _timed(f'attention_bwd<{d}>', 'wc_attention_bwd6', 10.0 * B * N * N * C, *args, _stream())
-        return
+        return False
     _timed(f'attention_bwd<{d}>', 'wc_attention_bwd', 10.0 * B * N * N * C, *args, _stream())
+    return False
 
 
 def gemm_small(M: int, N: int, K: int, A: torch.Tensor, sa: Tuple[int, int], Bm: torch.Tensor, sb: Tuple[int, int],

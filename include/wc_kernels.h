@@ -479,8 +479,14 @@ int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out
 /* The same backward on f16x3 (two round-to-nearest fp16 pieces per operand, three products per block):
  * Q, K, V scaled by 2^eq, 2^ek, 2^ev — the training forward's exponents from the in-projection bounds
  * (|Q| 2^eq <= 2^14 ...); dO by 2^edo from dobound[b] = per-image max |dO| (device, wc_absmax_images);
- * P by 2^14; dS by 2^eds with the bound |dS| <= 2 d max|dO| max|V|.  Head dim in {32, 64, 128}.
+ * P by 2^14; dS by 2^eds with the bound |dS| <= 2 d max|dO| max|V|.  Head dim in {32, 64, 128}, or 192
+ * (dQ on f16x3, dK / dV on fp32 MFMA; dqkv_absmax must then be NULL).
  * dqkv_absmax (optional, [B], caller-zeroed): raised to the max |dqkv| written per image. */
+/* The fp32-MFMA dK / dV kernel of wc_attention_bwd alone, head dim 192, after wc_attention_bwd_prep:
+ * wc_attention_bwd_f16x3 pairs it with its f16x3 dQ kernel at that width. */
+int wc_attention_bwd_dkdv192(const float* qkv, int ld_qkv, const float* dout, int ld_dout, const float* lse,
+                             const float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C, int heads,
+                             float scale, void* stream);
 int wc_attention_bwd_f16x3(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
                            int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
                            int C, int heads, float scale, int eq, int ek, int ev, const float* dobound,

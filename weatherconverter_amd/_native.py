@@ -26,7 +26,7 @@ EXPORTS = [
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
     'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name',
     'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse',
-    'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_prep', 'wc_pack_split'
+    'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_dkdv192', 'wc_attention_bwd_prep', 'wc_pack_split'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
@@ -118,6 +118,7 @@ _SIGS = {
     'wc_absmax_images': [_P, _I, _I, _I, _I, _P, _P],
     'wc_attention_bwd6': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_bwd_f16x3': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P, _P, _P],
+    'wc_attention_bwd_dkdv192': [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
     'wc_attention_bwd_prep': [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P],
     'wc_pack_split': [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _P],
     'wc_wgrad_reduce': [_P, _I, _I, _I, _I, _I, _I, _P, _L, _L, _L, _P, _L, _I, _P],

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restr
 
 template <int D>
 int launch_bwd(const float* qkv, int ldq, const float* dO, int lddo, const float* lse, const float* Dv, float* dqkv,
-               int lddq, int B, int N, int C, int heads, float scale, hipStream_t s) {
+               int lddq, int B, int N, int C, int heads, float scale, hipStream_t s, int parts = 3) {
     using Cf = BwdCfg<D>;
     const size_t lds = (size_t)Cf::LDS_FLOATS * sizeof(float);
     static bool attr_set = false;
@@ -284,12 +284,18 @@ int launch_bwd(const float* qkv, int ldq, const float* dO, int lddo, const float
     }
     const dim3 grid((N + 127) / 128, heads, B);
     const float scale_log2 = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, grid, dim3(256), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N, C,
-                       scale_log2, scale);
-    WC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(256), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N, C,
-                       scale_log2, scale);
-    WC_CHECK_LAUNCH();
+    if (parts & 1) {
+        WC_SET_NAME("attn_bwd_dkdv_kernel", {WC_TI(D)});
+        hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, grid, dim3(256), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N,
+                           C, scale_log2, scale);
+        WC_CHECK_LAUNCH();
+    }
+    if (parts & 2) {
+        WC_SET_NAME("attn_bwd_dq_kernel", {WC_TI(D)});
+        hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(256), lds, s, qkv, ldq, dO, lddo, lse, Dv, dqkv, lddq, N,
+                           C, scale_log2, scale);
+        WC_CHECK_LAUNCH();
+    }
     return WC_OK;
 }
 
@@ -334,4 +340,16 @@ extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* 
                        reinterpret_cast<hipStream_t>(stream), out, ld_out, dout, ld_dout, B, N, heads, D, dv_work);
     WC_CHECK_LAUNCH();
     return WC_OK;
+}
+
+// The fp32-MFMA dK / dV kernel alone at head dim 192, after wc_attention_bwd_prep (the f16x3 backward
+// runs its dQ kernel beside it: wc_attention_bwd6.hip).
+extern "C" int wc_attention_bwd_dkdv192(const float* qkv, int ld_qkv, const float* dout, int ld_dout, const float* lse,
+                                        const float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C,
+                                        int heads, float scale, void* stream) {
+    if (!qkv || !dout || !lse || !dv_work || !dqkv) return WC_E_ARG;
+    if (heads <= 0 || C != 192 * heads || B <= 0 || N <= 0) return WC_E_SHAPE;
+    if (ld_qkv % 4 || ld_dout % 4 || ld_dqkv % 4 || ld_qkv < 3 * C || ld_dqkv < 3 * C || ld_dout < C) return WC_E_SHAPE;
+    return launch_bwd<192>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale,
+                           reinterpret_cast<hipStream_t>(stream), 1);
 }

@@ -495,6 +495,9 @@ int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const floa
 // (wc_attention_bwd6 runs it itself through wc_attention_bwd_prep).
 extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* dout, int ld_dout, int B, int N,
                                      int heads, int D, float* dv_work, void* stream);
+extern "C" int wc_attention_bwd_dkdv192(const float* qkv, int ld_qkv, const float* dout, int ld_dout, const float* lse,
+                                        const float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C,
+                                        int heads, float scale, void* stream);
 
 static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
                                int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
@@ -521,7 +524,30 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
         case 32: return WC_BWD6(32);
         case 64: return WC_BWD6(64);
         case 128: return WC_BWD6(128);
-        default: return WC_E_SHAPE;  // D = 192: the own K / V rows spill even with the output dims split (DS)
+        case 192: {
+            // f16x3 only: dQ with the output dims in three parts (its own Q / dO rows fit at a third of
+            // the accumulators); dK / dV on the fp32-MFMA kernel (its own K and V rows spill in the split
+            // forms even with the outputs split), which raises no bound: amx stays the caller's job
+            if (!f3 || amx) return WC_E_SHAPE;
+            st = wc_attention_bwd_dkdv192(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale,
+                                          stream);
+            if (st != WC_OK) return st;
+            using Cf = B6Cfg<192, true>;
+            static bool attr_set = false;
+            if (!attr_set) {
+                hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<192, true, 3>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+                if (e != hipSuccess) return (int)e;
+                attr_set = true;
+            }
+            WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(192), WC_TB(true)});
+            hipLaunchKernelGGL((attn_bwd6_dq_kernel<192, true, 3>), dim3((N + 127) / 128 * 3, heads, B), dim3(256),
+                               Cf::LDS, s, qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, N, C,
+                               scale * 1.4426950408889634f, scale, eq, ek, ev, dobound, nullptr);
+            WC_CHECK_LAUNCH();
+            return WC_OK;
+        }
+        default: return WC_E_SHAPE;
     }
 #undef WC_BWD6
 }

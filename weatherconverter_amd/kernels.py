@@ -1262,8 +1262,14 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
     dv = torch.empty(B * heads * N, dtype=torch.float32, device=qkv.device)
     args = (qkv.data_ptr(), 3 * C, out.data_ptr(), C, dout.data_ptr(), C, lse.data_ptr(), dv.data_ptr(),
             dqkv.data_ptr(), 3 * C, B, N, C, heads, float(d**-0.5))
+    f3ok = precision == 'f16x3' and exps is not None and dout_bound is not None and attention_bwd_f16x3_enabled()
+    if d == 192 and f3ok and attention_bwd6_enabled():  # dQ on f16x3, dK / dV on fp32 MFMA (no bound raised)
+        _req(_bound_ok(dout_bound, B), 'dout_bound: float32 [B] on the device')
+        _timed(f'attention_bwd<{d}>', 'wc_attention_bwd_f16x3', 10.0 * B * N * N * C, *args, int(exps[0]),
+               int(exps[1]), int(exps[2]), dout_bound.data_ptr(), None, _stream())
+        return False
     if precision != 'fp32' and d in (32, 64, 128) and attention_bwd6_enabled():
-        if precision == 'f16x3' and exps is not None and dout_bound is not None and attention_bwd_f16x3_enabled():
+        if f3ok:
             _req(dout_bound.is_cuda and dout_bound.dtype == torch.float32 and dout_bound.numel() >= B,
                  'dout_bound: float32 [B] on the device')
             if dqkv_absmax is not None:

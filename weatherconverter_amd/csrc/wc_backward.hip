@@ -739,6 +739,26 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(int M, int N, int K, co
     *c = beta != 0.f ? alpha * s + beta * *c : alpha * s;
 }
 
+// The same with one wave per output for long K (the time-embedding input gradient: K = all ResBlock
+// channels): lanes stride K, then a fixed butterfly (deterministic).
+__global__ __launch_bounds__(256) void gemm_small_wave_kernel(int M, int N, int K, const float* __restrict__ A, long sam,
+                                                              long sak, const float* __restrict__ Bm, long sbk,
+                                                              long sbn, float* __restrict__ Cm, long ldc, float alpha,
+                                                              float beta) {
+    const long o = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (o >= (long)M * N) return;
+    const int m = (int)(o / N), n = (int)(o - (long)m * N);
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s = fmaf(A[m * sam + k * sak], Bm[k * sbk + n * sbn], s);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) {
+        float* c = Cm + m * ldc + n;
+        *c = beta != 0.f ? alpha * s + beta * *c : alpha * s;
+    }
+}
+
 // mode 0: out = silu(y); mode 1: out = dz * silu'(y)
 __global__ __launch_bounds__(256) void silu_kernel(const float* __restrict__ y, const float* __restrict__ dz,
                                                    float* __restrict__ out, long n, int mode) {
@@ -1008,6 +1028,14 @@ extern "C" int wc_gemm_small(int M, int N, int K, const float* A, int64_t sam, i
                              int64_t sbn, float* Cm, int64_t ldc, float alpha, float beta, void* stream) {
     if (!A || !Bm || !Cm) return WC_E_ARG;
     if (M <= 0 || N <= 0 || K <= 0) return WC_E_SHAPE;
+    if (K >= 256) {
+        wc_last_kernel = "gemm_small_wave_kernel";
+        hipLaunchKernelGGL(gemm_small_wave_kernel, dim3(blocks_for((long)M * N, 4)), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), M, N, K, A, (long)sam, (long)sak, Bm, (long)sbk,
+                           (long)sbn, Cm, (long)ldc, alpha, beta);
+        WC_CHECK_LAUNCH();
+        return WC_OK;
+    }
     hipLaunchKernelGGL(gemm_small_kernel, dim3(blocks_for((long)M * N, 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), M, N, K, A, (long)sam, (long)sak, Bm, (long)sbk,
                        (long)sbn, Cm, (long)ldc, alpha, beta);

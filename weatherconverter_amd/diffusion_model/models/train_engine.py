@@ -303,9 +303,12 @@ class TrainEngine:
         return tracked
 
     def _pgrad(self, p: torch.nn.Parameter) -> torch.Tensor:
+        """p's gradient: a view into one zeroed buffer holding every parameter's (one fill per backward
+        instead of one per parameter)."""
         g = self.pgrads.get(id(p))
         if g is None:
-            g = torch.zeros_like(p, dtype=torch.float32)
+            o, n = self.pflat_off[id(p)]
+            g = self.pflat[o:o + n].view(p.shape)
             self.pgrads[id(p)] = g
         return g
 
@@ -514,6 +517,12 @@ class TrainEngine:
         self.gmap: Dict[int, Tuple[torch.Tensor, int]] = {}
         self.gbnd: Dict[int, torch.Tensor] = {}
         self.pgrads: Dict[int, torch.Tensor] = {}
+        self.pflat_off: Dict[int, Tuple[int, int]] = {}
+        tot = 0
+        for prm in m.parameters():
+            self.pflat_off[id(prm)] = (tot, prm.numel())
+            tot += (prm.numel() + 63) // 64 * 64  # 256-byte aligned views
+        self.pflat = torch.zeros(tot, dtype=torch.float32, device=self.device)
         self.keep = []
         B = gout.shape[0]
         self.dproj = torch.zeros((B, self.P), dtype=torch.float32, device=self.device)
@@ -527,7 +536,8 @@ class TrainEngine:
         self.keep = []
         for f in Tape._FIELDS[1:]:  # the tape's tensors die with it, not with the engine
             setattr(self, f, None)
-        return self.pgrads
+        grads, self.pgrads, self.pflat = self.pgrads, {}, None
+        return grads
 
     @staticmethod
     def _dgrad3_ok(g: View, n_out: int) -> bool:
@@ -759,4 +769,8 @@ class UnetTrainFunction(torch.autograd.Function):
     def backward(ctx, gout):
         grads = ctx.engine.backward(gout, ctx.tape)
         ctx.tape = None
-        return (None, None, None) + tuple(grads.get(i) for i in ctx.param_ids)
+        # hand autograd the only references, so it can take each gradient as param.grad instead of
+        # copying it
+        out = tuple(grads.pop(i, None) for i in ctx.param_ids)
+        del grads
+        return (None, None, None) + out

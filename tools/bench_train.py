@@ -35,6 +35,8 @@ def main():
     ap.add_argument('--seed', type=int, default=3455)
     ap.add_argument('--mode', default='step', choices=['step', 'forward'])
     ap.add_argument('--profile', action='store_true', help='per-kernel-class event times of one step')
+    ap.add_argument('--precision', default='fp32-class', choices=['fp32-class', 'f16'],
+                    help="'f16': the 16-bit training line (Unet.set_train_precision('f16'), single-piece build)")
     args = ap.parse_args()
     if args.mode == 'step':
         return train_step(args)
@@ -83,6 +85,15 @@ def main():
     }))
 
 
+DTYPES = {
+    'fp32-class': 'fp32-class (f16x3: forward convs, projections, attention; data and weight gradients and the '
+                  'attention backward under per-image range bounds raised by the gradients\' writers; bf16x6 where '
+                  'no bound exists; fp32 MFMA for the dK/dV of head dim 192)',
+    'f16': '16-bit line (the f16x3 kernels with one fp16 piece per operand, fp32 accumulation, power-of-two range '
+           'scaling; bf16x6 / fp32 MFMA where no bound exists) -- the analog of the reference\'s bf16 training',
+}
+
+
 def train_step(args):
     from weatherconverter_amd import kernels
     from weatherconverter_amd.diffusion_model.config import model_config
@@ -93,6 +104,8 @@ def train_step(args):
     mc = model_config(args.size)
     net = Unet(mc)
     init_synthetic_(net, seed=0)
+    if args.precision == 'f16':
+        net.set_train_precision('f16')
     net = net.to(dev).train()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)  # train_ddpm.py:176 (lr from config.yaml)
     crit = torch.nn.MSELoss()
@@ -154,11 +167,10 @@ def train_step(args):
         'ms_forward': round(fwd, 2), 'ms_backward': round(bwd, 2), 'ms_adam_and_host': round(ms - fwd - bwd, 2),
         'images_per_s': round(B * args.steps / el, 2), 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
         'higher_is_better': True,
-        'dtype': 'fp32-class (f16x3: forward convs, projections, attention, and the data gradients under per-image '
-                 'absmax bounds; bf16x6: weight gradients, attention backward (fp32 MFMA at head dim 192))',
+        'dtype': DTYPES[args.precision],
         'data': 'synthetic (keyed random-init weights; images U[-1,1], Philox N(0,1) noise, t ~ U[0,1000))',
         'config': {'workload': 'BASELINE config 3 full training iteration', 'global_batch': B, 'image_size': S,
-                   'backward': True, 'optimizer': 'torch.optim.Adam lr 1e-4'},
+                   'backward': True, 'optimizer': 'torch.optim.Adam lr 1e-4', 'precision': args.precision},
         'train_tflops_algorithmic': round(3 * GFLOP_PER_IMAGE_STEP_256 * B / (ms * 1e-3) / 1e3, 1) if S == 256 else None,
         'loss_finite': bool(torch.isfinite(ls).all()), 'loss_first': float(ls[0]), 'loss_last': float(ls[-1]),
         'kernel_classes': prof,

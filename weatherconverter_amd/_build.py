@@ -21,6 +21,11 @@ ARCH = os.environ.get('WC_OFFLOAD_ARCH', 'gfx950')
 
 SOURCES = ['wc_conv.hip', 'wc_conv6.hip', 'wc_igemm6.hip', 'wc_gn.hip', 'wc_attention.hip', 'wc_attention6.hip', 'wc_misc.hip', 'wc_old.hip', 'wc_train.hip', 'wc_srgan.hip', 'wc_backward.hip', 'wc_attention_bwd.hip', 'wc_wgrad3.hip', 'wc_attention_bwd6.hip', 'wc_pack.hip']
 HEADERS = ['wc_common.hpp', 'wc_x6.hpp']
+# The single-piece build (the 16-bit training line): the sources holding f16x3 correction products
+# recompiled with -DWC_SINGLE16=1 (wc_x6.hpp: mfma_f16c), every other object shared.
+SINGLE16_SOURCES = ['wc_conv6.hip', 'wc_igemm6.hip', 'wc_attention6.hip', 'wc_wgrad3.hip', 'wc_backward.hip',
+                    'wc_attention_bwd6.hip']
+SINGLE16_LIB_PATH = os.path.join(LIBDIR, 'libwc_kernels_single16.so')
 
 CFLAGS = [
     '-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-munsafe-fp-atomics',
@@ -35,8 +40,9 @@ def _stale(obj, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
-    os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
+def build(verbose: bool = False, force: bool = False, single16: bool = True) -> str:
+    """Build libwc_kernels.so (and, with single16, libwc_kernels_single16.so); returns the first's path."""
+    os.makedirs(os.path.join(LIBDIR, 'obj', 'single16'), exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'wc_kernels.h')]
     jobs = []
     objs = []
@@ -46,6 +52,17 @@ def build(verbose: bool = False, force: bool = False) -> str:
         objs.append(obj)
         if force or _stale(obj, [sp] + hdrs):
             jobs.append([HIPCC] + CFLAGS + ['-c', sp, '-o', obj])
+    objs16 = []
+    if single16:
+        for src in SOURCES:
+            if src not in SINGLE16_SOURCES:
+                objs16.append(os.path.join(LIBDIR, 'obj', src.replace('.hip', '.o')))
+                continue
+            sp = os.path.join(CSRC, src)
+            obj = os.path.join(LIBDIR, 'obj', 'single16', src.replace('.hip', '.o'))
+            objs16.append(obj)
+            if force or _stale(obj, [sp] + hdrs):
+                jobs.append([HIPCC] + CFLAGS + ['-DWC_SINGLE16=1', '-c', sp, '-o', obj])
 
     def run(cmd):
         if verbose:
@@ -57,16 +74,19 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    if jobs or force or _stale(LIB_PATH, objs):
-        run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', LIB_PATH] + objs)
-        # A kernel whose body the host pass rejects (a device-only builtin used directly in a
-        # __global__ template) loses its host stub without any diagnostic and the library then
-        # fails to load: refuse to produce such a library.
-        nm = subprocess.run(['nm', '-D', '--undefined-only', LIB_PATH], capture_output=True, text=True)
-        lost = [ln.split()[-1] for ln in nm.stdout.splitlines() if '_GLOBAL__N_' in ln]
-        if lost:
-            os.remove(LIB_PATH)
-            raise RuntimeError(f'{len(lost)} kernel stub(s) missing from the library, e.g. {lost[0]}')
+    for path, lobjs in ((LIB_PATH, objs), (SINGLE16_LIB_PATH, objs16)):
+        if not lobjs:
+            continue
+        if jobs or force or _stale(path, lobjs):
+            run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', path] + lobjs)
+            # A kernel whose body the host pass rejects (a device-only builtin used directly in a
+            # __global__ template) loses its host stub without any diagnostic and the library then
+            # fails to load: refuse to produce such a library.
+            nm = subprocess.run(['nm', '-D', '--undefined-only', path], capture_output=True, text=True)
+            lost = [ln.split()[-1] for ln in nm.stdout.splitlines() if '_GLOBAL__N_' in ln]
+            if lost:
+                os.remove(path)
+                raise RuntimeError(f'{len(lost)} kernel stub(s) missing from the library, e.g. {lost[0]}')
     return LIB_PATH
 
 

@@ -4,8 +4,10 @@ There is deliberately no CPU fallback: every product entry point goes through th
 missing or failing library raises.  ``torch`` is imported before the library is opened so the HIP
 runtime torch ships (soname ``libamdhip64.so.7``) is the one the kernels bind to.
 """
+import contextlib
 import ctypes
 import os
+import threading
 
 import torch  # noqa: F401  (loads the HIP runtime first)
 
@@ -136,20 +138,38 @@ _SIGS = {
     'wc_nchw_to_nhwc': [_P, _I, _I, _I, _I, _P, _I, _P],
 }
 
-_lib = None
+_libs = {}
+_active = threading.local()
 
 
-def lib_path() -> str:
-    """The in-tree library; WC_KERNEL_LIB points at another build (developer experiments only)."""
+def lib_path(variant: str = '') -> str:
+    """The in-tree library (variant 'single16': the single-piece build); WC_KERNEL_LIB points at
+    another build of the default one (developer experiments only)."""
+    if variant == 'single16':
+        return _build.SINGLE16_LIB_PATH
     return os.environ.get('WC_KERNEL_LIB', _build.LIB_PATH)
 
 
+@contextlib.contextmanager
+def variant(name: str):
+    """Route every kernel call of this thread to a library variant inside the block ('' = default,
+    'single16' = the single-piece f16 build).  Both libraries stay loaded side by side (RTLD_LOCAL)."""
+    prev = getattr(_active, 'v', '')
+    _active.v = name
+    try:
+        yield
+    finally:
+        _active.v = prev
+
+
 def load(build_if_missing: bool = True):
-    """Open the kernel library (building it first if it is absent and hipcc exists)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    path = lib_path()
+    """Open the kernel library of the active variant (building it first if it is absent and hipcc
+    exists)."""
+    v = getattr(_active, 'v', '')
+    lib = _libs.get(v)
+    if lib is not None:
+        return lib
+    path = lib_path(v)
     if not os.path.exists(path):
         if not build_if_missing or not os.path.exists(_build.HIPCC):
             raise RuntimeError(f'weatherconverter_amd: HIP kernel library missing at {path}; run '
@@ -164,7 +184,7 @@ def load(build_if_missing: bool = True):
     lib.wc_version.restype = ctypes.c_char_p
     lib.wc_last_kernel_name.argtypes = []
     lib.wc_last_kernel_name.restype = ctypes.c_char_p
-    _lib = lib
+    _libs[v] = lib
     return lib
 
 

@@ -95,8 +95,8 @@ template <bool F3>
 WC_DEVICE void mfma_split(f32x16& acc, const u32x4 (&a)[F3 ? 2 : 3], const u32x4 (&b)[F3 ? 2 : 3]) {
     if constexpr (F3) {
         acc = mfma_f16(a[0], b[0], acc);
-        acc = mfma_f16(a[0], b[1], acc);
-        acc = mfma_f16(a[1], b[0], acc);
+        acc = mfma_f16c(a[0], b[1], acc);
+        acc = mfma_f16c(a[1], b[0], acc);
     } else {
         acc = mfma_bf16(a[0], b[0], acc);
         acc = mfma_bf16(a[0], b[1], acc);

@@ -80,8 +80,8 @@ WC_DEVICE void pieces8(const f32x16& v, int off, float sc, u32x4 (&out)[F3 ? 2 :
 }
 WC_DEVICE void mfmaP(f32x16& acc, const u32x4 (&a)[2], const u32x4 (&b)[2]) {
     acc = mfma_f16(a[0], b[0], acc);
-    acc = mfma_f16(a[0], b[1], acc);
-    acc = mfma_f16(a[1], b[0], acc);
+    acc = mfma_f16c(a[0], b[1], acc);
+    acc = mfma_f16c(a[1], b[0], acc);
 }
 
 WC_DEVICE void mfmaP(f32x16& acc, const u32x4 (&a)[3], const u32x4 (&b)[3]) {

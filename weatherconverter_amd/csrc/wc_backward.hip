@@ -324,8 +324,8 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
                     acc[mb][nb] = wcx6::mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
-                    acc[mb][nb] = wcx6::mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
-                    acc[mb][nb] = wcx6::mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_f16c(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                    acc[mb][nb] = wcx6::mfma_f16c(fa[mb][1], fb[nb][0], acc[mb][nb]);
                 }
         } else if constexpr (X6) {
             const unsigned char* a = lds + buf * STAGE + tr_a;

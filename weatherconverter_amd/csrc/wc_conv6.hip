@@ -451,8 +451,8 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
-                acc[mb][nb] = mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
-                acc[mb][nb] = mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                acc[mb][nb] = mfma_f16c(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = mfma_f16c(fa[mb][1], fb[nb][0], acc[mb][nb]);
             }
     };
     auto compute0 = [&](int hs, int toff, int bs, int tt) {
@@ -506,8 +506,8 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
-                    acc[mb][nb] = mfma_f16(fa[mb][0], wreg[set][nb][1], acc[mb][nb]);
-                    acc[mb][nb] = mfma_f16(fa[mb][1], wreg[set][nb][0], acc[mb][nb]);
+                    acc[mb][nb] = mfma_f16c(fa[mb][0], wreg[set][nb][1], acc[mb][nb]);
+                    acc[mb][nb] = mfma_f16c(fa[mb][1], wreg[set][nb][0], acc[mb][nb]);
                 }
         };
         // Chunk c uses halo buffer and weight-set parity PV = (nck0 - 1 - c) & 1, counted from the

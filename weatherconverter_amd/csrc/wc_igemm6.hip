@@ -379,8 +379,8 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
-                acc[mb][nb] = TR ? mfma_f16(fb[nb][1], fa[mb][0], acc[mb][nb]) : mfma_f16(fa[mb][0], fb[nb][1], acc[mb][nb]);
-                acc[mb][nb] = TR ? mfma_f16(fb[nb][0], fa[mb][1], acc[mb][nb]) : mfma_f16(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                acc[mb][nb] = TR ? mfma_f16c(fb[nb][1], fa[mb][0], acc[mb][nb]) : mfma_f16c(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                acc[mb][nb] = TR ? mfma_f16c(fb[nb][0], fa[mb][1], acc[mb][nb]) : mfma_f16c(fa[mb][1], fb[nb][0], acc[mb][nb]);
             }
     };
     // the data of K-step `step` is segment 0 iff step < steps0

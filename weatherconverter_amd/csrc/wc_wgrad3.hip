@@ -252,8 +252,8 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
                     for (int pc = 0; pc < Cf::NPC; ++pc) bf[pc] = tr_frag(q0 + pc * Cf::CPL * Cf::PLANE);
                     if constexpr (F3) {
                         acc[tap] = mfma_f16(af[0], bf[0], acc[tap]);
-                        acc[tap] = mfma_f16(af[0], bf[1], acc[tap]);
-                        acc[tap] = mfma_f16(af[1], bf[0], acc[tap]);
+                        acc[tap] = mfma_f16c(af[0], bf[1], acc[tap]);
+                        acc[tap] = mfma_f16c(af[1], bf[0], acc[tap]);
                     } else {
                         acc[tap] = mfma_bf16(af[0], bf[0], acc[tap]);
                         acc[tap] = mfma_bf16(af[0], bf[1], acc[tap]);

@@ -59,6 +59,21 @@ WC_DEVICE f32x16 mfma_f16(u32x4 a, u32x4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
                                                   0, 0, 0);
 }
+// A correction product of the f16x3 split (h*l or l*h).  The single-piece build (-DWC_SINGLE16=1,
+// libwc_kernels_single16.so: the 16-bit training line) drops them: every f16x3 kernel then computes
+// with one fp16 piece per operand (h*h), fp32 accumulation, the same power-of-two range scaling.
+#ifndef WC_SINGLE16
+#define WC_SINGLE16 0
+#endif
+WC_DEVICE f32x16 mfma_f16c(u32x4 a, u32x4 b, f32x16 c) {
+#if WC_SINGLE16
+    (void)a;
+    (void)b;
+    return c;
+#else
+    return mfma_f16(a, b, c);
+#endif
+}
 
 WC_DEVICE float silu_fast(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
 

@@ -88,7 +88,13 @@ class TrainEngine:
         K._native.load()
         self.model = model
         self.device = params[0].device
-        p = precision or getattr(model, 'conv_precision', None) or K.default_conv_precision()
+        p = (precision or getattr(model, 'train_precision', None) or getattr(model, 'conv_precision', None)
+             or K.default_conv_precision())
+        # 'f16': the 16-bit training line — the f16x3 arithmetic of mode f16x3 run on the single-piece
+        # build (one fp16 piece per operand: wc_x6.hpp mfma_f16c), every kernel call routed to it
+        self.variant = 'single16' if p == 'f16' else ''
+        if p == 'f16':
+            p = 'f16x3'
         # f16x3 needs range bounds that gradients do not have: the backward runs bf16x6; the forward's
         # GroupNorm-prologue convs and projections run f16x3 under their static bounds (as inference)
         self.precision = 'fp32' if p == 'fp32' else 'bf16x6'
@@ -314,6 +320,10 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, t) -> torch.Tensor:
+        with K._native.variant(self.variant):
+            return self._forward(x, t)
+
+    def _forward(self, x: torch.Tensor, t) -> torch.Tensor:
         m = self.model
         mc = m.model_config
         self._pack()
@@ -499,6 +509,11 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ backward
     def backward(self, gout: torch.Tensor, tape: Optional[Tape] = None) -> Dict[int, torch.Tensor]:
+        """Gradients of every parameter (see _backward), on this engine's library variant."""
+        with K._native.variant(self.variant):
+            return self._backward(gout, tape)
+
+    def _backward(self, gout: torch.Tensor, tape: Optional[Tape] = None) -> Dict[int, torch.Tensor]:
         """Gradients of every parameter given d loss / d output (B, C, S, S) for the forward that
         recorded ``tape`` (default: the latest forward); returns {id(param): grad}.  A tape is
         consumed (its activations freed) by its backward: a second backward through it raises."""

@@ -11,7 +11,7 @@ fp32 MFMA implicit-GEMM convolutions with fused GroupNorm+SiLU prologues, flash 
 time-embedding).  There is no CPU fallback: on a machine without the HIP library or GPU the forward
 raises.  The CPU reference restatement used to check it lives in ``oracle/`` (test-only).
 """
-from typing import List
+from typing import Optional, List
 
 import torch
 import torch.nn as nn
@@ -149,6 +149,7 @@ class Unet(nn.Module):
         self.conv_out = nn.Conv2d(self.down_channels[0], mc.im_channels, kernel_size=3, padding=1)
         self._engine = None
         self.conv_precision = None  # None = kernels.default_conv_precision()
+        self.train_precision = None  # None = conv_precision (training only: also 'f16')
 
     def level_has_attn(self, i: int) -> bool:
         """Attention placement rule of ``unet_base.py:404-405,434-435``."""
@@ -171,6 +172,18 @@ class Unet(nn.Module):
             raise ValueError(f'conv precision must be one of {kernels.CONV_PRECISIONS}')
         self.conv_precision = precision
         self._engine = None
+        self._train_engine = None
+        return self
+
+    def set_train_precision(self, precision: Optional[str]) -> 'Unet':
+        """Training arithmetic: None (= the conv precision: fp32-class), or 'f16' — the 16-bit line
+        (BASELINE config 3 trains in bf16): the f16x3 kernels with one fp16 piece per operand
+        (libwc_kernels_single16.so), fp32 accumulation, the same range scaling; gradients about 1e-3
+        relative to float64 instead of 1e-6."""
+        from ... import kernels
+        if precision is not None and precision not in kernels.CONV_PRECISIONS + ('f16', ):
+            raise ValueError(f"train precision must be None, 'f16' or one of {kernels.CONV_PRECISIONS}")
+        self.train_precision = precision
         self._train_engine = None
         return self
 

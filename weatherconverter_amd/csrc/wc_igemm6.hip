@@ -95,7 +95,9 @@ struct IgTile {
 // PA (with P1): the A operand arrives pre-scaled and pre-split in the LDS stage order
 // (wc_split_f16x3_tiled), so both operands of a K-step are 16 KiB copied HBM/L2 -> LDS by
 // LDS-DMA (4 wave-instructions per wave, no registers, no VALU) into a 3-stage ring: the copy of
-// step s + 2 is issued while step s computes, one barrier per step.
+// step s + 2 is issued while step s computes, one barrier per step.  (Measured and dropped: a 4-stage
+// ring walked in pairs of steps, one barrier per pair: 254 vs 274 TF/s at two instead of three
+// workgroups per CU -- the projections are not barrier-bound.)
 template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false, bool P1 = false,
           bool PA = false>
 __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_kernel(IgDev p) {
@@ -104,7 +106,8 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
     // PA: the 3 ring stages are distinct LDS objects, so the compiler sees that a step's fragment
     // reads cannot alias the LDS-DMA in flight into another stage (one array would make it wait
     // vmcnt(0) before every read, i.e. for the copy just issued)
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * T::STAGE];
+    // (PA: 48 KiB of stages, three workgroups per CU)
+    __shared__ __attribute__((aligned(16))) unsigned char smem[PA ? T::STAGE : 2 * T::STAGE];
     __shared__ __attribute__((aligned(16))) unsigned char smem_b[PA ? T::STAGE : 16];
     __shared__ __attribute__((aligned(16))) unsigned char smem_c[PA ? T::STAGE : 16];
 
@@ -738,9 +741,10 @@ int launch(const IgDev& d, hipStream_t stream) {
                     p.steps == p.steps0 && p.H0 == p.Hm && p.W0 == p.Wm;
     if constexpr (F3 && UNIB && PRO == 0 && ACT == WC_ACT_NONE && BM == 128 && BN == 128) {
         if (p.a3) {  // pre-split A operand: LDS-DMA pipeline, transposed accumulators (both epilogues)
-            WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(0), WC_TB(true), WC_TI(ACT), WC_TB(true), WC_TI(4), WC_TB(true), WC_TB(true), WC_TB(true)});
-            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, 0, true, ACT, true, 4, true, true, true>), grid, dim3(NT), 0,
-                               stream, p);
+            WC_SET_NAME("conv_igemm_x6_kernel", {WC_TI(BM), WC_TI(BN), WC_TI(0), WC_TB(true), WC_TI(ACT), WC_TB(true),
+                                                 WC_TI(4), WC_TB(true), WC_TB(true), WC_TB(true)});
+            hipLaunchKernelGGL((conv_igemm_x6_kernel<BM, BN, 0, true, ACT, true, 4, true, true, true>), grid, dim3(NT),
+                               0, stream, p);
             WC_CHECK_LAUNCH();
             return WC_OK;
         }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-3 evidence on the final tree: the whole GPU suite, smoke(), the full T=1000 bench (all legs),
-# rocprofv3 trace of the timed replays -> step table + reconciliation, PMC traffic, training line.
+# rocprofv3 trace of the timed replays -> step table + reconciliation, PMC traffic, training lines
+# (fp32-class and the 16-bit line).
 # usage: TAG=r03d bash tools/gpu_r3_final.sh
 TAG=${TAG:-r03d}
 mkdir -p gpurun_out
@@ -19,5 +20,7 @@ tail -1 gpurun_out/${TAG}_step_table.txt; tail -2 gpurun_out/${TAG}_reconcile.tx
 bash tools/pmc_traffic.sh > gpurun_out/${TAG}_traffic.log 2>&1
 rc=$?; echo traffic_rc=$rc; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u tools/bench_train.py --steps 5 --warmup 2 --profile > gpurun_out/${TAG}_train.log 2>&1
-rc=$?; echo train_rc=$rc; tail -1 gpurun_out/${TAG}_train.log | cut -c1-300
+rc=$?; echo train_rc=$rc; tail -1 gpurun_out/${TAG}_train.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/bench_train.py --steps 5 --warmup 2 --precision f16 > gpurun_out/${TAG}_train_f16.log 2>&1
+rc=$?; echo train_f16_rc=$rc; tail -1 gpurun_out/${TAG}_train_f16.log | cut -c1-300
 exit $rc

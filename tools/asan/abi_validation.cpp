@@ -66,13 +66,46 @@ int main() {
     EXPECT(wc_mse_loss(p, p, 0, nullptr, 1.f, ws.data(), p, nullptr), WC_E_SHAPE);
     EXPECT(wc_mse_loss(p + 1, p, 16, nullptr, 1.f, ws.data(), p, nullptr), WC_E_SHAPE);  // misaligned
 
+    // Round-3 training entry points: weight gradients, split-precision attention backward, bounds.
+    wc_wgrad_args wg;
+    std::memset(&wg, 0, sizeof(wg));
+    EXPECT(wc_conv_wgrad3(nullptr, p, 1, nullptr), WC_E_ARG);
+    EXPECT(wc_conv_wgrad3_f16x3(&wg, p, 1, 0, p, nullptr), WC_E_ARG);  // g == NULL
+    wg.g = p;
+    wg.nseg = 1;
+    wg.seg[0].src = p;
+    EXPECT(wc_conv_wgrad3_f16x3(&wg, p, 1, 0, nullptr, nullptr), WC_E_ARG);  // no gradient bound
+    EXPECT(wc_conv_wgrad3_f16x3(&wg, p, 1, 99, p, nullptr), WC_E_ARG);       // exponent out of range
+    EXPECT(wc_conv_wgrad3(&wg, p, 1, nullptr), WC_E_SHAPE);                   // not a 3x3 tap grid
+    EXPECT(wc_conv_wgrad_f16x3(nullptr, p, 1, p, 0, nullptr, nullptr, nullptr), WC_E_ARG);
+    EXPECT(wc_conv_wgrad_f16x3(&wg, p, 1, nullptr, 0, nullptr, nullptr, nullptr), WC_E_ARG);  // no G bound
+    wg.nseg = 2;
+    wg.seg[1].src = p;
+    EXPECT(wc_conv_wgrad_f16x3(&wg, p, 1, p, 0, nullptr, nullptr, nullptr), WC_E_ARG);  // segment 1 unbounded
+    EXPECT(wc_wgrad_reduce(nullptr, 1, 4, 4, 4, 4, 4, p, 0, 0, 0, nullptr, 0, 0, nullptr), WC_E_ARG);
+    EXPECT(wc_wgrad_reduce(p, 1, 4, 8, 4, 4, 4, p, 0, 0, 0, nullptr, 0, 0, nullptr), WC_E_ARG);  // dw1 missing
+    EXPECT(wc_attention_bwd_f16x3(p, 96, p, 32, p, 32, p, p, p, 96, 1, 64, 32, 4, 1.f, 0, 0, 0, nullptr, nullptr,
+                                  nullptr), WC_E_ARG);  // no dO bound
+    EXPECT(wc_attention_bwd_f16x3(p, 96, p, 32, p, 32, p, p, p, 96, 1, 64, 32, 4, 1.f, 99, 0, 0, p, nullptr, nullptr),
+           WC_E_ARG);  // exponent out of range
+    EXPECT(wc_attention_bwd_f16x3(p, 96, p, 32, p, 32, p, p, p, 96, 1, 64, 30, 4, 1.f, 0, 0, 0, p, nullptr, nullptr),
+           WC_E_SHAPE);  // heads do not divide C
+    EXPECT(wc_attention_bwd_dkdv192(p, 96, p, 32, p, p, p, 96, 1, 64, 32, 4, 1.f, nullptr), WC_E_SHAPE);  // D != 192
+    EXPECT(wc_attention_bwd6(nullptr, 96, p, 32, p, 32, p, p, p, 96, 1, 64, 32, 4, 1.f, nullptr), WC_E_ARG);
+    EXPECT(wc_gn_bwd_apply(nullptr, 4, p, 4, p, p, nullptr, nullptr, 1, p, 1, 16, 4, p, 4, 0, p, nullptr), WC_E_ARG);
+    EXPECT(wc_gn_bwd_apply(p, 3, p, 4, p, p, nullptr, nullptr, 1, p, 1, 16, 4, p, 4, 0, p, nullptr), WC_E_SHAPE);
+    EXPECT(wc_absmax_images(nullptr, 4, 1, 16, 4, p, nullptr), WC_E_ARG);
+    EXPECT(wc_pack_split(p, 144, 4, 16, 9, 0, 0, 0, 0, 100, p, 0, p, nullptr), WC_E_ARG);  // BN not 64 / 128
+
     // Host-only sizing helpers must be positive and deterministic.
     if (wc_conv3x3_x6_tile_n(64) != 64 || wc_conv3x3_x6_tile_n(320) != 128) {
         std::printf("FAIL wc_conv3x3_x6_tile_n\n");
         ++failures;
     }
     if (wc_gn_num_splits(16, 4096, 320) <= 0 || wc_gn_bwd_splits(16, 4096) <= 0 ||
-        wc_conv_wgrad_splits(320, 2880, 65536, 1024) <= 0 || wc_mse_workspace_doubles() <= 0) {
+        wc_conv_wgrad_splits(320, 2880, 65536, 1024) <= 0 || wc_mse_workspace_doubles() <= 0 ||
+        wc_conv_wgrad3_splits(128, 128, 32, 256, 256, 512) <= 0 ||
+        wc_conv_wgrad3_splits(128, 128, 32, 256, 256, 512) != wc_conv_wgrad3_splits(128, 128, 32, 256, 256, 512)) {
         std::printf("FAIL sizing helpers\n");
         ++failures;
     }

@@ -84,7 +84,10 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     constexpr int NP = F3 ? 2 : 3;
     constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
-    constexpr int KP = X6 ? 16 : WG_KP;        // pixels per K-step
+    // pixels per K-step (per barrier): 16 for bf16x6 (three planes) and the narrow f16x3 tiles, 32 for
+    // the wide f16x3 tiles and fp32 (twice the loads in flight per step: the 1x1 weight gradients are
+    // HBM-bound)
+    constexpr int KP = (X6 && (!F3 || BN > 128)) ? 16 : WG_KP;
     constexpr int AS = BM + 32, BS = BN + 32;  // fp32 LDS row strides: lane halves on disjoint banks
     constexpr int ASB = BM * 2 + 64, BSB = BN * 2 + 64;  // X6 row bytes
     constexpr int APL = KP * ASB, BPL = KP * BSB;        // X6 bytes of one piece plane
@@ -309,24 +312,27 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
         const int buf = s & 1;
         if (s + 1 < nsteps) load(s + 1);
         if constexpr (F3) {
-            const unsigned char* a = lds + buf * STAGE + tr_a;
-            const unsigned char* bb = lds + buf * STAGE + 2 * APL + tr_b;
-            wcx6::u32x4 fa[2][2], fb[2][2];
 #pragma unroll
-            for (int pc = 0; pc < 2; ++pc) {
+            for (int ks = 0; ks < KP / 16; ++ks) {  // 16-pixel MFMA K-steps of the stage
+                const unsigned char* a = lds + buf * STAGE + tr_a + ks * 16 * ASB;
+                const unsigned char* bb = lds + buf * STAGE + 2 * APL + tr_b + ks * 16 * BSB;
+                wcx6::u32x4 fa[2][2], fb[2][2];
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb) fa[mb][pc] = tr_frag(a + pc * APL + mb * 64, ASB);
+                for (int pc = 0; pc < 2; ++pc) {
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) fb[nb][pc] = tr_frag(bb + pc * BPL + nb * 64, BSB);
-            }
+                    for (int mb = 0; mb < 2; ++mb) fa[mb][pc] = tr_frag(a + pc * APL + mb * 64, ASB);
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    acc[mb][nb] = wcx6::mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
-                    acc[mb][nb] = wcx6::mfma_f16c(fa[mb][0], fb[nb][1], acc[mb][nb]);
-                    acc[mb][nb] = wcx6::mfma_f16c(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                    for (int nb = 0; nb < 2; ++nb) fb[nb][pc] = tr_frag(bb + pc * BPL + nb * 64, BSB);
                 }
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb) {
+                        acc[mb][nb] = wcx6::mfma_f16(fa[mb][0], fb[nb][0], acc[mb][nb]);
+                        acc[mb][nb] = wcx6::mfma_f16c(fa[mb][0], fb[nb][1], acc[mb][nb]);
+                        acc[mb][nb] = wcx6::mfma_f16c(fa[mb][1], fb[nb][0], acc[mb][nb]);
+                    }
+            }
         } else if constexpr (X6) {
             const unsigned char* a = lds + buf * STAGE + tr_a;
             const unsigned char* bb = lds + buf * STAGE + 3 * APL + tr_b;
@@ -437,7 +443,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_groups_kernel(float* __restr
 }
 template <int BM, int BN, int PRO, bool X6, bool F3 = false>
 int wgrad_launch(const WgDev& d, int grid, hipStream_t s) {
-    constexpr int KP = X6 ? 16 : WG_KP;
+    constexpr int KP = (X6 && (!F3 || BN > 128)) ? 16 : WG_KP;
     constexpr int bytes =
         2 * (X6 ? (F3 ? 2 : 3) * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
     static bool attr_set = false;

@@ -84,10 +84,9 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     constexpr int NP = F3 ? 2 : 3;
     constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
-    // pixels per K-step (per barrier): 16 for bf16x6 (three planes) and the narrow f16x3 tiles, 32 for
-    // the wide f16x3 tiles and fp32 (twice the loads in flight per step: the 1x1 weight gradients are
-    // HBM-bound)
-    constexpr int KP = (X6 && (!F3 || BN > 128)) ? 16 : WG_KP;
+    // pixels per K-step (per barrier): 16 for the split forms, 32 for fp32 (32 pixels per barrier for
+    // the f16x3 tiles measured slower: 292 vs 264 us at the 1x1 shapes)
+    constexpr int KP = X6 ? 16 : WG_KP;
     constexpr int AS = BM + 32, BS = BN + 32;  // fp32 LDS row strides: lane halves on disjoint banks
     constexpr int ASB = BM * 2 + 64, BSB = BN * 2 + 64;  // X6 row bytes
     constexpr int APL = KP * ASB, BPL = KP * BSB;        // X6 bytes of one piece plane
@@ -443,7 +442,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_groups_kernel(float* __restr
 }
 template <int BM, int BN, int PRO, bool X6, bool F3 = false>
 int wgrad_launch(const WgDev& d, int grid, hipStream_t s) {
-    constexpr int KP = (X6 && (!F3 || BN > 128)) ? 16 : WG_KP;
+    constexpr int KP = X6 ? 16 : WG_KP;
     constexpr int bytes =
         2 * (X6 ? (F3 ? 2 : 3) * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
     static bool attr_set = false;

@@ -25,7 +25,7 @@ def load(dirs):
 def main():
     acc = load(sys.argv[1:])
     for kern, cs in acc.items():
-        if 'conv' not in kern and 'attention' not in kern:
+        if 'conv' not in kern and 'attention' not in kern and 'attn' not in kern:
             continue
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         print(kern[:100])
@@ -33,8 +33,8 @@ def main():
             print(f'  {c:28s} {m[c]:16.4g}')
         busy = m.get('SQ_BUSY_CYCLES') or m.get('GRBM_GUI_ACTIVE')
         if 'SQ_VALU_MFMA_BUSY_CYCLES' in m and 'GRBM_GUI_ACTIVE' in m:
-            # MFMA busy per SIMD: counter summed over all SIMDs (256 CUs x 4)
-            print(f'  MFMA busy fraction ~ {m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] * 1024):.3f}')
+            # MFMA busy per SIMD: the counter sums 1024 SIMDs; GRBM_GUI_ACTIVE sums the 8 XCDs
+            print(f'  MFMA busy fraction ~ {m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024):.3f}')
         if 'SQ_WAIT_INST_ANY' in m and 'SQ_WAVE_CYCLES' in m:
             print(f'  wait_inst_any / wave_cycles = {m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"]:.3f}, '
                   f'wait_any / wave_cycles = {m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]:.3f}')

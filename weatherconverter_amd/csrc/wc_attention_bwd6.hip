@@ -308,7 +308,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int qi = (r & 3) + 8 * (r >> 2) + 4 * half;
-            const float pr = exp2f(s[r] * s_log2 - Ls[qi]);
+            // one fma + v_exp_f32 (results below 2^-126 flush to 0: negligible, as the forward)
+            const float pr = __builtin_amdgcn_exp2f(fmaf(s[r], s_log2, -Ls[qi]));
             s[r] = pr;
             dp[r] = pr * (F3 ? dp[r] * dp_un - Ls[32 + qi] : dp[r] - Ls[32 + qi]);
         }
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            const float pr = key < N ? exp2f(s[r] * s_log2 - lq) : 0.f;
+            const float pr = key < N ? __builtin_amdgcn_exp2f(fmaf(s[r], s_log2, -lq)) : 0.f;
             dp[r] = pr * (F3 ? dp[r] * dp_un - dq : dp[r] - dq);
         }
         // dQ^T += K^T dS^T

@@ -132,6 +132,12 @@ int wc_conv3x3_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes,
  * wc_absmax_images — the 3x3 data gradients of the training backward, unet_base.py:92,106.) */
 /* The output-channel tile (BN) wc_conv3x3_x6 and wc_conv_igemm_x6 use for N output channels. */
 int wc_conv3x3_x6_tile_n(int N);
+/* Selects the kernel form of wc_conv3x3_f16x3's GN(+SiLU) 3x3 conv without residual segment
+ * (N % 128 == 0, Hm % 16 == 0): 0 (default) the three-wave halo kernel; 1 the one-wave-per-SIMD
+ * 16 x 16-pixel form wherever it applies; -1 that form where its tiles fill the chip (>= 1024
+ * workgroups).  Both forms give bit-identical results.  Returns the previous mode (or WC_E_ARG).
+ * Process-wide, not thread-safe against concurrent launches. */
+int wc_conv3x3_set_onewave(int mode);
 
 /* General implicit-GEMM conv at the same bf16x6 arithmetic: exactly wc_conv_igemm's contract
  * (tap grids, input strides, the 1x1 residual segment, output maps, NCHW store; an activation

@@ -475,6 +475,51 @@ def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier, bounde
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,silu,sw', [(2, 32, 32, 48, 128, True, 16), (1, 48, 16, 128, 256, False, 8),
+                                                 (3, 16, 32, 80, 128, True, 32), (1, 64, 64, 256, 384, True, 4)])
+def test_conv3x3_f16x3_onewave_bit_identical(B, H, W, Ci, Co, silu, sw):
+    """The one-wave-per-SIMD 16 x 16-pixel form (conv3x3_w1_kernel, forced on) against the
+    three-wave halo kernel (forced off): bit-identical output (with bias + temb), per-image absmax
+    and GroupNorm tile partials; and within the f16x3 tolerance of float64.  Odd and even chunk
+    counts (Ci / 16 = 3, 8, 5, 16), non-square images, several N tiles."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(77)
+    h = torch.randn((B, Ci, H, W), generator=g) * 2 + 0.3
+    gamma = 1 + 0.3 * torch.randn(Ci, generator=g)
+    beta = 0.5 * torch.randn(Ci, generator=g)
+    sc, sh = _gn_affine(h, gamma, beta)
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    temb = torch.randn((B, Co + 32), generator=g)
+    a = h.double() * sc[:, :, None, None] + sh[:, :, None, None]
+    if silu:
+        a = F.silu(a)
+    ref = F.conv2d(a, w.double(), b.double(), padding=1) + temb[:, :Co].double()[:, :, None, None]
+    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.float().cuda(), shift=sh.float().cuda(), silu=silu)]
+    w3 = K.pack_f16x3(_pack(w).contiguous().cuda(), Ci, 0)
+    e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * W * Ci // 8)
+    res = {}
+    prev = K.set_conv3_onewave(1)
+    try:
+        for mode in (1, 0):
+            K.set_conv3_onewave(mode)
+            out = torch.full((B, H, W, Co), 7.0, device='cuda')
+            gp = K.GnPart.attach(out, sw)
+            am = torch.zeros(B, device='cuda')
+            K.conv3x3_f16x3(segs, w3, b.cuda(), K.View.full(out), Hm=H, Wm=W, a_exp=e, temb=temb.cuda(),
+                            temb_ld=Co + 32, absmax=am, gn=gp)
+            torch.cuda.synchronize()
+            res[mode] = (out.cpu(), am.cpu(), gp.part.cpu(), K._native.last_kernel_name())
+    finally:
+        K.set_conv3_onewave(prev)
+    assert res[1][3].startswith('conv3x3_w1_kernel') and res[0][3].startswith('conv3x3_x6_kernel'), (res[1][3], res[0][3])
+    for u, v in zip(res[1][:3], res[0][:3]):
+        assert torch.equal(u, v), (u - v).abs().max()
+    assert rel_l2(_nchw(res[1][0]).double(), ref) < 1e-5
+    assert torch.equal(res[1][1], res[1][0].reshape(B, -1).abs().amax(1))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('B,N,C,heads,gs', [(2, 300, 128, 4, 1.0), (1, 1024, 256, 4, 1.0), (2, 257, 512, 4, 3.0),
                                             (1, 200, 768, 4, 1.0), (1, 96, 384, 4, 1.0), (1, 64, 640, 4, 0.5)])
 def test_attention_f16x3_vs_float64(B, N, C, heads, gs):

@@ -460,6 +460,13 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
     return max(-60, min(60, math.floor(math.log2(2.0**14 / bound))))
 
 
+def set_conv3_onewave(mode: int) -> int:
+    """wc_conv3x3_set_onewave: 0 off (default), 1 forced, -1 where it fills the chip; returns the previous mode."""
+    prev = _native.load().wc_conv3x3_set_onewave(int(mode))
+    _req(prev >= -1, 'onewave mode')
+    return prev
+
+
 def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                   a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
                   temb_ld: int = 0, res: Optional[View] = None, act: int = 0,

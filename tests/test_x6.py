@@ -1081,3 +1081,52 @@ def test_qkv_presplit_attention_bit_identical(B, H, C, heads):
     a = (x.double() * sc[:, :, None, None] + sh[:, :, None, None]).permute(0, 2, 3, 1).reshape(B, N, C)
     ref64 = _attn_ref((a @ w_in.double().t() + b_in.double()).float(), B, N, C, heads)
     assert rel_l2(out.cpu().double().reshape(B, N, C), ref64) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,C,heads', [(2, 16, 16, 128, 4), (1, 32, 32, 512, 4), (2, 16, 32, 768, 4),
+                                           (1, 64, 64, 256, 4), (3, 16, 24, 256, 2)])
+def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
+    """The pre-split projection GEMM on 256 x 128 tiles (proj_pa256_kernel) against the 128 x 128
+    form: the out-projection form (in-place residual, bias, per-image absmax, GroupNorm tile
+    partials) and the pre-split qkv form give bit-identical results; 16 x 24 images (HW % 256 != 0)
+    fall back to 128 rows.  And the out-projection within the f16x3 tolerance of float64."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(91)
+    HW = H * W
+    o = torch.rand((B, H, W, C), generator=g) * 14 - 7
+    e = K.f16x3_a_exp(0.0, 7.0, 2)
+    ov = K.View.full(o.cuda())
+    a3 = K.split_f16x3_tiled(ov, e)
+    w = torch.randn((C, C), generator=g) / C**0.5
+    b = 0.1 * torch.randn(C, generator=g)
+    w3 = K.pack_f16x3(w.cuda(), C, ntaps=1, order='natural')
+    y0 = torch.randn((B, H, W, C), generator=g)
+    w_in = torch.randn((3 * C, C), generator=g) / C**0.5
+    b_in = 0.1 * torch.randn(3 * C, generator=g)
+    w3q = K.pack_f16x3(w_in.cuda(), C, ntaps=1, order='natural')
+    res = {}
+    prev = K.set_proj_tile(256)
+    try:
+        for rows in (256, 128):
+            K.set_proj_tile(rows)
+            y = y0.cuda()
+            yv = K.View.full(y)
+            gp = K.GnPart.attach(y, 8)
+            am = torch.zeros(B, device='cuda')
+            K.proj_f16x3(ov, a3, w3, b.cuda(), yv, a_exp=e, res=yv, absmax=am, gn=gp)
+            name = K._native.last_kernel_name()
+            qkv3 = torch.zeros(B * 6 * C * HW, dtype=torch.int16, device='cuda')
+            K.proj_f16x3_qkv(ov, a3, w3q, b_in.cuda(), qkv3, a_exp=e, C=C, heads=heads, exps=(9, 8, 7))
+            torch.cuda.synchronize()
+            res[rows] = (y.cpu(), am.cpu(), gp.part.cpu(), qkv3.cpu(), name)
+    finally:
+        K.set_proj_tile(prev)
+    big = HW % 256 == 0
+    assert res[256][4].startswith('proj_pa256_kernel' if big else 'conv_igemm_x6_kernel'), res[256][4]
+    assert res[128][4].startswith('conv_igemm_x6_kernel'), res[128][4]
+    for u, v in zip(res[256][:4], res[128][:4]):
+        assert torch.equal(u, v)
+    ref = o.double() @ w.double().t() + b.double() + y0.double()
+    assert rel_l2(res[256][0].double(), ref) < 2e-6
+    assert torch.equal(res[256][1], res[256][0].reshape(B, -1).abs().amax(1))

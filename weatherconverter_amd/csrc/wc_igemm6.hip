@@ -1009,6 +1009,280 @@ __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restric
     }
 }
 
+// The pre-split projection GEMM at 256 x 128 tiles: each wave owns 128 pixels x 64 channels (4 x 2
+// transposed 32x32 accumulators, 24 MFMAs per K-step instead of 12), so a K-step's barrier and its
+// fragment reads are paid per 24 MFMAs; a 3-stage LDS-DMA ring of 24 KiB stages (the A rows of two
+// consecutive 128-row a3 tiles + the B step), two workgroups per CU.  Same fragments, products and
+// per-accumulator order as conv_igemm_x6_kernel<128, 128, ..., PA> (transposed accumulation): the
+// results are bit-identical to it (tests/test_x6.py).  QKV: the pre-split attention epilogue.
+template <bool QKV>
+__global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
+    constexpr int BM = 256, BN = 128;
+    constexpr int APLANE = 128 * 16, BPLANE = BN * 16;  // one (piece, k-half) plane of a 128-row half / of B
+    constexpr int AHALF = 4 * APLANE;                    // 8 KiB: one a3 step of 128 rows
+    constexpr int STAGE = 2 * AHALF + 4 * BPLANE;        // 24 KiB
+    __shared__ __attribute__((aligned(16))) unsigned char st0[STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char st1[STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char st2[STAGE];
+    __shared__ __attribute__((aligned(16))) float sbias[2 * BN];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int tile_m = bid / p.ntiles_n;
+    const int tile_n = bid % p.ntiles_n;
+    const int m0 = tile_m * BM;
+    const int n0 = tile_n * BN;
+    const int HWm = p.Hm * p.Wm;
+    const int b_tile = m0 / HWm;
+    const float ainv = ldexpf(1.0f, -p.a_exp);
+    const int steps = p.steps;
+
+    const unsigned char* asrc0 = p.a3 + (long)(2 * tile_m) * steps * AHALF + tid * 16;
+    const unsigned char* asrc1 = asrc0 + (long)steps * AHALF;
+    const unsigned char* bsrc = reinterpret_cast<const unsigned char*>(p.w6) + (long)tile_n * steps * (4 * BPLANE) + tid * 16;
+    auto stage = [&](auto S) -> unsigned char* {
+        constexpr int SV = decltype(S)::value;
+        if constexpr (SV == 0) return st0;
+        else if constexpr (SV == 1) return st1;
+        else return st2;
+    };
+    // six LDS-DMA wave-instructions per wave (1 KiB each): A half 0, A half 1, B; issued as inline
+    // assembly outside the compiler's wait tracking, ordered by the ring's own s_waitcnt (as the
+    // 128 x 128 form)
+    auto dma = [&](int st, unsigned char* buf) {
+        const unsigned dst = __builtin_amdgcn_readfirstlane(
+            (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(buf) + wave * 1024);
+        const unsigned char* a0 = asrc0 + (long)st * AHALF;
+        const unsigned char* a1 = asrc1 + (long)st * AHALF;
+        const unsigned char* b0 = bsrc + (long)st * (4 * BPLANE);
+        asm volatile(
+            "s_mov_b32 m0, %6\n\t"
+            "global_load_lds_dwordx4 %0, off\n\t"
+            "s_add_u32 m0, %6, 0x1000\n\t"
+            "global_load_lds_dwordx4 %1, off\n\t"
+            "s_add_u32 m0, %6, 0x2000\n\t"
+            "global_load_lds_dwordx4 %2, off\n\t"
+            "s_add_u32 m0, %6, 0x3000\n\t"
+            "global_load_lds_dwordx4 %3, off\n\t"
+            "s_add_u32 m0, %6, 0x4000\n\t"
+            "global_load_lds_dwordx4 %4, off\n\t"
+            "s_add_u32 m0, %6, 0x5000\n\t"
+            "global_load_lds_dwordx4 %5, off"
+            :
+            : "v"(a0), "v"(a0 + 4096), "v"(a1), "v"(a1 + 4096), "v"(b0), "v"(b0 + 4096), "s"(dst)
+            : "memory", "m0");
+    };
+
+    f32x16 acc[2][2][2];  // [64-row pair][mb in the pair][nb]; acc = transposed block (lanes = pixels)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[h][i][j][r] = 0.f;
+    const int l32 = lane & 31;
+    const int half = lane >> 5;
+    const int a_rd = wm * AHALF + half * APLANE + l32 * 16;
+    const int b_rd = 2 * AHALF + half * BPLANE + (wn * 64 + l32) * 16;
+    auto compute = [&](const unsigned char* buf) {
+        u32x4 fa[4][2], fb[2][2];
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * APLANE);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * BPLANE);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                acc[mb >> 1][mb & 1][nb] = mfma_f16(fb[nb][0], fa[mb][0], acc[mb >> 1][mb & 1][nb]);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                f32x16& a = acc[mb >> 1][mb & 1][nb];
+                a = mfma_f16c(fb[nb][1], fa[mb][0], a);
+                a = mfma_f16c(fb[nb][0], fa[mb][1], a);
+            }
+    };
+    const std::integral_constant<int, 0> S0;
+    const std::integral_constant<int, 1> S1;
+    const std::integral_constant<int, 2> S2;
+    auto kstep = [&](auto S, int step) {
+        constexpr int SV = decltype(S)::value;
+        // this wave's copy of `step` landed (step + 1's six may still fly), then everyone's; and
+        // every wave is done with step - 1, whose stage step + 2 reuses
+        if (step + 1 < steps) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (step + 2 < steps) dma(step + 2, stage(std::integral_constant<int, (SV + 2) % 3>{}));
+        compute(stage(S));
+    };
+    dma(0, st0);
+    if (steps > 1) dma(1, st1);
+    int step = 0;
+    for (; step + 3 <= steps; step += 3) {
+        kstep(S0, step);
+        kstep(S1, step + 1);
+        kstep(S2, step + 2);
+    }
+    if (step < steps) kstep(S0, step);
+    if (step + 1 < steps) kstep(S1, step + 1);
+
+    // per-channel bias and 2^-(sA + sW[n]) of the tile through LDS (global loads between the
+    // epilogue's stores would wait for their acks: vmcnt counts both)
+    if (tid < BN) {
+        const int n = n0 + tid;
+        sbias[tid] = p.bias ? p.bias[n] : 0.f;
+        sbias[BN + tid] = p.wsinv[n] * ainv;
+    }
+    __syncthreads();
+    const int prow0 = m0 - b_tile * HWm + wm * 128 + l32;  // pixel of this lane in block mb = 0
+    if constexpr (QKV) {
+        // as conv_igemm_x6_kernel's pre-split qkv epilogue, over 4 row blocks
+        const long img = (long)b_tile * 6 * p.qC * HWm;
+        const long plane = (long)p.qD * HWm;
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int nblk = n0 + wn * 64 + nb * 32;
+            const int part = nblk / p.qC;
+            const int c0 = nblk - part * p.qC;
+            const int head = c0 / p.qD, d0 = c0 - head * p.qD;
+            const float sc = p.qscale[part];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+                const f32x16& a = acc[mb >> 1][mb & 1][nb];
+                const int pix = prow0 + mb * 32;
+                if (part < 2) {
+                    unsigned short* dst = p.qkv3 + img + (long)((part * (p.qC / p.qD) + head) * 2) * plane +
+                                          ((long)(d0 >> 3) * HWm + pix) * 8 + 4 * half;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        f32x4 v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int n = nblk + 8 * j + 4 * half + e;
+                            v[e] = (a[4 * j + e] * sbias[BN + n - n0] + sbias[n - n0]) * sc;
+                        }
+                        u32x2 ph, pl;
+                        split2_f16(v, ph, pl);
+                        *reinterpret_cast<u32x2*>(dst + (long)j * HWm * 8) = ph;
+                        *reinterpret_cast<u32x2*>(dst + plane + (long)j * HWm * 8) = pl;
+                    }
+                } else {
+                    const long pos = (pix & ~31) + attn_key_pos(pix & 31);
+                    unsigned short* dst = p.qkv3 + img + 4L * p.qC * HWm + (long)(head * 2) * plane + pos;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                        const int n = nblk + row;
+                        const float v = (a[r] * sbias[BN + n - n0] + sbias[n - n0]) * sc;
+                        const _Float16 h = (_Float16)v;
+                        const _Float16 l = (_Float16)(v - (float)h);
+                        dst[(long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, h);
+                        dst[plane + (long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, l);
+                    }
+                }
+            }
+        }
+    } else {
+        // as conv_igemm_x6_kernel's transposed NHWC epilogue: 16-byte residual loads (all before the
+        // first store) and stores, per-image absmax, GroupNorm tile partials per 64-row pair
+        const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + (long)b_tile * HWm * p.ldo);
+        const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + (long)b_tile * HWm * p.ldres : p.out);
+        const int ncol = wn * 64 + 4 * half;
+        float vmax = 0.f;
+        f32x4 rv[2][2][2][4];
+        if (p.res) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            rv[h][i][nb][j] = bload_f4(srd_res, (unsigned)((prow0 + 32 * (2 * h + i)) * p.ldres + n0 + ncol +
+                                                                          32 * nb + 8 * j) * 4u);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = ncol + 32 * nb + 8 * j;
+                    const f32x4 badd = *reinterpret_cast<const f32x4*>(sbias + c);
+                    const f32x4 bmul = *reinterpret_cast<const f32x4*>(sbias + BN + c);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        f32x16& a = acc[h][i][nb];
+                        f32x4 v = f32x4{a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]} * bmul + badd;
+                        if (p.res) v += rv[h][i][nb][j];
+                        bstore_f4(srd_out, (unsigned)((prow0 + 32 * (2 * h + i)) * p.ldo + n0 + c) * 4u, v);
+                        vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) a[4 * j + e] = v[e];
+                    }
+                }
+            }
+        }
+        if (p.absmax) block_absmax_atomic(p.absmax, b_tile, vmax);
+        if (p.gn_part) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
+                         (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + 2 * wm + h,
+                         (p.gn_c0 + n0 + wn * 64) / 32};
+                gn_tile_partials_tr(acc[h], g, 2);
+            }
+        }
+    }
+}
+
+// 0: the 128 x 128 form only; 2: the 256 x 128 form wherever the pixels per image are a multiple
+// of 256; 1 (default): the 256 x 128 form for the pre-split qkv epilogue at >= 2048 of its tiles,
+// the one place it measured faster (64^2, C 512 -> 1536: 341 vs 373 us; the out-projections and
+// the smaller qkv grids ran 4-16 % slower at two workgroups per CU, tools/proj_probe.py).
+// WC_PROJ_BM256 for A/B runs, wc_proj_set_tile for tests.
+int g_pa256 = [] {
+    const char* e = getenv("WC_PROJ_BM256");
+    return e ? atoi(e) : 1;
+}();
+
+int launch_pa(const IgDev& d, hipStream_t stream) {
+    const bool fits = (d.Hm * d.Wm) % 256 == 0 && d.N % 128 == 0 && !d.abound;
+    const long tiles256 = (long)(d.M / 256) * (d.N / 128);
+    if (fits && (g_pa256 == 2 || (g_pa256 == 1 && d.qkv3 && tiles256 >= 2048))) {
+        IgDev p = d;
+        p.ntiles_n = p.N / 128;
+        dim3 grid((p.M / 256) * p.ntiles_n);
+        if (p.qkv3) {
+            WC_SET_NAME("proj_pa256_kernel", {WC_TB(true)});
+            hipLaunchKernelGGL((proj_pa256_kernel<true>), grid, dim3(NT), 0, stream, p);
+        } else {
+            WC_SET_NAME("proj_pa256_kernel", {WC_TB(false)});
+            hipLaunchKernelGGL((proj_pa256_kernel<false>), grid, dim3(NT), 0, stream, p);
+        }
+        WC_CHECK_LAUNCH();
+        return WC_OK;
+    }
+    return launch<128, 128, 0, true, WC_ACT_NONE, true>(d, stream);
+}
+
 // shared checks of the two PA entry points: the A operand's view shape in args->seg[0] (1x1,
 // stride 1, no prologue: a3 already carries it), a3 of M x C x 4 bytes
 int prepare_pa(const wc_conv_args* a, const void* a3, int64_t a3_bytes, const void* w3, IgDev& d, long& k) {
@@ -1059,7 +1333,7 @@ extern "C" int wc_proj_f16x3(const wc_conv_args* a, const void* a3, int64_t a3_b
     if (w3_bytes != (long)(a->N / 128) * d.steps0 * 128 * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
     d.a_exp = a_exp;
     d.wsinv = w_inv_scale;
-    return launch<128, 128, 0, true, WC_ACT_NONE, true>(d, reinterpret_cast<hipStream_t>(stream));
+    return launch_pa(d, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int wc_proj_f16x3_qkv(const wc_conv_args* a, const void* a3, int64_t a3_bytes, const void* w3,
@@ -1086,5 +1360,12 @@ extern "C" int wc_proj_f16x3_qkv(const wc_conv_args* a, const void* a3, int64_t 
     d.qC = C;
     d.qD = C / heads;
     for (int i = 0; i < 3; ++i) d.qscale[i] = ldexpf(1.0f, exps[i]);
-    return launch<128, 128, 0, true, WC_ACT_NONE, true>(d, reinterpret_cast<hipStream_t>(stream));
+    return launch_pa(d, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int wc_proj_set_tile(int rows) {
+    if (rows != 0 && rows != 128 && rows != 256) return WC_E_ARG;
+    const int prev = g_pa256 == 0 ? 128 : g_pa256 == 2 ? 256 : 0;
+    g_pa256 = rows == 128 ? 0 : rows == 256 ? 2 : 1;
+    return prev;
 }

@@ -641,6 +641,14 @@ def split_f16x3_tiled(v: View, a_exp: int, scale: Optional[torch.Tensor] = None,
     return a3
 
 
+def set_proj_tile(rows: int) -> int:
+    """wc_proj_set_tile: row tile of the pre-split projection GEMMs (0 the measured default, 256 or 128);
+    returns the previous setting."""
+    prev = _native.load().wc_proj_set_tile(int(rows))
+    _req(prev in (0, 128, 256), 'projection row tile')
+    return prev
+
+
 def proj_f16x3(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[torch.Tensor], out: View, *, a_exp: int,
                res: Optional[View] = None, absmax: Optional[torch.Tensor] = None, gn: Optional[GnPart] = None):
     """out = (a3 . W^T) x 2^-(a_exp + sW) + bias (+ res): the 1x1 projection of the view v that a3 was

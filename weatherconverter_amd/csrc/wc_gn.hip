@@ -234,9 +234,6 @@ __global__ __launch_bounds__(256) void gn_partials_kernel(const float* __restric
 // division-free passes over the partials, lane butterflies in a fixed order (deterministic); then
 // the same per-(b, c) affine (and optional bound) as gn_finalize.
 constexpr int GNF_THREADS = 512;
-constexpr int GNF_KMAX = 16;  // register-cached path: up to 1024 pixel blocks (64 x 64 px per image)
-constexpr int GNF_SMAX = 4;   // ... and up to 4 sub-slots per group
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
     const float* __restrict__ part, int np64, int ncb, int sw, int c0, int C, int G,
@@ -259,59 +256,6 @@ __global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
         const float* base = part + ((long)b * np64 * NS + (c0 + g * cpg) / sw) * 2 + (long)j * NS * 2;
         const int items = np64 * spg;
         float sm = 0.f;
-        if (np64 <= 64 * GNF_KMAX && spg <= GNF_SMAX) {
-            // every partial this lane reads, loaded up front (one memory latency instead of one per
-            // loop trip of each pass); both passes then sum the registers in exactly the order of
-            // the streaming loop below, so the results are bit-identical to it
-            f32x2 x[GNF_SMAX][GNF_KMAX];
-#pragma unroll
-            for (int s = 0; s < GNF_SMAX; ++s)
-#pragma unroll
-                for (int k = 0; k < GNF_KMAX; ++k)
-                    x[s][k] = (s < spg && j + 64 * k < np64)
-                                  ? *reinterpret_cast<const f32x2*>(base + 2 * s + (long)k * pstride)
-                                  : f32x2{0.f, 0.f};
-            auto pass = [&](auto term) {
-                float tot = 0.f;
-#pragma unroll
-                for (int s = 0; s < GNF_SMAX; ++s) {
-                    if (s >= spg) break;
-                    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-                    bool main = true;
-#pragma unroll
-                    for (int k = 0; k + 3 < GNF_KMAX; k += 4) {  // pp = j + 64 k, k a multiple of 4
-                        main = main && j + 64 * (k + 3) < np64;
-                        if (main) {
-                            a0 = term(a0, x[s][k]);
-                            a1 = term(a1, x[s][k + 1]);
-                            a2 = term(a2, x[s][k + 2]);
-                            a3 = term(a3, x[s][k + 3]);
-                        } else {  // the tail: the remaining pp of this lane into a0, in order
-#pragma unroll
-                            for (int t = 0; t < 4; ++t)
-                                if (j + 64 * (k + t) < np64) a0 = term(a0, x[s][k + t]);
-                        }
-                    }
-                    tot += (a0 + a1) + (a2 + a3);
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-                return tot;
-            };
-            sm = pass([](float a, f32x2 v) { return a + v.x; });
-            const float mean = sm / (float)items;
-            const float q = pass([&](float a, f32x2 v) {
-                const float d = v.x - mean;
-                return a + fmaf(n0 * d, d, v.y);
-            });
-            if (j == 0) {
-                const float n = n0 * (float)items;
-                const float var = fmaxf(q / n, 0.f);
-                s_mean[g] = mean;
-                s_rstd[g] = 1.0f / sqrtf(var + eps);
-                s_bound[g] = (fabsf(mean) + sqrtf(fmaxf(n - 1.f, 0.f)) * sqrtf(var)) * 1.001f;
-            }
-        } else {
         for (int s = 0; s < spg; ++s) {
             const float* ps = base + 2 * s;
             float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -358,7 +302,6 @@ __global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
             s_mean[g] = mean;
             s_rstd[g] = 1.0f / sqrtf(var + eps);
             s_bound[g] = (fabsf(mean) + sqrtf(fmaxf(n - 1.f, 0.f)) * sqrtf(var)) * 1.001f;
-        }
         }
     }
     __syncthreads();

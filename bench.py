@@ -171,6 +171,18 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
                            + (f'; algorithmic {rec["algorithmic_bytes"] / 1e9:.3f}' if 'algorithmic_bytes' in rec
                               else ''))
     ev_n, ev_sec = ev.get(name, (0, 0.0))
+    # what a bare f16 MFMA stream sustains on this power-capped chip (committed probe, median of its
+    # power-settled launches): the split-precision kernels' work against it, beside the data-sheet peak
+    sustained = None
+    probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r03_mfma_peak.jsonl')
+    if peak == F16X3_PEAK_TFLOPS and os.path.exists(probe):
+        rates = sorted(r['tflops'] for r in map(json.loads, open(probe)) if r.get('mfma') == 'f32_32x32x16_f16')
+        if rates:
+            f16 = rates[len(rates) // 2]
+            sustained = {'f16_mfma_tflops': f16, 'fp32_equiv_tflops': round(f16 / 3, 1),
+                         'frac': round(achieved / (f16 / 3), 4),
+                         'source': 'profiles/r03_mfma_peak.jsonl (tools/probes/mfma_peak.hip: back-to-back '
+                                   'v_mfma_f32_32x32x16_f16, 8 waves/SIMD, ~70 ms launches; median)'}
     return {
         'kernel': name,
         'kernel_desc': _describe(name),
@@ -179,6 +191,7 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
         'peak': peak,
         'unit': 'TFLOP/s',
         'frac': round(achieved / peak, 4),
+        'sustained_mfma_stream': sustained,
         'traffic': traffic,
         'traffic_source': traffic_src,
         'launches_per_step': n * groups,

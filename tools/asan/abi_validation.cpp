@@ -97,6 +97,17 @@ int main() {
     EXPECT(wc_absmax_images(nullptr, 4, 1, 16, 4, p, nullptr), WC_E_ARG);
     EXPECT(wc_pack_split(p, 144, 4, 16, 9, 0, 0, 0, 0, 100, p, 0, p, nullptr), WC_E_ARG);  // BN not 64 / 128
 
+    // Kernel-form selectors: out-of-range modes rejected, valid ones return the previous setting.
+    EXPECT(wc_conv3x3_set_onewave(2), WC_E_ARG);
+    EXPECT(wc_proj_set_tile(64), WC_E_ARG);
+    if (wc_conv3x3_set_onewave(1) != 0 || wc_conv3x3_set_onewave(0) != 1 || wc_proj_set_tile(256) != 0 ||
+        wc_proj_set_tile(128) != 256 || wc_proj_set_tile(0) != 128) {
+        std::printf("FAIL kernel-form selectors\n");
+        ++failures;
+    }
+    // the 256-row projection launcher checks run before any launch (null / misaligned A operand)
+    EXPECT(wc_proj_f16x3_qkv(&a, nullptr, 0, p, 0, 0, p, p, 128, 4, nullptr, nullptr), WC_E_ARG);
+
     // Host-only sizing helpers must be positive and deterministic.
     if (wc_conv3x3_x6_tile_n(64) != 64 || wc_conv3x3_x6_tile_n(320) != 128) {
         std::printf("FAIL wc_conv3x3_x6_tile_n\n");

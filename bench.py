@@ -83,7 +83,7 @@ KERNEL_DESC = {
     'attention_x6': 'split-precision MFMA flash attention',
     'conv_igemm_kernel': 'fp32 MFMA implicit-GEMM conv',
     'attention_kernel': 'fp32 MFMA flash attention',
-    'proj_pa256_kernel': 'split-precision MFMA pre-split projection GEMM, 256 x 128 tiles',
+    'proj_pa_kernel': 'split-precision MFMA pre-split projection GEMM',
     'conv3x3_w1_kernel': 'split-precision MFMA 3x3 conv, one wave per SIMD, 16 x 16-pixel tiles',
 }
 
@@ -224,7 +224,7 @@ def _mode_peak(name: str) -> float:
         return F16X3_PEAK_TFLOPS if len(targs) >= 6 and targs[5] == 'true' else BF16X6_PEAK_TFLOPS
     if name.startswith('attention_x6'):
         return F16X3_PEAK_TFLOPS if targs[1] == 'true' else BF16X6_PEAK_TFLOPS
-    if name.startswith(('conv3x3_w1_kernel', 'proj_pa256_kernel')):  # f16x3-only forms
+    if name.startswith(('conv3x3_w1_kernel', 'proj_pa_kernel')):  # f16x3-only forms
         return F16X3_PEAK_TFLOPS
     return FP32_PEAK_TFLOPS
 

@@ -217,9 +217,11 @@ int wc_proj_f16x3(const wc_conv_args* args, const void* a3, int64_t a3_bytes, co
 int wc_proj_f16x3_qkv(const wc_conv_args* args, const void* a3, int64_t a3_bytes, const void* w3, int64_t w3_bytes,
                       int a_exp, const float* w_inv_scale, void* qkv3, int C, int heads, const int* exps,
                       void* stream);
-/* Row tile of the two pre-split projection GEMMs above: 0 (default) the measured choice (256 rows
- * for wc_proj_f16x3_qkv at >= 2048 tiles of 256 x 128, else 128), 256 (wherever the pixels per
- * image are a multiple of 256) or 128.  Both tiles give bit-identical results.  Returns the previous
+/* Form of the two pre-split projection GEMMs above: 0 (default) the measured choice (256 x 128
+ * tiles for wc_proj_f16x3_qkv at >= 2048 of them, else 128 x 128), 256 (wherever the pixels per
+ * image are a multiple of 256), 128 (the 128 x 128 LDS-DMA form), -128 (128 x 128 tiles with the
+ * B fragments from L2 in registers) or -129 (A and B in registers, no LDS).  All forms give
+ * bit-identical results.  Returns the previous
  * setting (or WC_E_ARG).  Process-wide, not thread-safe against concurrent launches. */
 int wc_proj_set_tile(int rows);
 

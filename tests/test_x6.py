@@ -1087,8 +1087,8 @@ def test_qkv_presplit_attention_bit_identical(B, H, C, heads):
 @pytest.mark.parametrize('B,H,W,C,heads', [(2, 16, 16, 128, 4), (1, 32, 32, 512, 4), (2, 16, 32, 768, 4),
                                            (1, 64, 64, 256, 4), (3, 16, 24, 256, 2)])
 def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
-    """The pre-split projection GEMM on 256 x 128 tiles (proj_pa256_kernel) against the 128 x 128
-    form: the out-projection form (in-place residual, bias, per-image absmax, GroupNorm tile
+    """The pre-split projection GEMM on 256 x 128 tiles and on 128 x 128 tiles with B in registers
+    (proj_pa_kernel<QKV, 2, false> / <QKV, 1, true>) against the 128 x 128 LDS-DMA form: the out-projection form (in-place residual, bias, per-image absmax, GroupNorm tile
     partials) and the pre-split qkv form give bit-identical results; 16 x 24 images (HW % 256 != 0)
     fall back to 128 rows.  And the out-projection within the f16x3 tolerance of float64."""
     from weatherconverter_amd import kernels as K
@@ -1108,7 +1108,7 @@ def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
     res = {}
     prev = K.set_proj_tile(256)
     try:
-        for rows in (256, 128):
+        for rows in (256, -128, -129, 128):  # 256 x 128; 128 x 128 with B / A and B in registers; LDS-DMA
             K.set_proj_tile(rows)
             y = y0.cuda()
             yv = K.View.full(y)
@@ -1123,10 +1123,13 @@ def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
     finally:
         K.set_proj_tile(prev)
     big = HW % 256 == 0
-    assert res[256][4].startswith('proj_pa256_kernel' if big else 'conv_igemm_x6_kernel'), res[256][4]
+    assert res[256][4].startswith('proj_pa_kernel<false, 2' if big else 'conv_igemm_x6_kernel'), res[256][4]
+    assert res[-128][4].startswith('proj_pa_kernel<false, 1, true, false>'), res[-128][4]
+    assert res[-129][4].startswith('proj_pa_kernel<false, 1, true, true>'), res[-129][4]
     assert res[128][4].startswith('conv_igemm_x6_kernel'), res[128][4]
-    for u, v in zip(res[256][:4], res[128][:4]):
-        assert torch.equal(u, v)
+    for form in (256, -128, -129):
+        for u, v in zip(res[form][:4], res[128][:4]):
+            assert torch.equal(u, v), form
     ref = o.double() @ w.double().t() + b.double() + y0.double()
     assert rel_l2(res[256][0].double(), ref) < 2e-6
     assert torch.equal(res[256][1], res[256][0].reshape(B, -1).abs().amax(1))

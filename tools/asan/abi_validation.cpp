@@ -101,7 +101,7 @@ int main() {
     EXPECT(wc_conv3x3_set_onewave(2), WC_E_ARG);
     EXPECT(wc_proj_set_tile(64), WC_E_ARG);
     if (wc_conv3x3_set_onewave(1) != 0 || wc_conv3x3_set_onewave(0) != 1 || wc_proj_set_tile(256) != 0 ||
-        wc_proj_set_tile(128) != 256 || wc_proj_set_tile(0) != 128) {
+        wc_proj_set_tile(-128) != 256 || wc_proj_set_tile(128) != -128 || wc_proj_set_tile(0) != 128) {
         std::printf("FAIL kernel-form selectors\n");
         ++failures;
     }

@@ -1009,18 +1009,26 @@ __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restric
     }
 }
 
-// The pre-split projection GEMM at 256 x 128 tiles: each wave owns 128 pixels x 64 channels (4 x 2
-// transposed 32x32 accumulators, 24 MFMAs per K-step instead of 12), so a K-step's barrier and its
-// fragment reads are paid per 24 MFMAs; a 3-stage LDS-DMA ring of 24 KiB stages (the A rows of two
-// consecutive 128-row a3 tiles + the B step), two workgroups per CU.  Same fragments, products and
-// per-accumulator order as conv_igemm_x6_kernel<128, 128, ..., PA> (transposed accumulation): the
-// results are bit-identical to it (tests/test_x6.py).  QKV: the pre-split attention epilogue.
-template <bool QKV>
-__global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
-    constexpr int BM = 256, BN = 128;
+// The pre-split projection GEMM, H = 64-row blocks per wave: H = 2 (proj_pa256_kernel) = 256 x 128
+// tiles, each wave 128 pixels x 64 channels (4 x 2 transposed 32x32 accumulators, 24 MFMAs per
+// K-step), a 3-stage LDS-DMA ring of 24 KiB stages (the A rows of two consecutive 128-row a3 tiles +
+// the B step), two workgroups per CU.  WR (H = 1, proj_pa_wr_kernel: 128 x 128 tiles): the B
+// fragments go from L2 straight into registers two steps ahead (three register sets, as the halo
+// conv's weights) and only A rides the LDS-DMA ring (8 KiB stages): half the LDS traffic per MFMA.
+// Same fragments, products and per-accumulator order as conv_igemm_x6_kernel<128, 128, ..., PA>
+// (transposed accumulation): the results are bit-identical to it (tests/test_x6.py).  QKV: the
+// pre-split attention epilogue.
+// DA (with WR): the A fragments also go from the pre-split rows straight into registers two steps
+// ahead: no LDS and no barrier in the K loop (each wave streams its own operands; the two waves
+// sharing A rows or B columns read them twice, through the CU's L1).
+template <bool QKV, int H, bool WR, bool DA = false>
+__global__ __launch_bounds__(NT, H == 2 || DA ? 2 : 3) void proj_pa_kernel(IgDev p) {
+    static_assert((H == 2 && !WR && !DA) || (H == 1 && WR), "the instantiated forms");
+    constexpr int BM = 128 * H, BN = 128;
     constexpr int APLANE = 128 * 16, BPLANE = BN * 16;  // one (piece, k-half) plane of a 128-row half / of B
     constexpr int AHALF = 4 * APLANE;                    // 8 KiB: one a3 step of 128 rows
-    constexpr int STAGE = 2 * AHALF + 4 * BPLANE;        // 24 KiB
+    constexpr int STAGE = H * AHALF + (WR ? 0 : 4 * BPLANE);
+    constexpr int NDMA = 2 * H + (WR ? 0 : 2);           // LDS-DMA wave-instructions per step
     __shared__ __attribute__((aligned(16))) unsigned char st0[STAGE];
     __shared__ __attribute__((aligned(16))) unsigned char st1[STAGE];
     __shared__ __attribute__((aligned(16))) unsigned char st2[STAGE];
@@ -1045,7 +1053,7 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
     const float ainv = ldexpf(1.0f, -p.a_exp);
     const int steps = p.steps;
 
-    const unsigned char* asrc0 = p.a3 + (long)(2 * tile_m) * steps * AHALF + tid * 16;
+    const unsigned char* asrc0 = p.a3 + (long)(H * tile_m) * steps * AHALF + tid * 16;
     const unsigned char* asrc1 = asrc0 + (long)steps * AHALF;
     const unsigned char* bsrc = reinterpret_cast<const unsigned char*>(p.w6) + (long)tile_n * steps * (4 * BPLANE) + tid * 16;
     auto stage = [&](auto S) -> unsigned char* {
@@ -1054,36 +1062,62 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
         else if constexpr (SV == 1) return st1;
         else return st2;
     };
-    // six LDS-DMA wave-instructions per wave (1 KiB each): A half 0, A half 1, B; issued as inline
+    // LDS-DMA wave-instructions (1 KiB each) per wave: the A halves, then (not WR) B; inline
     // assembly outside the compiler's wait tracking, ordered by the ring's own s_waitcnt (as the
     // 128 x 128 form)
+    auto dma1 = [&](unsigned dst, const unsigned char* src) {
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(dst) : "memory", "m0");
+    };
     auto dma = [&](int st, unsigned char* buf) {
         const unsigned dst = __builtin_amdgcn_readfirstlane(
             (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(buf) + wave * 1024);
         const unsigned char* a0 = asrc0 + (long)st * AHALF;
-        const unsigned char* a1 = asrc1 + (long)st * AHALF;
-        const unsigned char* b0 = bsrc + (long)st * (4 * BPLANE);
-        asm volatile(
-            "s_mov_b32 m0, %6\n\t"
-            "global_load_lds_dwordx4 %0, off\n\t"
-            "s_add_u32 m0, %6, 0x1000\n\t"
-            "global_load_lds_dwordx4 %1, off\n\t"
-            "s_add_u32 m0, %6, 0x2000\n\t"
-            "global_load_lds_dwordx4 %2, off\n\t"
-            "s_add_u32 m0, %6, 0x3000\n\t"
-            "global_load_lds_dwordx4 %3, off\n\t"
-            "s_add_u32 m0, %6, 0x4000\n\t"
-            "global_load_lds_dwordx4 %4, off\n\t"
-            "s_add_u32 m0, %6, 0x5000\n\t"
-            "global_load_lds_dwordx4 %5, off"
-            :
-            : "v"(a0), "v"(a0 + 4096), "v"(a1), "v"(a1 + 4096), "v"(b0), "v"(b0 + 4096), "s"(dst)
-            : "memory", "m0");
+        dma1(dst, a0);
+        dma1(dst + 0x1000, a0 + 4096);
+        if constexpr (H == 2) {
+            const unsigned char* a1 = asrc1 + (long)st * AHALF;
+            dma1(dst + 0x2000, a1);
+            dma1(dst + 0x3000, a1 + 4096);
+        }
+        if constexpr (!WR) {
+            const unsigned char* b0 = bsrc + (long)st * (4 * BPLANE);
+            dma1(dst + H * 0x2000, b0);
+            dma1(dst + H * 0x2000 + 0x1000, b0 + 4096);
+        }
+    };
+    // WR: B fragments of step st into register set `set` (steps past the end re-read the last one:
+    // every load issued unconditionally keeps the compiler's vmcnt counts straight)
+    u32x4 wreg[WR ? 3 : 1][2][2];
+    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w6);
+    const unsigned wlane = (unsigned)((lane >> 5) * BPLANE + (wn * 64 + (lane & 31)) * 16);
+    const int wtile = tile_n * steps * (4 * BPLANE);
+    u32x4 areg[DA ? 3 : 1][2][2];  // DA: [set][mb][piece]
+    const __amdgpu_buffer_rsrc_t srda = make_srd(p.a3 + (long)tile_m * steps * AHALF);
+    const unsigned alane = (unsigned)((lane >> 5) * APLANE + (wm * 64 + (lane & 31)) * 16);
+    auto load_a = [&](int set, int st) {
+        if constexpr (DA) {
+            const int off = (st < steps ? st : steps - 1) * AHALF;
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int pc = 0; pc < 2; ++pc)
+                    areg[set][mb][pc] = bload_u4s(srda, alane + (unsigned)(mb * 32 * 16 + pc * 2 * APLANE), off);
+        }
+    };
+    auto load_b = [&](int set, int st) {
+        if constexpr (WR) {
+            const int off = wtile + (st < steps ? st : steps - 1) * (4 * BPLANE);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int pc = 0; pc < 2; ++pc)
+                    wreg[set][nb][pc] = bload_u4s(srdw, wlane + (unsigned)(nb * 32 * 16 + pc * 2 * BPLANE), off);
+        }
     };
 
-    f32x16 acc[2][2][2];  // [64-row pair][mb in the pair][nb]; acc = transposed block (lanes = pixels)
+    f32x16 acc[H][2][2];  // [64-row block of the wave][mb in the block][nb]; transposed (lanes = pixels)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < H; ++h)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1092,26 +1126,34 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
                 for (int r = 0; r < 16; ++r) acc[h][i][j][r] = 0.f;
     const int l32 = lane & 31;
     const int half = lane >> 5;
-    const int a_rd = wm * AHALF + half * APLANE + l32 * 16;
-    const int b_rd = 2 * AHALF + half * BPLANE + (wn * 64 + l32) * 16;
-    auto compute = [&](const unsigned char* buf) {
-        u32x4 fa[4][2], fb[2][2];
+    // row r0 = wm * 64 H + 32 mb of the tile: A half r0 / 128, row r0 % 128 of it
+    const int a_rd = ((wm * 64 * H) >> 7) * AHALF + ((wm * 64 * H) & 127) * 16 + half * APLANE + l32 * 16;
+    const int b_rd = H * AHALF + half * BPLANE + (wn * 64 + l32) * 16;
+    auto compute = [&](const unsigned char* buf, int set) {
+        u32x4 fa[2 * H][2], fb[2][2];
 #pragma unroll
         for (int pc = 0; pc < 2; ++pc) {
 #pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-                fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * APLANE);
+            for (int mb = 0; mb < 2 * H; ++mb) {
+                if constexpr (DA) fa[mb][pc] = areg[set][mb & 1][pc];
+                else fa[mb][pc] = *reinterpret_cast<const u32x4*>(buf + a_rd + mb * 32 * 16 + pc * 2 * APLANE);
+            }
+            if constexpr (!WR) {
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-                fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * BPLANE);
+                for (int nb = 0; nb < 2; ++nb)
+                    fb[nb][pc] = *reinterpret_cast<const u32x4*>(buf + b_rd + nb * 32 * 16 + pc * 2 * BPLANE);
+            } else {
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) fb[nb][pc] = wreg[set][nb][pc];
+            }
         }
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < 2 * H; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
                 acc[mb >> 1][mb & 1][nb] = mfma_f16(fb[nb][0], fa[mb][0], acc[mb >> 1][mb & 1][nb]);
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < 2 * H; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
                 f32x16& a = acc[mb >> 1][mb & 1][nb];
@@ -1122,18 +1164,56 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
     const std::integral_constant<int, 0> S0;
     const std::integral_constant<int, 1> S1;
     const std::integral_constant<int, 2> S2;
+    // Step s (stage and B set s % 3): issue B(s + 2) and the copy of s + 2, then wait for this wave's
+    // copy of s (younger ops may fly: not WR, the copy of s + 1; WR, B(s + 1) and the copy of s + 1),
+    // barrier (everyone's copy landed; everyone is done with s - 1, whose stage s + 2 reuses).  WR:
+    // the compiler's own wait for B(s) counts only the B loads after it (8), which leaves the copy
+    // of s + 1 in flight (in-order vmcnt: B(s + 1) and older are complete by then).
     auto kstep = [&](auto S, int step) {
         constexpr int SV = decltype(S)::value;
-        // this wave's copy of `step` landed (step + 1's six may still fly), then everyone's; and
-        // every wave is done with step - 1, whose stage step + 2 reuses
-        if (step + 1 < steps) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (WR) {
+            if (step + 1 < steps) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" : : "n"(4 + NDMA) : "memory");
+            else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+            load_b((SV + 2) % 3, step + 2);
+        } else {
+            if (step + 1 < steps) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" : : "n"(NDMA) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
         if (step + 2 < steps) dma(step + 2, stage(std::integral_constant<int, (SV + 2) % 3>{}));
-        compute(stage(S));
+        compute(stage(S), SV);
     };
-    dma(0, st0);
-    if (steps > 1) dma(1, st1);
     int step = 0;
+    if constexpr (DA) {
+        auto kstep_d = [&](auto S) {
+            constexpr int SV = decltype(S)::value;
+            load_a((SV + 2) % 3, step + 2);
+            load_b((SV + 2) % 3, step + 2);
+            // keep the loads at the head of their step (the scheduler otherwise sinks them behind the
+            // MFMAs, leaving one step of cover and a vmcnt(0) per iteration)
+            __builtin_amdgcn_sched_barrier(0);
+            compute(st0, SV);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        load_a(0, 0);
+        load_b(0, 0);
+        load_a(1, 1);
+        load_b(1, 1);
+        for (; step + 3 <= steps; step += 3) {
+            kstep_d(S0);
+            ++step;
+            kstep_d(S1);
+            ++step;
+            kstep_d(S2);
+            step -= 2;
+        }
+        if (step < steps) kstep_d(S0);
+        ++step;
+        if (step < steps) kstep_d(S1);
+    } else {
+    load_b(0, 0);
+    dma(0, st0);
+    load_b(1, 1);
+    if (steps > 1) dma(1, st1);
     for (; step + 3 <= steps; step += 3) {
         kstep(S0, step);
         kstep(S1, step + 1);
@@ -1141,6 +1221,7 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
     }
     if (step < steps) kstep(S0, step);
     if (step + 1 < steps) kstep(S1, step + 1);
+    }
 
     // per-channel bias and 2^-(sA + sW[n]) of the tile through LDS (global loads between the
     // epilogue's stores would wait for their acks: vmcnt counts both)
@@ -1150,7 +1231,7 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
         sbias[BN + tid] = p.wsinv[n] * ainv;
     }
     __syncthreads();
-    const int prow0 = m0 - b_tile * HWm + wm * 128 + l32;  // pixel of this lane in block mb = 0
+    const int prow0 = m0 - b_tile * HWm + wm * 64 * H + l32;  // pixel of this lane in block mb = 0
     if constexpr (QKV) {
         // as conv_igemm_x6_kernel's pre-split qkv epilogue, over 4 row blocks
         const long img = (long)b_tile * 6 * p.qC * HWm;
@@ -1163,7 +1244,7 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
             const int head = c0 / p.qD, d0 = c0 - head * p.qD;
             const float sc = p.qscale[part];
 #pragma unroll
-            for (int mb = 0; mb < 4; ++mb) {
+            for (int mb = 0; mb < 2 * H; ++mb) {
                 const f32x16& a = acc[mb >> 1][mb & 1][nb];
                 const int pix = prow0 + mb * 32;
                 if (part < 2) {
@@ -1205,10 +1286,10 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
         const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + (long)b_tile * HWm * p.ldres : p.out);
         const int ncol = wn * 64 + 4 * half;
         float vmax = 0.f;
-        f32x4 rv[2][2][2][4];
+        f32x4 rv[H][2][2][4];
         if (p.res) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < H; ++h)
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1219,7 +1300,7 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
                                                                           32 * nb + 8 * j) * 4u);
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
 #pragma unroll
@@ -1243,9 +1324,9 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
         if (p.absmax) block_absmax_atomic(p.absmax, b_tile, vmax);
         if (p.gn_part) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < H; ++h) {
                 GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
-                         (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + 2 * wm + h,
+                         (long)b_tile * p.gn_np64 + p.gn_p64 + (m0 - b_tile * HWm) / 64 + H * wm + h,
                          (p.gn_c0 + n0 + wn * 64) / 32};
                 gn_tile_partials_tr(acc[h], g, 2);
             }
@@ -1253,30 +1334,46 @@ __global__ __launch_bounds__(NT, 2) void proj_pa256_kernel(IgDev p) {
     }
 }
 
-// 0: the 128 x 128 form only; 2: the 256 x 128 form wherever the pixels per image are a multiple
-// of 256; 1 (default): the 256 x 128 form for the pre-split qkv epilogue at >= 2048 of its tiles,
-// the one place it measured faster (64^2, C 512 -> 1536: 341 vs 373 us; the out-projections and
-// the smaller qkv grids ran 4-16 % slower at two workgroups per CU, tools/proj_probe.py).
-// WC_PROJ_BM256 for A/B runs, wc_proj_set_tile for tests.
+// Form of the two pre-split projection GEMMs.  g_pa256 -- 0: the 128 x 128 LDS-DMA form only;
+// 2: the 256 x 128 form wherever the pixels per image are a multiple of 256; 1 (default): the
+// 256 x 128 form for the pre-split qkv epilogue at >= 2048 of its tiles, the one place it measured
+// faster (64^2, C 512 -> 1536: 341 vs 373 us; the out-projections and the smaller qkv grids ran
+// 4-16 % slower at two workgroups per CU, tools/proj_probe.py).  g_pawr -- 1: the 128 x 128 tiles
+// with B in registers (proj_pa_wr_kernel) instead of conv_igemm_x6_kernel's LDS-DMA form.
+// WC_PROJ_BM256 / WC_PROJ_WR for A/B runs, wc_proj_set_tile for tests.
 int g_pa256 = [] {
     const char* e = getenv("WC_PROJ_BM256");
     return e ? atoi(e) : 1;
 }();
+int g_pawr = [] {
+    const char* e = getenv("WC_PROJ_WR");
+    return e ? atoi(e) : 0;
+}();
+
+template <bool QKV, int H, bool WR, bool DA = false>
+void launch_pa_form(const IgDev& d, hipStream_t stream) {
+    IgDev p = d;
+    p.ntiles_n = p.N / 128;
+    dim3 grid((p.M / (128 * H)) * p.ntiles_n);
+    WC_SET_NAME("proj_pa_kernel", {WC_TB(QKV), WC_TI(H), WC_TB(WR), WC_TB(DA)});
+    hipLaunchKernelGGL((proj_pa_kernel<QKV, H, WR, DA>), grid, dim3(NT), 0, stream, p);
+}
 
 int launch_pa(const IgDev& d, hipStream_t stream) {
     const bool fits = (d.Hm * d.Wm) % 256 == 0 && d.N % 128 == 0 && !d.abound;
     const long tiles256 = (long)(d.M / 256) * (d.N / 128);
     if (fits && (g_pa256 == 2 || (g_pa256 == 1 && d.qkv3 && tiles256 >= 2048))) {
-        IgDev p = d;
-        p.ntiles_n = p.N / 128;
-        dim3 grid((p.M / 256) * p.ntiles_n);
-        if (p.qkv3) {
-            WC_SET_NAME("proj_pa256_kernel", {WC_TB(true)});
-            hipLaunchKernelGGL((proj_pa256_kernel<true>), grid, dim3(NT), 0, stream, p);
-        } else {
-            WC_SET_NAME("proj_pa256_kernel", {WC_TB(false)});
-            hipLaunchKernelGGL((proj_pa256_kernel<false>), grid, dim3(NT), 0, stream, p);
-        }
+        if (d.qkv3) launch_pa_form<true, 2, false>(d, stream);
+        else launch_pa_form<false, 2, false>(d, stream);
+        WC_CHECK_LAUNCH();
+        return WC_OK;
+    }
+    if (g_pawr && d.N % 128 == 0 && !d.abound) {
+        if (g_pawr == 2) {
+            if (d.qkv3) launch_pa_form<true, 1, true, true>(d, stream);
+            else launch_pa_form<false, 1, true, true>(d, stream);
+        } else if (d.qkv3) launch_pa_form<true, 1, true>(d, stream);
+        else launch_pa_form<false, 1, true>(d, stream);
         WC_CHECK_LAUNCH();
         return WC_OK;
     }
@@ -1364,8 +1461,11 @@ extern "C" int wc_proj_f16x3_qkv(const wc_conv_args* a, const void* a3, int64_t 
 }
 
 extern "C" int wc_proj_set_tile(int rows) {
-    if (rows != 0 && rows != 128 && rows != 256) return WC_E_ARG;
-    const int prev = g_pa256 == 0 ? 128 : g_pa256 == 2 ? 256 : 0;
-    g_pa256 = rows == 128 ? 0 : rows == 256 ? 2 : 1;
+    // 0 the default choice, 128 / 256 the LDS-DMA forms, -128 the 128-row form with B in registers
+    // -129: 128 x 128 tiles with A and B in registers (no LDS)
+    if (rows != 0 && rows != 128 && rows != 256 && rows != -128 && rows != -129) return WC_E_ARG;
+    const int prev = g_pawr == 2 ? -129 : g_pawr ? -128 : g_pa256 == 0 ? 128 : g_pa256 == 2 ? 256 : 0;
+    g_pa256 = rows == 128 || rows < 0 ? 0 : rows == 256 ? 2 : 1;
+    g_pawr = rows == -128 ? 1 : rows == -129 ? 2 : 0;
     return prev;
 }

@@ -642,10 +642,11 @@ def split_f16x3_tiled(v: View, a_exp: int, scale: Optional[torch.Tensor] = None,
 
 
 def set_proj_tile(rows: int) -> int:
-    """wc_proj_set_tile: row tile of the pre-split projection GEMMs (0 the measured default, 256 or 128);
-    returns the previous setting."""
+    """wc_proj_set_tile: form of the pre-split projection GEMMs (0 the measured default, 256 or 128 rows
+    with LDS-DMA B, -128 = 128 rows with B in registers, -129 = A and B in registers); returns the
+    previous setting."""
     prev = _native.load().wc_proj_set_tile(int(rows))
-    _req(prev in (0, 128, 256), 'projection row tile')
+    _req(prev in (0, 128, 256, -128, -129), 'projection row tile')
     return prev
 
 

@@ -71,6 +71,9 @@ def parse(argv=None):
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--precision', default=None, choices=['f16x3', 'bf16x6', 'fp32'],
                     help='conv/attention arithmetic (default: kernels.default_conv_precision(), i.e. f16x3)')
+    ap.add_argument('--pg', action='store_true',
+                    help='initialise the process group and run the N-rank code (collectives included) even at '
+                         'world size 1 (exercises the RCCL branch on a one-GPU box)')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='process-group backend for N>1: nccl (= RCCL over xGMI, the benched path) or gloo '
                          '(x0 gather staged through host memory; lets N ranks share one GPU for rehearsal)')
@@ -171,18 +174,28 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
                            + (f'; algorithmic {rec["algorithmic_bytes"] / 1e9:.3f}' if 'algorithmic_bytes' in rec
                               else ''))
     ev_n, ev_sec = ev.get(name, (0, 0.0))
-    # what a bare f16 MFMA stream sustains on this power-capped chip (committed probe, median of its
-    # power-settled launches): the split-precision kernels' work against it, beside the data-sheet peak
+    # what a bare f16 MFMA stream sustains on this power-capped chip: the MAXIMUM over the committed
+    # waves-per-SIMD sweep (tools/probes/mfma_peak.hip, median of each point's three launches; the
+    # best point is one wave per SIMD issuing back to back), the split-precision kernels' work
+    # against it, beside the data-sheet peak
     sustained = None
-    probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r03_mfma_peak.jsonl')
+    probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r04a_mfma_sweep.jsonl')
     if peak == F16X3_PEAK_TFLOPS and os.path.exists(probe):
-        rates = sorted(r['tflops'] for r in map(json.loads, open(probe)) if r.get('mfma') == 'f32_32x32x16_f16')
-        if rates:
-            f16 = rates[len(rates) // 2]
+        pts = {}
+        for r in map(json.loads, open(probe)):
+            if r.get('mfma') == 'f32_32x32x16_f16':
+                pts.setdefault(r['waves_per_simd'], []).append(r['tflops'])
+        if pts:
+            med = {w: sorted(v)[len(v) // 2] for w, v in pts.items()}
+            wbest = max(med, key=med.get)
+            f16 = med[wbest]
             sustained = {'f16_mfma_tflops': f16, 'fp32_equiv_tflops': round(f16 / 3, 1),
-                         'frac': round(achieved / (f16 / 3), 4),
-                         'source': 'profiles/r03_mfma_peak.jsonl (tools/probes/mfma_peak.hip: back-to-back '
-                                   'v_mfma_f32_32x32x16_f16, 8 waves/SIMD, ~70 ms launches; median)'}
+                         'frac': round(achieved / (f16 / 3), 4), 'waves_per_simd': wbest,
+                         'sweep_f16_tflops_by_waves_per_simd': {str(w): med[w] for w in sorted(med)},
+                         'source': 'profiles/r04a_mfma_sweep.jsonl (tools/probes/mfma_peak.hip: back-to-back '
+                                   'v_mfma_f32_32x32x16_f16, waves/SIMD 8/4/3/2/1, ~70 ms launches on random '
+                                   'operands; the max over the sweep of each point\'s median; clock and MFMA busy '
+                                   'per point: profiles/r04a_mfma_sweep_table.txt)'}
     return {
         'kernel': name,
         'kernel_desc': _describe(name),
@@ -421,7 +434,16 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     dev = torch.device('cuda', local % ndev if args.backend == 'gloo' else local)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # the distributed code path: every rank count above one, or --pg at world size 1
+    dist_on = world > 1 or args.pg
+    if dist_on:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if 'MASTER_PORT' not in os.environ:
+            with socket.socket() as sk:
+                sk.bind(('127.0.0.1', 0))
+                os.environ['MASTER_PORT'] = str(sk.getsockname()[1])
+        os.environ.setdefault('RANK', str(rank))
+        os.environ.setdefault('WORLD_SIZE', str(world))
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
         else:
@@ -449,7 +471,7 @@ def main():
     ts = torch.arange(T, device=dev, dtype=torch.long)
 
     def barrier():
-        if world > 1:
+        if dist_on:
             dist.barrier()
 
     with torch.no_grad():
@@ -467,7 +489,7 @@ def main():
         del xw
         gathered = None
         gather_sec = 0.0
-        if world > 1:  # communicator set up outside the timed region
+        if dist_on:  # communicator set up outside the timed region
             _gather_x0(x, world, args.backend)
         barrier()
         torch.cuda.synchronize()
@@ -479,7 +501,7 @@ def main():
             else:
                 sched.step(x, eps, i, out=nxt, noise='philox', seed=args.seed, sample0=sample0)
             x, nxt = nxt, x
-        if world > 1:
+        if dist_on:
             torch.cuda.synchronize()
             g0 = time.perf_counter()
             gathered = _gather_x0(x, world, args.backend)
@@ -490,7 +512,7 @@ def main():
         elapsed = time.perf_counter() - t0
         per_rank = [elapsed]
         per_rank_gather = [gather_sec]
-        if world > 1:
+        if dist_on:
             allt = _gather_times([elapsed, gather_sec], world, args.backend, dev)
             per_rank = [float(v) for v in allt[:, 0].tolist()]
             per_rank_gather = [float(v) for v in allt[:, 1].tolist()]
@@ -529,8 +551,8 @@ def main():
                     'timesteps': T,
                     'parallelism': (f'batch-sharded x{world}, 1 all-gather of x0 over '
                                     + ('RCCL (xGMI)' if args.backend == 'nccl' else 'gloo (host-staged)'))
-                    if world > 1 else 'single GPU',
-                    'backend': args.backend if world > 1 else None,
+                    if dist_on else 'single GPU',
+                    'backend': args.backend if dist_on else None,
                     'devices': torch.cuda.device_count(),
                     'hip_graph': bool(args.graph),
                     'stream_groups': runner.split if runner is not None else 1,
@@ -547,7 +569,8 @@ def main():
                 },
                 'ms_per_unet_step': round(ms_step, 3),
                 'per_rank_ms_per_step': [round(v / K * 1e3, 3) for v in per_rank],
-                'all_gather_ms': [round(v * 1e3, 3) for v in per_rank_gather] if world > 1 else None,
+                'all_gather_ms': [round(v * 1e3, 3) for v in per_rank_gather] if dist_on else None,
+                'gathered_shape': list(gathered.shape) if gathered is not None else None,
                 'unet_step_tflops_algorithmic': round(unet_tflops, 2) if unet_tflops else None,
             }
             if not args.no_roofline:
@@ -562,7 +585,7 @@ def main():
         else:
             result['cpu_baseline'] = None
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         # ranks 1..N-1 wait here for rank 0's roofline / parity / CPU-baseline legs before tearing the
         # communicator down
         dist.barrier()

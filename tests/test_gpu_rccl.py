@@ -1,0 +1,109 @@
+"""GPU: the RCCL (backend ``nccl``) branch of config 5's sharded sampler, executed on one GPU.
+
+Config 5 (BASELINE.json: 256 px, T=1000, batch 128 over 8 GPUs, one RCCL all-gather over xGMI at the
+end) runs the ``nccl`` branches of ``bench._gather_x0`` / ``bench._gather_times`` and
+``distributed.gather_samples``; the other multi-rank tests use gloo.  Here a fresh child process
+(started before anything touches the GPU) initialises a world-size-1 RCCL process group with
+``device_id`` and drives every one of those branches, so the collective code is executed before the
+driver's 8-GPU run.  Reference loop being sharded: /root/reference/diffusion_model/sample_ddpm.py:35-44.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()), RANK='0', LOCAL_RANK='0',
+               WORLD_SIZE='1')
+    env['PYTHONPATH'] = os.pathsep.join([ROOT, os.path.join(ROOT, 'tests'), env.get('PYTHONPATH', '')])
+    return env
+
+
+CHILD = textwrap.dedent('''
+    import json, os, sys
+    import torch
+    import torch.distributed as dist
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('nccl', device_id=dev)
+    assert dist.get_backend() == 'nccl' and dist.get_world_size() == 1
+    import bench
+    from conftest import GOLDEN
+    from weatherconverter_amd.diffusion_model.config import ModelConfig
+    from weatherconverter_amd.diffusion_model.models.unet_base import Unet
+    from weatherconverter_amd.diffusion_model.distributed import gather_samples, sample_sharded
+    from weatherconverter_amd.diffusion_model.sample_ddpm import sample_tensor
+    from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    from weatherconverter_amd.synthetic import init_synthetic_
+    man = json.load(open(os.path.join(GOLDEN, 'manifest.json')))
+    mc = ModelConfig(**man['tiny']['config'])
+    net = Unet(mc)
+    init_synthetic_(net, seed=0)
+    net = net.to(dev).eval()
+    s = LinearNoiseScheduler(6, 0.0001, 0.02)
+    total = 4
+    ref = sample_tensor(net, s, total, mc.im_channels, mc.im_size, noise='philox', seed=77, graph=True)
+    x0 = sample_sharded(net, s, total, mc.im_channels, mc.im_size, noise='philox', seed=77, graph=True)
+    g = gather_samples(x0, total)
+    gx = bench._gather_x0(x0, 1, 'nccl')
+    tt = bench._gather_times([1.5, 0.25], 1, 'nccl', dev)
+    torch.cuda.synchronize()
+    out = {
+        'finite': bool(torch.isfinite(ref).all()),
+        'sharded_equal': bool(torch.equal(x0, ref)),
+        'gather_samples_equal': bool(torch.equal(g, ref)),
+        'gather_samples_on_device': g.device == dev,
+        'gather_x0_equal': bool(torch.equal(gx, ref)),
+        'gather_times': tt.tolist(),
+    }
+    dist.barrier()
+    dist.destroy_process_group()
+    print('RCCL_RESULT ' + json.dumps(out), flush=True)
+''')
+
+
+def test_rccl_world1_gathers_bit_identical():
+    r = subprocess.run([sys.executable, '-u', '-c', CHILD], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('RCCL_RESULT ')]
+    assert len(line) == 1, r.stdout[-2000:]
+    res = json.loads(line[0][len('RCCL_RESULT '):])
+    assert res['finite']
+    assert res['sharded_equal']
+    assert res['gather_samples_equal'] and res['gather_samples_on_device']
+    assert res['gather_x0_equal']
+    assert res['gather_times'] == [[1.5, 0.25]]
+
+
+def test_bench_pg_nccl_world1():
+    """bench.py's N-rank code with --pg at world size 1 over RCCL: the timed loop, the x0 all-gather
+    and the per-rank timing gather all run through the nccl branch."""
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '1', '--pg', '--backend', 'nccl', '--size', '64',
+           '--batch', '2', '--steps', '3', '--warmup', '1', '--timesteps', '50', '--no-roofline',
+           '--no-cpu-baseline']
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res['n_gpus'] == 1
+    assert res['config']['backend'] == 'nccl'
+    assert res['all_gather_ms'] is not None and len(res['all_gather_ms']) == 1
+    assert res['gathered_shape'] == [2, 3, 64, 64]
+    assert res['config']['x_finite'] is True

@@ -138,6 +138,21 @@ int wc_conv3x3_x6_tile_n(int N);
  * workgroups).  Both forms give bit-identical results.  Returns the previous mode (or WC_E_ARG).
  * Process-wide, not thread-safe against concurrent launches. */
 int wc_conv3x3_set_onewave(int mode);
+/* The ResBlock 3x3 conv (GN+SiLU prologue on segment 0, optional fused 1x1 residual segment 1)
+ * through a Winograd F(2,3) transform along x on f16x3 (csrc/wc_wino.hip): per output pair and
+ * kernel row, V = (d0-d2, d1+d2, d2-d1, d1-d3) of the prologue output, U = (g0, (g0+g1+g2)/2,
+ * (g0-g1+g2)/2, g2), M_p = sum V_p U_p, y = (M0+M1+M2, M1-M2-M3): 12 MFMA K-steps per chunk instead
+ * of 18 per output pair.  Same contract as wc_conv3x3_f16x3 (a_exp is the GroupNorm exponent; the
+ * kernel uses a_exp - 1 for the doubled V range) except: segment 0 must carry the GN scale/shift and
+ * SiLU, no epilogue activation, and a segment 1 needs a_bound (it runs on f16x3: the residual enters
+ * the transform domain as M0 += x_even W_r, M3 += -x_odd W_r).  w layout per N tile (BN =
+ * wc_conv3x3_wino_tile_n(N)): [C0/16][kernel row 3][position 4][piece 2][k-half 2][BN][8] fp16 bits of
+ * U * 2^sW[n], then [C1/16][piece 2][k-half 2][BN][8] of the residual weight (same scale);
+ * w_inv_scale[n] = 2^-sW[n].  H % (BN == 64 ? 16 : 8) == 0, W % 16 == 0.
+ * Replaces unet_base.py:92,106 (+ :107-109 residual_input_conv), forward :146-150. */
+int wc_conv3x3_wino_f16x3(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
+                          const float* w_inv_scale, const float* a_bound, void* stream);
+int wc_conv3x3_wino_tile_n(int N);
 
 /* General implicit-GEMM conv at the same bf16x6 arithmetic: exactly wc_conv_igemm's contract
  * (tap grids, input strides, the 1x1 residual segment, output maps, NCHW store; an activation

@@ -44,7 +44,10 @@ def mha(a: torch.Tensor, w_in, b_in, w_out, b_out, heads: int) -> torch.Tensor:
     (float64 / autograd, the training tests' reference) the same math written out."""
     B, N, C = a.shape
     if a.dtype == torch.float32 and not torch.is_grad_enabled() and not a.requires_grad:
-        return torch._native_multi_head_attention(a, a, a, C, heads, w_in, b_in, w_out, b_out, None, False, True,
+        # need_weights=True, average_attn_weights=True: the reference's own call (self.attentions[i](x, x, x),
+        # nn.MultiheadAttention's defaults), so the same native kernel path; the weights are discarded as
+        # the reference discards them (unet_base.py:158)
+        return torch._native_multi_head_attention(a, a, a, C, heads, w_in, b_in, w_out, b_out, None, True, True,
                                                   None)[0]
     d = C // heads
     qkv = F.linear(a, w_in, b_in)

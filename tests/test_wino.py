@@ -1,0 +1,206 @@
+"""The Winograd F(2,3)-along-x ResBlock conv (csrc/wc_wino.hip, kernels.pack_wino / conv3x3_wino).
+
+CPU: the transform algebra and the weight pack — the packed fp16 pieces, read back through the
+layout the kernel uses, reconstruct the float64 filter transform, and the F(2,3) algorithm evaluated in
+float64 on them reproduces the direct 3x3 conv (+ the 1x1 residual folded into positions 0 and 3).
+GPU: the kernel against a float64 direct conv (reference ResBlock convs unet_base.py:87-109,
+:146-150), within 4x (+2e-7) of the direct f16x3 kernel's own error and 1e-5, with bias, temb, residual
+segment (chunk counts equal and unequal), the epilogue residual view, per-image absmax and GroupNorm
+tile partials.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+TAPS3 = [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]
+
+
+def rel_l2(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm())
+
+
+def _pack(w):  # [Co][Ci][3][3] -> [Co][9 * Ci], K = (ky * 3 + kx, c) (engine.pack_conv)
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+
+def _unpack_wino(wp, N, C0, C1):
+    """Invert pack_wino's layout: (U [N][3][4][C0] float64, residual [N][C1] float64) from the pieces."""
+    BN, T = wp.BN, wp.data.shape[0]
+    d = wp.data.cpu()
+    n0 = 3 * 4 * C0 * 2 * BN
+    seg0 = d[:, :n0].reshape(T, C0 // 16, 3, 4, 2, 2, BN, 8).view(torch.float16).double()
+    u = (seg0[:, :, :, :, 0] + seg0[:, :, :, :, 1])  # [T][nc][3][4][kh][BN][8]
+    u = u.permute(0, 5, 2, 3, 1, 4, 6).reshape(T * BN, 3, 4, C0)
+    ws = wp.wsinv.cpu().double()
+    U = u[:N] * ws[:N, None, None, None]
+    R = None
+    if C1:
+        seg1 = d[:, n0:].reshape(T, C1 // 16, 2, 2, BN, 8).view(torch.float16).double()
+        r = (seg1[:, :, 0] + seg1[:, :, 1]).permute(0, 3, 1, 2, 4).reshape(T * BN, C1)
+        R = r[:N] * ws[:N, None]
+    return U, R
+
+
+def _wino_conv_f64(a, U, bias):
+    """F(2,3) along x in float64: a [B][C][H][W] (prologue applied), U [N][3][4][C] -> [B][N][H][W]."""
+    B, C, H, W = a.shape
+    ap = F.pad(a, (1, 1, 1, 1))
+    out = torch.zeros((B, U.shape[0], H, W), dtype=torch.float64)
+    for ky in range(3):
+        rows = ap[:, :, ky:ky + H, :]  # input rows oy + ky - 1
+        d = [rows[:, :, :, k:k + W - 1:2] for k in range(4)]  # d_k of output pair t: column 2t - 1 + k
+        V = [d[0] - d[2], d[1] + d[2], d[2] - d[1], d[1] - d[3]]
+        M = [torch.einsum('bcht,nc->bnht', V[p], U[:, ky, p]) for p in range(4)]
+        out[:, :, :, 0::2] += M[0] + M[1] + M[2]
+        out[:, :, :, 1::2] += M[1] - M[2] - M[3]
+    return out + bias[None, :, None, None]
+
+
+@pytest.mark.parametrize('N,C0,C1', [(128, 32, 0), (64, 48, 32), (192, 16, 64)])
+def test_pack_wino_reconstructs_the_filter_transform(N, C0, C1):
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(7)
+    w = torch.randn((N, 9 * C0 + C1), generator=g) * torch.rand((N, 1), generator=g) * 3
+    wp = K.pack_wino(w, C0, C1)
+    assert wp.order == 'wino' and wp.res_f16 == bool(C1)
+    assert wp.data.numel() * 2 == wp.data.shape[0] * (12 * C0 // 16 + C1 // 16) * wp.BN * 64
+    U, R = _unpack_wino(wp, N, C0, C1)
+    Uref = K.wino_filter(w, C0)
+    assert rel_l2(U, Uref) < 3e-7
+    # the per-channel scale puts every packed value under 2^14 and the largest at >= 2^13
+    ws = wp.wsinv[:N].double()
+    amax = Uref.abs().reshape(N, -1).amax(1)
+    if C1:
+        amax = torch.maximum(amax, w[:, 9 * C0:].double().abs().amax(1))
+        assert rel_l2(R, w[:, 9 * C0:].double()) < 3e-7
+    scaled = amax / ws
+    assert bool((scaled <= 2**14).all()) and bool((scaled >= 2**13).all())
+
+
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr', [(1, 4, 8, 16, 8, 0), (2, 6, 10, 8, 4, 5)])
+def test_wino_algebra_equals_direct_conv(B, H, W, Ci, Co, Cr):
+    """F(2,3) in float64 on the exact filter transform (+ the residual in positions 0 and 3) equals
+    the direct conv to rounding."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn((B, Ci, H, W), generator=g, dtype=torch.float64)
+    w = torch.randn((Co, Ci, 3, 3), generator=g, dtype=torch.float64)
+    b = torch.randn(Co, generator=g, dtype=torch.float64)
+    U = K.wino_filter(_pack(w), Ci)
+    got = _wino_conv_f64(a, U, b)
+    ref = F.conv2d(a, w, b, padding=1)
+    if Cr:
+        xr = torch.randn((B, Cr, H, W), generator=g, dtype=torch.float64)
+        wr = torch.randn((Co, Cr), generator=g, dtype=torch.float64)
+        r = torch.einsum('bchw,nc->bnhw', xr, wr)
+        ref = ref + r
+        # the residual in the transform domain: M0 += x_even W_r, M3 += (-x_odd) W_r
+        got = got + torch.stack([r[..., 0::2], r[..., 1::2]], -1).reshape(ref.shape)
+    assert rel_l2(got, ref) < 1e-14
+
+
+def _gn_affine(x, gamma, beta, G=8, eps=1e-5):
+    B, C = x.shape[:2]
+    xg = x.double().reshape(B, G, -1)
+    rstd = 1.0 / torch.sqrt(xg.var(-1, unbiased=False) + eps)
+    mean = xg.mean(-1)
+    sc = rstd.repeat_interleave(C // G, 1) * gamma.double()
+    sh = beta.double() - mean.repeat_interleave(C // G, 1) * sc
+    return sc, sh
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+WINO_CASES = [
+    # B, H, W, Ci, Co, Cr, gamma scale, outlier
+    (2, 16, 32, 64, 128, 0, 1.0, False),    # odd chunk count 4 -> even; two N tiles
+    (1, 8, 16, 48, 256, 48, 1.0, False),    # 3 chunks, residual chunks == 3x3 chunks
+    (2, 16, 16, 32, 128, 96, 1.0, False),   # residual chunks > 3x3 chunks
+    (1, 32, 16, 128, 64, 64, 1.0, False),   # the BN = 64 / TH = 16 form
+    (1, 16, 16, 64, 128, 32, 20.0, True),   # Samuelson-extreme outlier + large gamma
+    (1, 16, 16, 16, 64, 0, 1.0, False),     # one chunk, BN = 64
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr,gs,outlier', WINO_CASES)
+def test_conv3x3_wino_vs_float64(B, H, W, Ci, Co, Cr, gs, outlier):
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(41)
+    h = torch.randn((B, Ci, H, W), generator=g) * 3 + 0.7
+    if outlier:
+        h.zero_()
+        h[:, ::Ci // 8, 0, 0] = 1e4
+    gamma = gs * (1 + 0.3 * torch.randn(Ci, generator=g))
+    beta = 0.5 * torch.randn(Ci, generator=g)
+    sc, sh = _gn_affine(h, gamma, beta)
+    x2 = torch.randn((B, max(Cr, 16), H, W), generator=g) * 5
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    wr = torch.randn((Co, max(Cr, 16), 1, 1), generator=g) / max(Cr, 16)**0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    temb = torch.randn((B, Co + 8), generator=g)
+    a = F.silu(h.double() * sc[:, :, None, None] + sh[:, :, None, None])
+    ref = F.conv2d(a, w.double(), b.double(), padding=1) + temb[:, :Co].double()[:, :, None, None]
+    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.float().cuda(), shift=sh.float().cuda(), silu=True)]
+    wp = _pack(w)
+    xb = None
+    if Cr:
+        ref = ref + F.conv2d(x2.double(), wr.double())
+        segs.append(K.Seg(K.View.full(_nhwc(x2).cuda()), [(0, 0)], kbase=9 * Ci))
+        wp = torch.cat([wp, wr.reshape(Co, Cr)], 1)
+        _, _, xb = K.gn_affine(segs[1].view, None, None, bound=True)
+    wp = wp.contiguous().cuda()
+    e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * W * Ci // 8)
+    tcu = temb.cuda()
+    outs = {}
+    for mode in ('wino', 'f16x3'):
+        out = torch.empty((B, H, W, Co), device='cuda')
+        kw = dict(Hm=H, Wm=W, a_exp=e, a_bound=xb, temb=tcu, temb_ld=Co + 8)
+        if mode == 'wino':
+            assert K.wino_eligible(segs, Co, H, W)
+            K.conv3x3_wino(segs, K.pack_wino(wp, Ci, Cr), b.cuda(), K.View.full(out), **kw)
+        else:
+            K.conv3x3_f16x3(segs, K.pack_f16x3(wp, Ci, Cr, res_f16=bool(Cr)), b.cuda(), K.View.full(out), **kw)
+        torch.cuda.synchronize()
+        outs[mode] = _nchw(out.cpu()).double()
+    assert torch.isfinite(outs['wino']).all()
+    ew, ed = rel_l2(outs['wino'], ref), rel_l2(outs['f16x3'], ref)
+    assert ew < 1e-5 and ew <= 4 * ed + 2e-7, (ew, ed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('sw', [8, 32])
+def test_conv3x3_wino_epilogue_res_absmax_gn_partials(sw):
+    """Epilogue residual view (out = conv + res), per-image absmax and GroupNorm tile partials of the
+    Winograd kernel against the values it stored (partials vs a stats pass over the output)."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(43)
+    B, H, W, Ci, Co = 2, 16, 32, 64, 8 * sw if sw >= 16 else 128
+    x = (torch.randn((B, H, W, Ci), generator=g) * 2 + 3).cuda()
+    sc = (1 + 0.2 * torch.randn((B, Ci), generator=g)).cuda()
+    sh = (0.2 * torch.randn((B, Ci), generator=g)).cuda()
+    w = (torch.randn((Co, 9 * Ci), generator=g) / 24).cuda()
+    bias = (torch.randn(Co, generator=g) + 5).cuda()
+    r = torch.randn((B, H, W, Co), generator=g).cuda()
+    seg = [K.Seg(K.View.full(x), TAPS3, scale=sc, shift=sh, silu=True)]
+    wp = K.pack_wino(w, Ci)
+    y0 = torch.empty((B, H, W, Co), device='cuda')
+    K.conv3x3_wino(seg, wp, bias, K.View.full(y0), Hm=H, Wm=W, a_exp=6)
+    y = torch.empty((B, H, W, Co), device='cuda')
+    gp = K.GnPart.attach(y, sw)
+    amax = torch.zeros(B, device='cuda')
+    K.conv3x3_wino(seg, wp, bias, K.View.full(y), Hm=H, Wm=W, a_exp=6, res=K.View.full(r), absmax=amax, gn=gp)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0 + r)
+    assert torch.equal(amax, y.abs().amax((1, 2, 3)))
+    gamma, beta = (1 + torch.randn(Co, generator=g)).cuda(), torch.randn(Co, generator=g).cuda()
+    a1 = K.gn_affine(K.View.full(y), gamma, beta, bound=True, part=gp)
+    a0 = K.gn_affine(K.View.full(y), gamma, beta, bound=True)
+    for u, v in zip(a1, a0):
+        assert torch.allclose(u, v, rtol=2e-6, atol=1e-7), (u - v).abs().max()

@@ -45,9 +45,13 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps
     if res:
         xr = torch.randn((B, H, H, res), device='cuda', generator=g)
         segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=nt * Ci))
-    if mode in ('x6', 'f3') and nt != 9 or mode == 'f3' and not prologue:
+    if mode in ('x6', 'f3', 'wino') and nt != 9 or mode in ('f3', 'wino') and not prologue:
         return None, None, None
-    if mode == 'f3':  # a_exp 4 keeps |x*sc + sh| * 16 far inside fp16 for these synthetic inputs
+    if mode == 'wino':
+        ww = K.pack_wino(w, Ci, res)
+        xb = torch.full((B, ), 8.0, device='cuda') if res else None
+        fn = lambda: K.conv3x3_wino(segs, ww, b, K.View.full(out), Hm=H, Wm=H, a_exp=4, a_bound=xb)  # noqa: E731
+    elif mode == 'f3':  # a_exp 4 keeps |x*sc + sh| * 16 far inside fp16 for these synthetic inputs
         w3 = K.pack_f16x3(w, Ci, res, res_f16=bool(res))
         xb = torch.full((B, ), 8.0, device='cuda') if res else None  # |randn| residual input < 8
         fn = lambda: K.conv3x3_f16x3(segs, w3, b, K.View.full(out), Hm=H, Wm=H, a_exp=4, a_bound=xb)  # noqa: E731

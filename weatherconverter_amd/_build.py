@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('WC_OFFLOAD_ARCH', 'gfx950')
 
-SOURCES = ['wc_conv.hip', 'wc_conv6.hip', 'wc_igemm6.hip', 'wc_gn.hip', 'wc_attention.hip', 'wc_attention6.hip', 'wc_misc.hip', 'wc_old.hip', 'wc_train.hip', 'wc_srgan.hip', 'wc_backward.hip', 'wc_attention_bwd.hip', 'wc_wgrad3.hip', 'wc_attention_bwd6.hip', 'wc_pack.hip']
+SOURCES = ['wc_conv.hip', 'wc_conv6.hip', 'wc_igemm6.hip', 'wc_gn.hip', 'wc_attention.hip', 'wc_attention6.hip', 'wc_misc.hip', 'wc_old.hip', 'wc_train.hip', 'wc_srgan.hip', 'wc_backward.hip', 'wc_attention_bwd.hip', 'wc_wgrad3.hip', 'wc_attention_bwd6.hip', 'wc_pack.hip', 'wc_wino.hip']
 HEADERS = ['wc_common.hpp', 'wc_x6.hpp']
 # The single-piece build (the 16-bit training line): the sources holding f16x3 correction products
 # recompiled with -DWC_SINGLE16=1 (wc_x6.hpp: mfma_f16c), every other object shared.

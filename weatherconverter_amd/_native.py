@@ -17,7 +17,7 @@ MAX_TAPS = 16
 NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 
 EXPORTS = [
-    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_x6_tile_n', 'wc_conv3x3_set_onewave', 'wc_conv_igemm_x6',
+    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_conv3x3_x6_tile_n', 'wc_conv3x3_set_onewave', 'wc_conv_igemm_x6',
     'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
@@ -77,6 +77,8 @@ _SIGS = {
     'wc_conv3x3_set_onewave': [_I],
     'wc_proj_set_tile': [_I],
     'wc_conv3x3_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
+    'wc_conv3x3_wino_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
+    'wc_conv3x3_wino_tile_n': [_I],
     'wc_conv_igemm_x6': [ctypes.POINTER(ConvArgs), _P, _L, _P],
     'wc_conv_igemm_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
     'wc_conv4x4s2_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _P, _P, _P],
@@ -186,8 +188,29 @@ def load(build_if_missing: bool = True):
     lib.wc_version.restype = ctypes.c_char_p
     lib.wc_last_kernel_name.argtypes = []
     lib.wc_last_kernel_name.restype = ctypes.c_char_p
+    for name, value in _selectors.items():  # kernel-form selectors set before this variant was opened
+        getattr(lib, name)(value)
     _libs[v] = lib
     return lib
+
+
+# Process-wide kernel-form selectors (wc_conv3x3_set_onewave, wc_proj_set_tile): each library variant
+# keeps its own static state, so a setting is applied to every loaded variant and replayed into any
+# variant opened later (the single16 training line included).
+_selectors = {}
+
+
+def set_selector(name: str, value: int, valid=lambda prev: True) -> int:
+    """Apply selector `name` (an int -> previous-int entry point) to every library variant; returns the
+    previous value of the active variant's (a result `valid` rejects raises, and nothing is applied)."""
+    prev = getattr(load(), name)(int(value))
+    if not valid(prev):
+        raise RuntimeError(f'weatherconverter_amd kernel {name} failed: bad argument {value}')
+    for lib in list(_libs.values()):
+        if lib is not load():
+            getattr(lib, name)(int(value))
+    _selectors[name] = int(value)
+    return prev
 
 
 def check(status: int, op: str):

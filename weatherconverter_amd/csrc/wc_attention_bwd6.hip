@@ -479,11 +479,11 @@ int launch_bwd6(const float* qkv, int ldq, const float* dO, int lddo, const floa
     }
     const dim3 grid((N + 127) / 128 * DS, heads, B);
     const float scale_log2 = scale * 1.4426950408889634f;
-    WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D), WC_TB(F3)});
+    WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(D), WC_TB(F3), WC_TI(DS)});
     hipLaunchKernelGGL((attn_bwd6_dkdv_kernel<D, F3, DS>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
                        lddq, N, C, scale_log2, scale, eq, ek, ev, dobound, amx);
     WC_CHECK_LAUNCH();
-    WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D), WC_TB(F3)});
+    WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(D), WC_TB(F3), WC_TI(DS)});
     hipLaunchKernelGGL((attn_bwd6_dq_kernel<D, F3, DS>), grid, dim3(256), Cf::LDS, s, qkv, ldq, dO, lddo, lse, Dv, dqkv,
                        lddq, N, C, scale_log2, scale, eq, ek, ev, dobound, amx);
     WC_CHECK_LAUNCH();
@@ -541,7 +541,7 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
                 if (e != hipSuccess) return (int)e;
                 attr_set = true;
             }
-            WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(192), WC_TB(true)});
+            WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(192), WC_TB(true), WC_TI(3)});
             hipLaunchKernelGGL((attn_bwd6_dq_kernel<192, true, 3>), dim3((N + 127) / 128 * 3, heads, B), dim3(256),
                                Cf::LDS, s, qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, N, C,
                                scale * 1.4426950408889634f, scale, eq, ek, ev, dobound, nullptr);

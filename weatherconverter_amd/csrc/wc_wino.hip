@@ -1,0 +1,517 @@
+// ResBlock 3x3 stride-1 conv on f16x3 MFMA through a Winograd F(2,3) transform along x.
+//
+// The direct halo kernel (wc_conv6.hip) spends 9 MFMA K-steps per 16-channel chunk per output
+// pixel.  Along x a 3-tap filter over two outputs is the minimal filtering algorithm F(2,3): with the
+// four input values d0..d3 of an output pair (input columns 2t-1 .. 2t+2) and the three taps g0..g2
+// of one kernel row,
+//     V0 = d0 - d2,  V1 = d1 + d2,  V2 = d2 - d1,  V3 = d1 - d3            (input transform)
+//     U0 = g0,  U1 = (g0 + g1 + g2) / 2,  U2 = (g0 - g1 + g2) / 2,  U3 = g2   (filter transform, host)
+//     M_p = sum over (c, kernel row) of V_p U_p                               (4 GEMMs, one per p)
+//     y0 = M0 + M1 + M2,  y1 = M1 - M2 - M3                                  (output transform)
+// so an output pair costs 3 rows x 4 positions = 12 K-steps instead of 18: 1.5x fewer MFMAs for the
+// same algorithmic work.  Along y the conv stays direct (the kernel row is a halo-row offset), which
+// keeps the accumulator state at 2x the output tile and the transform VALU light.
+//
+// Arithmetic (f16x3, as wc_conv6.hip): V is formed in fp32 from the GN+SiLU prologue output scaled
+// by 2^s (|V| <= 2 x the Samuelson bound, so the host passes the GN exponent and the kernel uses
+// s = a_exp - 1), then split into two round-to-nearest fp16 pieces; U is formed in float64 on the
+// host, scaled per output channel by 2^sW[n] (max |U| 2^sW <= 2^14) and split the same way.
+// Products h_V h_U + h_V l_U + l_V h_U accumulate in fp32 in the MFMA.  Errors: the fp32 rounding of
+// each V (one add) and of the transforms' sums, at fp32-class size (tests/test_wino.py bounds the
+// whole conv against a float64 direct conv at <= 4x the direct kernel's own error).
+//
+// The fused 1x1 residual_input_conv (raw block input X, unet_base.py:146-150) enters the transform
+// domain exactly: y0 += r(x_2t) is M0 += x_2t W_r, and y1 += r(x_2t+1) is M3 += (-x_2t+1) W_r, so
+// one residual chunk is two position GEMMs sharing one weight fragment (12 MFMAs per wave, the
+// direct kernel's count).
+//
+// Tiling.  A workgroup owns TH image rows x 16 columns (8 output pairs = "tiles" per row) x BN
+// channels; each of its 4 waves owns 8 rows x 8 tiles (64 tiles = 128 pixels, two 32-row MFMA
+// blocks) x 32 channels x the 4 positions: acc[4][2] = 128 accumulator registers, 2 waves per SIMD.
+// Per 16-channel chunk the (TH+2) x 18 input halo is loaded once (items of one halo row x 6 pixels
+// x 4 channels: two tiles), GN+SiLU-transformed, Winograd-transformed and split by VALU, and
+// written to LDS as [piece][position][k-half][halo row][tile] 16-byte fragments; every K-step
+// (kernel row dy, position p) then reads its A fragments at a constant halo-row offset dy.  The
+// MFMA row -> (row, tile) map makes each ds_read_b128 lane group read 16 consecutive fragments
+// (two image rows x 8 tiles): conflict-free.  Weight fragments go from L2 straight into three
+// register sets two K-steps ahead (12 steps per chunk: the set of a step is compile-time); one
+// barrier per chunk.  Residual chunks follow the 3x3 chunks (one K-step each, centre values of two
+// chunks in flight).
+//
+// Epilogue as the direct kernel: x 2^-(s + sW[n]), + bias + temb, + residual view, NHWC store,
+// GroupNorm tile partials (each wave's two 64-pixel blocks), per-image absmax.
+// Reference: unet_base.py:87-109 (ResBlock convs), :146-150 (forward), SURVEY.md §8 row a3.
+#include <stdlib.h>
+
+#include "wc_x6.hpp"
+
+namespace {
+
+using namespace wcx6;
+
+constexpr int NT = 256;
+
+struct WDev {
+    const float* src0;
+    int C0, ldc0;
+    const float* scale;
+    const float* shift;
+    const float* src1;
+    int C1, ldc1;
+    int B, H, W, N;
+    const void* w;
+    const float* bias;
+    const float* temb;
+    int temb_ld;
+    const float* res;
+    int ldres;
+    float* out;
+    int ldo;
+    int nck0, nck1;
+    int a_exp;            // s of the transformed segment 0 (the GN exponent - 1)
+    const float* abound;  // per-image bound of segment 1's raw values (or NULL without residual)
+    const float* wsinv;   // 2^-sW[n]
+    float* absmax;
+    float* gn_part;
+    int gn_ncb, gn_sw, gn_c0, gn_np64;
+    int tiles_x, tiles_y, ntiles_n;
+};
+
+template <int TH, int BN>
+struct WTile {
+    static constexpr int WAVES_N = BN / 32;
+    static constexpr int WAVES_M = 4 / WAVES_N;
+    static_assert(WAVES_N * WAVES_M == 4 && WAVES_M * 8 == TH, "each wave owns 8 rows x 8 tiles x 32 channels");
+    static constexpr int HR = TH + 2;            // halo rows
+    // one (piece, position, k-half) plane of [halo row][tile] 16-byte fragments; the 16 extra bytes make
+    // the k-half stride 16 mod 128 so the item writes of a 16-lane group hit 16 distinct 8-byte slots
+    static constexpr int PSTR = HR * 128 + 16;
+    static constexpr int HSTAGE = 16 * PSTR;     // planes (piece 2) x (position 4) x (k-half 2)
+    static constexpr int CPSTR = TH * 128 + 16;  // residual centre plane ([row][tile])
+    static constexpr int CSTAGE = 8 * CPSTR;     // (piece 2) x (position 0 / 3) x (k-half 2)
+    static constexpr int ITEMS = HR * 16;        // (halo row, tile pair, channel quad)
+    static constexpr int I_PER_T = (ITEMS + NT - 1) / NT;
+    static constexpr int C_PER_T = TH * 16 * 4 / NT;  // centre float4 items per thread
+    static constexpr int BSTEP = BN * 64;        // weight bytes of one K-step: [piece 2][k-half 2][BN][8]
+    static constexpr int STEPS = 12;             // (kernel row, position) per chunk
+};
+
+// MFMA row r (0..31) -> (row, tile) of a 4-row x 8-tile block: the ds_read_b128 lane group
+// {0-3, 12-15, 20-27} reads rows 0-1 x tiles 0-7 (16 consecutive fragments), {4-11, 16-19, 28-31}
+// rows 2-3.  (grp, idx) as wc_conv6.hip's row_dy / row_dx.
+WC_DEVICE int wg_grp(int r) { return ((r >= 4 && r < 12) || (r >= 16 && r < 20) || r >= 28) ? 1 : 0; }
+WC_DEVICE int wg_idx(int r) { return r < 4 ? r : r < 12 ? r - 4 : r < 20 ? r - 8 : r < 28 ? r - 12 : r - 16; }
+WC_DEVICE int wg_row(int r) { return 2 * wg_grp(r) + (wg_idx(r) >> 3); }
+WC_DEVICE int wg_tile(int r) { return wg_idx(r) & 7; }
+
+// RES: the fused 1x1 residual segment (raw input, f16x3 under the per-image bound abound).
+template <int TH, int BN, bool RES>
+__global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
+    using T = WTile<TH, BN>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* const cbase = smem + 2 * T::HSTAGE;  // residual centre buffers
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / T::WAVES_N;
+    const int wn = wave % T::WAVES_N;
+
+    // XCD-aware bijective tile order (wc_conv6.hip): consecutive logical tiles on one XCD's L2
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int tile_n = bid % p.ntiles_n;
+    int tt = bid / p.ntiles_n;
+    const int txi = tt % p.tiles_x;
+    tt /= p.tiles_x;
+    const int tyi = tt % p.tiles_y;
+    const int b = tt / p.tiles_y;
+    const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
+
+    int s_exp = p.a_exp;
+    if (RES && p.abound) {
+        const float bnd = p.abound[b];
+        const int e = (int)((__float_as_uint(bnd) >> 23) & 0xffu) - 127;
+        if (bnd > 0.f) s_exp = min(s_exp, 13 - e);
+        s_exp = max(s_exp, -100);
+    }
+    const float ascale = ldexpf(1.0f, s_exp), ainv = ldexpf(1.0f, -s_exp);
+    const int S0 = T::STEPS * p.nck0;
+    const int S = S0 + (RES ? p.nck1 : 0);
+    const unsigned wtile = (unsigned)tile_n * (unsigned)(S * T::BSTEP);
+
+    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
+    const __amdgpu_buffer_rsrc_t srd1 = make_srd(RES ? p.src1 : p.src0);
+    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(p.scale);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(p.shift);
+
+    // ---- halo items: item i = tid + NT j = (halo row i >> 4, tile pair (i >> 2) & 3, quad i & 3) ----
+    const int q = tid & 3;
+    int hoff[T::I_PER_T][6];
+    unsigned hin[T::I_PER_T];
+    int hwr[T::I_PER_T];  // LDS byte offset of the item's (piece 0, position 0) fragment slot
+#pragma unroll
+    for (int j = 0; j < T::I_PER_T; ++j) {
+        const int i = tid + NT * j;
+        const int hrow = i >> 4, tp = (i >> 2) & 3;
+        const bool valid = i < T::ITEMS;
+        const int iy = y0 - 1 + hrow;
+        hin[j] = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int ix = x0 - 1 + 4 * tp + k;
+            const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+            hin[j] |= (inb ? 1u : 0u) << k;
+            hoff[j][k] = inb ? (((b * p.H + iy) * p.W + ix) * p.ldc0 + 4 * q) * 4 : (int)OOB;
+        }
+        hwr[j] = valid ? (q >> 1) * T::PSTR + (hrow * 8 + 2 * tp) * 16 + (q & 1) * 8 : -1;
+    }
+    f32x4 rh[T::I_PER_T][6];
+    f32x4 rsc, rsh;
+    auto load_halo = [&](int c) {
+#pragma unroll
+        for (int j = 0; j < T::I_PER_T; ++j)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) rh[j][k] = bload_f4s(srd0, (unsigned)hoff[j][k], c * 64);
+        const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
+        rsc = bload_f4(srdsc, o);
+        rsh = bload_f4(srdsh, o);
+    };
+    // GN + SiLU prologue (zero padding after it), x 2^s, Winograd input transform of the item's two
+    // tiles, 2-piece fp16 split, 16 fragment writes into halo buffer hs
+    auto write_items = [&](int hs) {
+        unsigned char* base = smem + hs * T::HSTAGE;
+#pragma unroll
+        for (int j = 0; j < T::I_PER_T; ++j) {
+            if (hwr[j] < 0) continue;  // idle item slot (ITEMS is not a multiple of NT)
+            f32x4 v[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                f32x4 a = rh[j][k] * rsc + rsh;
+                a.x = silu_fast(a.x); a.y = silu_fast(a.y);
+                a.z = silu_fast(a.z); a.w = silu_fast(a.w);
+                v[k] = ((hin[j] >> k) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const f32x4 d0 = v[2 * t], d1 = v[2 * t + 1], d2 = v[2 * t + 2], d3 = v[2 * t + 3];
+                const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
+#pragma unroll
+                for (int pos = 0; pos < 4; ++pos) {
+                    u32x2 a0, a1;
+                    split2_f16(V[pos], a0, a1);
+                    unsigned char* d = base + hwr[j] + t * 16 + pos * 2 * T::PSTR;
+                    *reinterpret_cast<u32x2*>(d) = a0;
+                    *reinterpret_cast<u32x2*>(d + 8 * T::PSTR) = a1;
+                }
+            }
+        }
+    };
+
+    // ---- residual centre items: item i = tid + NT j = (row i >> 6, pixel (i >> 2) & 15, quad i & 3) ----
+    f32x4 rc[2][RES ? T::C_PER_T : 1];
+    const int cpx = (tid >> 2) & 15, crow0 = tid >> 6;  // item j: row crow0 + 4 j
+    const unsigned coff0 = (unsigned)(((b * p.H + y0 + crow0) * p.W + x0 + cpx) * p.ldc1 + 4 * q);
+    const unsigned cstep = (unsigned)(4 * p.W * p.ldc1);
+    // position 0 takes x at even columns, position 3 takes -x at odd columns (plane index 1)
+    const int cwr0 = (cpx & 1) * 2 * T::CPSTR + (q >> 1) * T::CPSTR + (crow0 * 8 + (cpx >> 1)) * 16 + (q & 1) * 8;
+    auto load_centre = [&](auto P, int c) {
+        constexpr int PV = decltype(P)::value;
+#pragma unroll
+        for (int j = 0; j < T::C_PER_T; ++j)
+            rc[PV][j] = bload_f4s(srd1, coff0 * 4u, (int)(((unsigned)j * cstep + (unsigned)c * 16u) * 4u));
+    };
+    auto write_centre = [&](auto P, int cs) {
+        constexpr int PV = decltype(P)::value;
+        unsigned char* base = cbase + cs * T::CSTAGE + cwr0;
+        const float sg = (cpx & 1) ? -ascale : ascale;
+#pragma unroll
+        for (int j = 0; j < T::C_PER_T; ++j) {
+            u32x2 a0, a1;
+            split2_f16(rc[PV][j] * sg, a0, a1);
+            unsigned char* d = base + j * 4 * 8 * 16;  // + 4 rows
+            *reinterpret_cast<u32x2*>(d) = a0;
+            *reinterpret_cast<u32x2*>(d + 4 * T::CPSTR) = a1;
+        }
+    };
+
+    // ---- fragment addressing ----
+    const int l32 = lane & 31;
+    const int half = lane >> 5;
+    int abase[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) abase[mb] = ((8 * wm + 4 * mb + wg_row(l32)) * 8 + wg_tile(l32)) * 16;
+    const unsigned wlane = (unsigned)(half * BN * 16 + (wn * 32 + l32) * 16);
+
+    u32x4 wreg[3][2];  // [set][piece]
+    // weight fragments of K-step st (past the end: the last step again, unused): issued unconditionally
+    auto load_w = [&](int set, int st) {
+        const int s = st < S ? st : S - 1;
+        const int off = (int)(wtile + (unsigned)s * T::BSTEP);
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) wreg[set][pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * BN * 16), off);
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // K-step (kernel row dy, position pos) of the chunk in halo buffer hs, weights in set
+    auto compute = [&](int set, int hs, int dy, int pos) {
+        const unsigned char* ha = smem + hs * T::HSTAGE + (pos * 2 + half) * T::PSTR + dy * 128;
+        u32x4 fa[2][2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc)
+                fa[mb][pc] = *reinterpret_cast<const u32x4*>(ha + pc * 8 * T::PSTR + abase[mb]);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) acc[pos][mb] = mfma_f16(fa[mb][0], wreg[set][0], acc[pos][mb]);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            acc[pos][mb] = mfma_f16c(fa[mb][0], wreg[set][1], acc[pos][mb]);
+            acc[pos][mb] = mfma_f16c(fa[mb][1], wreg[set][0], acc[pos][mb]);
+        }
+    };
+    // residual K-step: positions 0 and 3 from centre buffer cs, one weight fragment
+    auto compute_res = [&](int set, int cs) {
+        const unsigned char* ca = cbase + cs * T::CSTAGE + half * T::CPSTR;
+        u32x4 fa[2][2][2];  // [position][mb][piece]
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int pc = 0; pc < 2; ++pc)
+                    fa[r][mb][pc] = *reinterpret_cast<const u32x4*>(ca + (pc * 4 + r * 2) * T::CPSTR +
+                                                                    abase[mb]);
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+                f32x16& a = acc[r ? 3 : 0][mb];
+                a = mfma_f16(fa[r][mb][0], wreg[set][0], a);
+                a = mfma_f16c(fa[r][mb][0], wreg[set][1], a);
+                a = mfma_f16c(fa[r][mb][1], wreg[set][0], a);
+            }
+    };
+
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, 1> I1;
+    // ---- K loop over the 3x3 chunks: chunk c in halo buffer c & 1; step st of a chunk uses weight
+    // set st % 3 (12 steps per chunk), the weights of step st + 2 are issued at its head ----
+    // Chunk c uses halo buffer (nck0 - 1 - c) & 1, counted from the end, so the peeled last chunk is one
+    // compile-time variant flowing into the epilogue (two variants joining there make the register
+    // allocator spill, as in wc_conv6.hip)
+    const int pv0 = (p.nck0 - 1) & 1;
+    load_halo(0);
+    load_w(0, 0);
+    load_w(1, 1);
+    write_items(pv0);
+    __syncthreads();
+    constexpr int HALO_AT = 8;  // the next chunk's halo goes out at this step (after its weight loads)
+    auto chunk = [&](auto P, auto L, int c) {
+        constexpr int PV = decltype(P)::value;
+        constexpr bool LAST = decltype(L)::value != 0;
+#pragma unroll
+        for (int st = 0; st < T::STEPS; ++st) {
+            load_w((st + 2) % 3, T::STEPS * c + st + 2);
+            if (st == HALO_AT) {
+                if constexpr (!LAST) load_halo(c + 1);
+                else if constexpr (RES) load_centre(I0, 0);
+            }
+            if constexpr (LAST && RES) {
+                if (st == HALO_AT + 1) load_centre(I1, p.nck1 > 1 ? 1 : 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            compute(st % 3, PV, st >> 2, st & 3);
+        }
+        if constexpr (!LAST) write_items(PV ^ 1);
+        else if constexpr (RES) write_centre(I0, 0);
+        __syncthreads();
+    };
+    const std::integral_constant<int, 0> NL;
+    const std::integral_constant<int, 1> LL;
+    {
+        int c = 0;
+        if (pv0) chunk(I1, NL, c++);
+        for (; c + 1 < p.nck0 - 1; c += 2) {
+            chunk(I0, NL, c);
+            chunk(I1, NL, c + 1);
+        }
+        chunk(I0, LL, p.nck0 - 1);
+    }
+    if constexpr (RES) {
+        // residual chunk r: weights in set (S0 + r) % 3 = r % 3 ... after the 3x3 loop sets 0 and 1 hold
+        // steps S0 and S0 + 1; from here on the residual steps alternate sets 0 / 1 (one ahead, the load
+        // of step r + 2 issued after step r's MFMAs), centre register set and buffer r & 1
+        auto rstep = [&](auto P, int r) {
+            constexpr int PV = decltype(P)::value;
+            compute_res(PV, PV);
+            load_w(PV, S0 + r + 2);
+            load_centre(P, r + 2 < p.nck1 ? r + 2 : p.nck1 - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (r + 1 < p.nck1) write_centre(std::integral_constant<int, PV ^ 1>{}, PV ^ 1);
+            __syncthreads();
+        };
+        int r = 0;
+        for (; r + 1 < p.nck1; r += 2) {
+            rstep(I0, r);
+            rstep(I1, r + 1);
+        }
+        if (r < p.nck1) rstep(I0, r);
+    }
+
+    // ---- epilogue: output transform, x 2^-(s + sW[n]), + bias + temb, + residual view, NHWC store ----
+    const long img_px = (long)b * p.H * p.W;
+    const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + img_px * p.ldo);
+    const __amdgpu_buffer_rsrc_t srd_res = make_srd(p.res ? p.res + img_px * p.ldres : p.out);
+    const int n = n0 + wn * 32 + l32;
+    const bool nok = n < p.N;
+    float eadd = (nok && p.bias) ? p.bias[n] : 0.f;
+    if (nok && p.temb) eadd += p.temb[b * p.temb_ld + n];
+    const float emul = nok ? p.wsinv[n] * ainv : 0.f;
+    float vmax = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        // output pixel of accumulator row (r & 3) + 8 (r >> 2) + 4 half: (row, 2 tile) and (row, 2 tile + 1)
+        const int pix0 = (y0 + 8 * wm + 4 * mb) * p.W + x0;
+        float rv[2][16];
+        if (p.res) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int px = pix0 + wg_row(row) * p.W + 2 * wg_tile(row);
+                const unsigned o = (unsigned)(px * p.ldres + (nok ? n : 0)) * 4u;
+                rv[0][r] = bload_f1(srd_res, o);
+                rv[1][r] = bload_f1(srd_res, o + (unsigned)p.ldres * 4u);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float m0 = acc[0][mb][r], m1 = acc[1][mb][r], m2 = acc[2][mb][r], m3 = acc[3][mb][r];
+            float ya = ((m0 + m1) + m2) * emul + eadd;
+            float yb = ((m1 - m2) - m3) * emul + eadd;
+            if (p.res) {
+                ya += rv[0][r];
+                yb += rv[1][r];
+            }
+            acc[0][mb][r] = ya;
+            acc[1][mb][r] = yb;
+        }
+        if (nok) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int px = pix0 + wg_row(row) * p.W + 2 * wg_tile(row);
+                const unsigned o = (unsigned)(px * p.ldo + n) * 4u;
+                bstore_f1(srd_out, o, acc[0][mb][r]);
+                bstore_f1(srd_out, o + (unsigned)p.ldo * 4u, acc[1][mb][r]);
+                vmax = fmaxf(vmax, fmaxf(fabsf(acc[0][mb][r]), fabsf(acc[1][mb][r])));
+            }
+        }
+    }
+    if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);
+    if (p.gn_part) {
+        // this wave's two 64-pixel blocks (rows 4 mb .. 4 mb + 3 of its 8) in the direct kernel's numbering
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const f32x16 blk[2][1] = {{acc[0][mb]}, {acc[1][mb]}};
+            GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
+                     (long)b * p.gn_np64 + ((long)(tyi * p.tiles_x + txi) * T::WAVES_M + wm) * 2 + mb,
+                     (p.gn_c0 + n0 + wn * 32) / 32};
+            gn_tile_partials(blk, g, p.N - n0 - wn * 32 >= 32 ? 1 : 0);
+        }
+    }
+}
+
+template <int TH, int BN, bool RES>
+int launch_wino(const WDev& d, hipStream_t stream) {
+    using T = WTile<TH, BN>;
+    constexpr int lds = 2 * T::HSTAGE + (RES ? 2 * T::CSTAGE : 0);
+    static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, RES>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    WDev p = d;
+    p.tiles_x = p.W / 16;
+    p.tiles_y = p.H / TH;
+    p.ntiles_n = (p.N + BN - 1) / BN;
+    dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
+    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TB(RES)});
+    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, RES>), grid, dim3(NT), lds, stream, p);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+}  // namespace
+
+extern "C" int wc_conv3x3_wino_tile_n(int N) { return N <= 64 ? 64 : 128; }
+
+extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
+                                     const float* w_inv_scale, const float* a_bound, void* stream) {
+    if (!a || !w || !a->out || !w_inv_scale) return WC_E_ARG;
+    if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src || !s0.scale || !s0.shift || !s0.silu) return WC_E_ARG;  // the GN + SiLU prologue (its bound)
+    if (a->act != WC_ACT_NONE) return WC_E_ARG;
+    if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    const int BN = wc_conv3x3_wino_tile_n(a->N);
+    const int TH = BN == 64 ? 16 : 8;
+    if (s0.ntaps != 9 || s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
+    for (int t = 0; t < 9; ++t)
+        if (s0.dy[t] != t / 3 - 1 || s0.dx[t] != t % 3 - 1) return WC_E_SHAPE;
+    if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
+    if (a->B <= 0 || a->N <= 0 || s0.H != a->Hm || s0.W != a->Wm || a->Hm % TH || a->Wm % 16) return WC_E_SHAPE;
+    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+    if (reinterpret_cast<uintptr_t>(w) & 15) return WC_E_SHAPE;
+    WDev d{};
+    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.scale = s0.scale; d.shift = s0.shift;
+    d.nck0 = s0.C / 16;
+    const bool res = a->nseg == 2;
+    if (res) {
+        const wc_conv_seg& s1 = a->seg[1];
+        if (!s1.src || s1.scale || !a_bound) return WC_E_ARG;  // the residual runs on f16x3 under a_bound
+        if (s1.ntaps != 1 || s1.dy[0] != 0 || s1.dx[0] != 0 || s1.sy != 1 || s1.sx != 1) return WC_E_SHAPE;
+        if (s1.H != s0.H || s1.W != s0.W || s1.kbase != 9 * s0.C) return WC_E_SHAPE;
+        if (s1.C <= 0 || s1.C % 16 || s1.ldc % 4 || (reinterpret_cast<uintptr_t>(s1.src) & 15)) return WC_E_SHAPE;
+        if ((long)a->B * s1.H * s1.W * s1.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
+        d.src1 = s1.src; d.C1 = s1.C; d.ldc1 = s1.ldc; d.nck1 = s1.C / 16;
+    }
+    if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox)
+        return WC_E_SHAPE;
+    if ((long)a->Hm * a->Wm * a->ldo * 4 >= (1L << 31) || (a->res && (long)a->Hm * a->Wm * a->ldres * 4 >= (1L << 31)))
+        return WC_E_SHAPE;
+    d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
+    d.w = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
+    d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo;
+    d.a_exp = a_exp - 1;  // |V| <= 2 x the GN bound
+    d.abound = res ? a_bound : nullptr;
+    d.wsinv = w_inv_scale;
+    d.absmax = a->absmax_out;
+    d.gn_part = a->gn_part;
+    if (a->gn_part) {
+        const int sw = a->gn_sw;
+        if ((sw != 4 && sw != 8 && sw != 16 && sw != 32) || a->N % 32 || a->gn_c0 % 32 || a->gn_c0 < 0 ||
+            a->gn_c0 + a->N > a->gn_ncb * 32 || a->gn_p64 != 0 || a->gn_np64 * 64 != a->Hm * a->Wm)
+            return WC_E_SHAPE;
+        d.gn_ncb = a->gn_ncb; d.gn_sw = sw; d.gn_c0 = a->gn_c0; d.gn_np64 = a->gn_np64;
+    }
+    const long ntn = (a->N + BN - 1) / BN;
+    if (w_bytes != ntn * (12L * d.nck0 + d.nck1) * BN * 64 || w_bytes >= (1L << 31)) return WC_E_SHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return res ? launch_wino<16, 64, true>(d, s) : launch_wino<16, 64, false>(d, s);
+    return res ? launch_wino<8, 128, true>(d, s) : launch_wino<8, 128, false>(d, s);
+}

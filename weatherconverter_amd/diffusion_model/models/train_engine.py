@@ -778,10 +778,15 @@ class UnetTrainFunction(torch.autograd.Function):
         ctx.tape = engine.last_tape  # this forward's own saved state (gradient accumulation safe)
         engine.last_tape = None
         ctx.param_ids = [id(p) for p in engine.model.parameters()]
+        # the backward builds its data-gradient weight packs lazily from the live parameters: saving
+        # them makes autograd's version check raise if one is modified in place (an optimizer / EMA
+        # step) between this forward and its backward, instead of mixing old and new weights
+        ctx.save_for_backward(*params)
         return out
 
     @staticmethod
     def backward(ctx, gout):
+        ctx.saved_tensors  # noqa: B018  (raises if a parameter changed in place since the forward)
         grads = ctx.engine.backward(gout, ctx.tape)
         ctx.tape = None
         # hand autograd the only references, so it can take each gradient as param.grad instead of

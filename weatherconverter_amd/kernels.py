@@ -462,8 +462,7 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
 
 def set_conv3_onewave(mode: int) -> int:
     """wc_conv3x3_set_onewave: 0 off (default), 1 forced, -1 where it fills the chip; returns the previous mode."""
-    prev = _native.load().wc_conv3x3_set_onewave(int(mode))
-    _req(prev >= -1, 'onewave mode')
+    prev = _native.set_selector('wc_conv3x3_set_onewave', int(mode), lambda v: v >= -1)
     return prev
 
 
@@ -492,6 +491,95 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
            _flops(segs, Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
            w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream(),
            nbytes=_abytes(segs, w3.N, Hm * Wm, res))
+
+
+@functools.lru_cache(maxsize=None)
+def wino_tile(N: int) -> Tuple[int, int]:
+    """(TH, BN) of wc_conv3x3_wino_f16x3 for N output channels."""
+    bn = _native.load().wc_conv3x3_wino_tile_n(N)
+    return (16 if bn == 64 else 8), bn
+
+
+def wino_enabled() -> bool:
+    """ResBlock 3x3 convs through the Winograd F(2,3)-along-x kernel (WC_WINO=0: the direct halo
+    kernel, kept for A/B and as the reference the Winograd kernel is tested against)."""
+    return os.environ.get('WC_WINO', '1') != '0'
+
+
+def wino_filter(w: torch.Tensor, C0: int) -> torch.Tensor:
+    """The F(2,3) filter transform of the 3x3 part of a [N][9*C0 (+ C1)] weight (K = (ky*3 + kx, c)),
+    in float64: U[n][ky][p][c] = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2) of row ky."""
+    g = w[:, :9 * C0].double().reshape(w.shape[0], 3, 3, C0)
+    g0, g1, g2 = g[:, :, 0], g[:, :, 1], g[:, :, 2]
+    return torch.stack([g0, (g0 + g1 + g2) * 0.5, (g0 - g1 + g2) * 0.5, g2], 2)
+
+
+def pack_wino(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
+    """Pack a [N][9*C0 + C1] ResBlock conv weight (3x3 taps then the 1x1 residual columns, as
+    engine.pack_conv) for wc_conv3x3_wino_f16x3: the F(2,3) filter transform in float64, a per-channel
+    power-of-two scale 2^sW[n] with max |U|, |w_res| * 2^sW <= 2^14, each value rounded once to fp32 and
+    split into two round-to-nearest fp16 pieces; layout [N tile][C0/16][ky 3][p 4][piece][k-half][BN][8]
+    then [N tile][C1/16][piece][k-half][BN][8]."""
+    N, K = w.shape
+    _req(K == 9 * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'wino weight shape')
+    _, BN = wino_tile(N)
+    Np = -(-N // BN) * BN
+    T = Np // BN
+    wd = torch.zeros((Np, K), dtype=torch.float64, device=w.device)
+    wd[:N] = w.double()
+    U = wino_filter(wd, C0)  # [Np][3][4][C0]
+    r = wd[:, 9 * C0:]
+    amax = U.abs().reshape(Np, -1).amax(1)
+    if C1:
+        amax = torch.maximum(amax, r.abs().amax(1))
+    sw = torch.where(amax > 0, torch.floor(torch.log2(2.0**14 / amax.clamp_min(1e-300))), torch.zeros_like(amax))
+    sw = sw.clamp(-60, 60)
+    scale = torch.ldexp(torch.ones_like(sw), sw)
+
+    def pieces(v):  # exact power-of-two scaling, one rounding to fp32, two fp16 pieces
+        v32 = (v * scale.reshape((-1, ) + (1, ) * (v.dim() - 1))).float()
+        h = v32.half()
+        return torch.stack([h, (v32 - h.float()).half()]).view(torch.int16)
+
+    nc0 = C0 // 16
+    p0 = pieces(U).view(2, T, BN, 3, 4, nc0, 2, 8).permute(1, 5, 3, 4, 0, 6, 2, 7).reshape(T, -1)
+    parts = [p0]
+    if C1:
+        p1 = pieces(r).view(2, T, BN, C1 // 16, 2, 8).permute(1, 3, 0, 4, 2, 5).reshape(T, -1)
+        parts.append(p1)
+    data = torch.cat(parts, 1).contiguous()
+    wsinv = torch.ldexp(torch.ones(Np, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
+    return X6Weight(data, N, BN, C0, C1, 'wino', wsinv, bool(C1))
+
+
+def wino_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
+    """True when wc_conv3x3_wino_f16x3 accepts this conv (mirrors its host checks)."""
+    s0 = segs[0]
+    TH, _ = wino_tile(N)
+    if s0.scale is None or not s0.silu or len(s0.taps) != 9 or s0.view.C % 16 or Hm % TH or Wm % 16:
+        return False
+    if s0.view.H != Hm or s0.view.W != Wm or s0.stride != 1:
+        return False
+    return len(segs) == 1 or segs[1].view.C % 16 == 0
+
+
+def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
+                 a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
+                 temb_ld: int = 0, res: Optional[View] = None, absmax: Optional[torch.Tensor] = None,
+                 gn: Optional[GnPart] = None):
+    """The ResBlock 3x3 conv (GN+SiLU prologue, optional fused 1x1 residual under a_bound) through the
+    Winograd F(2,3)-along-x kernel (wc_conv3x3_wino_f16x3); a_exp = f16x3_a_exp of the GroupNorm."""
+    _req(w.data.is_cuda and w.data.is_contiguous() and w.order == 'wino', 'wino weight')
+    _req(w.C0 == segs[0].view.C and w.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'wino weight segments')
+    _req(len(segs) == 1 or a_bound is not None, 'the wino residual segment needs a per-image A bound')
+    if a_bound is not None:
+        _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
+    a = _conv_args(segs, w.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
+    TH, BN = wino_tile(w.N)
+    _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {"true" if len(segs) == 2 else "false"}>', 'wc_conv3x3_wino_f16x3',
+           _flops(segs, Hm, Wm, w.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
+           w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(),
+           _ptr(a_bound) if len(segs) == 2 else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res))
 
 
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,
@@ -645,8 +733,7 @@ def set_proj_tile(rows: int) -> int:
     """wc_proj_set_tile: form of the pre-split projection GEMMs (0 the measured default, 256 or 128 rows
     with LDS-DMA B, -128 = 128 rows with B in registers, -129 = A and B in registers); returns the
     previous setting."""
-    prev = _native.load().wc_proj_set_tile(int(rows))
-    _req(prev in (0, 128, 256, -128, -129), 'projection row tile')
+    prev = _native.set_selector('wc_proj_set_tile', int(rows), lambda v: v in (0, 128, 256, -128, -129))
     return prev
 
 

@@ -138,7 +138,8 @@ int wc_conv3x3_x6_tile_n(int N);
  * workgroups).  Both forms give bit-identical results.  Returns the previous mode (or WC_E_ARG).
  * Process-wide, not thread-safe against concurrent launches. */
 int wc_conv3x3_set_onewave(int mode);
-/* The ResBlock 3x3 conv (GN+SiLU prologue on segment 0, optional fused 1x1 residual segment 1)
+/* The ResBlock 3x3 conv (GN+SiLU prologue on segment 0, optional fused 1x1 residual segment 1; or
+ * one raw segment 0 under the per-image bound a_bound, s = min(a_exp - 1, 12 - floor(log2 a_bound[b])))
  * through a Winograd F(2,3) transform along x on f16x3 (csrc/wc_wino.hip): per output pair and
  * kernel row, V = (d0-d2, d1+d2, d2-d1, d1-d3) of the prologue output, U = (g0, (g0+g1+g2)/2,
  * (g0-g1+g2)/2, g2), M_p = sum V_p U_p, y = (M0+M1+M2, M1-M2-M3): 12 MFMA K-steps per chunk instead
@@ -153,6 +154,12 @@ int wc_conv3x3_set_onewave(int mode);
 int wc_conv3x3_wino_f16x3(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
                           const float* w_inv_scale, const float* a_bound, void* stream);
 int wc_conv3x3_wino_tile_n(int N);
+/* Device re-pack of a [N][9*C0 + C1] fp32 ResBlock conv weight (K = (ky*3 + kx, c), then the 1x1
+ * residual columns) into wc_conv3x3_wino_f16x3's layout and w_inv_scale[ceil(N/BN)*BN]: the F(2,3)
+ * filter transform in float64, the per-channel power-of-two scale, one rounding to fp32, two fp16
+ * pieces (bit-identical to kernels.pack_wino's definition).  out_bytes must equal the layout size. */
+int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_bytes, float* w_inv_scale,
+                 void* stream);
 
 /* General implicit-GEMM conv at the same bf16x6 arithmetic: exactly wc_conv_igemm's contract
  * (tap grids, input strides, the 1x1 residual segment, output maps, NCHW store; an activation

@@ -392,8 +392,8 @@ def _model_grads(mc, B, precision, seed=0):
     net = Unet(mc)
     init_synthetic_(net, seed=seed)
     sd = {k: v.detach().clone().double().requires_grad_(True) for k, v in net.state_dict().items()}
-    if precision == 'f16':
-        net.set_train_precision('f16')
+    if precision in ('f16', 'bf16'):
+        net.set_train_precision(precision)
     else:
         net.set_conv_precision(precision)
     net = net.cuda().train()
@@ -439,23 +439,27 @@ def test_unet_grads_tiny_vs_oracle_autograd(precision, monkeypatch):
     _check(ours, ref)
 
 
-def test_unet_grads_f16_training_line_vs_oracle_autograd(monkeypatch):
-    """The 16-bit training line (train precision 'f16': the single-piece build, one fp16 piece per
-    operand, fp32 accumulation) on the 256-px architecture at B=2: its gradient error against float64
-    autograd is that of 16-bit operands — bounded here at 2e-2 overall and 1e-1 per tensor (the fp32-class
-    modes: 1e-5 / 1e-4) — and the single-piece kernels actually ran (their error is far above f16x3's)."""
+@pytest.mark.parametrize('line', ['f16', 'bf16'])
+def test_unet_grads_16bit_training_lines_vs_oracle_autograd(line, monkeypatch):
+    """The 16-bit training lines (train precision 'f16': the single-piece build, one fp16 piece per
+    operand; 'bf16': one bf16 piece per operand on the bf16 MFMA, BASELINE config 3's arithmetic; fp32
+    accumulation) on the 256-px architecture at B=2: their gradient error against float64 autograd is
+    that of 16-bit operands — bounded here at 2e-2 (f16) / 6e-2 (bf16) overall and 1e-1 / 3e-1 per
+    tensor (the fp32-class modes: 1e-5 / 1e-4) — and the single-piece kernels actually ran (their error
+    is far above f16x3's)."""
     monkeypatch.setenv('WC_CHECK_GBOUND', '1')
     from weatherconverter_amd import _native
     from weatherconverter_amd.diffusion_model.config import model_config
-    ours, ref, lo, lr = _model_grads(model_config(256), 2, 'f16')
-    assert 'single16' in _native._libs
+    ours, ref, lo, lr = _model_grads(model_config(256), 2, line)
+    assert {'f16': 'single16', 'bf16': 'bf16'}[line] in _native._libs
     a = torch.cat([ours[k].flatten() for k in ref])
     b = torch.cat([ref[k].flatten() for k in ref])
     tot = rel_l2(a, b)
-    print(f'f16 training line: overall grad rel-L2 {tot:.3e}, loss {lo:.6f} vs {lr:.6f}')
-    assert abs(lo - lr) <= 1e-3 * abs(lr)
-    assert 1e-5 < tot < 2e-2
-    _check(ours, ref, per_tensor=1e-1, overall=2e-2)
+    print(f'{line} training line: overall grad rel-L2 {tot:.3e}, loss {lo:.6f} vs {lr:.6f}')
+    assert abs(lo - lr) <= (1e-3 if line == 'f16' else 8e-3) * abs(lr)
+    overall = 2e-2 if line == 'f16' else 6e-2
+    assert 1e-5 < tot < overall
+    _check(ours, ref, per_tensor=1e-1 if line == 'f16' else 3e-1, overall=overall)
 
 
 def test_unet_grads_256_baseline_architecture_vs_oracle_autograd(monkeypatch):

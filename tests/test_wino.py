@@ -204,3 +204,50 @@ def test_conv3x3_wino_epilogue_res_absmax_gn_partials(sw):
     a0 = K.gn_affine(K.View.full(y), gamma, beta, bound=True)
     for u, v in zip(a1, a0):
         assert torch.allclose(u, v, rtol=2e-6, atol=1e-7), (u - v).abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,C0,C1', [(128, 32, 0), (64, 48, 32), (192, 16, 64), (256, 128, 128)])
+def test_pack_wino_device_bit_identical_to_cpu_definition(N, C0, C1):
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(11)
+    w = torch.randn((N, 9 * C0 + C1), generator=g) * torch.rand((N, 1), generator=g) * 3
+    w[0] = 0.0  # an all-zero channel: scale 2^0
+    w[1, 0] = 2.0**-3  # a channel whose max is an exact power of two
+    w[1, 1:] = 0.0
+    cpu = K.pack_wino(w, C0, C1, device=False)
+    dev = K.pack_wino(w.cuda(), C0, C1, device=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dev.data.cpu(), cpu.data)
+    assert torch.equal(dev.wsinv.cpu(), cpu.wsinv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co', [(2, 16, 32, 128, 64), (1, 8, 16, 48, 128), (2, 32, 16, 64, 64)])
+def test_conv3x3_wino_raw_segment_vs_float64(B, H, W, Ci, Co):
+    """One raw segment under its per-image bound (the training data gradients: dY (*) W flipped), images
+    of different scale."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(47)
+    x = torch.randn((B, Ci, H, W), generator=g) * 3
+    x[0] *= 1e-3
+    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    xn = _nhwc(x).cuda()
+    bound = xn.abs().reshape(B, -1).amax(1).contiguous()
+    segs = [K.Seg(K.View.full(xn), TAPS3)]
+    assert K.wino_eligible(segs, Co, H, W)
+    outs = {}
+    for mode in ('wino', 'f16x3'):
+        out = torch.empty((B, H, W, Co), device='cuda')
+        if mode == 'wino':
+            K.conv3x3_wino(segs, K.pack_wino(_pack(w).cuda(), Ci), None, K.View.full(out), Hm=H, Wm=W, a_exp=60,
+                           a_bound=bound)
+        else:
+            K.conv3x3_f16x3(segs, K.pack_f16x3(_pack(w).cuda(), Ci), None, K.View.full(out), Hm=H, Wm=W, a_exp=60,
+                            a_bound=bound)
+        torch.cuda.synchronize()
+        outs[mode] = _nchw(out.cpu()).double()
+    for b in range(B):  # per image (their scales differ by 1e3)
+        ew, ed = rel_l2(outs['wino'][b], ref[b]), rel_l2(outs['f16x3'][b], ref[b])
+        assert ew < 1e-5 and ew <= 4 * ed + 2e-7, (b, ew, ed)

@@ -35,8 +35,8 @@ def main():
     ap.add_argument('--seed', type=int, default=3455)
     ap.add_argument('--mode', default='step', choices=['step', 'forward'])
     ap.add_argument('--profile', action='store_true', help='per-kernel-class event times of one step')
-    ap.add_argument('--precision', default='fp32-class', choices=['fp32-class', 'f16'],
-                    help="'f16': the 16-bit training line (Unet.set_train_precision('f16'), single-piece build)")
+    ap.add_argument('--precision', default='fp32-class', choices=['fp32-class', 'f16', 'bf16'],
+                    help="'bf16' / 'f16': the 16-bit training lines (Unet.set_train_precision, single-piece builds)")
     args = ap.parse_args()
     if args.mode == 'step':
         return train_step(args)
@@ -90,7 +90,9 @@ DTYPES = {
                   'attention backward under per-image range bounds raised by the gradients\' writers; bf16x6 where '
                   'no bound exists; fp32 MFMA for the dK/dV of head dim 192)',
     'f16': '16-bit line (the f16x3 kernels with one fp16 piece per operand, fp32 accumulation, power-of-two range '
-           'scaling; bf16x6 / fp32 MFMA where no bound exists) -- the analog of the reference\'s bf16 training',
+           'scaling; bf16x6 / fp32 MFMA where no bound exists)',
+    'bf16': 'bf16 (BASELINE config 3): the f16x3 kernels with one bf16 piece per operand on the bf16 MFMA, fp32 '
+            'accumulation; bf16x6 / fp32 MFMA where no bound exists',
 }
 
 
@@ -104,8 +106,8 @@ def train_step(args):
     mc = model_config(args.size)
     net = Unet(mc)
     init_synthetic_(net, seed=0)
-    if args.precision == 'f16':
-        net.set_train_precision('f16')
+    if args.precision in ('f16', 'bf16'):
+        net.set_train_precision(args.precision)
     net = net.to(dev).train()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)  # train_ddpm.py:176 (lr from config.yaml)
     crit = torch.nn.MSELoss()

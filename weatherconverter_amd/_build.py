@@ -24,8 +24,11 @@ HEADERS = ['wc_common.hpp', 'wc_x6.hpp']
 # The single-piece build (the 16-bit training line): the sources holding f16x3 correction products
 # recompiled with -DWC_SINGLE16=1 (wc_x6.hpp: mfma_f16c), every other object shared.
 SINGLE16_SOURCES = ['wc_conv6.hip', 'wc_igemm6.hip', 'wc_attention6.hip', 'wc_wgrad3.hip', 'wc_backward.hip',
-                    'wc_attention_bwd6.hip']
+                    'wc_attention_bwd6.hip', 'wc_wino.hip', 'wc_pack.hip']
 SINGLE16_LIB_PATH = os.path.join(LIBDIR, 'libwc_kernels_single16.so')
+# The bf16 single-piece build (the bf16 training line, BASELINE config 3): the same sources with
+# -DWC_SINGLE16=2 (bf16 pieces on the bf16 MFMA; packs and pre-split writers emit bf16 bits).
+BF16_LIB_PATH = os.path.join(LIBDIR, 'libwc_kernels_bf16.so')
 
 CFLAGS = [
     '-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-munsafe-fp-atomics',
@@ -41,8 +44,8 @@ def _stale(obj, deps):
 
 
 def build(verbose: bool = False, force: bool = False, single16: bool = True) -> str:
-    """Build libwc_kernels.so (and, with single16, libwc_kernels_single16.so); returns the first's path."""
-    os.makedirs(os.path.join(LIBDIR, 'obj', 'single16'), exist_ok=True)
+    """Build libwc_kernels.so (and, with single16, the single-piece variants libwc_kernels_single16.so and
+    libwc_kernels_bf16.so); returns the first's path."""
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'wc_kernels.h')]
     jobs = []
     objs = []
@@ -52,17 +55,21 @@ def build(verbose: bool = False, force: bool = False, single16: bool = True) -> 
         objs.append(obj)
         if force or _stale(obj, [sp] + hdrs):
             jobs.append([HIPCC] + CFLAGS + ['-c', sp, '-o', obj])
-    objs16 = []
+    variants = []  # (library path, objects)
     if single16:
-        for src in SOURCES:
-            if src not in SINGLE16_SOURCES:
-                objs16.append(os.path.join(LIBDIR, 'obj', src.replace('.hip', '.o')))
-                continue
-            sp = os.path.join(CSRC, src)
-            obj = os.path.join(LIBDIR, 'obj', 'single16', src.replace('.hip', '.o'))
-            objs16.append(obj)
-            if force or _stale(obj, [sp] + hdrs):
-                jobs.append([HIPCC] + CFLAGS + ['-DWC_SINGLE16=1', '-c', sp, '-o', obj])
+        for tag, flag, path in (('single16', '1', SINGLE16_LIB_PATH), ('bf16', '2', BF16_LIB_PATH)):
+            os.makedirs(os.path.join(LIBDIR, 'obj', tag), exist_ok=True)
+            vobjs = []
+            for src in SOURCES:
+                if src not in SINGLE16_SOURCES:
+                    vobjs.append(os.path.join(LIBDIR, 'obj', src.replace('.hip', '.o')))
+                    continue
+                sp = os.path.join(CSRC, src)
+                obj = os.path.join(LIBDIR, 'obj', tag, src.replace('.hip', '.o'))
+                vobjs.append(obj)
+                if force or _stale(obj, [sp] + hdrs):
+                    jobs.append([HIPCC] + CFLAGS + [f'-DWC_SINGLE16={flag}', '-c', sp, '-o', obj])
+            variants.append((path, vobjs))
 
     def run(cmd):
         if verbose:
@@ -74,7 +81,7 @@ def build(verbose: bool = False, force: bool = False, single16: bool = True) -> 
 
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    for path, lobjs in ((LIB_PATH, objs), (SINGLE16_LIB_PATH, objs16)):
+    for path, lobjs in [(LIB_PATH, objs)] + variants:
         if not lobjs:
             continue
         if jobs or force or _stale(path, lobjs):

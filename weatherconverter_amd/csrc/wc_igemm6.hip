@@ -524,10 +524,10 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
                             const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
                             const int n = nblk + row;
                             const float v = (acc[mb][nb][r] * sbias[BN + n - n0] + sbias[n - n0]) * sc;
-                            const _Float16 h = (_Float16)v;
-                            const _Float16 l = (_Float16)(v - (float)h);
-                            dst[(long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, h);
-                            dst[plane + (long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, l);
+                            unsigned short h, l;
+                            split2_one(v, h, l);
+                            dst[(long)(d0 + row) * HWm] = h;
+                            dst[plane + (long)(d0 + row) * HWm] = l;
                         }
                     }
                 }
@@ -1271,10 +1271,10 @@ __global__ __launch_bounds__(NT, H == 2 || DA ? 2 : 3) void proj_pa_kernel(IgDev
                         const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
                         const int n = nblk + row;
                         const float v = (a[r] * sbias[BN + n - n0] + sbias[n - n0]) * sc;
-                        const _Float16 h = (_Float16)v;
-                        const _Float16 l = (_Float16)(v - (float)h);
-                        dst[(long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, h);
-                        dst[plane + (long)(d0 + row) * HWm] = __builtin_bit_cast(unsigned short, l);
+                        unsigned short h, l;
+                        split2_one(v, h, l);
+                        dst[(long)(d0 + row) * HWm] = h;
+                        dst[plane + (long)(d0 + row) * HWm] = l;
                     }
                 }
             }

@@ -183,11 +183,19 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
                                                         int C, const float* __restrict__ w,
                                                         const float* __restrict__ bias, int NO,
                                                         float* __restrict__ out, int tiles_x, int tiles_y) {
+    // halo image [channel quad][pixel]: with the lane -> pixel map below every ds_read_b128 lane group
+    // ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) reads 16 consecutive pixels of one halo row, so all
+    // 9 tap offsets are bank-conflict-free (the [pixel][quad] image with thread = row-major pixel was
+    // 4-way conflicted: 2.8e7 conflict cycles per step, profiles/r03j_pmc_step.txt)
     __shared__ f32x4 halo[HD_ITEMS];
+    constexpr int HPIX = (HD_T + 2) * (HD_T + 2);
     const int tile = blockIdx.x;
     const int tx = tile % tiles_x, ty = (tile / tiles_x) % tiles_y, b = tile / (tiles_x * tiles_y);
     const int x0 = tx * HD_T, y0 = ty * HD_T;
-    const int px = threadIdx.x % HD_T, py = threadIdx.x / HD_T;
+    const int lane = threadIdx.x & 63, l32 = lane & 31;
+    const int grp = ((l32 >= 4 && l32 < 12) || (l32 >= 16 && l32 < 20) || l32 >= 28) ? 1 : 0;
+    const int px = l32 < 4 ? l32 : l32 < 12 ? l32 - 4 : l32 < 20 ? l32 - 8 : l32 < 28 ? l32 - 12 : l32 - 16;
+    const int py = (threadIdx.x >> 6) * 4 + (lane >> 5) * 2 + grp;
     float acc0 = bias[0], acc1 = NO > 1 ? bias[1] : 0.f, acc2 = NO > 2 ? bias[2] : 0.f,
           acc3 = (NOC > 3 && NO > 3) ? bias[3] : 0.f;
     // halo item i = threadIdx.x + 256 k: pixel i >> 2, channels 4 (i & 3) ..
@@ -225,7 +233,8 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(ra[k][e], rs[e], rh[e]));
             }
-            halo[threadIdx.x + 256 * k] = v;  // zero padding after the prologue, as the reference pads
+            const int i = threadIdx.x + 256 * k;
+            halo[(i & 3) * HPIX + (i >> 2)] = v;  // zero padding after the prologue, as the reference pads
         }
         __syncthreads();
         if (c0 + 16 < C) load(c0 + 16);
@@ -235,7 +244,7 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
             const int hy = py + tap / 3, hx = px + tap % 3;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const f32x4 a = halo[(hy * (HD_T + 2) + hx) * 4 + q];
+                const f32x4 a = halo[q * HPIX + hy * (HD_T + 2) + hx];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const f32x4 wv = *reinterpret_cast<const f32x4*>(wc + ((tap * 16) + 4 * q + e) * 4);

@@ -16,7 +16,7 @@
 //   bf16 pieces, same scale; wsinv[n] = 2^-sW[n].  Rows n >= N (tile padding) are zero, wsinv 1.
 #include <hip/hip_fp16.h>
 
-#include "wc_common.hpp"
+#include "wc_x6.hpp"
 
 namespace {
 
@@ -89,11 +89,11 @@ __global__ __launch_bounds__(PK_THREADS) void pack_split_kernel(const float* __r
         }
         const long idx0 = base + (s * P * 2 + (kk >> 3)) * BN * 8 + nn * 8 + (kk & 7);
         const long pstride = 2L * BN * 8;
-        if (f16) {
-            const __half h = __float2half_rn(v);
-            const __half l = __float2half_rn(v - __half2float(h));
-            dst[idx0] = (short)__half_as_ushort(h);
-            dst[idx0 + pstride] = (short)__half_as_ushort(l);
+        if (f16) {  // (the bf16 single-piece build: the bf16 piece, wcx6::split2_one)
+            unsigned short h, l;
+            wcx6::split2_one(v, h, l);
+            dst[idx0] = (short)h;
+            dst[idx0 + pstride] = (short)l;
         } else {
             const unsigned short p0 = bf16_hi(v);
             const float r1 = v - bf16_val(p0);

@@ -104,9 +104,12 @@ WC_DEVICE int wg_idx(int r) { return r < 4 ? r : r < 12 ? r - 4 : r < 20 ? r - 8
 WC_DEVICE int wg_row(int r) { return 2 * wg_grp(r) + (wg_idx(r) >> 3); }
 WC_DEVICE int wg_tile(int r) { return wg_idx(r) & 7; }
 
-// RES: the fused 1x1 residual segment (raw input, f16x3 under the per-image bound abound).
-template <int TH, int BN, bool RES>
+// PRO: 2 = GroupNorm affine + SiLU prologue on segment 0 (static Samuelson bound), 0 = raw segment 0
+// under the per-image bound abound (the training data gradients).  RES: the fused 1x1 residual segment
+// (raw input, f16x3 under the per-image bound abound).
+template <int TH, int BN, int PRO, bool RES>
 __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
+    static_assert((PRO == 2 || PRO == 0) && !(PRO == 0 && RES), "GN+SiLU (+ residual) or one raw segment");
     using T = WTile<TH, BN>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* const cbase = smem + 2 * T::HSTAGE;  // residual centre buffers
@@ -132,29 +135,39 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     const int b = tt / p.tiles_y;
     const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
 
+    // s: the transformed segment 0 needs |V| 2^s <= 2^14 (p.a_exp already counts V's doubling); a raw
+    // value under the per-image bound needs bound * 2^s < 2^14 (residual: s <= 13 - e; a raw segment 0,
+    // doubled by the transform: s <= 12 - e)
     int s_exp = p.a_exp;
-    if (RES && p.abound) {
+    if ((RES || PRO == 0) && p.abound) {
         const float bnd = p.abound[b];
         const int e = (int)((__float_as_uint(bnd) >> 23) & 0xffu) - 127;
-        if (bnd > 0.f) s_exp = min(s_exp, 13 - e);
+        if (bnd > 0.f) s_exp = min(s_exp, (PRO == 0 ? 12 : 13) - e);
         s_exp = max(s_exp, -100);
     }
     const float ascale = ldexpf(1.0f, s_exp), ainv = ldexpf(1.0f, -s_exp);
     const int S0 = T::STEPS * p.nck0;
     const int S = S0 + (RES ? p.nck1 : 0);
+    // residual chunk r < nri rides in 3x3 chunk r as a 13th K-step; the rest (nck1 > nck0) follow as a
+    // tail phase, one K-step and one barrier each
+    // (TH = 16: the centre staging of four items per thread does not fit beside the halo's; all tail)
+    constexpr bool RI = RES && TH == 8;
+    const int nri = RI ? min(p.nck0, p.nck1) : 0;
+    const int ntail = RES ? p.nck1 - nri : 0;
     const unsigned wtile = (unsigned)tile_n * (unsigned)(S * T::BSTEP);
 
     const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
     const __amdgpu_buffer_rsrc_t srd1 = make_srd(RES ? p.src1 : p.src0);
     const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w);
-    const __amdgpu_buffer_rsrc_t srdsc = make_srd(p.scale);
-    const __amdgpu_buffer_rsrc_t srdsh = make_srd(p.shift);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
 
     // ---- halo items: item i = tid + NT j = (halo row i >> 4, tile pair (i >> 2) & 3, quad i & 3) ----
     const int q = tid & 3;
-    int hoff[T::I_PER_T][6];
+    int hbase[T::I_PER_T];  // byte offset of the item's first pixel (chunk 0); OOB pixels re-masked per load
     unsigned hin[T::I_PER_T];
     int hwr[T::I_PER_T];  // LDS byte offset of the item's (piece 0, position 0) fragment slot
+    const int hpx = p.ldc0 * 4;  // bytes between horizontally adjacent pixels
 #pragma unroll
     for (int j = 0; j < T::I_PER_T; ++j) {
         const int i = tid + NT * j;
@@ -167,49 +180,65 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
             const int ix = x0 - 1 + 4 * tp + k;
             const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
             hin[j] |= (inb ? 1u : 0u) << k;
-            hoff[j][k] = inb ? (((b * p.H + iy) * p.W + ix) * p.ldc0 + 4 * q) * 4 : (int)OOB;
         }
+        hbase[j] = (((b * p.H + iy) * p.W + x0 - 1 + 4 * tp) * p.ldc0 + 4 * q) * 4;
         hwr[j] = valid ? (q >> 1) * T::PSTR + (hrow * 8 + 2 * tp) * 16 + (q & 1) * 8 : -1;
     }
     f32x4 rh[T::I_PER_T][6];
     f32x4 rsc, rsh;
+    auto load_ss = [&](int c) {
+        if constexpr (PRO != 0) {
+            const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
+            rsc = bload_f4(srdsc, o);
+            rsh = bload_f4(srdsh, o);
+        }
+    };
+    auto load_slot = [&](int j, int c) {  // item slot j of chunk c (every load issued; OOB pixels read 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            rh[j][k] = bload_f4s(srd0, ((hin[j] >> k) & 1u) ? (unsigned)(hbase[j] + k * hpx) : OOB, c * 64);
+    };
     auto load_halo = [&](int c) {
 #pragma unroll
-        for (int j = 0; j < T::I_PER_T; ++j)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) rh[j][k] = bload_f4s(srd0, (unsigned)hoff[j][k], c * 64);
-        const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
-        rsc = bload_f4(srdsc, o);
-        rsh = bload_f4(srdsh, o);
+        for (int j = 0; j < T::I_PER_T; ++j) load_slot(j, c);
+        load_ss(c);
     };
-    // GN + SiLU prologue (zero padding after it), x 2^s, Winograd input transform of the item's two
-    // tiles, 2-piece fp16 split, 16 fragment writes into halo buffer hs
-    auto write_items = [&](int hs) {
-        unsigned char* base = smem + hs * T::HSTAGE;
+    // GN + SiLU prologue of slot j (zero padding after it), x 2^s
+    f32x4 hv[6];
+    auto prologue = [&](int j) {
 #pragma unroll
-        for (int j = 0; j < T::I_PER_T; ++j) {
-            if (hwr[j] < 0) continue;  // idle item slot (ITEMS is not a multiple of NT)
-            f32x4 v[6];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                f32x4 a = rh[j][k] * rsc + rsh;
+        for (int k = 0; k < 6; ++k) {
+            f32x4 a = rh[j][k];
+            if constexpr (PRO == 2) {
+                a = a * rsc + rsh;
                 a.x = silu_fast(a.x); a.y = silu_fast(a.y);
                 a.z = silu_fast(a.z); a.w = silu_fast(a.w);
-                v[k] = ((hin[j] >> k) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
             }
+            hv[k] = ((hin[j] >> k) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    // Winograd input transform of tile t (0, 1) of slot j, 2-piece fp16 split, 8 fragment writes into
+    // halo buffer hs
+    auto transform = [&](int j, int t, int hs) {
+        if (hwr[j] < 0) return;  // idle item slot (ITEMS is not a multiple of NT)
+        unsigned char* base = smem + hs * T::HSTAGE + hwr[j] + t * 16;
+        const f32x4 d0 = hv[2 * t], d1 = hv[2 * t + 1], d2 = hv[2 * t + 2], d3 = hv[2 * t + 3];
+        const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const f32x4 d0 = v[2 * t], d1 = v[2 * t + 1], d2 = v[2 * t + 2], d3 = v[2 * t + 3];
-                const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
+        for (int pos = 0; pos < 4; ++pos) {
+            u32x2 a0, a1;
+            split2_f16(V[pos], a0, a1);
+            unsigned char* d = base + pos * 2 * T::PSTR;
+            *reinterpret_cast<u32x2*>(d) = a0;
+            *reinterpret_cast<u32x2*>(d + 8 * T::PSTR) = a1;
+        }
+    };
+    auto write_items = [&](int hs) {
 #pragma unroll
-                for (int pos = 0; pos < 4; ++pos) {
-                    u32x2 a0, a1;
-                    split2_f16(V[pos], a0, a1);
-                    unsigned char* d = base + hwr[j] + t * 16 + pos * 2 * T::PSTR;
-                    *reinterpret_cast<u32x2*>(d) = a0;
-                    *reinterpret_cast<u32x2*>(d + 8 * T::PSTR) = a1;
-                }
-            }
+        for (int j = 0; j < T::I_PER_T; ++j) {
+            prologue(j);
+            transform(j, 0, hs);
+            transform(j, 1, hs);
         }
     };
 
@@ -220,11 +249,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     const unsigned cstep = (unsigned)(4 * p.W * p.ldc1);
     // position 0 takes x at even columns, position 3 takes -x at odd columns (plane index 1)
     const int cwr0 = (cpx & 1) * 2 * T::CPSTR + (q >> 1) * T::CPSTR + (crow0 * 8 + (cpx >> 1)) * 16 + (q & 1) * 8;
-    auto load_centre = [&](auto P, int c) {
+    // live = false: the same loads at an out-of-range offset (zeros, no traffic): every load is issued
+    // unconditionally (a load behind a runtime branch makes the compiler drain vmcnt at the join)
+    auto load_centre = [&](auto P, int c, bool live = true) {
         constexpr int PV = decltype(P)::value;
+        const unsigned v = live ? coff0 * 4u : OOB;
 #pragma unroll
         for (int j = 0; j < T::C_PER_T; ++j)
-            rc[PV][j] = bload_f4s(srd1, coff0 * 4u, (int)(((unsigned)j * cstep + (unsigned)c * 16u) * 4u));
+            rc[PV][j] = bload_f4s(srd1, v, (int)(((unsigned)j * cstep + (unsigned)c * 16u) * 4u));
     };
     auto write_centre = [&](auto P, int cs) {
         constexpr int PV = decltype(P)::value;
@@ -250,11 +282,21 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
 
     u32x4 wreg[3][2];  // [set][piece]
     // weight fragments of K-step st (past the end: the last step again, unused): issued unconditionally
+    // weight fragments of 3x3 K-step st (st >= S0: tail residual step st - S0; past the end: the last
+    // step again, unused): issued unconditionally
     auto load_w = [&](int set, int st) {
-        const int s = st < S ? st : S - 1;
+        int s = st < S0 ? st : S0 + nri + (st - S0);
+        s = s < S ? s : S - 1;
         const int off = (int)(wtile + (unsigned)s * T::BSTEP);
 #pragma unroll
         for (int pc = 0; pc < 2; ++pc) wreg[set][pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * BN * 16), off);
+    };
+    u32x4 wres[2];  // the interleaved residual step's weights (their own set: the 3-set cycle stays 12-periodic)
+    auto load_wres = [&](int r) {
+        const int s = S0 + r < S ? S0 + r : S - 1;
+        const int off = (int)(wtile + (unsigned)s * T::BSTEP);
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) wres[pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * BN * 16), off);
     };
 
     f32x16 acc[4][2];
@@ -283,7 +325,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
         }
     };
     // residual K-step: positions 0 and 3 from centre buffer cs, one weight fragment
-    auto compute_res = [&](int set, int cs) {
+    auto compute_res = [&](const u32x4 (&w)[2], int cs) {
         const unsigned char* ca = cbase + cs * T::CSTAGE + half * T::CPSTR;
         u32x4 fa[2][2][2];  // [position][mb][piece]
 #pragma unroll
@@ -292,16 +334,15 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
                 for (int pc = 0; pc < 2; ++pc)
-                    fa[r][mb][pc] = *reinterpret_cast<const u32x4*>(ca + (pc * 4 + r * 2) * T::CPSTR +
-                                                                    abase[mb]);
+                    fa[r][mb][pc] = *reinterpret_cast<const u32x4*>(ca + (pc * 4 + r * 2) * T::CPSTR + abase[mb]);
 #pragma unroll
         for (int r = 0; r < 2; ++r)
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb) {
                 f32x16& a = acc[r ? 3 : 0][mb];
-                a = mfma_f16(fa[r][mb][0], wreg[set][0], a);
-                a = mfma_f16c(fa[r][mb][0], wreg[set][1], a);
-                a = mfma_f16c(fa[r][mb][1], wreg[set][0], a);
+                a = mfma_f16(fa[r][mb][0], w[0], a);
+                a = mfma_f16c(fa[r][mb][0], w[1], a);
+                a = mfma_f16c(fa[r][mb][1], w[0], a);
             }
     };
 
@@ -314,29 +355,65 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     // allocator spill, as in wc_conv6.hip)
     const int pv0 = (p.nck0 - 1) & 1;
     load_halo(0);
+    if constexpr (RI) load_centre(I0, 0, nri > 0);
     load_w(0, 0);
     load_w(1, 1);
     write_items(pv0);
+    if constexpr (RI) write_centre(I0, pv0);
     __syncthreads();
-    constexpr int HALO_AT = 8;  // the next chunk's halo goes out at this step (after its weight loads)
+    // The next chunk's halo item slot j goes out at step load_at(j) (after that step's weight loads:
+    // vmcnt drains in issue order, so the weight waits of the following steps wait for it only from
+    // three steps later); its prologue (step pro_at(j)) and transform (tiles 0 / 1 at the next two
+    // steps) run under the MFMAs of those steps, into the other halo buffer, which nobody reads this
+    // chunk.  One slot (TH = 8): loads at 6, VALU at 9-11; two (TH = 16): 4 / 6-8 and 7 / 9-11.  The
+    // next chunk's residual centre rides with slot 0 and is split into the other centre buffer at step 11;
+    // this chunk's residual step (weights from step 7) runs after step 11.
+    constexpr int HALO_AT = T::I_PER_T == 1 ? 6 : 4;
+    auto load_at = [](int j) { return T::I_PER_T == 1 ? 6 : (j == 0 ? 4 : 7); };
+    auto pro_at = [](int j) { return T::I_PER_T == 1 ? 9 : (j == 0 ? 6 : 9); };
     auto chunk = [&](auto P, auto L, int c) {
         constexpr int PV = decltype(P)::value;
         constexpr bool LAST = decltype(L)::value != 0;
 #pragma unroll
         for (int st = 0; st < T::STEPS; ++st) {
             load_w((st + 2) % 3, T::STEPS * c + st + 2);
-            if (st == HALO_AT) {
-                if constexpr (!LAST) load_halo(c + 1);
-                else if constexpr (RES) load_centre(I0, 0);
+            if constexpr (!LAST) {
+#pragma unroll
+                for (int j = 0; j < T::I_PER_T; ++j)
+                    if (st == load_at(j)) load_slot(j, c + 1);
+                if (st == HALO_AT) {
+                    load_ss(c + 1);
+                    if constexpr (RI) load_centre(I0, c + 1, c + 1 < nri);
+                }
+            } else if constexpr (RES) {  // the tail's first two centres
+                if (st == HALO_AT) load_centre(I0, nri, ntail > 0);
+                if (st == HALO_AT + 1) load_centre(I1, nri + 1, ntail > 1);
             }
-            if constexpr (LAST && RES) {
-                if (st == HALO_AT + 1) load_centre(I1, p.nck1 > 1 ? 1 : 0);
+            if constexpr (RI) {
+                if (st == 7) load_wres(c);
             }
             __builtin_amdgcn_sched_barrier(0);
             compute(st % 3, PV, st >> 2, st & 3);
+            if constexpr (!LAST) {
+#pragma unroll
+                for (int j = 0; j < T::I_PER_T; ++j) {
+                    if (st == pro_at(j)) prologue(j);
+                    if (st == pro_at(j) + 1) transform(j, 0, PV ^ 1);
+                    if (st == pro_at(j) + 2) transform(j, 1, PV ^ 1);
+                }
+                if constexpr (RI) {
+                    if (st == T::STEPS - 1) write_centre(I0, PV ^ 1);
+                }
+            }
         }
-        if constexpr (!LAST) write_items(PV ^ 1);
-        else if constexpr (RES) write_centre(I0, 0);
+        if constexpr (RES) {
+            if constexpr (RI) {
+                if (c < nri) compute_res(wres, PV);
+            }
+            if constexpr (LAST) {
+                if (ntail > 0) write_centre(I0, 1);  // tail chunk k in centre buffer (k + 1) & 1
+            }
+        }
         __syncthreads();
     };
     const std::integral_constant<int, 0> NL;
@@ -351,24 +428,24 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
         chunk(I0, LL, p.nck0 - 1);
     }
     if constexpr (RES) {
-        // residual chunk r: weights in set (S0 + r) % 3 = r % 3 ... after the 3x3 loop sets 0 and 1 hold
-        // steps S0 and S0 + 1; from here on the residual steps alternate sets 0 / 1 (one ahead, the load
-        // of step r + 2 issued after step r's MFMAs), centre register set and buffer r & 1
-        auto rstep = [&](auto P, int r) {
+        // tail residual chunk nri + k: weights in set k & 1 (the last 3x3 chunk's prefetch put tail steps 0
+        // and 1 in sets 0 and 1; from here the load of step k + 2 is issued after step k's MFMAs), centre
+        // registers k & 1, centre buffer (k + 1) & 1
+        auto tstep = [&](auto P, int k) {
             constexpr int PV = decltype(P)::value;
-            compute_res(PV, PV);
-            load_w(PV, S0 + r + 2);
-            load_centre(P, r + 2 < p.nck1 ? r + 2 : p.nck1 - 1);
+            compute_res(wreg[PV], PV ^ 1);
+            load_w(PV, S0 + k + 2);
+            load_centre(P, nri + k + 2, k + 2 < ntail);
             __builtin_amdgcn_sched_barrier(0);
-            if (r + 1 < p.nck1) write_centre(std::integral_constant<int, PV ^ 1>{}, PV ^ 1);
+            if (k + 1 < ntail) write_centre(std::integral_constant<int, PV ^ 1>{}, PV);
             __syncthreads();
         };
-        int r = 0;
-        for (; r + 1 < p.nck1; r += 2) {
-            rstep(I0, r);
-            rstep(I1, r + 1);
+        int k = 0;
+        for (; k + 1 < ntail; k += 2) {
+            tstep(I0, k);
+            tstep(I1, k + 1);
         }
-        if (r < p.nck1) rstep(I0, r);
+        if (k < ntail) tstep(I0, k);
     }
 
     // ---- epilogue: output transform, x 2^-(s + sW[n]), + bias + temb, + residual view, NHWC store ----
@@ -434,13 +511,13 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     }
 }
 
-template <int TH, int BN, bool RES>
+template <int TH, int BN, int PRO, bool RES>
 int launch_wino(const WDev& d, hipStream_t stream) {
     using T = WTile<TH, BN>;
     constexpr int lds = 2 * T::HSTAGE + (RES ? 2 * T::CSTAGE : 0);
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, RES>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, PRO, RES>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -450,8 +527,8 @@ int launch_wino(const WDev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TB(RES)});
-    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, RES>), grid, dim3(NT), lds, stream, p);
+    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES)});
+    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, PRO, RES>), grid, dim3(NT), lds, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -465,7 +542,11 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     if (!a || !w || !a->out || !w_inv_scale) return WC_E_ARG;
     if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
     const wc_conv_seg& s0 = a->seg[0];
-    if (!s0.src || !s0.scale || !s0.shift || !s0.silu) return WC_E_ARG;  // the GN + SiLU prologue (its bound)
+    if (!s0.src || (s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
+    // segment 0: the GN + SiLU prologue (its static bound), or one raw segment under a_bound
+    const int pro = s0.scale ? 2 : 0;
+    if (pro == 2 && !s0.silu) return WC_E_ARG;
+    if (pro == 0 && (!a_bound || a->nseg != 1)) return WC_E_ARG;
     if (a->act != WC_ACT_NONE) return WC_E_ARG;
     if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
     const int BN = wc_conv3x3_wino_tile_n(a->N);
@@ -498,7 +579,7 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     d.w = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld;
     d.res = a->res; d.ldres = a->ldres; d.out = a->out; d.ldo = a->ldo;
     d.a_exp = a_exp - 1;  // |V| <= 2 x the GN bound
-    d.abound = res ? a_bound : nullptr;
+    d.abound = (res || pro == 0) ? a_bound : nullptr;
     d.wsinv = w_inv_scale;
     d.absmax = a->absmax_out;
     d.gn_part = a->gn_part;
@@ -512,6 +593,105 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     const long ntn = (a->N + BN - 1) / BN;
     if (w_bytes != ntn * (12L * d.nck0 + d.nck1) * BN * 64 || w_bytes >= (1L << 31)) return WC_E_SHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (BN == 64) return res ? launch_wino<16, 64, true>(d, s) : launch_wino<16, 64, false>(d, s);
-    return res ? launch_wino<8, 128, true>(d, s) : launch_wino<8, 128, false>(d, s);
+    if (pro == 0) return BN == 64 ? launch_wino<16, 64, 0, false>(d, s) : launch_wino<8, 128, 0, false>(d, s);
+    if (BN == 64) return res ? launch_wino<16, 64, 2, true>(d, s) : launch_wino<16, 64, 2, false>(d, s);
+    return res ? launch_wino<8, 128, 2, true>(d, s) : launch_wino<8, 128, 2, false>(d, s);
+}
+
+// ---- device re-pack for wc_conv3x3_wino_f16x3 (training: the weights change every step) ----
+// One workgroup per output channel n (of the N-tile-padded count): max |U|, |w_res| over the row, the
+// power-of-two scale 2^sW with max * 2^sW <= 2^14 (sW from the exponent: exact, no log2), then every
+// value of the row: U in float64 (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2) x 2^sW, rounded once
+// to fp32, split into two round-to-nearest fp16 pieces -- the same IEEE operations in the same order as
+// kernels.pack_wino's torch definition, so the two are bit-identical.
+namespace {
+
+__device__ double wino_u(const float* row, int C0, int ky, int pos, int c) {
+    const double g0 = row[(ky * 3 + 0) * C0 + c], g1 = row[(ky * 3 + 1) * C0 + c], g2 = row[(ky * 3 + 2) * C0 + c];
+    switch (pos) {
+        case 0: return g0;
+        case 1: return ((g0 + g1) + g2) * 0.5;
+        case 2: return ((g0 - g1) + g2) * 0.5;
+        default: return g2;
+    }
+}
+
+__global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict__ w, int K, int N, int C0, int C1,
+                                                        int BN, short* __restrict__ out, float* __restrict__ wsinv) {
+    const int n = blockIdx.x;
+    const bool live = n < N;
+    const float* row = w + (long)(live ? n : 0) * K;
+    const int n0 = 12 * C0, nall = n0 + C1;
+    double m = 0.0;
+    if (live) {
+        for (int i = threadIdx.x; i < nall; i += blockDim.x) {
+            double v;
+            if (i < n0) {
+                const int c = i % C0, kp = i / C0;
+                v = wino_u(row, C0, kp / 4, kp % 4, c);
+            } else {
+                v = row[9 * C0 + (i - n0)];
+            }
+            m = fmax(m, fabs(v));
+        }
+    }
+    __shared__ double red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    const double amax = red[0];
+    int sw = 0;
+    if (amax > 0.0) {
+        int e;
+        const double mant = frexp(amax, &e);  // amax = mant 2^e, mant in [0.5, 1)
+        sw = (mant == 0.5 ? 15 : 14) - e;     // floor(log2(2^14 / amax))
+        sw = sw < -60 ? -60 : sw > 60 ? 60 : sw;
+    }
+    const double scale = ldexp(1.0, sw);
+    if (threadIdx.x == 0) wsinv[n] = ldexpf(1.0f, -sw);
+    const int T = n / BN, nn = n % BN;
+    const long rowlen = (long)(12 * (C0 / 16) + C1 / 16) * 2 * 2 * BN * 8;  // int16 per N tile
+    short* trow = out + (long)T * rowlen;
+    for (int i = threadIdx.x; i < nall; i += blockDim.x) {
+        double v = 0.0;
+        long o;
+        int plane;  // distance between the two pieces (int16 units)
+        if (i < n0) {
+            const int c = i % C0, kp = i / C0, ky = kp / 4, pos = kp % 4;
+            if (live) v = wino_u(row, C0, ky, pos, c);
+            const int chunk = c / 16, kh = (c % 16) / 8, e = c % 8;
+            o = ((((long)(chunk * 3 + ky) * 4 + pos) * 2 * 2 + kh) * BN + nn) * 8 + e;  // piece 0
+            plane = 2 * BN * 8;
+        } else {
+            const int c = i - n0;
+            if (live) v = row[9 * C0 + c];
+            const int chunk = c / 16, kh = (c % 16) / 8, e = c % 8;
+            o = (long)(C0 / 16) * 12 * 2 * 2 * BN * 8 + (((long)chunk * 2 * 2 + kh) * BN + nn) * 8 + e;
+            plane = 2 * BN * 8;
+        }
+        const float v32 = (float)(v * scale);
+        unsigned short h, l;
+        split2_one(v32, h, l);
+        trow[o] = (short)h;
+        trow[o + plane] = (short)l;
+    }
+}
+
+}  // namespace
+
+extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_bytes, float* w_inv_scale,
+                            void* stream) {
+    if (!w || !out || !w_inv_scale) return WC_E_ARG;
+    if (N <= 0 || C0 <= 0 || C0 % 16 || C1 < 0 || C1 % 16) return WC_E_SHAPE;
+    const int BN = wc_conv3x3_wino_tile_n(N);
+    const long ntn = (N + BN - 1) / BN;
+    if (out_bytes != ntn * (12L * (C0 / 16) + C1 / 16) * BN * 64) return WC_E_SHAPE;
+    hipLaunchKernelGGL(pack_wino_kernel, dim3((unsigned)(ntn * BN)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       w, 9 * C0 + C1, N, C0, C1, BN, reinterpret_cast<short*>(out), w_inv_scale);
+    wc_last_kernel = "pack_wino_kernel";
+    WC_CHECK_LAUNCH();
+    return WC_OK;
 }

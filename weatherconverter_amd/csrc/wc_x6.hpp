@@ -55,16 +55,24 @@ WC_DEVICE f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-WC_DEVICE f32x16 mfma_f16(u32x4 a, u32x4 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
-                                                  0, 0, 0);
-}
-// A correction product of the f16x3 split (h*l or l*h).  The single-piece build (-DWC_SINGLE16=1,
-// libwc_kernels_single16.so: the 16-bit training line) drops them: every f16x3 kernel then computes
-// with one fp16 piece per operand (h*h), fp32 accumulation, the same power-of-two range scaling.
+// A correction product of the f16x3 split (h*l or l*h).  The single-piece builds drop them: every
+// f16x3 kernel then computes with one 16-bit piece per operand (h*h), fp32 accumulation, the same
+// power-of-two range scaling.  -DWC_SINGLE16=1 (libwc_kernels_single16.so, the 16-bit training line):
+// the piece is fp16; -DWC_SINGLE16=2 (libwc_kernels_bf16.so, the bf16 training line of BASELINE
+// config 3): the piece is bf16 (round to nearest even) on v_mfma_f32_32x32x16_bf16, and every pack /
+// pre-split writer emits bf16 bits through the helpers below.
 #ifndef WC_SINGLE16
 #define WC_SINGLE16 0
 #endif
+WC_DEVICE f32x16 mfma_f16(u32x4 a, u32x4 b, f32x16 c) {
+#if WC_SINGLE16 == 2
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+#else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+#endif
+}
 WC_DEVICE f32x16 mfma_f16c(u32x4 a, u32x4 b, f32x16 c) {
 #if WC_SINGLE16
     (void)a;
@@ -112,12 +120,29 @@ typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 // l = fp16(v - h) by v_fma_mix (f32 v, f16 h): v - h is exact in fp32 (at most 12 significant bits
 // below h), so rounding the exact fma result to fp16 once is bit for bit the convert-back / subtract /
 // convert sequence, in 3 instructions per pair instead of 5-6
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 WC_DEVICE void split2_pair(f32x2 v, unsigned& h, unsigned& l) {
+#if WC_SINGLE16 == 2
+    h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2v));  // v_cvt_pk_bf16_f32 (RNE)
+    l = 0u;  // the single-piece line has no correction products
+#else
     const f16x2v hh = __builtin_convertvector(v, f16x2v);
     h = __builtin_bit_cast(unsigned, hh);
     asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
         "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
         : "=&v"(l) : "v"(v.x), "v"(h), "v"(v.y));
+#endif
+}
+// The two 16-bit pieces of one value (h = piece(v), l = piece(v - h); bf16 line: l = 0), as bit patterns.
+WC_DEVICE void split2_one(float v, unsigned short& h, unsigned short& l) {
+#if WC_SINGLE16 == 2
+    h = __builtin_bit_cast(unsigned short, (__bf16)v);
+    l = 0;
+#else
+    const _Float16 hh = (_Float16)v;
+    h = __builtin_bit_cast(unsigned short, hh);
+    l = __builtin_bit_cast(unsigned short, (_Float16)(v - (float)hh));
+#endif
 }
 WC_DEVICE void split2_f16(f32x4 v, u32x2& ph, u32x2& pl) {
     unsigned h0, l0, h1, l1;

@@ -92,8 +92,10 @@ class TrainEngine:
              or K.default_conv_precision())
         # 'f16': the 16-bit training line — the f16x3 arithmetic of mode f16x3 run on the single-piece
         # build (one fp16 piece per operand: wc_x6.hpp mfma_f16c), every kernel call routed to it
-        self.variant = 'single16' if p == 'f16' else ''
-        if p == 'f16':
+        # 'bf16': the same on the bf16 single-piece build (one bf16 piece per operand on the bf16 MFMA:
+        # BASELINE config 3's bf16 training)
+        self.variant = {'f16': 'single16', 'bf16': 'bf16'}.get(p, '')
+        if p in ('f16', 'bf16'):
             p = 'f16x3'
         # f16x3 needs range bounds that gradients do not have: the backward runs bf16x6; the forward's
         # GroupNorm-prologue convs and projections run f16x3 under their static bounds (as inference)
@@ -129,6 +131,7 @@ class TrainEngine:
         ci, co = w1.shape[1], w1.shape[0]
         wr2 = wr.reshape(co, ci)
         f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
+        wino = K.wino_enabled()
         w2cat = torch.cat([pack_conv(w2), wr2], 1)
         L = _Pack.lazy
         return _Pack(
@@ -147,7 +150,14 @@ class TrainEngine:
             f3_1T=L(lambda: K.pack_f16x3(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co)) if self.f3d else None,
             f3_2T=L(lambda: K.pack_f16x3(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co)) if self.f3d else None,
             f3_rT=L(lambda: K.pack_f16x3(wr2.t().contiguous().float(), co, ntaps=1, order='natural'))
-            if self.f3d else None)
+            if self.f3d else None,
+            # the Winograd F(2,3)-along-x forms of the same f16x3 convs (forward and data gradients)
+            wn_1=L(lambda: K.pack_wino(pack_conv(w1).float(), ci)) if f3 and wino else None,
+            wn_2=L(lambda: K.pack_wino(w2cat.float(), co, ci)) if f3 and wino else None,
+            wn_1T=L(lambda: K.pack_wino(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co))
+            if self.f3d and wino and ci % 16 == 0 and co % 16 == 0 else None,
+            wn_2T=L(lambda: K.pack_wino(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co))
+            if self.f3d and wino and co % 16 == 0 else None)
 
     def _pack_attn(self, blk, i: int):
         mha, gn = blk.attentions[i], blk.attention_norms[i]
@@ -459,7 +469,10 @@ class TrainEngine:
         h = View.full(self._new(B, H, W, co))
         seg1 = [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)]
         b1 = rp['conv1'].bias.detach().float().contiguous()
-        if rp['f3_1'] is not None and K.x6_eligible(seg1, co, H, W):
+        if rp['wn_1'] is not None and K.wino_eligible(seg1, co, H, W):
+            K.conv3x3_wino(seg1, rp['wn_1'], b1, h, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8),
+                           temb=temb[:, rp['off']:], temb_ld=temb.shape[1])
+        elif rp['f3_1'] is not None and K.x6_eligible(seg1, co, H, W):
             K.conv3x3_f16x3(seg1, rp['f3_1'], b1, h, Hm=H, Wm=W,
                             a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8), temb=temb[:, rp['off']:],
                             temb_ld=temb.shape[1])
@@ -467,7 +480,12 @@ class TrainEngine:
             self._conv(seg1, rp['pk1'], b1, h, H, W, temb=temb[:, rp['off']:], temb_ld=temb.shape[1])
         st2 = K.gn_stats_pair(h, g2.weight.detach().float(), g2.bias.detach().float())
         seg2 = [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)]
-        if rp['f3_2'] is not None and K.x6_eligible(seg2, co, H, W):
+        if rp['wn_2'] is not None and K.wino_eligible(seg2, co, H, W):
+            K.conv3x3_wino(seg2, rp['wn_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
+                           a_bound=st1[4], absmax=amx)
+            if amx is not None:
+                self._raised[id(amx)] = True
+        elif rp['f3_2'] is not None and K.x6_eligible(seg2, co, H, W):
             # the residual segment (raw X) in fp16 under GN1's per-image bound of |X|
             K.conv3x3_f16x3(seg2, rp['f3_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
                             a_bound=st1[4], absmax=amx)
@@ -606,7 +624,10 @@ class TrainEngine:
                     f3=K.F3Bounds(bY, K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), None, bXf) if f3Y else None)
         dz2 = View.full(self._new(B, H, W, co))
         if f3Y:
-            K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
+            if rp['wn_2T'] is not None and K.wino_eligible([Seg(gY, TAPS3)], co, H, W):
+                K.conv3x3_wino([Seg(gY, TAPS3)], rp['wn_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
+            else:
+                K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
             if (H * W) % (256 if ci <= 64 else 128) == 0 and co % 16 == 0:  # one-image M tiles (per-image bound)
                 K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=gX,
                                    absmax=bX)
@@ -628,7 +649,10 @@ class TrainEngine:
                     (ci * 9, 9, 1), f3=K.F3Bounds(bh, K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8)) if f3h else None)
         dz1 = View.full(self._new(B, H, W, ci))
         if f3h:
-            K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
+            if rp['wn_1T'] is not None and K.wino_eligible([Seg(dh, TAPS3)], ci, H, W):
+                K.conv3x3_wino([Seg(dh, TAPS3)], rp['wn_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
+            else:
+                K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
         else:
             self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
         g1 = rp['gn1']

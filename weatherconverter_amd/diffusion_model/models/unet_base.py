@@ -176,13 +176,14 @@ class Unet(nn.Module):
         return self
 
     def set_train_precision(self, precision: Optional[str]) -> 'Unet':
-        """Training arithmetic: None (= the conv precision: fp32-class), or 'f16' — the 16-bit line
-        (BASELINE config 3 trains in bf16): the f16x3 kernels with one fp16 piece per operand
-        (libwc_kernels_single16.so), fp32 accumulation, the same range scaling; gradients about 1e-3
-        relative to float64 instead of 1e-6."""
+        """Training arithmetic: None (= the conv precision: fp32-class), or a 16-bit line: 'bf16' (BASELINE
+        config 3 trains in bf16) — the f16x3 kernels with one bf16 piece per operand on the bf16 MFMA
+        (libwc_kernels_bf16.so), fp32 accumulation; or 'f16' — one fp16 piece per operand
+        (libwc_kernels_single16.so, 3 more significand bits, the same range scaling).  Gradients about
+        1e-3 (f16) / 1e-2 (bf16) relative to float64 instead of 1e-6."""
         from ... import kernels
-        if precision is not None and precision not in kernels.CONV_PRECISIONS + ('f16', ):
-            raise ValueError(f"train precision must be None, 'f16' or one of {kernels.CONV_PRECISIONS}")
+        if precision is not None and precision not in kernels.CONV_PRECISIONS + ('f16', 'bf16'):
+            raise ValueError(f"train precision must be None, 'f16', 'bf16' or one of {kernels.CONV_PRECISIONS}")
         self.train_precision = precision
         self._train_engine = None
         return self

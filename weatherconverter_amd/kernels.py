@@ -299,6 +299,19 @@ def default_conv_precision() -> str:
     return p
 
 
+def _piece_dtype() -> torch.dtype:
+    """16-bit piece format of the f16x3 packs for the active library variant: fp16, or bf16 on the bf16
+    single-piece build (the bf16 training line), whose kernels read their operands as bf16."""
+    return torch.bfloat16 if _native.active_variant() == 'bf16' else torch.float16
+
+
+def _split2(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(h, l) 16-bit pieces of an fp32 tensor: h = piece(v), l = piece(v - h) (round to nearest even)."""
+    dt = _piece_dtype()
+    h = v.to(dt)
+    return h, (v - h.float()).to(dt)
+
+
 @dataclass
 class X6Weight:
     """A conv weight re-packed for the bf16x6 kernels: its three exact bf16 pieces, laid out as
@@ -430,15 +443,13 @@ def pack_f16x3(w: torch.Tensor, C0: int, C1: int = 0, *, ntaps: int = 9, order: 
     else:
         _req(order == 'natural', f'unknown f16x3 order {order!r}')
         main = ws[:, :K0].reshape(Np, S0, 2, 8)
-    h = main.half()
-    lo = (main - h.float()).half()
+    h, lo = _split2(main)
     pm = torch.stack([h, lo]).view(torch.int16).view(2, T, BN, S0, 2, 8).permute(1, 3, 0, 4, 2, 5)
     parts = [pm.reshape(T, -1)]
     if C1:
         rw = ws[:, K0:].reshape(Np, S1, 2, 8)
         if res_f16:
-            rh = rw.half()
-            pr = torch.stack([rh, (rw - rh.float()).half()]).view(torch.int16).view(2, T, BN, S1, 2, 8)
+            pr = torch.stack(_split2(rw)).view(torch.int16).view(2, T, BN, S1, 2, 8)
         else:
             pr = split3_bits(rw).view(3, T, BN, S1, 2, 8)
         parts.append(pr.permute(1, 3, 0, 4, 2, 5).reshape(T, -1))
@@ -514,17 +525,26 @@ def wino_filter(w: torch.Tensor, C0: int) -> torch.Tensor:
     return torch.stack([g0, (g0 + g1 + g2) * 0.5, (g0 - g1 + g2) * 0.5, g2], 2)
 
 
-def pack_wino(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
+def pack_wino(w: torch.Tensor, C0: int, C1: int = 0, *, device: Optional[bool] = None) -> X6Weight:
     """Pack a [N][9*C0 + C1] ResBlock conv weight (3x3 taps then the 1x1 residual columns, as
     engine.pack_conv) for wc_conv3x3_wino_f16x3: the F(2,3) filter transform in float64, a per-channel
     power-of-two scale 2^sW[n] with max |U|, |w_res| * 2^sW <= 2^14, each value rounded once to fp32 and
     split into two round-to-nearest fp16 pieces; layout [N tile][C0/16][ky 3][p 4][piece][k-half][BN][8]
-    then [N tile][C1/16][piece][k-half][BN][8]."""
+    then [N tile][C1/16][piece][k-half][BN][8].  A CUDA weight is packed by the device kernel (device=None:
+    unless WC_PACK_DEVICE=0)."""
     N, K = w.shape
     _req(K == 9 * C0 + C1 and C0 % 16 == 0 and C1 % 16 == 0, 'wino weight shape')
     _, BN = wino_tile(N)
     Np = -(-N // BN) * BN
     T = Np // BN
+    if (device if device is not None else pack_device_enabled()) and w.is_cuda:
+        # one launch (wc_pack_wino), bit-identical to the definition below evaluated on the CPU
+        data = torch.empty((T, (12 * C0 + C1) // 16 * 2 * 2 * BN * 8), dtype=torch.int16, device=w.device)
+        wsinv = torch.empty(Np, dtype=torch.float32, device=w.device)
+        wf = w.float().contiguous()
+        _timed('pack_wino_kernel', 'wc_pack_wino', 0.0, wf.data_ptr(), N, C0, C1, data.data_ptr(), data.numel() * 2,
+               wsinv.data_ptr(), _stream())
+        return X6Weight(data, N, BN, C0, C1, 'wino', wsinv, bool(C1))
     wd = torch.zeros((Np, K), dtype=torch.float64, device=w.device)
     wd[:N] = w.double()
     U = wino_filter(wd, C0)  # [Np][3][4][C0]
@@ -532,14 +552,15 @@ def pack_wino(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
     amax = U.abs().reshape(Np, -1).amax(1)
     if C1:
         amax = torch.maximum(amax, r.abs().amax(1))
-    sw = torch.where(amax > 0, torch.floor(torch.log2(2.0**14 / amax.clamp_min(1e-300))), torch.zeros_like(amax))
+    # sW = floor(log2(2^14 / amax)) from the exponent (exact): amax = m 2^e, m in [0.5, 1)
+    m, e = torch.frexp(amax)
+    sw = torch.where(amax > 0, torch.where(m == 0.5, 15 - e, 14 - e).double(), torch.zeros_like(amax))
     sw = sw.clamp(-60, 60)
     scale = torch.ldexp(torch.ones_like(sw), sw)
 
     def pieces(v):  # exact power-of-two scaling, one rounding to fp32, two fp16 pieces
         v32 = (v * scale.reshape((-1, ) + (1, ) * (v.dim() - 1))).float()
-        h = v32.half()
-        return torch.stack([h, (v32 - h.float()).half()]).view(torch.int16)
+        return torch.stack(_split2(v32)).view(torch.int16)
 
     nc0 = C0 // 16
     p0 = pieces(U).view(2, T, BN, 3, 4, nc0, 2, 8).permute(1, 5, 3, 4, 0, 6, 2, 7).reshape(T, -1)
@@ -553,33 +574,41 @@ def pack_wino(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
 
 
 def wino_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
-    """True when wc_conv3x3_wino_f16x3 accepts this conv (mirrors its host checks)."""
+    """True when wc_conv3x3_wino_f16x3 accepts this conv (mirrors its host checks): segment 0 with the
+    GN+SiLU prologue (+ an optional 1x1 residual segment), or one raw segment (given a per-image bound)."""
     s0 = segs[0]
     TH, _ = wino_tile(N)
-    if s0.scale is None or not s0.silu or len(s0.taps) != 9 or s0.view.C % 16 or Hm % TH or Wm % 16:
+    if len(s0.taps) != 9 or s0.view.C % 16 or Hm % TH or Wm % 16 or s0.stride != 1:
         return False
-    if s0.view.H != Hm or s0.view.W != Wm or s0.stride != 1:
+    if list(s0.taps) != [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]:
         return False
-    return len(segs) == 1 or segs[1].view.C % 16 == 0
+    if s0.view.H != Hm or s0.view.W != Wm:
+        return False
+    if s0.scale is None:
+        return len(segs) == 1
+    return s0.silu and (len(segs) == 1 or segs[1].view.C % 16 == 0)
 
 
 def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                  a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
                  temb_ld: int = 0, res: Optional[View] = None, absmax: Optional[torch.Tensor] = None,
                  gn: Optional[GnPart] = None):
-    """The ResBlock 3x3 conv (GN+SiLU prologue, optional fused 1x1 residual under a_bound) through the
-    Winograd F(2,3)-along-x kernel (wc_conv3x3_wino_f16x3); a_exp = f16x3_a_exp of the GroupNorm."""
+    """The ResBlock 3x3 conv through the Winograd F(2,3)-along-x kernel (wc_conv3x3_wino_f16x3): segment 0
+    with the GN+SiLU prologue (a_exp = f16x3_a_exp of that GroupNorm) and an optional fused 1x1
+    residual under the per-image bound a_bound, or one raw segment under a_bound (a_exp = 60: the
+    training data gradients)."""
     _req(w.data.is_cuda and w.data.is_contiguous() and w.order == 'wino', 'wino weight')
     _req(w.C0 == segs[0].view.C and w.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'wino weight segments')
-    _req(len(segs) == 1 or a_bound is not None, 'the wino residual segment needs a per-image A bound')
+    raw = segs[0].scale is None
+    _req((len(segs) == 1 and not raw) or a_bound is not None, 'a raw or residual wino segment needs a per-image A bound')
     if a_bound is not None:
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     a = _conv_args(segs, w.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     TH, BN = wino_tile(w.N)
-    _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {"true" if len(segs) == 2 else "false"}>', 'wc_conv3x3_wino_f16x3',
-           _flops(segs, Hm, Wm, w.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
-           w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(),
-           _ptr(a_bound) if len(segs) == 2 else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res))
+    _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {0 if raw else 2}, {"true" if len(segs) == 2 else "false"}>',
+           'wc_conv3x3_wino_f16x3', _flops(segs, Hm, Wm, w.N) if PROFILE is not None or REPLAY is not None else 0.0,
+           ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(),
+           _ptr(a_bound) if (len(segs) == 2 or raw) else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res))
 
 
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,

@@ -88,6 +88,8 @@ KERNEL_DESC = {
     'attention_kernel': 'fp32 MFMA flash attention',
     'proj_pa_kernel': 'split-precision MFMA pre-split projection GEMM',
     'conv3x3_w1_kernel': 'split-precision MFMA 3x3 conv, one wave per SIMD, 16 x 16-pixel tiles',
+    'conv3x3_wino_kernel': 'split-precision MFMA 3x3 conv through Winograd F(2,3) along x (12 K-steps per 16-channel '
+                           'chunk and output pair instead of 18: 2/3 of the direct MFMA work), GN+SiLU prologue',
 }
 
 
@@ -98,6 +100,8 @@ def _describe(name: str) -> str:
     mode = 'f16x3' if _mode_peak(name) == F16X3_PEAK_TFLOPS else ('bf16x6' if _mode_peak(name) == BF16X6_PEAK_TFLOPS
                                                                    else 'fp32')
     d = KERNEL_DESC.get(base, base)
+    if base == 'conv3x3_wino_kernel' and len(targs) >= 4 and targs[3] == 'true':
+        d += ', fused 1x1 residual in positions 0 / 3'
     if base == 'conv3x3_x6_kernel' and len(targs) >= 9:
         if targs[7] == '1':
             d = 'split-precision MFMA 4x4/s2 down conv over the space-to-depth input (halo-tiled)'
@@ -237,7 +241,7 @@ def _mode_peak(name: str) -> float:
         return F16X3_PEAK_TFLOPS if len(targs) >= 6 and targs[5] == 'true' else BF16X6_PEAK_TFLOPS
     if name.startswith('attention_x6'):
         return F16X3_PEAK_TFLOPS if targs[1] == 'true' else BF16X6_PEAK_TFLOPS
-    if name.startswith(('conv3x3_w1_kernel', 'proj_pa_kernel')):  # f16x3-only forms
+    if name.startswith(('conv3x3_w1_kernel', 'proj_pa_kernel', 'conv3x3_wino_kernel')):  # f16x3-only forms
         return F16X3_PEAK_TFLOPS
     return FP32_PEAK_TFLOPS
 

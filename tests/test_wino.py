@@ -154,7 +154,8 @@ def test_conv3x3_wino_vs_float64(B, H, W, Ci, Co, Cr, gs, outlier):
         ref = ref + F.conv2d(x2.double(), wr.double())
         segs.append(K.Seg(K.View.full(_nhwc(x2).cuda()), [(0, 0)], kbase=9 * Ci))
         wp = torch.cat([wp, wr.reshape(Co, Cr)], 1)
-        _, _, xb = K.gn_affine(segs[1].view, None, None, bound=True)
+        # the residual input's per-image bound (the engine takes GN1's Samuelson bound; any bound >= max |x|)
+        xb = x2.abs().reshape(B, -1).amax(1).cuda() * 1.5
     wp = wp.contiguous().cuda()
     e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * W * Ci // 8)
     tcu = temb.cuda()
@@ -202,8 +203,9 @@ def test_conv3x3_wino_epilogue_res_absmax_gn_partials(sw):
     gamma, beta = (1 + torch.randn(Co, generator=g)).cuda(), torch.randn(Co, generator=g).cuda()
     a1 = K.gn_affine(K.View.full(y), gamma, beta, bound=True, part=gp)
     a0 = K.gn_affine(K.View.full(y), gamma, beta, bound=True)
-    for u, v in zip(a1, a0):
-        assert torch.allclose(u, v, rtol=2e-6, atol=1e-7), (u - v).abs().max()
+    for u, v in zip(a1, a0):  # (shift = beta - mean * scale cancels to ~0 for some channels: atol of the
+        # output magnitude (~5) x 2e-7)
+        assert torch.allclose(u, v, rtol=2e-6, atol=1e-6), (u - v).abs().max()
 
 
 @pytest.mark.gpu
@@ -218,8 +220,11 @@ def test_pack_wino_device_bit_identical_to_cpu_definition(N, C0, C1):
     cpu = K.pack_wino(w, C0, C1, device=False)
     dev = K.pack_wino(w.cuda(), C0, C1, device=True)
     torch.cuda.synchronize()
-    assert torch.equal(dev.data.cpu(), cpu.data)
     assert torch.equal(dev.wsinv.cpu(), cpu.wsinv)
+    dd, cd = dev.data.cpu(), cpu.data
+    bad = (dd != cd).nonzero()
+    assert bad.numel() == 0, (len(bad), bad[:4].tolist(), dd[tuple(bad[:4].t())].tolist(),
+                              cd[tuple(bad[:4].t())].tolist())
 
 
 @pytest.mark.gpu

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Winograd conv after the A-fragment prefetch: tests, per-shape timing, bench.
+O=gpurun_out/r04c
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_wino.py -q -x --timeout 120 --timeout-method thread > $O/wino_tests.log 2>&1
+rc=$?; echo test_rc=$rc; tail -2 $O/wino_tests.log; [ $rc -ne 0 ] && { grep -E "Error|error|assert" $O/wino_tests.log | head -20; exit $rc; }
+timeout -k 10 300 python -u tools/bench_conv.py --modes f3,wino --no-misc > $O/bench_conv.log 2>&1
+rc=$?; echo bench_rc=$rc; cat $O/bench_conv.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench20.log 2>&1
+rc=$?; echo bench_rc=$rc; grep metric $O/bench20.log | cut -c1-300
+exit $rc

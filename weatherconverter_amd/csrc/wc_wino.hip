@@ -308,42 +308,46 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     // K-step (kernel row dy, position pos) of the chunk in halo buffer hs, weights in set
-    auto compute = [&](int set, int hs, int dy, int pos) {
+    // A fragments of a K-step, two register sets: the fragments of step st + 1 are read from LDS while
+    // step st's MFMAs run (a step is only 6 MFMAs per wave; reading its own fragments at its head left
+    // the LDS latency exposed at every step)
+    u32x4 fa[2][2][2];  // [set][mb][piece]
+    auto read_a = [&](int fs, int hs, int dy, int pos) {
         const unsigned char* ha = smem + hs * T::HSTAGE + (pos * 2 + half) * T::PSTR + dy * 128;
-        u32x4 fa[2][2];
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int pc = 0; pc < 2; ++pc)
-                fa[mb][pc] = *reinterpret_cast<const u32x4*>(ha + pc * 8 * T::PSTR + abase[mb]);
+                fa[fs][mb][pc] = *reinterpret_cast<const u32x4*>(ha + pc * 8 * T::PSTR + abase[mb]);
+    };
+    auto mfma_a = [&](int fs, int set, int pos) {
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) acc[pos][mb] = mfma_f16(fa[mb][0], wreg[set][0], acc[pos][mb]);
+        for (int mb = 0; mb < 2; ++mb) acc[pos][mb] = mfma_f16(fa[fs][mb][0], wreg[set][0], acc[pos][mb]);
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
-            acc[pos][mb] = mfma_f16c(fa[mb][0], wreg[set][1], acc[pos][mb]);
-            acc[pos][mb] = mfma_f16c(fa[mb][1], wreg[set][0], acc[pos][mb]);
+            acc[pos][mb] = mfma_f16c(fa[fs][mb][0], wreg[set][1], acc[pos][mb]);
+            acc[pos][mb] = mfma_f16c(fa[fs][mb][1], wreg[set][0], acc[pos][mb]);
         }
     };
     // residual K-step: positions 0 and 3 from centre buffer cs, one weight fragment
     auto compute_res = [&](const u32x4 (&w)[2], int cs) {
         const unsigned char* ca = cbase + cs * T::CSTAGE + half * T::CPSTR;
-        u32x4 fa[2][2][2];  // [position][mb][piece]
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
+        for (int r = 0; r < 2; ++r) {  // position 0 (x_even), position 3 (-x_odd): 16 fragment registers at a time
+            u32x4 fr[2][2];  // [mb][piece]
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
                 for (int pc = 0; pc < 2; ++pc)
-                    fa[r][mb][pc] = *reinterpret_cast<const u32x4*>(ca + (pc * 4 + r * 2) * T::CPSTR + abase[mb]);
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
+                    fr[mb][pc] = *reinterpret_cast<const u32x4*>(ca + (pc * 4 + r * 2) * T::CPSTR + abase[mb]);
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb) {
                 f32x16& a = acc[r ? 3 : 0][mb];
-                a = mfma_f16(fa[r][mb][0], w[0], a);
-                a = mfma_f16c(fa[r][mb][0], w[1], a);
-                a = mfma_f16c(fa[r][mb][1], w[0], a);
+                a = mfma_f16(fr[mb][0], w[0], a);
+                a = mfma_f16c(fr[mb][0], w[1], a);
+                a = mfma_f16c(fr[mb][1], w[0], a);
             }
+        }
     };
 
     const std::integral_constant<int, 0> I0;
@@ -374,6 +378,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     auto chunk = [&](auto P, auto L, int c) {
         constexpr int PV = decltype(P)::value;
         constexpr bool LAST = decltype(L)::value != 0;
+        read_a(0, PV, 0, 0);  // step 0's fragments (the halo buffer was written before the last barrier)
 #pragma unroll
         for (int st = 0; st < T::STEPS; ++st) {
             load_w((st + 2) % 3, T::STEPS * c + st + 2);
@@ -390,10 +395,11 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
                 if (st == HALO_AT + 1) load_centre(I1, nri + 1, ntail > 1);
             }
             if constexpr (RI) {
-                if (st == 7) load_wres(c);
+                if (st == 9) load_wres(c);
             }
             __builtin_amdgcn_sched_barrier(0);
-            compute(st % 3, PV, st >> 2, st & 3);
+            if (st + 1 < T::STEPS) read_a((st + 1) & 1, PV, (st + 1) >> 2, (st + 1) & 3);
+            mfma_a(st & 1, st % 3, st & 3);
             if constexpr (!LAST) {
 #pragma unroll
                 for (int j = 0; j < T::I_PER_T; ++j) {
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
                     if (st == pro_at(j) + 2) transform(j, 1, PV ^ 1);
                 }
                 if constexpr (RI) {
-                    if (st == T::STEPS - 1) write_centre(I0, PV ^ 1);
+                    if (st == 9) write_centre(I0, PV ^ 1);
                 }
             }
         }
@@ -672,7 +678,10 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
             o = (long)(C0 / 16) * 12 * 2 * 2 * BN * 8 + (((long)chunk * 2 * 2 + kh) * BN + nn) * 8 + e;
             plane = 2 * BN * 8;
         }
-        const float v32 = (float)(v * scale);
+        float v32 = (float)(v * scale);
+        // materialize the fp32 value: without this the compiler folds double -> fp32 -> fp16 into one
+        // double -> fp16 rounding, which differs on fp16 ties (the definition rounds twice, fp32 first)
+        asm volatile("" : "+v"(v32));
         unsigned short h, l;
         split2_one(v32, h, l);
         trow[o] = (short)h;

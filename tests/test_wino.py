@@ -164,7 +164,9 @@ def test_conv3x3_wino_vs_float64(B, H, W, Ci, Co, Cr, gs, outlier):
         out = torch.empty((B, H, W, Co), device='cuda')
         kw = dict(Hm=H, Wm=W, a_exp=e, a_bound=xb, temb=tcu, temb_ld=Co + 8)
         if mode == 'wino':
-            assert K.wino_eligible(segs, Co, H, W)
+            # (the 64-channel form with a residual is supported by the kernel but routed to the direct
+            # one by the engine: wino_eligible says no)
+            assert K.wino_eligible(segs, Co, H, W) == (not (Co <= 64 and Cr))
             K.conv3x3_wino(segs, K.pack_wino(wp, Ci, Cr), b.cuda(), K.View.full(out), **kw)
         else:
             K.conv3x3_f16x3(segs, K.pack_f16x3(wp, Ci, Cr, res_f16=bool(Cr)), b.cuda(), K.View.full(out), **kw)

@@ -170,6 +170,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     const int hpx = p.ldc0 * 4;  // bytes between horizontally adjacent pixels
 #pragma unroll
     for (int j = 0; j < T::I_PER_T; ++j) {
+        // item tid + NT j: the items fill waves 0 .. in order (spreading them thinner over all four waves
+        // would not shorten any wave's instruction stream, only add wave 3's)
         const int i = tid + NT * j;
         const int hrow = i >> 4, tp = (i >> 2) & 3;
         const bool valid = i < T::ITEMS;
@@ -203,29 +205,28 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
         for (int j = 0; j < T::I_PER_T; ++j) load_slot(j, c);
         load_ss(c);
     };
-    // GN + SiLU prologue of slot j (zero padding after it), x 2^s
-    f32x4 hv[6];
-    auto prologue = [&](int j) {
+    // GN + SiLU prologue of pixels k0 .. k1 - 1 of slot j, in place (zero padding after it), x 2^s
+    auto prologue = [&](int j, int k0, int k1) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = k0; k < k1; ++k) {
             f32x4 a = rh[j][k];
             if constexpr (PRO == 2) {
                 a = a * rsc + rsh;
                 a.x = silu_fast(a.x); a.y = silu_fast(a.y);
                 a.z = silu_fast(a.z); a.w = silu_fast(a.w);
             }
-            hv[k] = ((hin[j] >> k) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
+            rh[j][k] = ((hin[j] >> k) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
     // Winograd input transform of tile t (0, 1) of slot j, 2-piece fp16 split, 8 fragment writes into
     // halo buffer hs
-    auto transform = [&](int j, int t, int hs) {
+    auto transform = [&](int j, int t, int hs, int p0 = 0, int p1 = 4) {
         if (hwr[j] < 0) return;  // idle item slot (ITEMS is not a multiple of NT)
         unsigned char* base = smem + hs * T::HSTAGE + hwr[j] + t * 16;
-        const f32x4 d0 = hv[2 * t], d1 = hv[2 * t + 1], d2 = hv[2 * t + 2], d3 = hv[2 * t + 3];
+        const f32x4 d0 = rh[j][2 * t], d1 = rh[j][2 * t + 1], d2 = rh[j][2 * t + 2], d3 = rh[j][2 * t + 3];
         const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
 #pragma unroll
-        for (int pos = 0; pos < 4; ++pos) {
+        for (int pos = p0; pos < p1; ++pos) {
             u32x2 a0, a1;
             split2_f16(V[pos], a0, a1);
             unsigned char* d = base + pos * 2 * T::PSTR;
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     auto write_items = [&](int hs) {
 #pragma unroll
         for (int j = 0; j < T::I_PER_T; ++j) {
-            prologue(j);
+            prologue(j, 0, 6);
             transform(j, 0, hs);
             transform(j, 1, hs);
         }
@@ -372,9 +373,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     // chunk.  One slot (TH = 8): loads at 6, VALU at 9-11; two (TH = 16): 4 / 6-8 and 7 / 9-11.  The
     // next chunk's residual centre rides with slot 0 and is split into the other centre buffer at step 11;
     // this chunk's residual step (weights from step 7) runs after step 11.
-    constexpr int HALO_AT = T::I_PER_T == 1 ? 6 : 4;
-    auto load_at = [](int j) { return T::I_PER_T == 1 ? 6 : (j == 0 ? 4 : 7); };
-    auto pro_at = [](int j) { return T::I_PER_T == 1 ? 9 : (j == 0 ? 6 : 9); };
+    // One slot (TH = 8): the halo goes out at step 2 and its VALU is spread thin over steps 5-11 (prologue
+    // two pixels a step at 5-7, then each tile's positions 0-1 / 2-3 a step at 8-11), so that it fits the
+    // vector-issue slots the MFMAs leave.  Two slots (TH = 16, registers for both only briefly): slot 0
+    // loads at 3, prologue at 5, tiles at 6 and 7; slot 1 loads at 7, prologue at 9, tiles at 10 and 11.
+    constexpr int HALO_AT = T::I_PER_T == 1 ? 2 : 3;
+    auto load_at = [](int j) { return T::I_PER_T == 1 ? 2 : (j == 0 ? 3 : 7); };
+    auto pro_at = [](int j) { return j == 0 ? 5 : 9; };
+    // the slot's VALU at step st (relative step k = st - pro_at(j))
+    auto slot_work = [&](int j, int k, int hs) {
+        if constexpr (T::I_PER_T == 1) {
+            if (k >= 0 && k < 3) prologue(j, 2 * k, 2 * k + 2);
+            if (k >= 3 && k < 7) transform(j, (k - 3) >> 1, hs, ((k - 3) & 1) * 2, ((k - 3) & 1) * 2 + 2);
+        } else {
+            if (k == 0) prologue(j, 0, 6);
+            if (k == 1 || k == 2) transform(j, k - 1, hs);
+        }
+    };
     auto chunk = [&](auto P, auto L, int c) {
         constexpr int PV = decltype(P)::value;
         constexpr bool LAST = decltype(L)::value != 0;
@@ -402,11 +417,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
             mfma_a(st & 1, st % 3, st & 3);
             if constexpr (!LAST) {
 #pragma unroll
-                for (int j = 0; j < T::I_PER_T; ++j) {
-                    if (st == pro_at(j)) prologue(j);
-                    if (st == pro_at(j) + 1) transform(j, 0, PV ^ 1);
-                    if (st == pro_at(j) + 2) transform(j, 1, PV ^ 1);
-                }
+                for (int j = 0; j < T::I_PER_T; ++j) slot_work(j, st - pro_at(j), PV ^ 1);
                 if constexpr (RI) {
                     if (st == 9) write_centre(I0, PV ^ 1);
                 }
@@ -464,19 +475,27 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     if (nok && p.temb) eadd += p.temb[b * p.temb_ld + n];
     const float emul = nok ? p.wsinv[n] * ainv : 0.f;
     float vmax = 0.f;
+    // accumulator register r of block mb is MFMA row (r & 3) + 8 (r >> 2) + 4 half: the four registers of
+    // a group j = r >> 2 are four consecutive tiles of one image row.  One per-lane byte offset per
+    // (mb, j) and the tile steps (r & 3) x 2 pixels as wave-uniform scalar offsets: no per-store VALU.
+    const int so_px = 4 * p.ldo;  // bytes between horizontally adjacent output pixels
+    const int so_rs = 4 * p.ldres;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
-        // output pixel of accumulator row (r & 3) + 8 (r >> 2) + 4 half: (row, 2 tile) and (row, 2 tile + 1)
-        const int pix0 = (y0 + 8 * wm + 4 * mb) * p.W + x0;
+        unsigned vo[4], vr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 8 * j + 4 * half;
+            const int pix = (y0 + 8 * wm + 4 * mb + wg_row(row)) * p.W + x0 + 2 * wg_tile(row);
+            vo[j] = (unsigned)(pix * p.ldo + n) * 4u;
+            vr[j] = (unsigned)(pix * p.ldres + (nok ? n : 0)) * 4u;
+        }
         float rv[2][16];
         if (p.res) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int px = pix0 + wg_row(row) * p.W + 2 * wg_tile(row);
-                const unsigned o = (unsigned)(px * p.ldres + (nok ? n : 0)) * 4u;
-                rv[0][r] = bload_f1(srd_res, o);
-                rv[1][r] = bload_f1(srd_res, o + (unsigned)p.ldres * 4u);
+                rv[0][r] = bload_f1s(srd_res, vr[r >> 2], (r & 3) * 2 * so_rs);
+                rv[1][r] = bload_f1s(srd_res, vr[r >> 2], ((r & 3) * 2 + 1) * so_rs);
             }
         }
 #pragma unroll
@@ -490,19 +509,17 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
             }
             acc[0][mb][r] = ya;
             acc[1][mb][r] = yb;
+            vmax = fmaxf(vmax, fmaxf(fabsf(ya), fabsf(yb)));
         }
         if (nok) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int px = pix0 + wg_row(row) * p.W + 2 * wg_tile(row);
-                const unsigned o = (unsigned)(px * p.ldo + n) * 4u;
-                bstore_f1(srd_out, o, acc[0][mb][r]);
-                bstore_f1(srd_out, o + (unsigned)p.ldo * 4u, acc[1][mb][r]);
-                vmax = fmaxf(vmax, fmaxf(fabsf(acc[0][mb][r]), fabsf(acc[1][mb][r])));
+                bstore_f1s(srd_out, vo[r >> 2], (r & 3) * 2 * so_px, acc[0][mb][r]);
+                bstore_f1s(srd_out, vo[r >> 2], ((r & 3) * 2 + 1) * so_px, acc[1][mb][r]);
             }
         }
     }
+    if (!nok) vmax = 0.f;
     if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);
     if (p.gn_part) {
         // this wave's two 64-pixel blocks (rows 4 mb .. 4 mb + 3 of its 8) in the direct kernel's numbering

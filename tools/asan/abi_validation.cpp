@@ -48,6 +48,16 @@ int main() {
     EXPECT(wc_conv3x3_f16x3(&a, p, 0, 0, p, nullptr, nullptr), WC_E_ARG);
     a.seg[0].scale = nullptr;
     EXPECT(wc_conv_igemm_x6(nullptr, p, 0, nullptr), WC_E_ARG);
+    // Winograd conv: null struct, a raw segment without its per-image bound, a raw segment that is
+    // not a 3x3 grid; tile width; the device pack's null / channel / size checks.
+    EXPECT(wc_conv3x3_wino_f16x3(nullptr, p, 0, 0, p, p, nullptr), WC_E_ARG);
+    EXPECT(wc_conv3x3_wino_f16x3(&a, p, 0, 0, p, nullptr, nullptr), WC_E_ARG);
+    EXPECT(wc_conv3x3_wino_f16x3(&a, p, 0, 0, p, p, nullptr), WC_E_SHAPE);  // ntaps 0, C = 30
+    EXPECT(wc_conv3x3_wino_tile_n(64), 64);
+    EXPECT(wc_conv3x3_wino_tile_n(65), 128);
+    EXPECT(wc_pack_wino(nullptr, 128, 32, 0, p, 0, p, nullptr), WC_E_ARG);
+    EXPECT(wc_pack_wino(p, 128, 30, 0, p, 0, p, nullptr), WC_E_SHAPE);
+    EXPECT(wc_pack_wino(p, 128, 32, 0, p, 12, p, nullptr), WC_E_SHAPE);  // wrong output size
 
     // Attention: null operands, heads not dividing C, unsupported head width, misaligned strides.
     EXPECT(wc_attention_fwd(nullptr, 96, p, 32, 1, 64, 32, 4, 1.f, nullptr), WC_E_ARG);

@@ -154,6 +154,10 @@ int wc_conv3x3_set_onewave(int mode);
 int wc_conv3x3_wino_f16x3(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
                           const float* w_inv_scale, const float* a_bound, void* stream);
 int wc_conv3x3_wino_tile_n(int N);
+/* Form of wc_conv3x3_wino_f16x3 for BN = 128: 0 (default) two waves per SIMD, 8-row tiles; 1 one wave
+ * per SIMD with 16-row tiles (each weight fragment feeds four MFMA row blocks) where H % 16 == 0.
+ * Bit-identical results.  Returns the previous mode (or WC_E_ARG); process-wide. */
+int wc_conv3x3_wino_set_onewave(int mode);
 /* Device re-pack of a [N][9*C0 + C1] fp32 ResBlock conv weight (K = (ky*3 + kx, c), then the 1x1
  * residual columns) into wc_conv3x3_wino_f16x3's layout and w_inv_scale[ceil(N/BN)*BN]: the F(2,3)
  * filter transform in float64, the per-channel power-of-two scale, one rounding to fp32, two fp16

@@ -258,3 +258,49 @@ def test_conv3x3_wino_raw_segment_vs_float64(B, H, W, Ci, Co):
     for b in range(B):  # per image (their scales differ by 1e3)
         ew, ed = rel_l2(outs['wino'][b], ref[b]), rel_l2(outs['f16x3'][b], ref[b])
         assert ew < 1e-5 and ew <= 4 * ed + 2e-7, (b, ew, ed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr,raw', [(2, 16, 32, 64, 128, 0, False), (1, 32, 16, 48, 256, 48, False),
+                                                (1, 16, 16, 32, 128, 96, False), (2, 32, 32, 128, 128, 128, False),
+                                                (1, 16, 32, 64, 128, 0, True)])
+def test_conv3x3_wino_onewave_bit_identical(B, H, W, Ci, Co, Cr, raw):
+    """The one-wave-per-SIMD 16-row form (wc_conv3x3_wino_set_onewave(1)) against the two-wave form:
+    bit-identical output (bias, temb), per-image absmax and GroupNorm tile partials — the same products
+    in the same order per output; residual chunks interleaved (equal and unequal chunk counts) and the
+    raw-segment form."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(53)
+    x = (torch.randn((B, H, W, Ci), generator=g) * 2 + 1).cuda()
+    w = (torch.randn((Co, 9 * Ci + Cr), generator=g) / (9 * Ci)**0.5).cuda()
+    bias = torch.randn(Co, generator=g).cuda()
+    temb = torch.randn((B, Co), generator=g).cuda()
+    if raw:
+        segs = [K.Seg(K.View.full(x), TAPS3)]
+        bound = x.abs().reshape(B, -1).amax(1).contiguous()
+        kw = dict(a_exp=60, a_bound=bound)
+    else:
+        sc = (1 + 0.2 * torch.randn((B, Ci), generator=g)).cuda()
+        sh = (0.2 * torch.randn((B, Ci), generator=g)).cuda()
+        segs = [K.Seg(K.View.full(x), TAPS3, scale=sc, shift=sh, silu=True)]
+        kw = dict(a_exp=6, temb=temb, temb_ld=Co)
+        if Cr:
+            xr = torch.randn((B, H, W, Cr), generator=g).cuda()
+            segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=9 * Ci))
+            kw['a_bound'] = xr.abs().reshape(B, -1).amax(1).contiguous() * 1.5
+    wp = K.pack_wino(w, Ci, Cr)
+    res = {}
+    prev = K.set_wino_onewave(0)
+    try:
+        for mode in (0, 1):
+            K.set_wino_onewave(mode)
+            y = torch.empty((B, H, W, Co), device='cuda')
+            gp = K.GnPart.attach(y, 16)
+            amax = torch.zeros(B, device='cuda')
+            K.conv3x3_wino(segs, wp, None if raw else bias, K.View.full(y), Hm=H, Wm=W, absmax=amax, gn=gp, **kw)
+            torch.cuda.synchronize()
+            res[mode] = (y.cpu(), amax.cpu(), gp.part.cpu())
+    finally:
+        K.set_wino_onewave(prev)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b), (a - b).abs().max()

@@ -77,11 +77,14 @@ struct WDev {
     int tiles_x, tiles_y, ntiles_n;
 };
 
-template <int TH, int BN>
+// MB: 32-tile MFMA row blocks per wave (4 image rows x 8 tiles each): 2 (two waves per SIMD) or 4 (one
+// wave per SIMD, 512 registers: each weight fragment feeds twice the MFMAs, halving the vector-memory
+// traffic per MFMA that the two-wave form is bound by)
+template <int TH, int BN, int MB = 2>
 struct WTile {
     static constexpr int WAVES_N = BN / 32;
     static constexpr int WAVES_M = 4 / WAVES_N;
-    static_assert(WAVES_N * WAVES_M == 4 && WAVES_M * 8 == TH, "each wave owns 8 rows x 8 tiles x 32 channels");
+    static_assert(WAVES_N * WAVES_M == 4 && WAVES_M * 4 * MB == TH, "each wave owns 4 MB rows x 8 tiles x 32 channels");
     static constexpr int HR = TH + 2;            // halo rows
     // one (piece, position, k-half) plane of [halo row][tile] 16-byte fragments; the 16 extra bytes make
     // the k-half stride 16 mod 128 so the item writes of a 16-lane group hit 16 distinct 8-byte slots
@@ -107,10 +110,10 @@ WC_DEVICE int wg_tile(int r) { return wg_idx(r) & 7; }
 // PRO: 2 = GroupNorm affine + SiLU prologue on segment 0 (static Samuelson bound), 0 = raw segment 0
 // under the per-image bound abound (the training data gradients).  RES: the fused 1x1 residual segment
 // (raw input, f16x3 under the per-image bound abound).
-template <int TH, int BN, int PRO, bool RES>
-__global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
+template <int TH, int BN, int PRO, bool RES, int MB = 2>
+__global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev p) {
     static_assert((PRO == 2 || PRO == 0) && !(PRO == 0 && RES), "GN+SiLU (+ residual) or one raw segment");
-    using T = WTile<TH, BN>;
+    using T = WTile<TH, BN, MB>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* const cbase = smem + 2 * T::HSTAGE;  // residual centre buffers
 
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     // residual chunk r < nri rides in 3x3 chunk r as a 13th K-step; the rest (nck1 > nck0) follow as a
     // tail phase, one K-step and one barrier each
     // (TH = 16: the centre staging of four items per thread does not fit beside the halo's; all tail)
-    constexpr bool RI = RES && TH == 8;
+    constexpr bool RI = RES && (TH == 8 || MB == 4);
     const int nri = RI ? min(p.nck0, p.nck1) : 0;
     const int ntail = RES ? p.nck1 - nri : 0;
     const unsigned wtile = (unsigned)tile_n * (unsigned)(S * T::BSTEP);
@@ -276,9 +279,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     // ---- fragment addressing ----
     const int l32 = lane & 31;
     const int half = lane >> 5;
-    int abase[2];
+    int abase[MB];
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) abase[mb] = ((8 * wm + 4 * mb + wg_row(l32)) * 8 + wg_tile(l32)) * 16;
+    for (int mb = 0; mb < MB; ++mb) abase[mb] = ((4 * MB * wm + 4 * mb + wg_row(l32)) * 8 + wg_tile(l32)) * 16;
     const unsigned wlane = (unsigned)(half * BN * 16 + (wn * 32 + l32) * 16);
 
     u32x4 wreg[3][2];  // [set][piece]
@@ -300,11 +303,11 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
         for (int pc = 0; pc < 2; ++pc) wres[pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * BN * 16), off);
     };
 
-    f32x16 acc[4][2];
+    f32x16 acc[4][MB];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < MB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -312,20 +315,20 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     // A fragments of a K-step, two register sets: the fragments of step st + 1 are read from LDS while
     // step st's MFMAs run (a step is only 6 MFMAs per wave; reading its own fragments at its head left
     // the LDS latency exposed at every step)
-    u32x4 fa[2][2][2];  // [set][mb][piece]
+    u32x4 fa[2][MB][2];  // [set][mb][piece]
     auto read_a = [&](int fs, int hs, int dy, int pos) {
         const unsigned char* ha = smem + hs * T::HSTAGE + (pos * 2 + half) * T::PSTR + dy * 128;
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
+        for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
             for (int pc = 0; pc < 2; ++pc)
                 fa[fs][mb][pc] = *reinterpret_cast<const u32x4*>(ha + pc * 8 * T::PSTR + abase[mb]);
     };
     auto mfma_a = [&](int fs, int set, int pos) {
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) acc[pos][mb] = mfma_f16(fa[fs][mb][0], wreg[set][0], acc[pos][mb]);
+        for (int mb = 0; mb < MB; ++mb) acc[pos][mb] = mfma_f16(fa[fs][mb][0], wreg[set][0], acc[pos][mb]);
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
+        for (int mb = 0; mb < MB; ++mb) {
             acc[pos][mb] = mfma_f16c(fa[fs][mb][0], wreg[set][1], acc[pos][mb]);
             acc[pos][mb] = mfma_f16c(fa[fs][mb][1], wreg[set][0], acc[pos][mb]);
         }
@@ -335,14 +338,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
         const unsigned char* ca = cbase + cs * T::CSTAGE + half * T::CPSTR;
 #pragma unroll
         for (int r = 0; r < 2; ++r) {  // position 0 (x_even), position 3 (-x_odd): 16 fragment registers at a time
-            u32x4 fr[2][2];  // [mb][piece]
+            u32x4 fr[MB][2];  // [mb][piece]
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
+            for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
                 for (int pc = 0; pc < 2; ++pc)
                     fr[mb][pc] = *reinterpret_cast<const u32x4*>(ca + (pc * 4 + r * 2) * T::CPSTR + abase[mb]);
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
+            for (int mb = 0; mb < MB; ++mb) {
                 f32x16& a = acc[r ? 3 : 0][mb];
                 a = mfma_f16(fr[mb][0], w[0], a);
                 a = mfma_f16c(fr[mb][0], w[1], a);
@@ -481,12 +484,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     const int so_px = 4 * p.ldo;  // bytes between horizontally adjacent output pixels
     const int so_rs = 4 * p.ldres;
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
         unsigned vo[4], vr[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int row = 8 * j + 4 * half;
-            const int pix = (y0 + 8 * wm + 4 * mb + wg_row(row)) * p.W + x0 + 2 * wg_tile(row);
+            const int pix = (y0 + 4 * MB * wm + 4 * mb + wg_row(row)) * p.W + x0 + 2 * wg_tile(row);
             vo[j] = (unsigned)(pix * p.ldo + n) * 4u;
             vr[j] = (unsigned)(pix * p.ldres + (nok ? n : 0)) * 4u;
         }
@@ -522,25 +525,25 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wino_kernel(WDev p) {
     if (!nok) vmax = 0.f;
     if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);
     if (p.gn_part) {
-        // this wave's two 64-pixel blocks (rows 4 mb .. 4 mb + 3 of its 8) in the direct kernel's numbering
+        // this wave's 64-pixel blocks (rows 4 mb .. 4 mb + 3 of its 4 MB) in the direct kernel's numbering
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
+        for (int mb = 0; mb < MB; ++mb) {
             const f32x16 blk[2][1] = {{acc[0][mb]}, {acc[1][mb]}};
             GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
-                     (long)b * p.gn_np64 + ((long)(tyi * p.tiles_x + txi) * T::WAVES_M + wm) * 2 + mb,
+                     (long)b * p.gn_np64 + ((long)(tyi * p.tiles_x + txi) * T::WAVES_M + wm) * MB + mb,
                      (p.gn_c0 + n0 + wn * 32) / 32};
             gn_tile_partials(blk, g, p.N - n0 - wn * 32 >= 32 ? 1 : 0);
         }
     }
 }
 
-template <int TH, int BN, int PRO, bool RES>
+template <int TH, int BN, int PRO, bool RES, int MB = 2>
 int launch_wino(const WDev& d, hipStream_t stream) {
-    using T = WTile<TH, BN>;
+    using T = WTile<TH, BN, MB>;
     constexpr int lds = 2 * T::HSTAGE + (RES ? 2 * T::CSTAGE : 0);
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, PRO, RES>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, PRO, RES, MB>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -550,15 +553,29 @@ int launch_wino(const WDev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES)});
-    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, PRO, RES>), grid, dim3(NT), lds, stream, p);
+    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES), WC_TI(MB)});
+    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, PRO, RES, MB>), grid, dim3(NT), lds, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
+// 0: the two-waves-per-SIMD form (MB = 2); 1: the one-wave form (MB = 4, 16-row tiles) for BN = 128
+// where H % 16 == 0.  Initial value from WC_WINO_ONEWAVE (A/B runs); wc_conv3x3_wino_set_onewave.
+int g_wino_onewave = [] {
+    const char* e = getenv("WC_WINO_ONEWAVE");
+    return e ? atoi(e) : 0;
+}();
+
 }  // namespace
 
 extern "C" int wc_conv3x3_wino_tile_n(int N) { return N <= 64 ? 64 : 128; }
+
+extern "C" int wc_conv3x3_wino_set_onewave(int mode) {
+    if (mode < 0 || mode > 1) return WC_E_ARG;
+    const int prev = g_wino_onewave;
+    g_wino_onewave = mode;
+    return prev;
+}
 
 extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
                                      const float* w_inv_scale, const float* a_bound, void* stream) {
@@ -616,6 +633,10 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     const long ntn = (a->N + BN - 1) / BN;
     if (w_bytes != ntn * (12L * d.nck0 + d.nck1) * BN * 64 || w_bytes >= (1L << 31)) return WC_E_SHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 128 && g_wino_onewave == 1 && d.H % 16 == 0) {  // the one-wave form (16-row tiles)
+        if (pro == 0) return launch_wino<16, 128, 0, false, 4>(d, s);
+        return res ? launch_wino<16, 128, 2, true, 4>(d, s) : launch_wino<16, 128, 2, false, 4>(d, s);
+    }
     if (pro == 0) return BN == 64 ? launch_wino<16, 64, 0, false>(d, s) : launch_wino<8, 128, 0, false>(d, s);
     if (BN == 64) return res ? launch_wino<16, 64, 2, true>(d, s) : launch_wino<16, 64, 2, false>(d, s);
     return res ? launch_wino<8, 128, 2, true>(d, s) : launch_wino<8, 128, 2, false>(d, s);

@@ -511,6 +511,12 @@ def wino_tile(N: int) -> Tuple[int, int]:
     return (16 if bn == 64 else 8), bn
 
 
+def set_wino_onewave(mode: int) -> int:
+    """wc_conv3x3_wino_set_onewave: 0 the two-wave form (default), 1 the one-wave 16-row form; returns the
+    previous mode (applied to every library variant)."""
+    return _native.set_selector('wc_conv3x3_wino_set_onewave', int(mode), lambda v: v in (0, 1))
+
+
 def wino_enabled() -> bool:
     """ResBlock 3x3 convs through the Winograd F(2,3)-along-x kernel (WC_WINO=0: the direct halo
     kernel, kept for A/B and as the reference the Winograd kernel is tested against)."""

@@ -525,12 +525,15 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
     if (!nok) vmax = 0.f;
     if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);
     if (p.gn_part) {
-        // this wave's 64-pixel blocks (rows 4 mb .. 4 mb + 3 of its 4 MB) in the direct kernel's numbering
+        // this wave's 64-pixel blocks (4 rows x 16 px each), numbered by pixel position alone (image 4-row
+        // block r4 -> ((r4 / 2) * tiles_x + tile x) * 2 + r4 % 2), so every tile height / wave form writes the
+        // same partial to the same slot and the GroupNorm merge order (and result) does not depend on the form
+        const int r4 = tyi * (TH / 4) + MB * wm;
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) {
             const f32x16 blk[2][1] = {{acc[0][mb]}, {acc[1][mb]}};
             GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
-                     (long)b * p.gn_np64 + ((long)(tyi * p.tiles_x + txi) * T::WAVES_M + wm) * MB + mb,
+                     (long)b * p.gn_np64 + (long)(((r4 + mb) >> 1) * p.tiles_x + txi) * 2 + ((r4 + mb) & 1),
                      (p.gn_c0 + n0 + wn * 32) / 32};
             gn_tile_partials(blk, g, p.N - n0 - wn * 32 >= 32 ? 1 : 0);
         }

@@ -331,6 +331,12 @@ int wc_temb(const int64_t* t, int nt, int D, const float* w1, const float* b1, c
 /* conv_in: NCHW input (B, Cin<=4, H, W) → NHWC view, 3x3 pad 1 (unet_base.py:400,456). */
 int wc_conv_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* b,
                int Cout, float* out, int ldo, void* stream);
+/* conv_in for the 3 -> 64 stem with the output's GroupNorm tile partials (the wc_gn_partials format
+ * and arithmetic, bit-identical) from the same launch: part / ncb / sw as wc_gn_partials, c0 = the
+ * output view's first channel in the partials tensor (% 32); H*W % 64 == 0.  Replaces the stem conv
+ * (unet_base.py:456) followed by the first GroupNorm's statistics pass (unet_base.py:97). */
+int wc_conv_in_gn(const float* x, int B, int Cin, int H, int W, const float* w, const float* b, int Cout,
+                  float* out, int ldo, float* part, int ncb, int sw, int c0, void* stream);
 /* Head (unet_base.py:448-449,483-485): out = conv3x3(SiLU(x*scale[b,c] + shift[b,c])) + bias for
  * NO <= 4 output channels, x an NHWC view (C % 16 == 0), out NCHW (B, NO, H, W), pad 1 after the
  * prologue.  w packed as [C/16][9 taps (ky-major)][16 channels][4 outputs, zero-padded]. */

@@ -225,6 +225,30 @@ def test_conv_in_nchw_to_nhwc(K):
     assert torch.count_nonzero(buf[..., :64]) == 0
 
 
+@pytest.mark.parametrize('B,H,W,sw', [(2, 32, 48, 8), (3, 16, 20, 16), (1, 64, 64, 32)])
+def test_conv_in_gn_partials_bit_identical(K, B, H, W, sw):
+    """wc_conv_in_gn: the stem's output bit-identical to wc_conv_in, and its GroupNorm tile partials
+    bit-identical to the separate wc_gn_partials pass over that output (ragged last workgroup: B*H*W not
+    a multiple of 256)."""
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn((B, 3, H, W), generator=g).cuda()
+    w = (torch.randn((64, 3, 3, 3), generator=g) / 27**0.5).cuda()
+    b = (torch.randn(64, generator=g) * 0.1).cuda()
+    ref = torch.zeros((B, H, W, 128)).cuda()
+    gr = K.GnPart.attach(ref, sw)
+    gr.part.fill_(-7.0)
+    assert K.conv_in(x, w, b, K.View(ref, 64, 64)) is False
+    K.gn_partials(K.View(ref, 64, 64), gr)
+    buf = torch.zeros((B, H, W, 128)).cuda()
+    gp = K.GnPart.attach(buf, sw)
+    gp.part.fill_(-7.0)
+    assert K.conv_in(x, w, b, K.View(buf, 64, 64), gn=gp) is True
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    assert torch.equal(gp.part, gr.part)
+    assert rel_l2(_nchw(buf[..., 64:].cpu()), F.conv2d(x.cpu(), w.cpu(), b.cpu(), padding=1)) < TOL
+
+
 TABLES = ('betas', 'alphas', 'alpha_cum_prod', 'sqrt_alpha_cum_prod', 'one_minus_cum_prod',
           'sqrt_one_minus_alpha_cum_prod')
 

@@ -21,7 +21,7 @@ EXPORTS = [
     'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
-    'wc_temb', 'wc_conv_in', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
+    'wc_temb', 'wc_conv_in', 'wc_conv_in_gn', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
     'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_f16x3', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
@@ -104,6 +104,7 @@ _SIGS = {
     'wc_attention_fwd_x6_lse': [_P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P],
     'wc_temb': [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     'wc_conv_in': [_P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
+    'wc_conv_in_gn': [_P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
     'wc_head_conv': [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P],
     'wc_ddpm_step': [_P, _P, _P, _P, _P, _L, _L, _F, _F, _F, _F, _I, _U, _L, _L, _P],
     'wc_add_noise': [_P, _P, _P, _P, _P, _L, _L, _P],

@@ -67,25 +67,39 @@ __global__ __launch_bounds__(TE_THREADS) void temb_kernel(const int64_t* __restr
 // --------------------------------------------------------------------------------------------
 // conv_in: 3x3 pad-1 conv from the NCHW image to an NHWC view (unet_base.py:400,456).  The
 // NCHW->NHWC transpose is fused here.
-// conv_in_px_kernel<COUT>: thread = pixel, all COUT outputs in registers; the Cin*9 inputs are
-// loaded once per pixel (coalesced across the wave), weights are LDS broadcasts, and the pixel's
-// COUT outputs leave as 16-byte stores: HBM-bound (12 B in + 4*COUT B out per pixel).
+// conv_in_px_kernel<COUT, CIN, GN>: thread = pixel, all COUT outputs in registers; the Cin*9 inputs
+// are loaded once per pixel (coalesced across the wave), weights are LDS broadcasts.  The outputs
+// leave through a per-wave LDS tile, 32 channels at a time: each store instruction then writes eight
+// pixels' 128 contiguous bytes (whole lines; thread-per-pixel 16-byte stores at the skip buffer's
+// 512-byte pixel pitch touched a line per lane).  GN: the wave's 64 pixels are one GroupNorm
+// 64-pixel block, and its (mean, M2) tile partials are computed from the same LDS tile with
+// gn_partials_kernel's lane map and summation order (wc_gn.hip): bit-identical partials without the
+// separate pass over the output.
 // conv_in_kernel (any Cout % 4): thread = (pixel, 4 output channels).
 // Both accumulate bias, then (ci, ky, kx) in order, one fma each (out-of-image taps add 0 * w).
 // --------------------------------------------------------------------------------------------
-template <int COUT, int CIN>
-__global__ __launch_bounds__(256) void conv_in_px_kernel(const float* __restrict__ x, int B, int Cin, int H, int W,
+constexpr int CI_TS = 36;  // LDS tile row pitch (floats): 32 channels + 4, conflict-free b128 access
+constexpr size_t CI_TILE_BYTES = 4 * 64 * CI_TS * sizeof(float);
+
+template <int COUT, int CIN, bool GN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void conv_in_px_kernel(const float* __restrict__ x, int B, int Cin, int H, int W,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
-                                                         float* __restrict__ out, int ldo) {
-    extern __shared__ float ws[];  // [Cin*9][COUT]
+                                                         float* __restrict__ out, int ldo, float* __restrict__ part,
+                                                         int ncb, int sw, int cb_off) {
+    static_assert(COUT % 32 == 0, "conv_in_px: 32-channel store rounds");
+    extern __shared__ float ws[];  // [Cin*9][COUT], then 4 wave tiles [64 px][CI_TS]
     const int K = Cin * 9;
     for (int i = threadIdx.x; i < K * COUT; i += blockDim.x) {
         const int co = i % COUT, k = i / COUT;
         ws[i] = w[(long)co * K + k];
     }
     __syncthreads();
-    const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (pix >= (long)B * H * W) return;
+    const int lane = threadIdx.x & 63;
+    float* tile = ws + CIN * 9 * COUT + (threadIdx.x >> 6) * 64 * CI_TS;
+    const long npix = (long)B * H * W;
+    const long pix0 = (long)blockIdx.x * blockDim.x + (threadIdx.x & ~63);  // the wave's first pixel
+    // lanes past the end compute a copy of the last pixel (no branch around the loads), never stored
+    const long pix = min(pix0 + lane, npix - 1);
     const int xw = (int)(pix % W);
     const int yh = (int)((pix / W) % H);
     const int b = (int)(pix / ((long)W * H));
@@ -114,9 +128,68 @@ __global__ __launch_bounds__(256) void conv_in_px_kernel(const float* __restrict
             acc[4 * q + 3] = fmaf(v, wv.w, acc[4 * q + 3]);
         }
     }
-    f32x4* o = reinterpret_cast<f32x4*>(out + pix * ldo);
+    const int q = lane & 7, row = lane >> 3;  // (channel quad, pixel row) of the store / GN lane map
+    // branch-free stores (a divergent branch around them made the compiler spill the accumulators):
+    // a row past the end holds the clamped last pixel's values (lanes past the end computed it), so it
+    // is stored to that pixel again, the same bytes
+    float* orow[8];
 #pragma unroll
-    for (int q = 0; q < COUT / 4; ++q) o[q] = f32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+    for (int i = 0; i < 8; ++i) orow[i] = out + min(pix0 + row + 8 * i, npix - 1) * ldo + 4 * q;
+#pragma unroll
+    for (int cb = 0; cb < COUT / 32; ++cb) {
+        // the tile is this wave's own: a wave's LDS operations complete in order, so only the compiler
+        // has to be kept from moving them across (no workgroup barrier)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            *reinterpret_cast<f32x4*>(tile + lane * CI_TS + 4 * j) =
+                f32x4{acc[32 * cb + 4 * j], acc[32 * cb + 4 * j + 1], acc[32 * cb + 4 * j + 2], acc[32 * cb + 4 * j + 3]};
+        __builtin_amdgcn_wave_barrier();
+        f32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(tile + (row + 8 * i) * CI_TS + 4 * q);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            *reinterpret_cast<f32x4*>(orow[i] + 32 * cb) = v[i];
+        if constexpr (GN) {
+            // gn_partials_kernel (wc_gn.hip) on this 64-pixel block x 32 channels, same lanes, same order
+            const int qw = sw / 4;
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sum += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) {
+                const float t = __shfl_xor(sum, o, 64);
+                sum = o < qw ? sum + t : sum;
+            }
+            sum += __shfl_xor(sum, 8, 64);
+            sum += __shfl_xor(sum, 16, 64);
+            sum += __shfl_xor(sum, 32, 64);
+            const float mean = sum / (64.0f * (float)sw);
+            float m2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float d = v[i][e] - mean;
+                    m2 = fmaf(d, d, m2);
+                }
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) {
+                const float t = __shfl_xor(m2, o, 64);
+                m2 = o < qw ? m2 + t : m2;
+            }
+            m2 += __shfl_xor(m2, 8, 64);
+            m2 += __shfl_xor(m2, 16, 64);
+            m2 += __shfl_xor(m2, 32, 64);
+            // after the butterflies every lane of a sub-slot holds its (mean, M2): all of them store it
+            // (the same bytes to one address; no branch)
+            const long bp = pix0 / 64;  // b * np64 + p (HW % 64 == 0)
+            float* o = part + ((bp * ncb + cb_off + cb) * (32 / sw) + q / qw) * 2;
+            o[0] = mean;
+            o[1] = m2;
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void conv_in_kernel(const float* __restrict__ x, int B, int Cin,
@@ -469,15 +542,33 @@ extern "C" int wc_conv_in(const float* x, int B, int Cin, int H, int W, const fl
     if (Cout == 64 && Cin == 3 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
         (reinterpret_cast<uintptr_t>(b) & 15) == 0) {
         const long npix = (long)B * H * W;
-        wc_last_kernel = "conv_in_px_kernel<64, 3>";
-        hipLaunchKernelGGL((conv_in_px_kernel<64, 3>), dim3((unsigned)((npix + 255) / 256)), dim3(256), lds,
-                           reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, out, ldo);
+        wc_last_kernel = "conv_in_px_kernel<64, 3, false>";
+        hipLaunchKernelGGL((conv_in_px_kernel<64, 3, false>), dim3((unsigned)((npix + 255) / 256)), dim3(256),
+                           lds + CI_TILE_BYTES, reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, out,
+                           ldo, nullptr, 0, 0, 0);
         WC_CHECK_LAUNCH();
         return WC_OK;
     }
     long total = (long)B * H * W * (Cout / 4);
     hipLaunchKernelGGL(conv_in_kernel, dim3(grid_for(total, 256)), dim3(256), lds,
                        reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, Cout, out, ldo);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_conv_in_gn(const float* x, int B, int Cin, int H, int W, const float* w, const float* b,
+                             int Cout, float* out, int ldo, float* part, int ncb, int sw, int c0, void* stream) {
+    if (!x || !w || !b || !out || !part) return WC_E_ARG;
+    if (Cin != 3 || Cout != 64 || ldo % 4 != 0 || ldo < Cout || (H * W) % 64 != 0 || c0 % 32 != 0 || c0 < 0 ||
+        c0 + Cout > ncb * 32 || (sw != 4 && sw != 8 && sw != 16 && sw != 32) ||
+        ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(b)) & 15) != 0)
+        return WC_E_SHAPE;
+    const long npix = (long)B * H * W;
+    const size_t lds = (size_t)Cin * 9 * Cout * sizeof(float) + CI_TILE_BYTES;
+    wc_last_kernel = "conv_in_px_kernel<64, 3, true>";
+    hipLaunchKernelGGL((conv_in_px_kernel<64, 3, true>), dim3((unsigned)((npix + 255) / 256)), dim3(256), lds,
+                       reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, out, ldo, part, ncb, sw,
+                       c0 / 32);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

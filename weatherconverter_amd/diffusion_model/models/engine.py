@@ -481,8 +481,7 @@ class UnetEngine:
         U = [self._new(B, sizes[i][0], sizes[i][1], 2 * dc[i], gn_sw=self._sw(dc[i])) for i in range(L)]
 
         cur = View(U[0], dc[0], dc[0])
-        K.conv_in(x, self.conv_in_w, self.conv_in_b, cur)
-        self._gn_fill(cur)
+        self._gn_fill(cur, K.conv_in(x, self.conv_in_w, self.conv_in_b, cur, gn=K.GnPart.of(cur)))
 
         # per-image max |x| of each resampling conv's input, emitted by its producer's epilogue
         # (the f16x3 down / transposed convs scale by it; one row per resampling conv)

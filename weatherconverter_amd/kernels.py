@@ -985,13 +985,20 @@ def temb(t: torch.Tensor, w1, b1, w2, b2, proj_w, proj_b) -> torch.Tensor:
     return out
 
 
-def conv_in(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: View):
+def conv_in(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: View, gn: Optional[GnPart] = None):
+    """The stem conv (wc_conv_in); with gn (the output's tile partials, a 3 -> 64 stem) the same launch
+    writes the output's GroupNorm partials (wc_conv_in_gn).  Returns True when it did."""
     _req(x.is_contiguous() and x.dtype == torch.float32 and x.dim() == 4, 'conv_in input must be NCHW fp32')
     B, Cin, H, W = x.shape
     out.check()
     _req(out.H == H and out.W == W and out.B == B, 'conv_in output view shape')
+    if gn is not None and gn.covers(out) and Cin == 3 and out.C == 64 and (H * W) % 64 == 0:
+        _native.call('wc_conv_in_gn', x.data_ptr(), B, Cin, H, W, w.data_ptr(), b.data_ptr(), out.C, out.ptr,
+                     out.ldc, gn.part.data_ptr(), gn.ncb, gn.sw, out.c0, _stream())
+        return True
     _native.call('wc_conv_in', x.data_ptr(), B, Cin, H, W, w.data_ptr(), b.data_ptr(), out.C, out.ptr, out.ldc,
                  _stream())
+    return False
 
 
 def pack_head(w: torch.Tensor) -> torch.Tensor:

@@ -306,7 +306,8 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     torch.cuda.synchronize()
     K.profile_conv(False)
     if C // heads in (32, 64, 128) or (C // heads == 192 and precision == 'f16x3'):
-        # the split-precision backward ran (D = 192: its dQ kernel on f16x3, dK / dV on fp32 MFMA)
+        # the split-precision backward ran (D = 192: dQ with the output dims in three parts, dK / dV with
+        # the V rows in LDS; both raise the per-image bound)
         # the exact instantiation rocprofv3 prints, output-dim split DS included (3 at D = 192, else 1)
         f3 = 'true' if precision == 'f16x3' else 'false'
         ds = 3 if C // heads == 192 else 1

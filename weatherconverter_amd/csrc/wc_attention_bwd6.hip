@@ -48,6 +48,8 @@ struct B6Cfg {
     static constexpr int LDS = 2 * STAGE;                // double-buffered: tile t + 1 staged under tile t
     static constexpr int IPT = D / 32;                   // float4 items per thread of one 32 x D tile
     static constexpr bool PRESPLIT = D <= 128;   // own rows kept as pieces (else fp32, split per use)
+    static constexpr int VROWB = NCH * NP * 64 * 16;  // one wave's own rows as pieces in get() order (VL)
+    static constexpr int LDS_VL = STAGE + 4 * VROWB;  // VL: one Q / dO stage + the four waves' V rows
 };
 
 // Split-precision pieces of 8 consecutive values as MFMA operands: three exact bf16 pieces, or (F3)
@@ -226,7 +228,11 @@ WC_DEVICE BwdScales bwd_scales(int eq, int ek, int ev, const float* dobound, int
 
 // DS: the output dims split over DS workgroups (each computes S and dP in full, and dK / dV — or dQ —
 // for D / DS of the dims): at D = 192 the whole width does not fit one wave's registers.
-template <int D, bool F3, int DS = 1>
+// VL: the wave's own V rows live in LDS as pieces in the order the MFMAs read them ([K-step][piece]
+// [lane] 16-byte fragments, one ds_read_b128 each, conflict-free) instead of registers, and the Q / dO
+// tiles are single-staged to make room (the next tile's global loads still fly under the MFMAs): at
+// D = 192 the K and V rows together would take 192 registers and the kernel spilled.
+template <int D, bool F3, int DS = 1, bool VL = false>
 __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
@@ -251,7 +257,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
 
     OwnRows<D, F3> kr, vr;
     kr.load(base + (long)key * ldq + kcol, key < N, half, sc.sk);
-    vr.load(base + (long)key * ldq + vcol, key < N, half, sc.sv);
+    constexpr int NSTAGE = VL ? 1 : 2;
+    unsigned char* vls = smem + NSTAGE * Cf::STAGE + wave * Cf::VROWB;
+    if constexpr (VL) {
+        const float* row = base + (long)key * ldq + vcol;
+#pragma unroll
+        for (int ch = 0; ch < Cf::NCH; ++ch) {
+            float v[8];
+            f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, c = a;
+            if (key < N) {
+                a = *reinterpret_cast<const f32x4*>(row + 16 * ch + 8 * half);
+                c = *reinterpret_cast<const f32x4*>(row + 16 * ch + 8 * half + 4);
+            }
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+            u32x4 pc[NP];
+            pieces8<F3>(v, sc.sv, pc);
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp) *reinterpret_cast<u32x4*>(vls + ((ch * NP + pp) * 64 + lane) * 16) = pc[pp];
+        }
+    } else {
+        vr.load(base + (long)key * ldq + vcol, key < N, half, sc.sv);
+    }
 
     f32x16 dvT[NDBP], dkT[NDBP];
 #pragma unroll
@@ -286,7 +312,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
     swrite(0);
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
-        unsigned char* Qs = smem + (t & 1) * Cf::STAGE;
+        unsigned char* Qs = smem + (NSTAGE == 2 ? (t & 1) : 0) * Cf::STAGE;
         unsigned char* Os = Qs + Cf::TILE;
         const float* Ls = reinterpret_cast<const float*>(Qs + 2 * Cf::TILE);
         if (t + 1 < ntiles) gload(t + 1);  // in flight under this tile's MFMAs
@@ -301,7 +327,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
             kr.get(ch, bk);
             mfmaP(s, a, bk);
             tile_rows<D, F3>(Os, l32, half, ch, a);
-            vr.get(ch, bk);
+            if constexpr (VL) {
+#pragma unroll
+                for (int pp = 0; pp < NP; ++pp) bk[pp] = *reinterpret_cast<const u32x4*>(vls + ((ch * NP + pp) * 64 + lane) * 16);
+            } else {
+                vr.get(ch, bk);
+            }
             mfmaP(dp, a, bk);
         }
         // P and dS in place (register r <-> query (r&3) + 8(r>>2) + 4 half of the tile)
@@ -328,7 +359,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
                 mfmaP(dkT[db], a, ds);
             }
         }
-        if (t + 1 < ntiles) swrite((t + 1) & 1);  // the other stage: last read in tile t - 1
+        if constexpr (NSTAGE == 2) {
+            if (t + 1 < ntiles) swrite((t + 1) & 1);  // the other stage: last read in tile t - 1
+        } else if (t + 1 < ntiles) {
+            __syncthreads();  // every wave is done with the single stage
+            swrite(0);
+        }
         __syncthreads();
     }
 
@@ -500,6 +536,28 @@ extern "C" int wc_attention_bwd_dkdv192(const float* qkv, int ld_qkv, const floa
                                         const float* dv_work, float* dqkv, int ld_dqkv, int B, int N, int C,
                                         int heads, float scale, void* stream);
 
+// the D = 192 dK / dV kernel with V rows in LDS, output dims in DS parts (2: no spills, S and dP computed
+// twice; 1: computed once, 216 bytes of scratch per lane; WC_DKDV192_DS selects, default 2)
+template <int DS>
+int launch_dkdv192(const float* qkv, int ld_qkv, const float* dout, int ld_dout, const float* lse, const float* dv_work,
+                   float* dqkv, int ld_dqkv, int B, int N, int C, int heads, float scale, int eq, int ek, int ev,
+                   const float* dobound, float* amx, hipStream_t s) {
+    using Cf = B6Cfg<192, true>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dkdv_kernel<192, true, DS, true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS_VL);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    WC_SET_NAME("attn_bwd6_dkdv_kernel", {WC_TI(192), WC_TB(true), WC_TI(DS), WC_TB(true)});
+    hipLaunchKernelGGL((attn_bwd6_dkdv_kernel<192, true, DS, true>), dim3((N + 127) / 128 * DS, heads, B), dim3(256),
+                       Cf::LDS_VL, s, qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, N, C,
+                       scale * 1.4426950408889634f, scale, eq, ek, ev, dobound, amx);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
 static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, int ld_out, const float* dout,
                                int ld_dout, const float* lse, float* dv_work, float* dqkv, int ld_dqkv, int B, int N,
                                int C, int heads, float scale, bool f3, int eq, int ek, int ev, const float* dobound,
@@ -527,13 +585,20 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
         case 128: return WC_BWD6(128);
         case 192: {
             // f16x3 only: dQ with the output dims in three parts (its own Q / dO rows fit at a third of
-            // the accumulators); dK / dV on the fp32-MFMA kernel (its own K and V rows spill in the split
-            // forms even with the outputs split), which raises no bound: amx stays the caller's job
-            if (!f3 || amx) return WC_E_SHAPE;
-            st = wc_attention_bwd_dkdv192(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale,
-                                          stream);
-            if (st != WC_OK) return st;
+            // the accumulators); dK / dV with the V rows in LDS (VL, launch_dkdv192), or
+            // (WC_ATTN_BWD192_FP32=1) on the fp32-MFMA kernel, which raises no bound
+            if (!f3) return WC_E_SHAPE;
             using Cf = B6Cfg<192, true>;
+            static const bool fp32_dkdv = [] {
+                const char* e = getenv("WC_ATTN_BWD192_FP32");
+                return e && e[0] == '1';
+            }();
+            if (fp32_dkdv) {
+                if (amx) return WC_E_SHAPE;
+                st = wc_attention_bwd_dkdv192(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
+                                              scale, stream);
+                if (st != WC_OK) return st;
+            }
             static bool attr_set = false;
             if (!attr_set) {
                 hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<192, true, 3>),
@@ -541,10 +606,22 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
                 if (e != hipSuccess) return (int)e;
                 attr_set = true;
             }
+            const float scale_log2 = scale * 1.4426950408889634f;
+            if (!fp32_dkdv) {
+                static const int ds = [] {
+                    const char* e = getenv("WC_DKDV192_DS");
+                    return e && e[0] == '1' ? 1 : 2;
+                }();
+                st = ds == 1 ? launch_dkdv192<1>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
+                                                 scale, eq, ek, ev, dobound, amx, s)
+                             : launch_dkdv192<2>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
+                                                 scale, eq, ek, ev, dobound, amx, s);
+                if (st != WC_OK) return st;
+            }
             WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(192), WC_TB(true), WC_TI(3)});
             hipLaunchKernelGGL((attn_bwd6_dq_kernel<192, true, 3>), dim3((N + 127) / 128 * 3, heads, B), dim3(256),
-                               Cf::LDS, s, qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, N, C,
-                               scale * 1.4426950408889634f, scale, eq, ek, ev, dobound, nullptr);
+                               Cf::LDS, s, qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, N, C, scale_log2,
+                               scale, eq, ek, ev, dobound, fp32_dkdv ? nullptr : amx);
             WC_CHECK_LAUNCH();
             return WC_OK;
         }

@@ -1398,7 +1398,7 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
                   dout_bound: Optional[torch.Tensor] = None, dqkv_absmax: Optional[torch.Tensor] = None) -> bool:
     """d qkv (same [q | k | v] rows as qkv) of softmax(Q K^T / sqrt(d)) V from the forward's output and lse:
     fp32 MFMA (wc_attention_bwd), or with precision 'bf16x6' / 'f16x3' and a head dim in {32, 64, 128}
-    the split-precision kernels: f16x3 (wc_attention_bwd_f16x3) when the Q / K / V exponents of the
+    (f16x3 also 192) the split-precision kernels: f16x3 (wc_attention_bwd_f16x3) when the Q / K / V exponents of the
     forward (exps) and the per-image max |dout| (dout_bound, device float32 [B]) are given, else
     bf16x6 (wc_attention_bwd6).  dqkv_absmax: float32 [B] raised to the max |dqkv| written per image
     by the f16x3 kernels; returns whether it was (else the caller measures the bound itself)."""
@@ -1410,11 +1410,16 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
     args = (qkv.data_ptr(), 3 * C, out.data_ptr(), C, dout.data_ptr(), C, lse.data_ptr(), dv.data_ptr(),
             dqkv.data_ptr(), 3 * C, B, N, C, heads, float(d**-0.5))
     f3ok = precision == 'f16x3' and exps is not None and dout_bound is not None and attention_bwd_f16x3_enabled()
-    if d == 192 and f3ok and attention_bwd6_enabled():  # dQ on f16x3, dK / dV on fp32 MFMA (no bound raised)
+    if d == 192 and f3ok and attention_bwd6_enabled():
+        # dQ on f16x3 with the output dims in three parts; dK / dV on f16x3 with the V rows in LDS (or, with
+        # WC_ATTN_BWD192_FP32=1, on fp32 MFMA, which raises no bound)
         _req(_bound_ok(dout_bound, B), 'dout_bound: float32 [B] on the device')
+        amx = dqkv_absmax if os.environ.get('WC_ATTN_BWD192_FP32', '0') != '1' else None
+        if amx is not None:
+            _req(_bound_ok(amx, B), 'dqkv_absmax: float32 [B] on the device')
         _timed(f'attention_bwd<{d}>', 'wc_attention_bwd_f16x3', 10.0 * B * N * N * C, *args, int(exps[0]),
-               int(exps[1]), int(exps[2]), dout_bound.data_ptr(), None, _stream())
-        return False
+               int(exps[1]), int(exps[2]), dout_bound.data_ptr(), _ptr(amx), _stream())
+        return amx is not None
     if precision != 'fp32' and d in (32, 64, 128) and attention_bwd6_enabled():
         if f3ok:
             _req(dout_bound.is_cuda and dout_bound.dtype == torch.float32 and dout_bound.numel() >= B,

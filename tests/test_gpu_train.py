@@ -587,3 +587,18 @@ def test_attention_bwd_d192_dkdv_splits_bit_identical(tmp_path):
     assert torch.equal(res['1']['dqkv'], res['2']['dqkv'])
     assert torch.equal(res['1']['amx'], res['2']['amx'])
     assert float(res['2']['amx'].min()) > 0
+
+
+@pytest.mark.parametrize('B,H,W,C,ld', [(3, 17, 9, 4, 4), (2, 16, 16, 64, 128), (2, 8, 12, 768, 768), (1, 5, 7, 1536, 1600),
+                                        (2, 32, 33, 96, 96)])
+def test_absmax_images_vs_torch(B, H, W, C, ld):
+    """wc_absmax_images: per-image max |x| over a channel view (pitch ld), every channel-quad / pixel mapping
+    (C/4 dividing 256 or not, above 256 quads) and ragged pixel ranges."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import View
+    g = _gen(21)
+    t = torch.randn((B, H, W, ld), generator=g) * torch.rand((B, 1, 1, 1), generator=g) * 10
+    t[..., C:] = 1e6  # outside the view: must not count
+    got = K.absmax_images(View(t.cuda(), 0, C))
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), t[..., :C].abs().reshape(B, -1).amax(1))

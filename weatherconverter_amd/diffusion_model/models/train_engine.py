@@ -35,7 +35,7 @@ import torch
 
 from ... import kernels as K
 from ...kernels import Seg, View
-from .engine import TAPS1, TAPS3, TAPS4S2, pack_conv, pack_convT
+from .engine import TAPS1, TAPS3, TAPS4S2, UnetEngine, pack_conv, pack_convT
 
 _PARITIES = ((0, 0), (0, 1), (1, 0), (1, 1))
 
@@ -279,6 +279,22 @@ class TrainEngine:
     def _new(self, B, H, W, C) -> torch.Tensor:
         return torch.empty((B, H, W, C), dtype=torch.float32, device=self.device)
 
+    def _new_gn(self, B, H, W, C) -> torch.Tensor:
+        """A forward activation that also carries GroupNorm tile partials (kernels.GnPart), filled by its
+        producer's epilogue when that is a split-precision conv, so its GroupNorm needs no stats pass."""
+        t = self._new(B, H, W, C)
+        sw = UnetEngine._sw(C)
+        if sw is not None and K.GnPart.eligible(t) and os.environ.get('WC_TRAIN_GN_PARTIALS', '1') != '0':
+            K.GnPart.attach(t, sw)
+        return t
+
+    @staticmethod
+    def _gn_out(out: View, N: int, H: int, W: int, bm: Optional[int] = None) -> Optional['K.GnPart']:
+        """out's tile partials when the conv writing it can emit them from its epilogue, else None
+        (bm: the implicit GEMM's M tile)."""
+        gp = K.GnPart.of(out)
+        return gp if K.gn_conv_ok(out, gp, N, H, W, bm) else None
+
     def _grad(self, v: View) -> View:
         """The gradient view of a forward view (zero-initialised tensors, allocated on first use)."""
         key = id(v.t)
@@ -367,7 +383,7 @@ class TrainEngine:
             if att is None:
                 self._res_fwd(X, tgt, rp, temb, amx)
             else:
-                ypre = View.full(self._new(B, X.H, X.W, rp['co']))
+                ypre = View.full(self._new_gn(B, X.H, X.W, rp['co']))
                 self._res_fwd(X, ypre, rp, temb)
                 self._attn_fwd(ypre, tgt, att, amx)
             return tgt
@@ -389,7 +405,7 @@ class TrainEngine:
             amx = new_amx() if self.down_pk[i] is not None else None
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
-                tgt = final if (last and self.down_pk[i] is None) else View.full(self._new(B, H, W, rp['co']))
+                tgt = final if (last and self.down_pk[i] is None) else View.full(self._new_gn(B, H, W, rp['co']))
                 cur = block(cur, tgt, rp, att[li] if att else None, amx if last else None)
             if self.down_pk[i] is not None:
                 dp = self.down_pk[i]
@@ -414,13 +430,13 @@ class TrainEngine:
                 if last and self.up_pk[0] is None:
                     tgt = View(U[L - 1], 0, dc[L - 1])
                 else:
-                    tgt = View.full(self._new(B, H, W, rp['co']))
+                    tgt = View.full(self._new_gn(B, H, W, rp['co']))
                 if last and self.up_pk[0] is not None:
                     amx = new_amx()
                 self._res_fwd(cur, tgt, rp, temb, amx if last and li >= len(att) else None)
                 cur = tgt
                 if li < len(att):
-                    nxt = View.full(self._new(B, H, W, rp['co']))
+                    nxt = View.full(self._new_gn(B, H, W, rp['co']))
                     self._attn_fwd(cur, nxt, att[li], amx if last else None)
                     cur = nxt
 
@@ -447,12 +463,13 @@ class TrainEngine:
             for li, rp in enumerate(res):
                 last = li == len(res) - 1
                 tgt = View(U[i - 1], 0, dc[i - 1]) if (last and next_in_place) else View.full(
-                    self._new(B, H, W, rp['co']))
+                    self._new_gn(B, H, W, rp['co']))
                 cur = block(cur, tgt, rp, att[li] if att else None, amx if last else None)
 
         # head: GN -> SiLU -> conv_out, NCHW output
         gn = m.norm_out
-        sc, sh, a0, o0 = K.gn_stats_pair(cur, gn.weight.detach().float(), gn.bias.detach().float())
+        sc, sh, a0, o0 = K.gn_stats_pair(cur, gn.weight.detach().float(), gn.bias.detach().float(),
+                                         part=getattr(cur, '_wc_gn_done', None))
         out = torch.empty((B, mc.im_channels, S, S2), dtype=torch.float32, device=self.device)
         self._conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.head_pk,
                    m.conv_out.bias.detach().float().contiguous(), None, S, S2, out_nchw=out)
@@ -465,41 +482,51 @@ class TrainEngine:
         B, H, W = X.B, X.H, X.W
         g1, g2 = rp['gn1'], rp['gn2']
         co = rp['co']
-        st1 = K.gn_stats_pair(X, g1.weight.detach().float(), g1.bias.detach().float(), bound=True)
-        h = View.full(self._new(B, H, W, co))
+        st1 = K.gn_stats_pair(X, g1.weight.detach().float(), g1.bias.detach().float(), bound=True,
+                              part=getattr(X, '_wc_gn_done', None))
+        h = View.full(self._new_gn(B, H, W, co))
         seg1 = [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)]
         b1 = rp['conv1'].bias.detach().float().contiguous()
+        gp1 = None  # h's GroupNorm partials, when conv1's epilogue wrote them
         if rp['wn_1'] is not None and K.wino_eligible(seg1, co, H, W):
+            gp1 = self._gn_out(h, co, H, W)
             K.conv3x3_wino(seg1, rp['wn_1'], b1, h, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8),
-                           temb=temb[:, rp['off']:], temb_ld=temb.shape[1])
+                           temb=temb[:, rp['off']:], temb_ld=temb.shape[1], gn=gp1)
         elif rp['f3_1'] is not None and K.x6_eligible(seg1, co, H, W):
+            gp1 = self._gn_out(h, co, H, W)
             K.conv3x3_f16x3(seg1, rp['f3_1'], b1, h, Hm=H, Wm=W,
                             a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8), temb=temb[:, rp['off']:],
-                            temb_ld=temb.shape[1])
+                            temb_ld=temb.shape[1], gn=gp1)
         else:
             self._conv(seg1, rp['pk1'], b1, h, H, W, temb=temb[:, rp['off']:], temb_ld=temb.shape[1])
-        st2 = K.gn_stats_pair(h, g2.weight.detach().float(), g2.bias.detach().float())
+        st2 = K.gn_stats_pair(h, g2.weight.detach().float(), g2.bias.detach().float(), part=gp1)
         seg2 = [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)]
+        gp2 = None  # Y's partials (an attention block's input): the next GroupNorm's statistics
         if rp['wn_2'] is not None and K.wino_eligible(seg2, co, H, W):
+            gp2 = self._gn_out(Y, co, H, W)
             K.conv3x3_wino(seg2, rp['wn_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
-                           a_bound=st1[4], absmax=amx)
+                           a_bound=st1[4], absmax=amx, gn=gp2)
             if amx is not None:
                 self._raised[id(amx)] = True
         elif rp['f3_2'] is not None and K.x6_eligible(seg2, co, H, W):
             # the residual segment (raw X) in fp16 under GN1's per-image bound of |X|
+            gp2 = self._gn_out(Y, co, H, W)
             K.conv3x3_f16x3(seg2, rp['f3_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
-                            a_bound=st1[4], absmax=amx)
+                            a_bound=st1[4], absmax=amx, gn=gp2)
             if amx is not None:
                 self._raised[id(amx)] = True
         else:
             self._conv(seg2, rp['pk2'], rp['b2'], Y, H, W)
+        if gp2 is not None:
+            Y._wc_gn_done = gp2
         self.tape.append(('res', X, h, Y, rp, st1[:4], st2, st1[4]))
 
     def _attn_fwd(self, Ypre: View, Yout: View, ap, amx: Optional[torch.Tensor] = None):
         B, H, W, C = Ypre.B, Ypre.H, Ypre.W, Ypre.C
         N = H * W
         gn, mha = ap['gn'], ap['mha']
-        st = K.gn_stats_pair(Ypre, gn.weight.detach().float(), gn.bias.detach().float())
+        st = K.gn_stats_pair(Ypre, gn.weight.detach().float(), gn.bias.detach().float(),
+                             part=getattr(Ypre, '_wc_gn_done', None))
         qkv = self._new(B, H, W, 3 * C)
         seg = [Seg(Ypre, TAPS1, scale=st[0], shift=st[1], silu=False)]
         b_in = mha.in_proj_bias.detach().float().contiguous()
@@ -514,10 +541,13 @@ class TrainEngine:
             exps = K.attention_exps_from_norms(ap['qkv_l1'], ap['qkv_babs'], ap['gb'][0], ap['gb'][1], ng)
             K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'],
                                 precision='f16x3', exps=exps)
+            gpo = self._gn_out(Yout, C, H, W, 256 if C <= 64 else 128)
             K.conv_igemm_f16x3([Seg(View.full(o), TAPS1)], ap['f3_out'], b_out, Yout, Hm=H, Wm=W, a_exp=exps[2],
-                               res=Ypre, absmax=amx)
+                               res=Ypre, absmax=amx, gn=gpo)
             if amx is not None:
                 self._raised[id(amx)] = True
+            if gpo is not None:
+                Yout._wc_gn_done = gpo
         else:
             self._conv(seg, ap['pk_in'], b_in, View.full(qkv), H, W)
             K.attention_fwd_lse(qkv.view(B * N, 3 * C), o.view(B * N, C), lse, B, N, C, ap['heads'],

@@ -1282,12 +1282,17 @@ def conv_wgrad(g: View, segs: Sequence[Seg], dw0: torch.Tensor, s0: Tuple[int, i
 
 
 def gn_stats_pair(v: View, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5, groups: int = 8,
-                  bound: bool = False):
+                  bound: bool = False, part: Optional[GnPart] = None):
     """GroupNorm statistics of v once, finalized twice: (scale, shift) of the affine GN and
     (sc0, sh0) = (rstd, -mean*rstd) of the plain normalisation (what the backward needs); with
-    bound=True a fifth result, the per-image bound of |v| (wc_gn_finalize_bound)."""
+    bound=True a fifth result, the per-image bound of |v| (wc_gn_finalize_bound).  With `part` (tile
+    partials of v's tensor written by v's producer's epilogue) no pass over v: two wc_gn_finalize_part."""
     v.check()
     B, HW, C = v.B, v.H * v.W, v.C
+    if part is not None:
+        aff = gn_affine(v, gamma, beta, eps, groups, bound=bound, part=part)
+        plain = gn_affine(v, None, None, eps, groups, part=part)
+        return (aff[0], aff[1], plain[0], plain[1]) + ((aff[2], ) if bound else ())
     lib = _native.load()
     splits = lib.wc_gn_num_splits(B, HW, C)
     part = torch.empty((B, splits, groups, 2), dtype=torch.float32, device=v.t.device)

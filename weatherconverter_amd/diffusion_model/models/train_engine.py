@@ -140,8 +140,8 @@ class TrainEngine:
             pk2=L(lambda: self._pk(w2cat, co, 9, ci)),
             f3_1=K.pack_f16x3(pack_conv(w1).float(), ci) if f3 else None,
             f3_2=K.pack_f16x3(w2cat.float(), co, ci, res_f16=True) if f3 else None,
-            gb1=self._later(f[0].weight.abs().max(), f[0].bias.abs().max()),
-            gb2=self._later(s[0].weight.abs().max(), s[0].bias.abs().max()),
+            gb1=self._later_absmax(f[0].weight, f[0].bias),
+            gb2=self._later_absmax(s[0].weight, s[0].bias),
             b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
             pk1T=L(lambda: self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9)),
             pk2T=L(lambda: self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9)),
@@ -175,7 +175,7 @@ class TrainEngine:
             d['f3_out'] = K.pack_f16x3(w_out.float(), C, ntaps=1, order='natural')
             d['qkv_l1'] = self._later(w_in.double().abs().sum(1), vector=True)
             d['qkv_babs'] = self._later(mha.in_proj_bias.detach().double().abs(), vector=True)
-            d['gb'] = self._later(gn.weight.abs().max(), gn.bias.abs().max())
+            d['gb'] = self._later_absmax(gn.weight, gn.bias)
         return d
 
     def _later(self, *vals, vector: bool = False):
@@ -186,11 +186,21 @@ class TrainEngine:
         self._pending.append((slot, vals, vector))
         return slot
 
+    def _later_absmax(self, *tensors):
+        """A host tuple (max|t| for t in tensors), reduced with every other such request in one
+        multi-tensor launch (torch._foreach_norm, inf: exact) and copied with the rest in _resolve."""
+        slot = _Slot()
+        self._pending_max.append((slot, [t.detach() for t in tensors]))
+        return slot
+
     def _resolve(self, packs):
-        """Fill every slot _later handed out and replace the slots inside the pack dicts."""
-        if self._pending:
-            flat = torch.cat([v.detach().reshape(-1).double() for _, vals, _ in self._pending for v in vals])
-            host = flat.cpu()
+        """Fill every slot _later / _later_absmax handed out and replace the slots inside the pack dicts."""
+        parts = [v.detach().reshape(-1).double() for _, vals, _ in self._pending for v in vals]
+        mx = [t for _, ts in self._pending_max for t in ts]
+        if mx:
+            parts.append(torch.stack(torch._foreach_norm(mx, float('inf'))).double())
+        if parts:
+            host = torch.cat(parts).cpu()
             i = 0
             for slot, vals, vector in self._pending:
                 if vector:
@@ -200,7 +210,11 @@ class TrainEngine:
                 else:
                     slot.value = tuple(float(host[i + j]) for j in range(len(vals)))
                     i += len(vals)
+            for slot, ts in self._pending_max:
+                slot.value = tuple(float(host[i + j]) for j in range(len(ts)))
+                i += len(ts)
         self._pending = []
+        self._pending_max = []
         for d in packs:
             for k, v in list(d.items()):
                 if isinstance(v, _Slot):
@@ -210,6 +224,7 @@ class TrainEngine:
         m = self.model
         self.P = 0
         self._pending = []
+        self._pending_max = []
 
         def stage(blk, n_res):
             res = []
@@ -295,6 +310,16 @@ class TrainEngine:
         gp = K.GnPart.of(out)
         return gp if K.gn_conv_ok(out, gp, N, H, W, bm) else None
 
+    def _zrow(self, B: int) -> torch.Tensor:
+        """A zeroed float32[B] on the device (a per-image bound that writers raise): rows of one pooled
+        zero fill instead of a fill launch each.  A row is never handed out twice."""
+        pool = getattr(self, '_zpool', None)
+        if pool is None or pool.shape[1] != B or self._zi >= pool.shape[0]:
+            self._zpool = pool = torch.zeros((128, B), dtype=torch.float32, device=self.device)
+            self._zi = 0
+        self._zi += 1
+        return pool[self._zi - 1]
+
     def _grad(self, v: View) -> View:
         """The gradient view of a forward view (zero-initialised tensors, allocated on first use)."""
         key = id(v.t)
@@ -319,7 +344,7 @@ class TrainEngine:
         g = self._grad(v)
         t = self.gbnd.get(id(g.t))
         if t is None:
-            t = torch.zeros((v.B, ), dtype=torch.float32, device=self.device)
+            t = self._zrow(v.B)
             self.gbnd[id(g.t)] = t
         return t
 
@@ -389,7 +414,7 @@ class TrainEngine:
             return tgt
 
         def new_amx():
-            return torch.zeros((B, ), dtype=torch.float32, device=self.device) if (self.f3 or self.f3d) else None
+            return self._zrow(B) if (self.f3 or self.f3d) else None
 
         def bound_of(v: View, amx):
             """The producer-raised bound when it was raised (nonzero), else a pass over v."""
@@ -668,7 +693,7 @@ class TrainEngine:
             self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX, absmax=bX)
         g2 = rp['gn2']
         dh = View.full(self._new(B, H, W, co))
-        bdh = torch.zeros((B, ), dtype=torch.float32, device=self.device) if self.f3d else None
+        bdh = self._zrow(B) if self.f3d else None
         K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
                       dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh)
         sums = self._bias_grad(dh, rp['conv1'].bias)
@@ -704,7 +729,7 @@ class TrainEngine:
         self._wgrad(gY, [Seg(View.full(o), TAPS1)], self._pgrad(mha.out_proj.weight), (C, 1, 0),
                     f3=K.F3Bounds(bgY, exps[2]) if f3a else None)
         do = self._new(B, H, W, C)
-        bdo = torch.zeros((B, ), dtype=torch.float32, device=self.device) if self.f3d else None
+        bdo = self._zrow(B) if self.f3d else None
         f3p = 'f3_outT' in ap and (H * W) % (256 if C <= 64 else 128) == 0
         if f3p:
             K.conv_igemm_f16x3([Seg(gY, TAPS1)], ap['f3_outT'], None, View.full(do), Hm=H, Wm=W, a_exp=60,
@@ -716,7 +741,7 @@ class TrainEngine:
         if f3a:
             # f16x3 under the forward's Q / K / V exponents and the per-image max |dO|; the kernels raise
             # the per-image max |dqkv| as they write it (head dims 32 / 64 / 128)
-            bgq = torch.zeros((B, ), dtype=torch.float32, device=self.device)
+            bgq = self._zrow(B)
             if not K.attention_bwd(qkv.view(B * N, 3 * C), o.view(B * N, C), do.view(B * N, C), lse,
                                    dqkv.view(B * N, 3 * C), B, N, C, ap['heads'], precision='f16x3', exps=exps,
                                    dout_bound=self._bound(View.full(do), bdo), dqkv_absmax=bgq):

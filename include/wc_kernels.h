@@ -333,8 +333,10 @@ int wc_conv_in(const float* x, int B, int Cin, int H, int W, const float* w, con
                int Cout, float* out, int ldo, void* stream);
 /* conv_in for the 3 -> 64 stem with the output's GroupNorm tile partials (the wc_gn_partials format
  * and arithmetic, bit-identical) from the same launch: part / ncb / sw as wc_gn_partials, c0 = the
- * output view's first channel in the partials tensor (% 32); H*W % 64 == 0.  Replaces the stem conv
- * (unet_base.py:456) followed by the first GroupNorm's statistics pass (unet_base.py:97). */
+ * output view's first channel in the partials tensor (% 32); H*W % 64 == 0.  w is the weight
+ * TRANSPOSED, [Cin*9][Cout] (k = ci*9 + ky*3 + kx), 16-byte aligned; results bit-identical to
+ * wc_conv_in with the PyTorch layout.  Replaces the stem conv (unet_base.py:456) followed by the first
+ * GroupNorm's statistics pass (unet_base.py:97). */
 int wc_conv_in_gn(const float* x, int B, int Cin, int H, int W, const float* w, const float* b, int Cout,
                   float* out, int ldo, float* part, int ncb, int sw, int c0, void* stream);
 /* Head (unet_base.py:448-449,483-485): out = conv3x3(SiLU(x*scale[b,c] + shift[b,c])) + bias for

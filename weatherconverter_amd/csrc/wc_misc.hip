@@ -87,15 +87,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
                                                          float* __restrict__ out, int ldo, float* __restrict__ part,
                                                          int ncb, int sw, int cb_off) {
     static_assert(COUT % 32 == 0, "conv_in_px: 32-channel store rounds");
-    extern __shared__ float ws[];  // [Cin*9][COUT], then 4 wave tiles [64 px][CI_TS]
+    // GN (wc_conv_in_gn): w is already [Cin*9][COUT]; every weight is wave-uniform, so the taps read them
+    // as scalar loads (s_load_dwordx16) straight into SGPR operands of the FMAs: no LDS staging, no LDS
+    // broadcast reads.  Else w is the PyTorch [COUT][Cin*9] and is staged transposed into LDS.
+    extern __shared__ float ws[];  // (not GN) [Cin*9][COUT]; then 4 wave tiles [64 px][CI_TS]
     const int K = Cin * 9;
-    for (int i = threadIdx.x; i < K * COUT; i += blockDim.x) {
-        const int co = i % COUT, k = i / COUT;
-        ws[i] = w[(long)co * K + k];
+    const float* wk = w;
+    float* tiles = ws;
+    if constexpr (!GN) {
+        for (int i = threadIdx.x; i < K * COUT; i += blockDim.x) {
+            const int co = i % COUT, k = i / COUT;
+            ws[i] = w[(long)co * K + k];
+        }
+        __syncthreads();
+        wk = ws;
+        tiles = ws + CIN * 9 * COUT;
     }
-    __syncthreads();
     const int lane = threadIdx.x & 63;
-    float* tile = ws + CIN * 9 * COUT + (threadIdx.x >> 6) * 64 * CI_TS;
+    float* tile = tiles + (threadIdx.x >> 6) * 64 * CI_TS;
     const long npix = (long)B * H * W;
     const long pix0 = (long)blockIdx.x * blockDim.x + (threadIdx.x & ~63);  // the wave's first pixel
     // lanes past the end compute a copy of the last pixel (no branch around the loads), never stored
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 #pragma unroll
     for (int k = 0; k < CIN * 9; ++k) {
         const float v = xin[k];
-        const f32x4* wr = reinterpret_cast<const f32x4*>(ws + k * COUT);
+        const f32x4* wr = reinterpret_cast<const f32x4*>(wk + k * COUT);
 #pragma unroll
         for (int q = 0; q < COUT / 4; ++q) {
             const f32x4 wv = wr[q];
@@ -560,11 +569,12 @@ extern "C" int wc_conv_in_gn(const float* x, int B, int Cin, int H, int W, const
                              int Cout, float* out, int ldo, float* part, int ncb, int sw, int c0, void* stream) {
     if (!x || !w || !b || !out || !part) return WC_E_ARG;
     if (Cin != 3 || Cout != 64 || ldo % 4 != 0 || ldo < Cout || (H * W) % 64 != 0 || c0 % 32 != 0 || c0 < 0 ||
+        (reinterpret_cast<uintptr_t>(w) & 15) != 0 ||
         c0 + Cout > ncb * 32 || (sw != 4 && sw != 8 && sw != 16 && sw != 32) ||
         ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(b)) & 15) != 0)
         return WC_E_SHAPE;
     const long npix = (long)B * H * W;
-    const size_t lds = (size_t)Cin * 9 * Cout * sizeof(float) + CI_TILE_BYTES;
+    const size_t lds = CI_TILE_BYTES;
     wc_last_kernel = "conv_in_px_kernel<64, 3, true>";
     hipLaunchKernelGGL((conv_in_px_kernel<64, 3, true>), dim3((unsigned)((npix + 255) / 256)), dim3(256), lds,
                        reinterpret_cast<hipStream_t>(stream), x, B, Cin, H, W, w, b, out, ldo, part, ncb, sw,

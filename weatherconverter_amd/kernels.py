@@ -993,7 +993,12 @@ def conv_in(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: View, gn: Op
     out.check()
     _req(out.H == H and out.W == W and out.B == B, 'conv_in output view shape')
     if gn is not None and gn.covers(out) and Cin == 3 and out.C == 64 and (H * W) % 64 == 0:
-        _native.call('wc_conv_in_gn', x.data_ptr(), B, Cin, H, W, w.data_ptr(), b.data_ptr(), out.C, out.ptr,
+        # the weight transposed to [Cin*9][Cout], cached on the weight tensor (rebuilt if it changes in place)
+        wt = getattr(w, '_wc_t', None)
+        if wt is None or w._wc_t_version != w._version:
+            wt = w.reshape(out.C, Cin * 9).t().contiguous()
+            w._wc_t, w._wc_t_version = wt, w._version
+        _native.call('wc_conv_in_gn', x.data_ptr(), B, Cin, H, W, wt.data_ptr(), b.data_ptr(), out.C, out.ptr,
                      out.ldc, gn.part.data_ptr(), gn.ncb, gn.sw, out.c0, _stream())
         return True
     _native.call('wc_conv_in', x.data_ptr(), B, Cin, H, W, w.data_ptr(), b.data_ptr(), out.C, out.ptr, out.ldc,

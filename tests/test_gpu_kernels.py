@@ -376,7 +376,8 @@ def test_old_unet_helper_kernels(K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('B,H,W,C,NO', [(2, 32, 48, 64, 3), (1, 20, 13, 32, 4), (3, 16, 16, 128, 1)])
+@pytest.mark.parametrize('B,H,W,C,NO', [(2, 32, 48, 64, 3), (1, 20, 13, 32, 4), (3, 16, 16, 128, 1), (1, 45, 30, 32, 4),
+                                        (2, 64, 40, 64, 3)])
 def test_head_conv_vs_float64(B, H, W, C, NO):
     """norm_out -> SiLU -> conv_out on wc_head_conv (ragged tiles, strided view) vs float64."""
     from weatherconverter_amd import kernels as K

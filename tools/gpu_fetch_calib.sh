@@ -11,5 +11,5 @@ for r in rows:
     if r['Counter_Name'] == 'FETCH_SIZE' and 'absmax' in r['Kernel_Name']:
         agg[r['Dispatch_Id']] = agg.get(r['Dispatch_Id'], 0.0) + float(r['Counter_Value'])
 for d, v in agg.items():
-    print(f'dispatch {d}: FETCH_SIZE {v:.0f} KB = {v * 1024 / 2**30:.3f} GiB (tensor 1.000 GiB)')
+    print(f'dispatch {d}: FETCH_SIZE {v:.0f} KB = {v * 1024 / 2**30:.3f} GiB for a 4.000 GiB read (x2 = {2 * v * 1024 / 2**30:.3f})')
 PY

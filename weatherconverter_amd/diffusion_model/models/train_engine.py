@@ -60,6 +60,10 @@ class _Pack(dict):
             dict.__setitem__(self, k, v)
         return v
 
+    def has(self, k) -> bool:
+        """Whether form k exists for this layer, without building it (a lazy form is never None)."""
+        return dict.get(self, k) is not None
+
 
 class _Slot:
     """A host value of the packing pass, filled by TrainEngine._resolve."""
@@ -132,32 +136,38 @@ class TrainEngine:
         wr2 = wr.reshape(co, ci)
         f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
         wino = K.wino_enabled()
-        w2cat = torch.cat([pack_conv(w2), wr2], 1)
         L = _Pack.lazy
-        return _Pack(
+        # shared re-layouts, each built once and only if a pack that needs it is (the Winograd forms
+        # usually replace the direct f16x3 ones, so those are lazy too)
+        rp = _Pack(w1c=L(lambda: pack_conv(w1).float().contiguous()),
+                   w2cat=L(lambda: torch.cat([pack_conv(w2), wr2], 1).float().contiguous()),
+                   w1T=L(lambda: pack_conv(w1.flip([2, 3]).transpose(0, 1)).float().contiguous()),
+                   w2T=L(lambda: pack_conv(w2.flip([2, 3]).transpose(0, 1)).float().contiguous()))
+        rp.update(
             ci=ci, co=co, gn1=f[0], conv1=f[2], gn2=s[0], conv2=s[2], resc=r, temb=blk.t_emb_layers[i][1],
-            pk1=L(lambda: self._pk(pack_conv(w1), ci, 9)),
-            pk2=L(lambda: self._pk(w2cat, co, 9, ci)),
-            f3_1=K.pack_f16x3(pack_conv(w1).float(), ci) if f3 else None,
-            f3_2=K.pack_f16x3(w2cat.float(), co, ci, res_f16=True) if f3 else None,
+            pk1=L(lambda: self._pk(rp['w1c'], ci, 9)),
+            pk2=L(lambda: self._pk(rp['w2cat'], co, 9, ci)),
+            f3_1=L(lambda: K.pack_f16x3(rp['w1c'], ci)) if f3 else None,
+            f3_2=L(lambda: K.pack_f16x3(rp['w2cat'], co, ci, res_f16=True)) if f3 else None,
             gb1=self._later_absmax(f[0].weight, f[0].bias),
             gb2=self._later_absmax(s[0].weight, s[0].bias),
             b2=(s[2].bias.detach() + r.bias.detach()).float().contiguous(),
-            pk1T=L(lambda: self._pk(pack_conv(w1.flip([2, 3]).transpose(0, 1)), co, 9)),
-            pk2T=L(lambda: self._pk(pack_conv(w2.flip([2, 3]).transpose(0, 1)), co, 9)),
+            pk1T=L(lambda: self._pk(rp['w1T'], co, 9)),
+            pk2T=L(lambda: self._pk(rp['w2T'], co, 9)),
             pkrT=L(lambda: self._pk(wr2.t(), co, 1)),
             # f16x3 data gradients (raw gradient operand under its per-image absmax bound)
-            f3_1T=L(lambda: K.pack_f16x3(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co)) if self.f3d else None,
-            f3_2T=L(lambda: K.pack_f16x3(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co)) if self.f3d else None,
+            f3_1T=L(lambda: K.pack_f16x3(rp['w1T'], co)) if self.f3d else None,
+            f3_2T=L(lambda: K.pack_f16x3(rp['w2T'], co)) if self.f3d else None,
             f3_rT=L(lambda: K.pack_f16x3(wr2.t().contiguous().float(), co, ntaps=1, order='natural'))
             if self.f3d else None,
             # the Winograd F(2,3)-along-x forms of the same f16x3 convs (forward and data gradients)
-            wn_1=L(lambda: K.pack_wino(pack_conv(w1).float(), ci)) if f3 and wino else None,
-            wn_2=L(lambda: K.pack_wino(w2cat.float(), co, ci)) if f3 and wino else None,
-            wn_1T=L(lambda: K.pack_wino(pack_conv(w1.flip([2, 3]).transpose(0, 1)).float(), co))
+            wn_1=L(lambda: K.pack_wino(rp['w1c'], ci)) if f3 and wino else None,
+            wn_2=L(lambda: K.pack_wino(rp['w2cat'], co, ci)) if f3 and wino else None,
+            wn_1T=L(lambda: K.pack_wino(rp['w1T'], co))
             if self.f3d and wino and ci % 16 == 0 and co % 16 == 0 else None,
-            wn_2T=L(lambda: K.pack_wino(pack_conv(w2.flip([2, 3]).transpose(0, 1)).float(), co))
+            wn_2T=L(lambda: K.pack_wino(rp['w2T'], co))
             if self.f3d and wino and co % 16 == 0 else None)
+        return rp
 
     def _pack_attn(self, blk, i: int):
         mha, gn = blk.attentions[i], blk.attention_norms[i]
@@ -513,11 +523,11 @@ class TrainEngine:
         seg1 = [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)]
         b1 = rp['conv1'].bias.detach().float().contiguous()
         gp1 = None  # h's GroupNorm partials, when conv1's epilogue wrote them
-        if rp['wn_1'] is not None and K.wino_eligible(seg1, co, H, W):
+        if rp.has('wn_1') and K.wino_eligible(seg1, co, H, W):
             gp1 = self._gn_out(h, co, H, W)
             K.conv3x3_wino(seg1, rp['wn_1'], b1, h, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8),
                            temb=temb[:, rp['off']:], temb_ld=temb.shape[1], gn=gp1)
-        elif rp['f3_1'] is not None and K.x6_eligible(seg1, co, H, W):
+        elif rp.has('f3_1') and K.x6_eligible(seg1, co, H, W):
             gp1 = self._gn_out(h, co, H, W)
             K.conv3x3_f16x3(seg1, rp['f3_1'], b1, h, Hm=H, Wm=W,
                             a_exp=K.f16x3_a_exp(*rp['gb1'], H * W * X.C // 8), temb=temb[:, rp['off']:],
@@ -527,13 +537,13 @@ class TrainEngine:
         st2 = K.gn_stats_pair(h, g2.weight.detach().float(), g2.bias.detach().float(), part=gp1)
         seg2 = [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)]
         gp2 = None  # Y's partials (an attention block's input): the next GroupNorm's statistics
-        if rp['wn_2'] is not None and K.wino_eligible(seg2, co, H, W):
+        if rp.has('wn_2') and K.wino_eligible(seg2, co, H, W):
             gp2 = self._gn_out(Y, co, H, W)
             K.conv3x3_wino(seg2, rp['wn_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
                            a_bound=st1[4], absmax=amx, gn=gp2)
             if amx is not None:
                 self._raised[id(amx)] = True
-        elif rp['f3_2'] is not None and K.x6_eligible(seg2, co, H, W):
+        elif rp.has('f3_2') and K.x6_eligible(seg2, co, H, W):
             # the residual segment (raw X) in fp16 under GN1's per-image bound of |X|
             gp2 = self._gn_out(Y, co, H, W)
             K.conv3x3_f16x3(seg2, rp['f3_2'], rp['b2'], Y, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(*rp['gb2'], H * W * co // 8),
@@ -671,7 +681,7 @@ class TrainEngine:
         gX = self._grad(X)
         self._bias_grad(gY, rp['conv2'].bias, rp['resc'].bias)
         # per-image max |gY|: the range bound of the f16x3 data gradients and weight gradient
-        f3Y = rp['f3_2T'] is not None and self._dgrad3_ok(gY, co)
+        f3Y = rp.has('f3_2T') and self._dgrad3_ok(gY, co)
         bY = self._bound(gY, self._gb(Y)) if f3Y else None
         bX = self._gb(X)
         self._wgrad(gY, [Seg(h, TAPS3, scale=st2[0], shift=st2[1], silu=True), Seg(X, TAPS1, kbase=9 * co)],
@@ -679,7 +689,7 @@ class TrainEngine:
                     f3=K.F3Bounds(bY, K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), None, bXf) if f3Y else None)
         dz2 = View.full(self._new(B, H, W, co))
         if f3Y:
-            if rp['wn_2T'] is not None and K.wino_eligible([Seg(gY, TAPS3)], co, H, W):
+            if rp.has('wn_2T') and K.wino_eligible([Seg(gY, TAPS3)], co, H, W):
                 K.conv3x3_wino([Seg(gY, TAPS3)], rp['wn_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
             else:
                 K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
@@ -698,13 +708,13 @@ class TrainEngine:
                       dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh)
         sums = self._bias_grad(dh, rp['conv1'].bias)
         self.dproj[:, rp['off']:rp['off'] + co].copy_(sums[:, :, 0])
-        f3h = rp['f3_1T'] is not None and self._dgrad3_ok(dh, ci)
+        f3h = rp.has('f3_1T') and self._dgrad3_ok(dh, ci)
         bh = self._bound(dh, bdh) if f3h else None
         self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
                     (ci * 9, 9, 1), f3=K.F3Bounds(bh, K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8)) if f3h else None)
         dz1 = View.full(self._new(B, H, W, ci))
         if f3h:
-            if rp['wn_1T'] is not None and K.wino_eligible([Seg(dh, TAPS3)], ci, H, W):
+            if rp.has('wn_1T') and K.wino_eligible([Seg(dh, TAPS3)], ci, H, W):
                 K.conv3x3_wino([Seg(dh, TAPS3)], rp['wn_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
             else:
                 K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)

@@ -153,12 +153,6 @@ int wc_conv3x3_set_onewave(int mode);
  * Replaces unet_base.py:92,106 (+ :107-109 residual_input_conv), forward :146-150. */
 int wc_conv3x3_wino_f16x3(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
                           const float* w_inv_scale, const float* a_bound, void* stream);
-/* EXPERIMENTAL (off the product path): 2D Winograd F(2x2,3x3) form of the ResBlock conv1 (segment 0
- * with the GN + SiLU prologue only; N % 128 == 0, Hm % 8 == 0, Wm % 16 == 0; no residual, absmax or GN
- * partials).  w packed by kernels.pack_wino2d: [N/128][C0/16][16 positions][piece 2][k-half 2][128][8]
- * int16, U = G g G^T in float64 times 2^sW[n] (w_inv_scale = 2^-sW).  a_exp as wc_conv3x3_f16x3. */
-int wc_conv3x3_wino2d_f16x3(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
-                            const float* w_inv_scale, void* stream);
 int wc_conv3x3_wino_tile_n(int N);
 /* Form of wc_conv3x3_wino_f16x3 for BN = 128: 0 (default) two waves per SIMD, 8-row tiles; 1 one wave
  * per SIMD with 16-row tiles (each weight fragment feeds four MFMA row blocks) where H % 16 == 0.

@@ -45,14 +45,9 @@ def conv_case(B, H, Ci, Co, prologue=True, res=0, check=False, mode='fp32', taps
     if res:
         xr = torch.randn((B, H, H, res), device='cuda', generator=g)
         segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=nt * Ci))
-    if mode in ('x6', 'f3', 'wino', 'wino2d') and nt != 9 or mode in ('f3', 'wino', 'wino2d') and not prologue:
+    if mode in ('x6', 'f3', 'wino') and nt != 9 or mode in ('f3', 'wino') and not prologue:
         return None, None, None
-    if mode == 'wino2d':  # EXPERIMENTAL 2D F(2x2,3x3) (no residual)
-        if res:
-            return None, None, None
-        w2 = K.pack_wino2d(w, Ci)
-        fn = lambda: K.conv3x3_wino2d(segs, w2, b, K.View.full(out), Hm=H, Wm=H, a_exp=4)  # noqa: E731
-    elif mode == 'wino':
+    if mode == 'wino':
         ww = K.pack_wino(w, Ci, res)
         xb = torch.full((B, ), 8.0, device='cuda') if res else None
         fn = lambda: K.conv3x3_wino(segs, ww, b, K.View.full(out), Hm=H, Wm=H, a_exp=4, a_bound=xb)  # noqa: E731

@@ -745,259 +745,3 @@ extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, in
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
-
-// =====================================================================================================
-// EXPERIMENTAL: 2D Winograd F(2x2, 3x3) ResBlock conv1 (GN + SiLU prologue, no residual) on f16x3.
-// 16 transform positions per 2x2 output tile and 16 input channels: 4/9 of the direct conv's products
-// (the 1D form above does 2/3).  Workgroup = 8 output rows x 16 pixels = 32 tiles (one 32-row MFMA
-// block) x 128 channels, 8 waves: wave = (channel block cb = wave & 3, position half ph = wave >> 2), each
-// 8 positions (p = 2 ph, 2 ph + 1; q = 0..3) x 32 channels, 8 K-steps of 3 MFMAs per 16-channel chunk.
-// Input transform: thread = (tile, p, channel quad), 512 items, each loads its two halo rows x 4 columns
-// of the next chunk under the current chunk's MFMAs, applies GN + SiLU, V[p][q] = B^T d B, splits into
-// two fp16 pieces and writes the A planes [pos][piece][k-half][tile] of the other buffer; one barrier per
-// chunk.  Output transform Y = A^T M A: each position half forms its partial, the halves meet in LDS,
-// ph 0 finishes output row 0 of each tile and ph 1 row 1.  Range: |V| <= 4 max|d| (exponent - 2).
-// Filter transform U = G g G^T in float64 (kernels.pack_wino2d), per-channel power of two.
-// =====================================================================================================
-namespace {
-
-constexpr int W2T = 512;                          // threads
-constexpr int W2_PLANE = 32 * 16;                 // (pos, piece, k-half) plane: 32 tiles x 16 B
-constexpr int W2_STAGE = 16 * 2 * 2 * W2_PLANE;   // 32 KB
-constexpr int W2_BSTEP = 128 * 64;                // weight bytes of one (chunk, position): [piece][k-half][128][8]
-
-struct W2Dev {
-    const float* src0;
-    int C0, ldc0;
-    const float* scale;
-    const float* shift;
-    int B, H, W, N;
-    const void* w;
-    const float* bias;
-    const float* temb;
-    int temb_ld;
-    float* out;
-    int ldo;
-    int nck0;
-    int a_exp;
-    const float* wsinv;
-    int tiles_x, tiles_y, ntiles_n;
-};
-
-__global__ __launch_bounds__(W2T, 1) void conv3x3_wino2d_kernel(W2Dev p) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int cb = wave & 3, ph = wave >> 2;
-    const int l32 = lane & 31, half = lane >> 5;
-
-    const int nblk = gridDim.x;
-    int bid = blockIdx.x;
-    {
-        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    }
-    const int tile_n = bid % p.ntiles_n;
-    int tt = bid / p.ntiles_n;
-    const int txi = tt % p.tiles_x;
-    tt /= p.tiles_x;
-    const int tyi = tt % p.tiles_y;
-    const int b = tt / p.tiles_y;
-    const int y0 = tyi * 8, x0 = txi * 16, n0 = tile_n * 128;
-    const float ascale = ldexpf(1.0f, p.a_exp), ainv = ldexpf(1.0f, -p.a_exp);
-
-    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
-    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w);
-    const __amdgpu_buffer_rsrc_t srdsc = make_srd(p.scale);
-    const __amdgpu_buffer_rsrc_t srdsh = make_srd(p.shift);
-
-    // ---- transform item: tid = (tile t, row-transform index pr, channel quad qd) ----
-    const int qd = tid & 3, pr = (tid >> 2) & 3, t = tid >> 4;
-    const int ty = t >> 3, tx = t & 7;
-    // B^T row pr uses input rows (i0, i1) with signs (s0, s1)
-    const int i0 = pr == 0 ? 0 : 1, i1 = pr == 3 ? 3 : 2;
-    const float s1 = (pr == 0 || pr == 3) ? -1.f : 1.f;
-    const float s0x = pr == 2 ? -1.f : 1.f;  // p2: -d1 + d2
-    unsigned inb = 0;
-    int goff[2][4];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int iy = y0 - 1 + 2 * ty + (k ? i1 : i0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int ix = x0 - 1 + 2 * tx + j;
-            const bool in = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-            inb |= (in ? 1u : 0u) << (4 * k + j);
-            goff[k][j] = (((b * p.H + iy) * p.W + ix) * p.ldc0 + 4 * qd) * 4;
-        }
-    }
-    f32x4 rd[2][4], rsc, rsh;
-    auto load_in = [&](int c) {
-        const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * qd) * 4u;
-        rsc = bload_f4(srdsc, o);
-        rsh = bload_f4(srdsh, o);
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                rd[k][j] = bload_f4s(srd0, ((inb >> (4 * k + j)) & 1u) ? (unsigned)goff[k][j] : OOB, c * 64);
-    };
-    // GN + SiLU (zero padding after it), x 2^s, row combination, column transform, split, 8 writes
-    auto transform = [&](int buf) {
-        f32x4 d[2][4];
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                f32x4 a = rd[k][j] * rsc + rsh;
-                a.x = silu_fast(a.x); a.y = silu_fast(a.y); a.z = silu_fast(a.z); a.w = silu_fast(a.w);
-                d[k][j] = ((inb >> (4 * k + j)) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-        f32x4 r[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = d[0][j] * s0x + d[1][j] * s1;
-        const f32x4 V[4] = {r[0] - r[2], r[1] + r[2], r[2] - r[1], r[1] - r[3]};
-        unsigned char* base = smem + buf * W2_STAGE + t * 16 + (qd & 1) * 8;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            u32x2 a0, a1;
-            split2_f16(V[q], a0, a1);
-            const int pos = pr * 4 + q;
-            unsigned char* dst = base + ((pos * 2 + 0) * 2 + (qd >> 1)) * W2_PLANE;
-            *reinterpret_cast<u32x2*>(dst) = a0;
-            *reinterpret_cast<u32x2*>(dst + 2 * W2_PLANE) = a1;
-        }
-    };
-
-    // ---- weights: (chunk c, position pos) fragments of this wave's 32 columns ----
-    const unsigned wlane = (unsigned)(half * 128 * 16 + (cb * 32 + l32) * 16);
-    const unsigned wtile = (unsigned)tile_n * (unsigned)(p.nck0 * 16 * W2_BSTEP);
-    const int nsteps = p.nck0 * 8;  // this wave's K-steps
-    u32x4 wreg[3][2];
-    auto load_w = [&](int set, int g) {
-        int gg = g < nsteps ? g : nsteps - 1;
-        const int s = (gg >> 3) * 16 + ph * 8 + (gg & 7);
-        const int off = (int)(wtile + (unsigned)s * W2_BSTEP);
-#pragma unroll
-        for (int pc = 0; pc < 2; ++pc) wreg[set][pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * 128 * 16), off);
-    };
-
-    f32x16 acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
-
-    load_in(0);
-    load_w(0, 0);
-    load_w(1, 1);
-    transform(0);
-    __syncthreads();
-    for (int c = 0; c < p.nck0; ++c) {
-        const int buf = c & 1;
-        if (c + 1 < p.nck0) load_in(c + 1);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int g = c * 8 + k;
-            load_w((g + 2) % 3, g + 2);  // register set = global step % 3
-            const int pos = ph * 8 + k;
-            const unsigned char* ha = smem + buf * W2_STAGE + (pos * 4 + half) * W2_PLANE + l32 * 16;
-            const u32x4 a0 = *reinterpret_cast<const u32x4*>(ha);
-            const u32x4 a1 = *reinterpret_cast<const u32x4*>(ha + 2 * W2_PLANE);
-            const int set = g % 3;
-            acc[k] = mfma_f16(a0, wreg[set][0], acc[k]);
-            acc[k] = mfma_f16c(a0, wreg[set][1], acc[k]);
-            acc[k] = mfma_f16c(a1, wreg[set][0], acc[k]);
-            if (k == 5 && c + 1 < p.nck0) transform(buf ^ 1);
-        }
-        __syncthreads();
-    }
-
-    // ---- output transform: Z[p][j] = sum_q M[p][q] A[j][q]; this half's partials of Y[i][j] ----
-    // ph 0 (p = 0, 1): Y0j = Z0j + Z1j, Y1j = Z1j;  ph 1 (p = 2, 3): Y0j = Z2j, Y1j = -Z2j - Z3j
-    float* xb = reinterpret_cast<float*>(smem);  // [wave][j 2][reg 16][lane 64] (after the last barrier)
-    float keep[2][16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float za0 = (acc[0][r] + acc[1][r]) + acc[2][r], za1 = (acc[1][r] - acc[2][r]) - acc[3][r];
-        const float zb0 = (acc[4][r] + acc[5][r]) + acc[6][r], zb1 = (acc[5][r] - acc[6][r]) - acc[7][r];
-        float give0, give1;
-        if (ph == 0) {  // p = 0 (a), 1 (b)
-            keep[0][r] = za0 + zb0; keep[1][r] = za1 + zb1;  // Y0j (row i = 0)
-            give0 = zb0; give1 = zb1;                         // Y1j partial for ph 1
-        } else {        // p = 2 (a), 3 (b)
-            keep[0][r] = -za0 - zb0; keep[1][r] = -za1 - zb1;  // Y1j partial (row i = 1)
-            give0 = za0; give1 = za1;                           // Y0j partial for ph 0
-        }
-        xb[((wave * 2 + 0) * 16 + r) * 64 + lane] = give0;
-        xb[((wave * 2 + 1) * 16 + r) * 64 + lane] = give1;
-    }
-    __syncthreads();
-    const int partner = wave ^ 4;
-    const int n = n0 + cb * 32 + l32;
-    const bool nok = n < p.N;
-    float eadd = (nok && p.bias) ? p.bias[n] : 0.f;
-    if (nok && p.temb) eadd += p.temb[b * p.temb_ld + n];
-    const float emul = nok ? p.wsinv[n] * ainv : 0.f;
-    const long img_px = (long)b * p.H * p.W;
-    const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + img_px * p.ldo);
-    const int i = ph;  // output row of each tile this wave finishes
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float o0 = xb[((partner * 2 + 0) * 16 + r) * 64 + lane];
-        const float o1 = xb[((partner * 2 + 1) * 16 + r) * 64 + lane];
-        const float y0v = (ph == 0 ? keep[0][r] + o0 : o0 + keep[0][r]) * emul + eadd;
-        const float y1v = (ph == 0 ? keep[1][r] + o1 : o1 + keep[1][r]) * emul + eadd;
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * half;  // tile of MFMA row m
-        const int py = y0 + 2 * (m >> 3) + i, px = x0 + 2 * (m & 7);
-        const unsigned off = nok ? (unsigned)((py * p.W + px) * p.ldo + n) * 4u : OOB;
-        bstore_f1s(srd_out, off, 0, y0v);
-        bstore_f1s(srd_out, off, 4 * p.ldo, y1v);
-    }
-}
-
-}  // namespace
-
-extern "C" int wc_conv3x3_wino2d_f16x3(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
-                                       const float* w_inv_scale, void* stream) {
-    if (!a || !w || !a->out || !w_inv_scale) return WC_E_ARG;
-    if (a->nseg != 1) return WC_E_ARG;
-    const wc_conv_seg& s0 = a->seg[0];
-    if (!s0.src || !s0.scale || !s0.shift || !s0.silu) return WC_E_ARG;
-    if (a->act != WC_ACT_NONE || a->res || a->absmax_out || a->gn_part) return WC_E_ARG;
-    if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
-    if (s0.ntaps != 9 || s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
-    for (int t = 0; t < 9; ++t)
-        if (s0.dy[t] != t / 3 - 1 || s0.dx[t] != t % 3 - 1) return WC_E_SHAPE;
-    if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15)) return WC_E_SHAPE;
-    if (a->B <= 0 || a->N <= 0 || a->N % 128 || s0.H != a->Hm || s0.W != a->Wm || a->Hm % 8 || a->Wm % 16)
-        return WC_E_SHAPE;
-    if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31) || (reinterpret_cast<uintptr_t>(w) & 15)) return WC_E_SHAPE;
-    if (a->out_nchw || a->Ho != a->Hm || a->Wo != a->Wm || a->osy != 1 || a->osx != 1 || a->ooy || a->oox)
-        return WC_E_SHAPE;
-    if ((long)a->Hm * a->Wm * a->ldo * 4 >= (1L << 31)) return WC_E_SHAPE;
-    W2Dev d{};
-    d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.scale = s0.scale; d.shift = s0.shift;
-    d.B = a->B; d.H = a->Hm; d.W = a->Wm; d.N = a->N;
-    d.w = w; d.bias = a->bias; d.temb = a->temb; d.temb_ld = a->temb_ld; d.out = a->out; d.ldo = a->ldo;
-    d.nck0 = s0.C / 16;
-    d.a_exp = a_exp - 2;  // |V| <= 4 x the GN bound
-    d.wsinv = w_inv_scale;
-    d.tiles_x = d.W / 16; d.tiles_y = d.H / 8; d.ntiles_n = d.N / 128;
-    if (w_bytes != (long)d.ntiles_n * d.nck0 * 16 * W2_BSTEP) return WC_E_SHAPE;
-    const long nwg = (long)d.B * d.tiles_y * d.tiles_x * d.ntiles_n;
-    if (nwg >= (1L << 31)) return WC_E_SHAPE;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino2d_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * W2_STAGE);
-        if (e != hipSuccess) return (int)e;
-        attr = true;
-    }
-    wc_last_kernel = "conv3x3_wino2d_kernel";
-    hipLaunchKernelGGL(conv3x3_wino2d_kernel, dim3((unsigned)nwg), dim3(W2T), 2 * W2_STAGE,
-                       reinterpret_cast<hipStream_t>(stream), d);
-    WC_CHECK_LAUNCH();
-    return WC_OK;
-}

@@ -619,39 +619,6 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
            _ptr(a_bound) if (len(segs) == 2 or raw) else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res))
 
 
-def pack_wino2d(w: torch.Tensor, C0: int) -> X6Weight:
-    """EXPERIMENTAL: pack a [N][9*C0] conv weight (engine.pack_conv order) for the 2D Winograd
-    F(2x2,3x3) kernel wc_conv3x3_wino2d_f16x3: U = G g G^T in float64 ([N][4][4][C0]), a per-channel power of
-    two 2^sW[n] with max|U| 2^sW <= 2^14, one rounding to fp32, two round-to-nearest fp16 pieces; layout
-    [N/128][C0/16][16 positions][piece][k-half][128][8] (torch ops; no device kernel)."""
-    N, K = w.shape
-    _req(K == 9 * C0 and C0 % 16 == 0 and N % 128 == 0, 'wino2d weight shape')
-    g = w.double().reshape(N, 3, 3, C0)  # [n][ky][kx][c]
-    Gm = torch.tensor([[1., 0., 0.], [.5, .5, .5], [.5, -.5, .5], [0., 0., 1.]], dtype=torch.float64, device=w.device)
-    U = torch.einsum('pk,nklc,ql->npqc', Gm, g, Gm)  # [N][4][4][C0]
-    amax = U.abs().reshape(N, -1).amax(1)
-    m, e = torch.frexp(amax)
-    sw = torch.where(amax > 0, torch.where(m == 0.5, 15 - e, 14 - e).double(), torch.zeros_like(amax)).clamp(-60, 60)
-    v32 = (U * torch.ldexp(torch.ones_like(sw), sw)[:, None, None, None]).float()
-    h, lo = _split2(v32)
-    T, nc = N // 128, C0 // 16
-    pcs = torch.stack([h, lo]).view(torch.int16)  # [2][N][4][4][C0]
-    pcs = pcs.view(2, T, 128, 16, nc, 2, 8).permute(1, 4, 3, 0, 5, 2, 6).contiguous()  # [T][nc][pos][pc][kh][128][8]
-    wsinv = torch.ldexp(torch.ones(N, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
-    return X6Weight(pcs.reshape(T, -1), N, 128, C0, 0, 'wino2d', wsinv, False)
-
-
-def conv3x3_wino2d(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
-                   a_exp: int, temb: Optional[torch.Tensor] = None, temb_ld: int = 0):
-    """EXPERIMENTAL: the ResBlock conv1 (GN+SiLU prologue, no residual) through the 2D Winograd kernel."""
-    _req(w.data.is_cuda and w.data.is_contiguous() and w.order == 'wino2d', 'wino2d weight')
-    _req(len(segs) == 1 and segs[0].scale is not None and segs[0].silu and w.C0 == segs[0].view.C, 'wino2d segment')
-    a = _conv_args(segs, w.N, bias, out, Hm, Wm, temb, temb_ld, None, (1, 1, 0, 0), None, 0, None)
-    _timed('conv3x3_wino2d_kernel', 'wc_conv3x3_wino2d_f16x3',
-           _flops(segs, Hm, Wm, w.N) if PROFILE is not None or REPLAY is not None else 0.0,
-           ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(), _stream())
-
-
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,
                      Hm: int, Wm: int, a_exp: int, a_bound: Optional[torch.Tensor] = None,
                      temb: Optional[torch.Tensor] = None, temb_ld: int = 0, res: Optional[View] = None,

@@ -503,6 +503,14 @@ int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ldx, const fl
 int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, int HW, const float* sc0,
                        const float* gamma, float* sums, float* coef, void* stream);
 int wc_bsum(const float* sums, int B, int C, int idx, float* out, int accumulate, void* stream);
+/* Many wc_bsum in one launch (the training backward's deferred dgamma / dbeta / bias sums): jobs is a
+ * DEVICE array of njobs descriptors, max_c >= every job's C; no two jobs of one launch share an output. */
+typedef struct wc_bsum_job {
+    const float* sums;
+    float* out;
+    int C, idx, accumulate, pad;
+} wc_bsum_job;
+int wc_bsum_batch(const wc_bsum_job* jobs, int njobs, int B, int max_c, void* stream);
 int wc_gn_bwd_apply(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
                     const float* gamma, const float* beta, int silu, const float* coef, int B, int HW, int C,
                     float* dx, int lddx, int accumulate, float* absmax, void* stream);

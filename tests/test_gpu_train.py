@@ -227,12 +227,14 @@ def test_conv_wgrad_4x4_stride2_and_transposed(x6):
     assert rel_l2(dwt.cpu(), wt.grad) < 1e-5
 
 
-@pytest.mark.parametrize('silu', [True, False])
-def test_groupnorm_backward(silu):
+@pytest.mark.parametrize('silu,C', [(True, 64), (False, 64), (True, 768), (True, 32), (False, 2048)])
+def test_groupnorm_backward(silu, C):
+    """GN(+SiLU) backward vs float64 autograd; C = 32 ... 2048 spans the finalize's group widths
+    (4 ... 256 channels a workgroup)."""
     from weatherconverter_amd import kernels as K
     from weatherconverter_amd.kernels import View
     g = _gen(3)
-    B, H, W, C = 3, 16, 8, 64
+    B, H, W = 3, 16, 8
     x = torch.randn((B, H, W, C), generator=g) * 2 + 0.5
     gamma = torch.rand(C, generator=g) + 0.5
     beta = torch.randn(C, generator=g) * 0.2
@@ -253,6 +255,37 @@ def test_groupnorm_backward(silu):
     y.backward(dz.double().permute(0, 3, 1, 2))
     assert rel_l2(dx.cpu() - base, xd.grad.permute(0, 2, 3, 1)) < 1e-5
     assert rel_l2(dg.cpu(), gd.grad) < 1e-5 and rel_l2(db.cpu(), bd.grad) < 1e-5
+
+
+@pytest.mark.parametrize('C', [4, 96, 200, 768])
+def test_channel_sums_and_deferred_bsum(C):
+    """channel_sums (the finalize's 64-channel blocks, ragged last block) vs float64, and the deferred
+    bsum (one wc_bsum_batch launch, an output queued twice accumulating in queue order) bit-identical to
+    one wc_bsum launch each."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import View
+    g = _gen(5)
+    B, H, W = 4, 8, 24
+    x = torch.randn((B, H, W, C + 8), generator=g)
+    sums = K.channel_sums(View(x.cuda(), 4, C))
+    ref = x[..., 4:4 + C].double().sum((1, 2))
+    assert rel_l2(sums[..., 0].cpu(), ref) < 1e-6 and bool((sums[..., 1] == 0).all())
+    s2 = K.channel_sums(View(x.flip(0).contiguous().cuda(), 0, C))
+    init = torch.randn(C, generator=g).cuda()
+    outs_now = [init.clone(), torch.zeros(C, device='cuda')]
+    K.bsum(sums, 0, outs_now[0], accumulate=True)
+    K.bsum(s2, 0, outs_now[0], accumulate=True)
+    K.bsum(s2, 1, outs_now[1])
+    outs_def = [init.clone(), torch.full((C, ), 7.0, device='cuda')]
+    K.bsum_defer()
+    K.bsum(sums, 0, outs_def[0], accumulate=True)
+    K.bsum(s2, 0, outs_def[0], accumulate=True)
+    K.bsum(s2, 1, outs_def[1])
+    assert bool((outs_def[0] == init).all())  # nothing launched before the flush
+    K.bsum_flush()
+    torch.cuda.synchronize()
+    for a, b in zip(outs_now, outs_def):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize('C,heads,N', [(64, 4, 200), (128, 4, 256), (256, 4, 96), (512, 4, 160), (768, 4, 64),

@@ -25,7 +25,7 @@ EXPORTS = [
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
     'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_f16x3', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
-    'wc_gn_bwd_finalize', 'wc_bsum', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
+    'wc_gn_bwd_finalize', 'wc_bsum', 'wc_bsum_batch', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
     'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name',
     'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse',
     'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_dkdv192', 'wc_attention_bwd_prep', 'wc_pack_split'
@@ -135,6 +135,7 @@ _SIGS = {
     'wc_gn_bwd_reduce': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P],
     'wc_gn_bwd_finalize': [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     'wc_bsum': [_P, _I, _I, _I, _P, _I, _P],
+    'wc_bsum_batch': [_P, _I, _I, _I, _P],
     'wc_gn_bwd_apply': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P],
     'wc_attention_fwd_lse': [_P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P],
     'wc_attention_bwd': [_P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],

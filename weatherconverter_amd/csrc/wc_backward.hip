@@ -545,52 +545,77 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_reduce_kernel(const float* __r
     }
 }
 
-// One workgroup per image: sums[b][c] = (sum dy, sum dy*xhat) over the splits (fixed order); with
-// coef: per group A = sum_c gamma_c s1_c, Bs = sum_c gamma_c s2_c, n = (C/G)*HW, and
+// Workgroup (image b, channel block of cw channels): sums[b][c] = (sum dy, sum dy*xhat) over the splits
+// in a fixed order (slice k of the 256 / cw slices sums splits k, k + nsl, ...; the slices are added in
+// order).  With coef the block is one GroupNorm group (cw = C / G): A = sum_c gamma_c s1_c and
+// Bs = sum_c gamma_c s2_c by a fixed butterfly in wave 0, n = cw*HW, and
 // coef[b][c] = (rstd*gamma_c, -rstd*A/n, -rstd*Bs/n) so that dx = c0*dy + c1 + c2*xhat.
+// (One workgroup per image with a 64-split chain per channel took ~20 us a launch; this grid is
+// B x blocks.)
 __global__ __launch_bounds__(GB_THREADS) void gnb_finalize_kernel(const float* __restrict__ part, int splits, int C,
-                                                                   int G, int HW, const float* __restrict__ sc0,
+                                                                   int cw, int HW, const float* __restrict__ sc0,
                                                                    const float* __restrict__ gamma,
                                                                    float* __restrict__ sums, float* __restrict__ coef) {
-    extern __shared__ float sh[];  // [C][2] then [G][2]
+    __shared__ float red[2][GB_THREADS];
+    __shared__ float gs[2];
     const int b = blockIdx.x;
-    for (int c = threadIdx.x; c < C; c += GB_THREADS) {
-        float s1 = 0.f, s2 = 0.f;
+    const int nsl = GB_THREADS / cw;
+    const int ch = threadIdx.x % cw, sl = threadIdx.x / cw;
+    const int c = blockIdx.y * cw + ch;
+    const bool act = sl < nsl && c < C;
+    float s1 = 0.f, s2 = 0.f;
+    if (act) {
         const wcx6::f32x2* pp = reinterpret_cast<const wcx6::f32x2*>(part + ((long)b * splits * C + c) * 2);
-        // the splits in order (the sum is a chain), their loads issued eight ahead
-#pragma unroll 8
-        for (int sp = 0; sp < splits; ++sp) {
+#pragma unroll 4
+        for (int sp = sl; sp < splits; sp += nsl) {
             const wcx6::f32x2 v = pp[(long)sp * C];
             s1 += v.x;
             s2 += v.y;
         }
+    }
+    red[0][threadIdx.x] = s1;
+    red[1][threadIdx.x] = s2;
+    __syncthreads();
+    const bool lead = sl == 0 && c < C;
+    float ga = 1.f;
+    if (lead) {
+        for (int k = 1; k < nsl; ++k) {
+            s1 += red[0][k * cw + ch];
+            s2 += red[1][k * cw + ch];
+        }
         sums[((long)b * C + c) * 2] = s1;
         sums[((long)b * C + c) * 2 + 1] = s2;
-        const float ga = gamma ? gamma[c] : 1.f;
-        sh[2 * c] = ga * s1;
-        sh[2 * c + 1] = ga * s2;
+        if (gamma) ga = gamma[c];
     }
     if (!coef) return;
     __syncthreads();
-    float* gs = sh + 2 * C;
-    const int cpg = C / G;
-    if (threadIdx.x < G) {
-        float A = 0.f, Bs = 0.f;
-        for (int c = threadIdx.x * cpg; c < (threadIdx.x + 1) * cpg; ++c) {
-            A += sh[2 * c];
-            Bs += sh[2 * c + 1];
-        }
-        gs[2 * threadIdx.x] = A;
-        gs[2 * threadIdx.x + 1] = Bs;
+    if (sl == 0) {
+        red[0][ch] = lead ? ga * s1 : 0.f;
+        red[1][ch] = lead ? ga * s2 : 0.f;
     }
     __syncthreads();
-    const float inv_n = 1.0f / ((float)cpg * (float)HW);
-    for (int c = threadIdx.x; c < C; c += GB_THREADS) {
-        const int g = c / cpg;
+    if (threadIdx.x < 64) {
+        float A = 0.f, Bs = 0.f;
+        for (int k = threadIdx.x; k < cw; k += 64) {
+            A += red[0][k];
+            Bs += red[1][k];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            A += __shfl_xor(A, o, 64);
+            Bs += __shfl_xor(Bs, o, 64);
+        }
+        if (threadIdx.x == 0) {
+            gs[0] = A;
+            gs[1] = Bs;
+        }
+    }
+    __syncthreads();
+    if (lead) {
+        const float inv_n = 1.0f / ((float)cw * (float)HW);
         const float rstd = sc0[(long)b * C + c];
-        const float ga = gamma ? gamma[c] : 1.f;
-        float* cf = coef + ((long)b * C + c) * 4;
-        *reinterpret_cast<f32x4*>(cf) = f32x4{rstd * ga, -rstd * gs[2 * g] * inv_n, -rstd * gs[2 * g + 1] * inv_n, 0.f};
+        *reinterpret_cast<f32x4*>(coef + ((long)b * C + c) * 4) =
+            f32x4{rstd * ga, -rstd * gs[0] * inv_n, -rstd * gs[1] * inv_n, 0.f};
     }
 }
 
@@ -602,6 +627,17 @@ __global__ __launch_bounds__(256) void bsum_kernel(const float* __restrict__ sum
     float s = 0.f;
     for (int b = 0; b < B; ++b) s += sums[((long)b * C + c) * 2 + idx];
     out[c] = accumulate ? out[c] + s : s;
+}
+
+// Many bsums in one launch: job y = blockIdx.y does out[c] (+)= sum_b sums[(b*C + c)*2 + idx] (the
+// order of bsum_kernel; the caller gives each output at most one job per launch).
+__global__ __launch_bounds__(256) void bsum_batch_kernel(const wc_bsum_job* __restrict__ jobs, int B) {
+    const wc_bsum_job j = jobs[blockIdx.y];
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < j.C; c += gridDim.x * 256) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += j.sums[((long)b * j.C + c) * 2 + j.idx];
+        j.out[c] = j.accumulate ? j.out[c] + s : s;
+    }
 }
 
 // dx (+)= coef0*dy + coef1 + coef2*xhat, elementwise over (b, pixel, 4 channels)
@@ -990,11 +1026,11 @@ extern "C" int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ld
 extern "C" int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, int HW, const float* sc0,
                                   const float* gamma, float* sums, float* coef, void* stream) {
     if (!part || !sums || (coef && !sc0)) return WC_E_ARG;
-    if (C < 1 || (coef && (groups < 1 || groups > GB_THREADS || C % groups))) return WC_E_SHAPE;
-    const size_t lds = (size_t)(2 * C + 2 * (groups > 0 ? groups : 1)) * sizeof(float);
-    if (lds > 64 * 1024) return WC_E_SHAPE;
-    hipLaunchKernelGGL(gnb_finalize_kernel, dim3(B), dim3(GB_THREADS), lds, reinterpret_cast<hipStream_t>(stream), part,
-                       splits, C, groups, HW, sc0, gamma, sums, coef);
+    if (C < 1 || B < 1 || splits < 1 || (coef && (groups < 1 || C % groups))) return WC_E_SHAPE;
+    const int cw = coef ? C / groups : (C < 64 ? C : 64);
+    if (cw > GB_THREADS) return WC_E_SHAPE;
+    hipLaunchKernelGGL(gnb_finalize_kernel, dim3(B, (C + cw - 1) / cw), dim3(GB_THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), part, splits, C, cw, HW, sc0, gamma, sums, coef);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -1003,6 +1039,16 @@ extern "C" int wc_bsum(const float* sums, int B, int C, int idx, float* out, int
     if (!sums || !out || idx < 0 || idx > 1) return WC_E_ARG;
     hipLaunchKernelGGL(bsum_kernel, dim3(blocks_for(C, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), sums,
                        B, C, idx, out, accumulate);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_bsum_batch(const wc_bsum_job* jobs, int njobs, int B, int max_c, void* stream) {
+    if (!jobs || njobs < 0 || B < 1 || max_c < 0) return WC_E_ARG;
+    if (njobs == 0 || max_c == 0) return WC_OK;
+    if (njobs > 65535) return WC_E_SHAPE;
+    hipLaunchKernelGGL(bsum_batch_kernel, dim3(blocks_for(max_c, 256), njobs), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), jobs, B);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -625,10 +625,14 @@ class TrainEngine:
         B = gout.shape[0]
         self.dproj = torch.zeros((B, self.P), dtype=torch.float32, device=self.device)
         gout = gout.to(self.device, torch.float32).contiguous()
-        for rec in reversed(records):
-            getattr(self, '_bwd_' + rec[0])(rec, gout)
-        del records
-        self._temb_bwd()
+        K.bsum_defer()  # the ~200 per-layer dgamma / dbeta / bias sums go out in one launch at the end
+        try:
+            for rec in reversed(records):
+                getattr(self, '_bwd_' + rec[0])(rec, gout)
+            del records
+            self._temb_bwd()
+        finally:
+            K.bsum_flush()
         self.gmap = {}
         self.gbnd = {}
         self.keep = []
@@ -665,7 +669,7 @@ class TrainEngine:
         self._wgrad(g4, [Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], wtmp, (C * 9, 9, 1))
         self._pgrad(m.conv_out.weight).copy_(wtmp[:NO])
         btmp = torch.zeros(4, dtype=torch.float32, device=self.device)
-        K.bsum(K.channel_sums(g4), 0, btmp)
+        K.bsum(K.channel_sums(g4), 0, btmp, now=True)  # read by the copy below
         self._pgrad(m.conv_out.bias).copy_(btmp[:NO])
         dz = View.full(self._new(B, S, S2, C))
         self._conv([Seg(View.full(g32), TAPS3)], self.head_T, None, dz, S, S2)

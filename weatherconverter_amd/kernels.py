@@ -9,7 +9,7 @@ import ctypes
 import functools
 import os
 from dataclasses import dataclass
-from typing import NamedTuple, Optional, Sequence, Tuple
+from typing import Dict, List, NamedTuple, Optional, Sequence, Tuple
 
 import torch
 
@@ -1331,11 +1331,53 @@ def channel_sums(g: View) -> torch.Tensor:
     return sums
 
 
-def bsum(sums: torch.Tensor, idx: int, out: torch.Tensor, accumulate: bool = False):
-    """out[c] (+)= sum_b sums[b][c][idx] (fixed order)."""
+_BSUM_QUEUE: Optional[list] = None
+
+
+def bsum(sums: torch.Tensor, idx: int, out: torch.Tensor, accumulate: bool = False, now: bool = False):
+    """out[c] (+)= sum_b sums[b][c][idx] (fixed order).  Between bsum_defer() and bsum_flush() the sum is
+    queued and all queued sums go out in one launch (wc_bsum_batch) at the flush, each output's in
+    queue order (the same values as one launch each); now=True launches at once regardless (an output
+    the caller reads before the flush)."""
     B, C, _ = sums.shape
     _req(out.is_cuda and out.is_contiguous() and out.numel() == C, 'bsum output')
+    if _BSUM_QUEUE is not None and not now:
+        _req(not _BSUM_QUEUE or _BSUM_QUEUE[0][0].shape[0] == B, 'deferred bsums of one batch size')
+        _BSUM_QUEUE.append((sums, idx, out, accumulate))
+        return
     _native.call('wc_bsum', sums.data_ptr(), B, C, idx, out.data_ptr(), int(accumulate), _stream())
+
+
+def bsum_defer():
+    """Queue every bsum until bsum_flush() (the training backward: ~200 small sums -> one launch)."""
+    global _BSUM_QUEUE
+    _req(_BSUM_QUEUE is None, 'bsum_defer: already deferring')
+    _BSUM_QUEUE = []
+
+
+def bsum_flush():
+    """Launch the queued bsums (wc_bsum_batch): an output's k-th queued sum goes in launch k, so every
+    output accumulates in queue order; ends the deferral."""
+    global _BSUM_QUEUE
+    q, _BSUM_QUEUE = _BSUM_QUEUE, None
+    if not q:
+        return
+    launches: List[list] = []
+    seen: Dict[int, int] = {}
+    for sums, idx, out, acc in q:
+        k = seen.get(out.data_ptr(), -1) + 1
+        seen[out.data_ptr()] = k
+        if k == len(launches):
+            launches.append([])
+        launches[k].append((sums, idx, out, acc))
+    B = q[0][0].shape[0]
+    s = _stream()
+    for jobs in launches:
+        tab = torch.empty((len(jobs), 4), dtype=torch.int64, pin_memory=True)
+        rows = [[sm.data_ptr(), o.data_ptr(), sm.shape[1] | (idx << 32), int(acc)] for sm, idx, o, acc in jobs]
+        tab.copy_(torch.tensor(rows, dtype=torch.int64))
+        dtab = tab.to(q[0][2].device, non_blocking=True)
+        _native.call('wc_bsum_batch', dtab.data_ptr(), len(jobs), B, max(sm.shape[1] for sm, _, _, _ in jobs), s)
 
 
 def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,

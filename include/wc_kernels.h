@@ -492,6 +492,10 @@ int wc_wgrad_reduce(float* part, int splits, int M, int Kc, int K0, int C0, int 
  *         x == NULL: plain per-(b, c) sums of dz (bias / time-embedding gradients).
  * finalize: sums[B][C][2] in a fixed order; with coef: coef[B][C][4] = (rstd*gamma, -rstd*A/n,
  *         -rstd*Bs/n, 0), A / Bs the group sums of gamma*sum dy / gamma*sum dy*xhat.
+ *         part3 (optional, x != NULL, [B][splits][C]): the splits' sums of xhat; given to the finalize
+ *         with dsum [B][C][2] (and coef), dsum[b][c][0] = the image's sum over pixels of the value the
+ *         apply writes (accumulate off), c0*sum dy + HW*c1 + c2*sum xhat, second entry 0: the next
+ *         layer's bias / time-embedding gradient without a pass over dx.
  * bsum: out[c] (+)= sum_b sums[b][c][idx]  (idx 0: dbeta / bias grad, 1: dgamma).
  * apply: dx (+)= coef0*dy + coef1 + coef2*xhat.  C % 4 == 0, 16-byte aligned views.  absmax (optional,
  *         [B], caller-zeroed or carried over): raised to the max |dx| written per image, so that over
@@ -499,9 +503,10 @@ int wc_wgrad_reduce(float* part, int splits, int M, int Kc, int K0, int C0, int 
 int wc_gn_bwd_splits(int B, int HW);
 int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
                      const float* gamma, const float* beta, int silu, int B, int HW, int C, int splits,
-                     float* part, void* stream);
+                     float* part, float* part3, void* stream);
 int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, int HW, const float* sc0,
-                       const float* gamma, float* sums, float* coef, void* stream);
+                       const float* gamma, float* sums, float* coef, const float* part3, float* dsum,
+                       void* stream);
 int wc_bsum(const float* sums, int B, int C, int idx, float* out, int accumulate, void* stream);
 /* Many wc_bsum in one launch (the training backward's deferred dgamma / dbeta / bias sums): jobs is a
  * DEVICE array of njobs descriptors, max_c >= every job's C; no two jobs of one launch share an output. */

@@ -257,6 +257,39 @@ def test_groupnorm_backward(silu, C):
     assert rel_l2(dg.cpu(), gd.grad) < 1e-5 and rel_l2(db.cpu(), bd.grad) < 1e-5
 
 
+@pytest.mark.parametrize('silu,C,H,W', [(True, 128, 32, 32), (True, 768, 8, 8), (False, 64, 16, 24)])
+def test_groupnorm_backward_closed_form_dx_sums(silu, C, H, W):
+    """gn_backward(dx_sums=True): the per-(image, channel) sums of the dx it writes, from the reduce's
+    sums in closed form (c0 sum dy + HW c1 + c2 sum xhat), against float64 autograd's dx summed over the
+    pixels, within 1e-5 (rel-L2 over [B][C]) -- as close as a channel_sums pass over the written dx."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.kernels import View
+    g = _gen(9)
+    B = 3
+    x = torch.randn((B, H, W, C), generator=g) * 2 + 0.5
+    x[:, :, :, ::7] += 3.0  # channels whose mean is far from their group's
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.2
+    dz = torch.randn((B, H, W, C), generator=g)
+    xc = View.full(x.cuda())
+    sc, sh, a0, o0 = K.gn_stats_pair(xc, gamma.cuda(), beta.cuda())
+    dx = torch.empty((B, H, W, C), device='cuda')
+    dsum = K.gn_backward(View.full(dz.cuda()), xc, a0, o0, gamma.cuda(), beta.cuda(), silu, View.full(dx),
+                         accumulate=False, dx_sums=True)
+    direct = K.channel_sums(View.full(dx))
+    xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    y = F.group_norm(xd, 8, gamma.double(), beta.double(), 1e-5)
+    y = F.silu(y) if silu else y
+    y.backward(dz.double().permute(0, 3, 1, 2))
+    ref = xd.grad.sum((2, 3))
+    assert dsum.shape == (B, C, 2) and bool((dsum[..., 1] == 0).all())
+    e_closed, e_direct = rel_l2(dsum[..., 0].cpu(), ref), rel_l2(direct[..., 0].cpu(), ref)
+    assert e_closed < 1e-5, (e_closed, e_direct)
+    with pytest.raises(Exception):
+        K.gn_backward(View.full(dz.cuda()), xc, a0, o0, gamma.cuda(), beta.cuda(), silu, View.full(dx),
+                      accumulate=True, dx_sums=True)
+
+
 @pytest.mark.parametrize('C', [4, 96, 200, 768])
 def test_channel_sums_and_deferred_bsum(C):
     """channel_sums (the finalize's 64-channel blocks, ragged last block) vs float64, and the deferred

@@ -132,8 +132,8 @@ _SIGS = {
     'wc_pack_split': [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _P],
     'wc_wgrad_reduce': [_P, _I, _I, _I, _I, _I, _I, _P, _L, _L, _L, _P, _L, _I, _P],
     'wc_gn_bwd_splits': [_I, _I],
-    'wc_gn_bwd_reduce': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P],
-    'wc_gn_bwd_finalize': [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    'wc_gn_bwd_reduce': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
+    'wc_gn_bwd_finalize': [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     'wc_bsum': [_P, _I, _I, _I, _P, _I, _P],
     'wc_bsum_batch': [_P, _I, _I, _I, _P],
     'wc_gn_bwd_apply': [_P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P],

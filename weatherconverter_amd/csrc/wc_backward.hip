@@ -496,8 +496,9 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_reduce_kernel(const float* __r
                                                                  const float* __restrict__ sh0,
                                                                  const float* __restrict__ gamma,
                                                                  const float* __restrict__ beta, int HW, int C,
-                                                                 int splits, int pps, int nq, float* __restrict__ part) {
-    __shared__ f32x4 red[2][GB_THREADS];
+                                                                 int splits, int pps, int nq, float* __restrict__ part,
+                                                                 float* __restrict__ part3) {
+    __shared__ f32x4 red[3][GB_THREADS];
     const int ncb = C / 4 / nq;
     int t = blockIdx.x;
     const int cb = t % ncb;
@@ -510,7 +511,7 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_reduce_kernel(const float* __r
     const int c = (cb * nq + q) * 4;
     const int p0 = sp * pps;
     const int p1 = min(HW, p0 + pps);
-    f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
     f32x4 a = s1, o = s1, g = f32x4{1.f, 1.f, 1.f, 1.f}, be = s1;
     if constexpr (HAS_X) {
         a = *reinterpret_cast<const f32x4*>(sc0 + (long)b * C + c);
@@ -528,20 +529,24 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_reduce_kernel(const float* __r
                 d.x *= silu_grad(y.x); d.y *= silu_grad(y.y); d.z *= silu_grad(y.z); d.w *= silu_grad(y.w);
             }
             s2 += d * xh;
+            s3 += xh;
         }
         s1 += d;
     }
     red[0][threadIdx.x] = s1;
     red[1][threadIdx.x] = s2;
+    red[2][threadIdx.x] = s3;
     __syncthreads();
     if (r == 0) {
         for (int k = 1; k < R; ++k) {
             s1 += red[0][k * nq + q];
             s2 += red[1][k * nq + q];
+            s3 += red[2][k * nq + q];
         }
         float* dst = part + (((long)b * splits + sp) * C + c) * 2;
         *reinterpret_cast<f32x4*>(dst) = f32x4{s1.x, s2.x, s1.y, s2.y};
         *reinterpret_cast<f32x4*>(dst + 4) = f32x4{s1.z, s2.z, s1.w, s2.w};
+        if (HAS_X && part3) *reinterpret_cast<f32x4*>(part3 + ((long)b * splits + sp) * C + c) = s3;
     }
 }
 
@@ -555,15 +560,18 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_reduce_kernel(const float* __r
 __global__ __launch_bounds__(GB_THREADS) void gnb_finalize_kernel(const float* __restrict__ part, int splits, int C,
                                                                    int cw, int HW, const float* __restrict__ sc0,
                                                                    const float* __restrict__ gamma,
-                                                                   float* __restrict__ sums, float* __restrict__ coef) {
-    __shared__ float red[2][GB_THREADS];
+                                                                   float* __restrict__ sums, float* __restrict__ coef,
+                                                                   const float* __restrict__ part3,
+                                                                   float* __restrict__ dsum) {
+    __shared__ float red[3][GB_THREADS];
     __shared__ float gs[2];
     const int b = blockIdx.x;
     const int nsl = GB_THREADS / cw;
     const int ch = threadIdx.x % cw, sl = threadIdx.x / cw;
     const int c = blockIdx.y * cw + ch;
     const bool act = sl < nsl && c < C;
-    float s1 = 0.f, s2 = 0.f;
+    const bool want3 = part3 && dsum && coef;
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (act) {
         const wcx6::f32x2* pp = reinterpret_cast<const wcx6::f32x2*>(part + ((long)b * splits * C + c) * 2);
 #pragma unroll 4
@@ -572,9 +580,15 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_finalize_kernel(const float* _
             s1 += v.x;
             s2 += v.y;
         }
+        if (want3) {
+            const float* p3 = part3 + (long)b * splits * C + c;
+#pragma unroll 4
+            for (int sp = sl; sp < splits; sp += nsl) s3 += p3[(long)sp * C];
+        }
     }
     red[0][threadIdx.x] = s1;
     red[1][threadIdx.x] = s2;
+    red[2][threadIdx.x] = s3;
     __syncthreads();
     const bool lead = sl == 0 && c < C;
     float ga = 1.f;
@@ -582,6 +596,7 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_finalize_kernel(const float* _
         for (int k = 1; k < nsl; ++k) {
             s1 += red[0][k * cw + ch];
             s2 += red[1][k * cw + ch];
+            s3 += red[2][k * cw + ch];
         }
         sums[((long)b * C + c) * 2] = s1;
         sums[((long)b * C + c) * 2 + 1] = s2;
@@ -614,8 +629,13 @@ __global__ __launch_bounds__(GB_THREADS) void gnb_finalize_kernel(const float* _
     if (lead) {
         const float inv_n = 1.0f / ((float)cw * (float)HW);
         const float rstd = sc0[(long)b * C + c];
-        *reinterpret_cast<f32x4*>(coef + ((long)b * C + c) * 4) =
-            f32x4{rstd * ga, -rstd * gs[0] * inv_n, -rstd * gs[1] * inv_n, 0.f};
+        const f32x4 cf = f32x4{rstd * ga, -rstd * gs[0] * inv_n, -rstd * gs[1] * inv_n, 0.f};
+        *reinterpret_cast<f32x4*>(coef + ((long)b * C + c) * 4) = cf;
+        // sum over the image's pixels of dx = c0 dy + c1 + c2 xhat, in closed form from the same sums
+        if (want3) {
+            dsum[((long)b * C + c) * 2] = cf.x * s1 + (float)HW * cf.y + cf.z * s3;
+            dsum[((long)b * C + c) * 2 + 1] = 0.f;
+        }
     }
 }
 
@@ -1003,8 +1023,8 @@ extern "C" int wc_gn_bwd_splits(int B, int HW) {
 
 extern "C" int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ldx, const float* sc0, const float* sh0,
                                 const float* gamma, const float* beta, int silu, int B, int HW, int C, int splits,
-                                float* part, void* stream) {
-    if (!dz || !part || (x && (!sc0 || !sh0))) return WC_E_ARG;
+                                float* part, float* part3, void* stream) {
+    if (!dz || !part || (x && (!sc0 || !sh0)) || (part3 && !x)) return WC_E_ARG;
     const int nq = gnb_nq(C);
     if (nq < 0 || ldz % 4 || (x && ldx % 4) || splits < 1 || B < 1 || HW < 1) return WC_E_SHAPE;
     const int pps = (HW + splits - 1) / splits;
@@ -1012,25 +1032,27 @@ extern "C" int wc_gn_bwd_reduce(const float* dz, int ldz, const float* x, int ld
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!x)
         hipLaunchKernelGGL((gnb_reduce_kernel<false, false>), dim3((unsigned)grid), dim3(GB_THREADS), 0, s, dz, ldz, x,
-                           ldx, sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part);
+                           ldx, sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part, part3);
     else if (silu)
         hipLaunchKernelGGL((gnb_reduce_kernel<true, true>), dim3((unsigned)grid), dim3(GB_THREADS), 0, s, dz, ldz, x, ldx,
-                           sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part);
+                           sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part, part3);
     else
         hipLaunchKernelGGL((gnb_reduce_kernel<true, false>), dim3((unsigned)grid), dim3(GB_THREADS), 0, s, dz, ldz, x,
-                           ldx, sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part);
+                           ldx, sc0, sh0, gamma, beta, HW, C, splits, pps, nq, part, part3);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
 
 extern "C" int wc_gn_bwd_finalize(const float* part, int B, int splits, int C, int groups, int HW, const float* sc0,
-                                  const float* gamma, float* sums, float* coef, void* stream) {
-    if (!part || !sums || (coef && !sc0)) return WC_E_ARG;
+                                  const float* gamma, float* sums, float* coef, const float* part3, float* dsum,
+                                  void* stream) {
+    if (!part || !sums || (coef && !sc0) || ((part3 != nullptr) != (dsum != nullptr)) || (dsum && !coef))
+        return WC_E_ARG;
     if (C < 1 || B < 1 || splits < 1 || (coef && (groups < 1 || C % groups))) return WC_E_SHAPE;
     const int cw = coef ? C / groups : (C < 64 ? C : 64);
     if (cw > GB_THREADS) return WC_E_SHAPE;
     hipLaunchKernelGGL(gnb_finalize_kernel, dim3(B, (C + cw - 1) / cw), dim3(GB_THREADS), 0,
-                       reinterpret_cast<hipStream_t>(stream), part, splits, C, cw, HW, sc0, gamma, sums, coef);
+                       reinterpret_cast<hipStream_t>(stream), part, splits, C, cw, HW, sc0, gamma, sums, coef, part3, dsum);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -159,7 +159,12 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
             if constexpr (PRO != 0) {
                 v = v * rsc + rsh;
                 if constexpr (PRO == 2) {
-                    v.x = wc_silu(v.x); v.y = wc_silu(v.y); v.z = wc_silu(v.z); v.w = wc_silu(v.w);
+                    if constexpr (F3) {  // v_rcp instead of an IEEE division (~10 VALU ops a value):
+                        // ~1 ulp of fp32, far below the two fp16 pieces' 22 bits
+                        v.x = silu_fast(v.x); v.y = silu_fast(v.y); v.z = silu_fast(v.z); v.w = silu_fast(v.w);
+                    } else {
+                        v.x = wc_silu(v.x); v.y = wc_silu(v.y); v.z = wc_silu(v.z); v.w = wc_silu(v.w);
+                    }
                 }
             }
             if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // zero padding after the prologue
@@ -239,9 +244,12 @@ __global__ __launch_bounds__(W3_NT, 2) void conv_wgrad3_kernel(W3Dev p) {
                 }
                 if (r + 1 < TH) load_g(k, r + 1);
                 else load_g(k + 1, 0);
-                // the next block's halo goes out one K-step before the block's last (after that
-                // step's G loads: loads complete in issue order, so it is never waited for early)
-                if (r == TH - 2 || TH == 1) load_halo(k + 1);
+                // the next block's halo goes out in the block's first K-step (after that step's G
+                // loads), TH - 1 K-steps before write_halo needs it: its registers are live through
+                // the block's last K-step anyway, so the peak register count is unchanged, and the
+                // HBM latency of a first-touch halo is covered (with the fast SiLU below: 2.5-4 % on
+                // the ResBlock shapes, profiles/r04_wgrad3_ab.txt)
+                if (r == 0) load_halo(k + 1);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap) {

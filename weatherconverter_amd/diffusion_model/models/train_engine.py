@@ -708,9 +708,14 @@ class TrainEngine:
         g2 = rp['gn2']
         dh = View.full(self._new(B, H, W, co))
         bdh = self._zrow(B) if self.f3d else None
-        K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
-                      dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh)
-        sums = self._bias_grad(dh, rp['conv1'].bias)
+        # dh's per-(image, channel) sums (conv1's bias / time-embedding gradients) in closed form from the
+        # GN backward's own sums (WC_TRAIN_DH_SUMS=0: a channel_sums pass over dh)
+        sums = K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
+                             dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh,
+                             dx_sums=os.environ.get('WC_TRAIN_DH_SUMS', '1') != '0')
+        if sums is None:
+            sums = K.channel_sums(dh)
+        K.bsum(sums, 0, self._pgrad(rp['conv1'].bias), accumulate=True)
         self.dproj[:, rp['off']:rp['off'] + co].copy_(sums[:, :, 0])
         f3h = rp.has('f3_1T') and self._dgrad3_ok(dh, ci)
         bh = self._bound(dh, bdh) if f3h else None

@@ -1326,8 +1326,9 @@ def channel_sums(g: View) -> torch.Tensor:
     sums = torch.empty((B, C, 2), dtype=torch.float32, device=g.t.device)
     s = _stream()
     _native.call('wc_gn_bwd_reduce', g.ptr, g.ldc, None, 0, None, None, None, None, 0, B, HW, C, splits,
-                 part.data_ptr(), s)
-    _native.call('wc_gn_bwd_finalize', part.data_ptr(), B, splits, C, 0, HW, None, None, sums.data_ptr(), None, s)
+                 part.data_ptr(), None, s)
+    _native.call('wc_gn_bwd_finalize', part.data_ptr(), B, splits, C, 0, HW, None, None, sums.data_ptr(), None, None,
+                 None, s)
     return sums
 
 
@@ -1382,25 +1383,31 @@ def bsum_flush():
 
 def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
                 silu: bool, dx: View, *, dgamma: Optional[torch.Tensor] = None, dbeta: Optional[torch.Tensor] = None,
-                accumulate: bool = True, groups: int = 8, absmax: Optional[torch.Tensor] = None):
+                accumulate: bool = True, groups: int = 8, absmax: Optional[torch.Tensor] = None,
+                dx_sums: bool = False) -> Optional[torch.Tensor]:
     """Backward of SiLU(GroupNorm(x)) (silu) or GroupNorm(x): dx (+)= d/dx given dz = d/d output;
     dgamma / dbeta (+)= their gradients.  absmax: optional float32[B] raised to the max |dx| written
-    per image."""
+    per image.  dx_sums (accumulate off): also return float32 [B][C][2] whose [..., 0] is each image's
+    per-channel sum of dx (channel_sums(dx)'s layout, from the reduce's sums in closed form instead of
+    a pass over dx)."""
     for v in (dz, x, dx):
         v.check()
     B, HW, C = x.B, x.H * x.W, x.C
     _req(dz.C == C and dx.C == C and dz.B == B and dx.B == B, 'GN backward view shapes')
+    _req(not (dx_sums and accumulate), 'dx_sums needs accumulate=False (the sums are of the written values)')
     lib = _native.load()
     splits = lib.wc_gn_bwd_splits(B, HW)
     dev = x.t.device
     part = torch.empty(B * splits * C * 2, dtype=torch.float32, device=dev)
+    part3 = torch.empty(B * splits * C, dtype=torch.float32, device=dev) if dx_sums else None
+    dsum = torch.empty((B, C, 2), dtype=torch.float32, device=dev) if dx_sums else None
     sums = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
     coef = torch.empty((B, C, 4), dtype=torch.float32, device=dev)
     s = _stream()
     _timed('gnb_reduce_kernel', 'wc_gn_bwd_reduce', 8.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc, sc0.data_ptr(),
-           sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), B, HW, C, splits, part.data_ptr(), s)
+           sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), B, HW, C, splits, part.data_ptr(), _ptr(part3), s)
     _native.call('wc_gn_bwd_finalize', part.data_ptr(), B, splits, C, groups, HW, sc0.data_ptr(), _ptr(gamma),
-                 sums.data_ptr(), coef.data_ptr(), s)
+                 sums.data_ptr(), coef.data_ptr(), _ptr(part3), _ptr(dsum), s)
     if dbeta is not None:
         bsum(sums, 0, dbeta, accumulate=True)
     if dgamma is not None:
@@ -1408,6 +1415,7 @@ def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: 
     _timed('gnb_apply_kernel', 'wc_gn_bwd_apply', 16.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc, sc0.data_ptr(),
            sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), coef.data_ptr(), B, HW, C, dx.ptr, dx.ldc,
            int(accumulate), _ptr(absmax), s)
+    return dsum
 
 
 def attention_fwd_lse(qkv: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, B: int, N: int, C: int, heads: int,

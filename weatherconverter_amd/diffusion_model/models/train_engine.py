@@ -330,18 +330,40 @@ class TrainEngine:
         self._zi += 1
         return pool[self._zi - 1]
 
-    def _grad(self, v: View) -> View:
-        """The gradient view of a forward view (zero-initialised tensors, allocated on first use)."""
+    def _gview(self, v: View) -> View:
+        """The gradient view of a forward view, allocated on first use but NOT yet zeroed: a gradient
+        tensor stays unwritten ('fresh') until its first writer overwrites it whole (_grad_w) or
+        something reads or accumulates into it (_grad zeroes it then)."""
         key = id(v.t)
         if key not in self.gmap:
-            self.gmap[key] = (torch.zeros_like(v.t), 0)
+            self.gmap[key] = (torch.empty_like(v.t), 0)
+            self.gfresh.add(id(self.gmap[key][0]))
         g, off = self.gmap[key]
         return View(g, v.c0 + off, v.C)
+
+    def _grad(self, v: View) -> View:
+        """The gradient view of a forward view, zero-initialised if nothing has written it yet."""
+        gv = self._gview(v)
+        if id(gv.t) in self.gfresh:
+            self.gfresh.discard(id(gv.t))
+            gv.t.zero_()
+        return gv
+
+    def _grad_w(self, v: View) -> Tuple[View, bool]:
+        """(gradient view, overwrite) for a writer that adds into it (a conv's res=, an accumulating GN
+        backward): overwrite=True when the tensor is still unwritten and the view covers it whole, so the
+        writer stores its values instead of adding them to a zero fill (no fill, no read of zeros)."""
+        gv = self._gview(v)
+        if id(gv.t) in self.gfresh and gv.c0 == 0 and gv.C == gv.t.shape[-1] \
+                and os.environ.get('WC_TRAIN_LAZY_GRAD', '1') != '0':
+            self.gfresh.discard(id(gv.t))
+            return gv, True
+        return self._grad(v), False
 
     def _alias_grad(self, t: torch.Tensor, v: View):
         """The full tensor t's gradient IS the gradient of view v (t feeds v through an identity path
         and everything else adds into it afterwards in backward order)."""
-        g = self._grad(v)
+        g = self._gview(v)
         self.gmap[id(t)] = (g.t, g.c0)
         self.keep.append(t)
 
@@ -351,7 +373,7 @@ class TrainEngine:
         final values), zero while nothing has; None outside the f16x3 backward."""
         if not self.f3d:
             return None
-        g = self._grad(v)
+        g = self._gview(v)
         t = self.gbnd.get(id(g.t))
         if t is None:
             t = self._zrow(v.B)
@@ -613,6 +635,7 @@ class TrainEngine:
             self.last_tape = None
         m = self.model
         self.gmap: Dict[int, Tuple[torch.Tensor, int]] = {}
+        self.gfresh = set()  # gradient tensors allocated but not yet written (_gview)
         self.gbnd: Dict[int, torch.Tensor] = {}
         self.pgrads: Dict[int, torch.Tensor] = {}
         self.pflat_off: Dict[int, Tuple[int, int]] = {}
@@ -634,6 +657,7 @@ class TrainEngine:
         finally:
             K.bsum_flush()
         self.gmap = {}
+        self.gfresh = set()
         self.gbnd = {}
         self.keep = []
         for f in Tape._FIELDS[1:]:  # the tape's tensors die with it, not with the engine
@@ -674,15 +698,17 @@ class TrainEngine:
         dz = View.full(self._new(B, S, S2, C))
         self._conv([Seg(View.full(g32), TAPS3)], self.head_T, None, dz, S, S2)
         gn = m.norm_out
-        K.gn_backward(dz, cur, a0, o0, gn.weight.detach().float(), gn.bias.detach().float(), True, self._grad(cur),
-                      dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), absmax=self._gb(cur))
+        gcur, ow = self._grad_w(cur)
+        K.gn_backward(dz, cur, a0, o0, gn.weight.detach().float(), gn.bias.detach().float(), True, gcur,
+                      dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), accumulate=not ow,
+                      absmax=self._gb(cur))
 
     def _bwd_res(self, rec, gout):
         _, X, h, Y, rp, st1, st2, bXf = rec  # bXf: GN1's per-image bound of |X| (the forward's)
         B, H, W = X.B, X.H, X.W
         ci, co = rp['ci'], rp['co']
         gY = self._grad(Y)
-        gX = self._grad(X)
+        gX = self._gview(X)  # written first by the residual conv's data gradient below
         self._bias_grad(gY, rp['conv2'].bias, rp['resc'].bias)
         # per-image max |gY|: the range bound of the f16x3 data gradients and weight gradient
         f3Y = rp.has('f3_2T') and self._dgrad3_ok(gY, co)
@@ -697,14 +723,17 @@ class TrainEngine:
                 K.conv3x3_wino([Seg(gY, TAPS3)], rp['wn_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
             else:
                 K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
+            gX, ow = self._grad_w(X)
+            rX = None if ow else gX
             if (H * W) % (256 if ci <= 64 else 128) == 0 and co % 16 == 0:  # one-image M tiles (per-image bound)
-                K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=gX,
+                K.conv_igemm_f16x3([Seg(gY, TAPS1)], rp['f3_rT'], None, gX, Hm=H, Wm=W, a_exp=60, a_bound=bY, res=rX,
                                    absmax=bX)
             else:
-                self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX, absmax=bX)
+                self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=rX, absmax=bX)
         else:
             self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
-            self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=gX, absmax=bX)
+            gX, ow = self._grad_w(X)
+            self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=None if ow else gX, absmax=bX)
         g2 = rp['gn2']
         dh = View.full(self._new(B, H, W, co))
         bdh = self._zrow(B) if self.f3d else None
@@ -788,23 +817,23 @@ class TrainEngine:
     def _bwd_down(self, rec, gout):
         _, cur, final, dp, bcur = rec  # bcur: the forward's per-image max |cur|
         gF = self._grad(final)
-        gc = self._grad(cur)
         w = dp['mod'].weight
         self._bias_grad(gF, dp['mod'].bias)
         bgF = self._bound(gF, self._gb(final)) if self.f3d else None
         self._wgrad(gF, [Seg(cur, TAPS4S2, stride=2)], self._pgrad(w), (w.shape[1] * 16, 16, 1),
                     f3=K.F3Bounds(bgF, 60, bcur) if bgF is not None and bcur is not None else None)
+        gc, ow = self._grad_w(cur)  # the four output parities together cover every pixel
+        rc = None if ow else gc
         if dp['f3T'] is not None and K.convT4x4s2_f16x3_ok(Seg(gF, [(0, 0)]), gc.C) and gF.ptr % 16 == 0:
             # the ConvT of dY (same weight) in one launch on f16x3 under dY's tracked bound
-            K.convT4x4s2_f16x3(Seg(gF, [(0, 0)]), dp['f3T'], None, gc, a_bound=bgF, res=gc, absmax=self._gb(cur))
+            K.convT4x4s2_f16x3(Seg(gF, [(0, 0)]), dp['f3T'], None, gc, a_bound=bgF, res=rc, absmax=self._gb(cur))
             return
         for (py, px), (taps, pk) in zip(_PARITIES, dp['dT']):
-            self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=gc, absmax=self._gb(cur))
+            self._conv([Seg(gF, taps)], pk, None, gc, gF.H, gF.W, out_map=(2, 2, py, px), res=rc, absmax=self._gb(cur))
 
     def _bwd_up(self, rec, gout):
         _, cur, dst, up, bcur = rec
         gD = self._grad(dst)
-        gc = self._grad(cur)
         wt = up['mod'].weight  # [Cin][Cout][4][4]
         self._bias_grad(gD, up['mod'].bias)
         # dW[ci][co][ky][kx] = sum_pixels x[ci] * dY[co] at (2y - 1 + ky, 2x - 1 + kx): the 4x4/s2 tap
@@ -813,11 +842,13 @@ class TrainEngine:
         self._wgrad(cur, [Seg(gD, TAPS4S2, stride=2)], self._pgrad(wt), (wt.shape[1] * 16, 16, 1),
                     f3=K.F3Bounds(bcur, 60, bgD) if bgD is not None and bcur is not None else None)
         seg = Seg(gD, TAPS4S2, stride=2)
+        gc, ow = self._grad_w(cur)
+        rc = None if ow else gc
         if up['f3T'] is not None and K.conv4x4s2_f16x3_ok(seg, gc.C, cur.H, cur.W) and gD.ptr % 16 == 0:
             # the 4x4/s2 conv of dY on the space-to-depth halo kernel, f16x3 under dY's tracked bound
-            K.conv4x4s2_f16x3(seg, up['f3T'], None, gc, Hm=cur.H, Wm=cur.W, a_bound=bgD, res=gc, absmax=self._gb(cur))
+            K.conv4x4s2_f16x3(seg, up['f3T'], None, gc, Hm=cur.H, Wm=cur.W, a_bound=bgD, res=rc, absmax=self._gb(cur))
             return
-        self._conv([seg], up['dT'], None, gc, cur.H, cur.W, res=gc, absmax=self._gb(cur))
+        self._conv([seg], up['dT'], None, gc, cur.H, cur.W, res=rc, absmax=self._gb(cur))
 
     def _bwd_conv_in(self, rec, gout):
         m = self.model

@@ -164,6 +164,12 @@ int wc_conv3x3_wino_set_onewave(int mode);
  * pieces (bit-identical to kernels.pack_wino's definition).  out_bytes must equal the layout size. */
 int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_bytes, float* w_inv_scale,
                  void* stream);
+/* wc_pack_wino from the module's own [Co][Ci][3][3] fp32 weight (no host re-layout; bit-identical to
+ * wc_pack_wino of engine.pack_conv's layout): transposed = 0, the conv (N = Co, C0 = Ci) with the optional
+ * 1x1 residual wres [N][C1]; transposed = 1, its data gradient (N = Ci, C0 = Co: the flipped transposed
+ * filter), C1 = 0.  9 * C0 * 4 <= 64 KiB. */
+int wc_pack_wino_raw(const float* w, const float* wres, int N, int C0, int C1, int transposed, void* out,
+                     int64_t out_bytes, float* w_inv_scale, void* stream);
 
 /* General implicit-GEMM conv at the same bf16x6 arithmetic: exactly wc_conv_igemm's contract
  * (tap grids, input strides, the 1x1 residual segment, output maps, NCHW store; an activation

@@ -345,6 +345,26 @@ def test_attention_backward(C, heads, N):
     assert rel_l2(dqkv.cpu(), q_.grad.reshape(B * N, 3 * C)) < 1e-5
 
 
+@pytest.mark.parametrize('Co,Ci,res', [(128, 64, True), (256, 256, False), (64, 768, True), (48, 32, False)])
+def test_pack_wino_raw_bit_identical_to_relayout(Co, Ci, res):
+    """wc_pack_wino_raw from the module's [Co][Ci][3][3] weight (conv + residual, and the data gradient's
+    flipped transposed filter) equals wc_pack_wino of the host re-layouts the engine used to build, bit
+    for bit (pieces and scales)."""
+    from weatherconverter_amd import kernels as K
+    from weatherconverter_amd.diffusion_model.models.engine import pack_conv
+    g = _gen(12)
+    w = (torch.randn((Co, Ci, 3, 3), generator=g) * torch.rand((Co, 1, 1, 1), generator=g) * 3).cuda()
+    wr = torch.randn((Co, Ci), generator=g).cuda() if res else None
+    a = K.pack_wino_raw(w, wr)
+    ref = K.pack_wino(torch.cat([pack_conv(w), wr], 1).contiguous() if res else pack_conv(w), Ci, Ci if res else 0,
+                      device=True)
+    assert torch.equal(a.data, ref.data) and torch.equal(a.wsinv, ref.wsinv) and (a.N, a.C0, a.C1) == (ref.N, ref.C0, ref.C1)
+    if Co % 16 == 0:
+        at = K.pack_wino_raw(w, transposed=True)
+        reft = K.pack_wino(pack_conv(w.flip([2, 3]).transpose(0, 1)), Co, device=True)
+        assert torch.equal(at.data, reft.data) and torch.equal(at.wsinv, reft.wsinv) and at.N == Ci
+
+
 @pytest.mark.parametrize('precision', ['f16x3', 'bf16x6'])
 @pytest.mark.parametrize('C,heads,N', [(128, 4, 256), (512, 4, 160), (768, 4, 64), (256, 4, 33), (128, 2, 1000)])
 def test_split_attention_lse_matches_float64(precision, C, heads, N):

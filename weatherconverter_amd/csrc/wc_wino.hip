@@ -663,11 +663,10 @@ __device__ double wino_u(const float* row, int C0, int ky, int pos, int c) {
     }
 }
 
-__global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict__ w, int K, int N, int C0, int C1,
-                                                        int BN, short* __restrict__ out, float* __restrict__ wsinv) {
-    const int n = blockIdx.x;
-    const bool live = n < N;
-    const float* row = w + (long)(live ? n : 0) * K;
+// The row of output channel n: the 3x3 values at row3[(ky * 3 + kx) * C0 + c], the residual ones (C1)
+// at rres[j]; live = n < N (padding rows are zeros).
+__device__ void pack_wino_row(const float* row3, const float* rres, bool live, int n, int C0, int C1, int BN,
+                              short* __restrict__ out, float* __restrict__ wsinv) {
     const int n0 = 12 * C0, nall = n0 + C1;
     double m = 0.0;
     if (live) {
@@ -675,9 +674,9 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
             double v;
             if (i < n0) {
                 const int c = i % C0, kp = i / C0;
-                v = wino_u(row, C0, kp / 4, kp % 4, c);
+                v = wino_u(row3, C0, kp / 4, kp % 4, c);
             } else {
-                v = row[9 * C0 + (i - n0)];
+                v = rres[i - n0];
             }
             m = fmax(m, fabs(v));
         }
@@ -708,13 +707,13 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
         int plane;  // distance between the two pieces (int16 units)
         if (i < n0) {
             const int c = i % C0, kp = i / C0, ky = kp / 4, pos = kp % 4;
-            if (live) v = wino_u(row, C0, ky, pos, c);
+            if (live) v = wino_u(row3, C0, ky, pos, c);
             const int chunk = c / 16, kh = (c % 16) / 8, e = c % 8;
             o = ((((long)(chunk * 3 + ky) * 4 + pos) * 2 * 2 + kh) * BN + nn) * 8 + e;  // piece 0
             plane = 2 * BN * 8;
         } else {
             const int c = i - n0;
-            if (live) v = row[9 * C0 + c];
+            if (live) v = rres[c];
             const int chunk = c / 16, kh = (c % 16) / 8, e = c % 8;
             o = (long)(C0 / 16) * 12 * 2 * 2 * BN * 8 + (((long)chunk * 2 * 2 + kh) * BN + nn) * 8 + e;
             plane = 2 * BN * 8;
@@ -730,6 +729,38 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
     }
 }
 
+__global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict__ w, int K, int N, int C0, int C1,
+                                                        int BN, short* __restrict__ out, float* __restrict__ wsinv) {
+    const int n = blockIdx.x;
+    const bool live = n < N;
+    const float* row = w + (long)(live ? n : 0) * K;
+    pack_wino_row(row, row + 9 * C0, live, n, C0, C1, BN, out, wsinv);
+}
+
+// The same from the module's own [Co][Ci][3][3] weight (no host re-layout): TRANSPOSED = false, the conv
+// itself (N = Co, C0 = Ci; value (n, tap, c) = w[n][c][tap]), the residual row n of wres [N][C1];
+// TRANSPOSED = true, its data gradient (N = Ci, C0 = Co; value (n, tap, c) = w[c][n][8 - tap], the
+// flipped, transposed filter), no residual.  The row goes through LDS in the packed order first, so the
+// values -- and the pieces -- are those of pack_wino_kernel on the host re-layout.
+template <bool TRANSPOSED>
+__global__ __launch_bounds__(256) void pack_wino_raw_kernel(const float* __restrict__ w, const float* __restrict__ wres,
+                                                            int N, int C0, int C1, int BN, short* __restrict__ out,
+                                                            float* __restrict__ wsinv) {
+    extern __shared__ float row3[];  // [9][C0]
+    const int n = blockIdx.x;
+    const bool live = n < N;
+    if (live) {
+        for (int i = threadIdx.x; i < 9 * C0; i += blockDim.x) {
+            // i walks the source in memory order: (c, tap) with the tap fastest
+            const int c = i / 9, t = i - 9 * c;
+            const float v = TRANSPOSED ? w[((long)c * N + n) * 9 + t] : w[(long)n * 9 * C0 + i];
+            row3[(TRANSPOSED ? 8 - t : t) * C0 + c] = v;
+        }
+    }
+    __syncthreads();
+    pack_wino_row(row3, wres + (long)(live ? n : 0) * C1, live, n, C0, C1, BN, out, wsinv);
+}
+
 }  // namespace
 
 extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_bytes, float* w_inv_scale,
@@ -742,6 +773,26 @@ extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, in
     hipLaunchKernelGGL(pack_wino_kernel, dim3((unsigned)(ntn * BN)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        w, 9 * C0 + C1, N, C0, C1, BN, reinterpret_cast<short*>(out), w_inv_scale);
     wc_last_kernel = "pack_wino_kernel";
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_pack_wino_raw(const float* w, const float* wres, int N, int C0, int C1, int transposed, void* out,
+                                int64_t out_bytes, float* w_inv_scale, void* stream) {
+    if (!w || !out || !w_inv_scale || (C1 && !wres) || (transposed && C1)) return WC_E_ARG;
+    if (N <= 0 || C0 <= 0 || C0 % 16 || C1 < 0 || C1 % 16 || 9L * C0 * 4 > 64 * 1024) return WC_E_SHAPE;
+    const int BN = wc_conv3x3_wino_tile_n(N);
+    const long ntn = (N + BN - 1) / BN;
+    if (out_bytes != ntn * (12L * (C0 / 16) + C1 / 16) * BN * 64) return WC_E_SHAPE;
+    const size_t lds = (size_t)9 * C0 * sizeof(float);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (transposed)
+        hipLaunchKernelGGL(pack_wino_raw_kernel<true>, dim3((unsigned)(ntn * BN)), dim3(256), lds, s, w, wres, N, C0, C1,
+                           BN, reinterpret_cast<short*>(out), w_inv_scale);
+    else
+        hipLaunchKernelGGL(pack_wino_raw_kernel<false>, dim3((unsigned)(ntn * BN)), dim3(256), lds, s, w, wres, N, C0,
+                           C1, BN, reinterpret_cast<short*>(out), w_inv_scale);
+    wc_last_kernel = "pack_wino_raw_kernel";
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -136,6 +136,8 @@ class TrainEngine:
         wr2 = wr.reshape(co, ci)
         f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
         wino = K.wino_enabled()
+        raw = all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in (w1, w2)) \
+            and 9 * max(ci, co) * 4 <= 64 * 1024 and os.environ.get('WC_PACK_RAW', '1') != '0'
         L = _Pack.lazy
         # shared re-layouts, each built once and only if a pack that needs it is (the Winograd forms
         # usually replace the direct f16x3 ones, so those are lazy too)
@@ -161,11 +163,13 @@ class TrainEngine:
             f3_rT=L(lambda: K.pack_f16x3(wr2.t().contiguous().float(), co, ntaps=1, order='natural'))
             if self.f3d else None,
             # the Winograd F(2,3)-along-x forms of the same f16x3 convs (forward and data gradients)
-            wn_1=L(lambda: K.pack_wino(rp['w1c'], ci)) if f3 and wino else None,
-            wn_2=L(lambda: K.pack_wino(rp['w2cat'], co, ci)) if f3 and wino else None,
-            wn_1T=L(lambda: K.pack_wino(rp['w1T'], co))
+            # (from the module weights directly when they are fp32 on the device: no host re-layouts)
+            wn_1=L(lambda: K.pack_wino_raw(w1) if raw else K.pack_wino(rp['w1c'], ci)) if f3 and wino else None,
+            wn_2=L(lambda: K.pack_wino_raw(w2, wr2.float().contiguous()) if raw else K.pack_wino(rp['w2cat'], co, ci))
+            if f3 and wino else None,
+            wn_1T=L(lambda: K.pack_wino_raw(w1, transposed=True) if raw else K.pack_wino(rp['w1T'], co))
             if self.f3d and wino and ci % 16 == 0 and co % 16 == 0 else None,
-            wn_2T=L(lambda: K.pack_wino(rp['w2T'], co))
+            wn_2T=L(lambda: K.pack_wino_raw(w2, transposed=True) if raw else K.pack_wino(rp['w2T'], co))
             if self.f3d and wino and co % 16 == 0 else None)
         return rp
 

@@ -531,6 +531,31 @@ def wino_filter(w: torch.Tensor, C0: int) -> torch.Tensor:
     return torch.stack([g0, (g0 + g1 + g2) * 0.5, (g0 - g1 + g2) * 0.5, g2], 2)
 
 
+def pack_wino_raw(w4: torch.Tensor, wres: Optional[torch.Tensor] = None, transposed: bool = False) -> X6Weight:
+    """pack_wino straight from a conv module's [Co][Ci][3][3] weight on the device (wc_pack_wino_raw): the
+    conv itself (+ the residual 1x1 weight wres [Co][C1]), or with transposed=True its data gradient's
+    flipped, transposed filter (N = Ci, C0 = Co) -- bit-identical to pack_wino(pack_conv(...)) of the host
+    re-layouts, without them."""
+    _req(w4.is_cuda and w4.dtype == torch.float32 and w4.is_contiguous() and w4.dim() == 4 and w4.shape[2:] == (3, 3),
+         'pack_wino_raw: contiguous fp32 [Co][Ci][3][3] device weight')
+    Co, Ci = w4.shape[:2]
+    N, C0 = (Ci, Co) if transposed else (Co, Ci)
+    C1 = 0
+    if wres is not None:
+        _req(not transposed and wres.is_cuda and wres.dtype == torch.float32 and wres.is_contiguous()
+             and wres.shape[0] == Co, 'pack_wino_raw residual: contiguous fp32 [Co][C1]')
+        C1 = wres.shape[1]
+    _req(C0 % 16 == 0 and C1 % 16 == 0, 'wino weight shape')
+    _, BN = wino_tile(N)
+    Np = -(-N // BN) * BN
+    T = Np // BN
+    data = torch.empty((T, (12 * C0 + C1) // 16 * 2 * 2 * BN * 8), dtype=torch.int16, device=w4.device)
+    wsinv = torch.empty(Np, dtype=torch.float32, device=w4.device)
+    _timed('pack_wino_raw_kernel', 'wc_pack_wino_raw', 0.0, w4.data_ptr(), _ptr(wres), N, C0, C1, int(transposed),
+           data.data_ptr(), data.numel() * 2, wsinv.data_ptr(), _stream())
+    return X6Weight(data, N, BN, C0, C1, 'wino', wsinv, bool(C1))
+
+
 def pack_wino(w: torch.Tensor, C0: int, C1: int = 0, *, device: Optional[bool] = None) -> X6Weight:
     """Pack a [N][9*C0 + C1] ResBlock conv weight (3x3 taps then the 1x1 residual columns, as
     engine.pack_conv) for wc_conv3x3_wino_f16x3: the F(2,3) filter transform in float64, a per-channel

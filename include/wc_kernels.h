@@ -170,6 +170,18 @@ int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_b
  * filter), C1 = 0.  9 * C0 * 4 <= 64 KiB. */
 int wc_pack_wino_raw(const float* w, const float* wres, int N, int C0, int C1, int transposed, void* out,
                      int64_t out_bytes, float* w_inv_scale, void* stream);
+/* Many wc_pack_wino_raw in one launch.  jobs: a DEVICE array of njobs descriptors sorted by wg0, job j
+ * covering workgroups [wg0, wg0 + its N-tile-padded N) of the total_wg; out / wsinv sized as
+ * wc_pack_wino_raw's; max_c0 >= every job's C0 (9 * max_c0 * 4 <= 64 KiB).  The caller validates shapes
+ * (kernels.pack_wino_raw_batch does, as wc_pack_wino_raw). */
+typedef struct wc_wino_pack_job {
+    const float* w;
+    const float* wres;
+    void* out;
+    float* wsinv;
+    int N, C0, C1, transposed, BN, wg0, pad0, pad1;
+} wc_wino_pack_job;
+int wc_pack_wino_batch(const wc_wino_pack_job* jobs, int njobs, int total_wg, int max_c0, void* stream);
 
 /* General implicit-GEMM conv at the same bf16x6 arithmetic: exactly wc_conv_igemm's contract
  * (tap grids, input strides, the 1x1 residual segment, output maps, NCHW store; an activation

@@ -363,6 +363,13 @@ def test_pack_wino_raw_bit_identical_to_relayout(Co, Ci, res):
         at = K.pack_wino_raw(w, transposed=True)
         reft = K.pack_wino(pack_conv(w.flip([2, 3]).transpose(0, 1)), Co, device=True)
         assert torch.equal(at.data, reft.data) and torch.equal(at.wsinv, reft.wsinv) and at.N == Ci
+    # the batched launch (wc_pack_wino_batch, the training step's form) equals one launch each
+    w2 = torch.randn((Ci, Co, 3, 3), generator=g).cuda()
+    reqs = [(w, wr, False), (w, None, True), (w2, None, False), (w, None, False)]
+    batch = K.pack_wino_raw_batch(reqs)
+    for (w4, r, t), b in zip(reqs, batch):
+        one = K.pack_wino_raw(w4, r, transposed=t)
+        assert torch.equal(b.data, one.data) and torch.equal(b.wsinv, one.wsinv) and (b.N, b.C0, b.C1) == (one.N, one.C0, one.C1)
 
 
 @pytest.mark.parametrize('precision', ['f16x3', 'bf16x6'])

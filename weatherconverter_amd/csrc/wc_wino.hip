@@ -761,6 +761,33 @@ __global__ __launch_bounds__(256) void pack_wino_raw_kernel(const float* __restr
     pack_wino_row(row3, wres + (long)(live ? n : 0) * C1, live, n, C0, C1, BN, out, wsinv);
 }
 
+// Many raw packs in one launch (the training step's ~80 per-iteration Winograd packs): workgroup g runs
+// output channel g - wg0 of the job with the largest wg0 <= g (binary search over the sorted wg0s).
+__global__ __launch_bounds__(256) void pack_wino_batch_kernel(const wc_wino_pack_job* __restrict__ jobs, int njobs) {
+    extern __shared__ float row3[];
+    const int g = blockIdx.x;
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].wg0 <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    const wc_wino_pack_job jb = jobs[lo];
+    const int n = g - jb.wg0;
+    const bool live = n < jb.N;
+    const int C0 = jb.C0, N = jb.N;
+    if (live) {
+        for (int i = threadIdx.x; i < 9 * C0; i += blockDim.x) {
+            const int c = i / 9, t = i - 9 * c;
+            const float v = jb.transposed ? jb.w[((long)c * N + n) * 9 + t] : jb.w[(long)n * 9 * C0 + i];
+            row3[(jb.transposed ? 8 - t : t) * C0 + c] = v;
+        }
+    }
+    __syncthreads();
+    pack_wino_row(row3, jb.wres + (long)(live ? n : 0) * jb.C1, live, n, C0, jb.C1, jb.BN,
+                  reinterpret_cast<short*>(jb.out), jb.wsinv);
+}
+
 }  // namespace
 
 extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_bytes, float* w_inv_scale,
@@ -773,6 +800,17 @@ extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, in
     hipLaunchKernelGGL(pack_wino_kernel, dim3((unsigned)(ntn * BN)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        w, 9 * C0 + C1, N, C0, C1, BN, reinterpret_cast<short*>(out), w_inv_scale);
     wc_last_kernel = "pack_wino_kernel";
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_pack_wino_batch(const wc_wino_pack_job* jobs, int njobs, int total_wg, int max_c0, void* stream) {
+    if (!jobs || njobs < 0 || total_wg < 0) return WC_E_ARG;
+    if (njobs == 0) return WC_OK;
+    if (max_c0 <= 0 || 9L * max_c0 * 4 > 64 * 1024 || total_wg <= 0) return WC_E_SHAPE;
+    hipLaunchKernelGGL(pack_wino_batch_kernel, dim3((unsigned)total_wg), dim3(256), (size_t)9 * max_c0 * sizeof(float),
+                       reinterpret_cast<hipStream_t>(stream), jobs, njobs);
+    wc_last_kernel = "pack_wino_batch_kernel";
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

@@ -171,6 +171,10 @@ class TrainEngine:
             if self.f3d and wino and ci % 16 == 0 and co % 16 == 0 else None,
             wn_2T=L(lambda: K.pack_wino_raw(w2, transposed=True) if raw else K.pack_wino(rp['w2T'], co))
             if self.f3d and wino and co % 16 == 0 else None)
+        if raw:  # the raw-weight requests of the forms that exist, for _pack's one batched launch
+            want = {'wn_1': (w1, None, False), 'wn_2': (w2, wr2.float().contiguous(), False),
+                    'wn_1T': (w1, None, True), 'wn_2T': (w2, None, True)}
+            rp['_wino_raw'] = {k: v for k, v in want.items() if rp.has(k)}
         return rp
 
     def _pack_attn(self, blk, i: int):
@@ -293,6 +297,12 @@ class TrainEngine:
             self.tproj = [tp[0].weight.detach().float().contiguous(), tp[0].bias.detach().float().contiguous(),
                           tp[2].weight.detach().float().contiguous(), tp[2].bias.detach().float().contiguous()]
             rows = [rp for st in self.downs + self.mids + self.ups for rp in st[0]]
+            # every ResBlock's Winograd packs (forward and data-gradient forms; the weights change each
+            # step) in one launch instead of one each (WC_PACK_BATCH=0: built lazily one by one)
+            if os.environ.get('WC_PACK_BATCH', '1') != '0':
+                reqs = [(rp, k, r) for rp in rows for k, r in rp.get('_wino_raw', {}).items()]
+                for (rp, k, _), pk in zip(reqs, K.pack_wino_raw_batch([r for _, _, r in reqs])):
+                    dict.__setitem__(rp, k, pk)
             self._resolve(rows + [ap for st in self.downs + self.mids + self.ups for ap in st[1]])
             self.temb_w = torch.cat([rp['temb'].weight.detach().float() for rp in rows], 0).contiguous()
             self.temb_b = torch.cat([rp['temb'].bias.detach().float() for rp in rows], 0).contiguous()

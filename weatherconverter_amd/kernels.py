@@ -556,6 +556,41 @@ def pack_wino_raw(w4: torch.Tensor, wres: Optional[torch.Tensor] = None, transpo
     return X6Weight(data, N, BN, C0, C1, 'wino', wsinv, bool(C1))
 
 
+def pack_wino_raw_batch(reqs: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], bool]]) -> List[X6Weight]:
+    """pack_wino_raw of every (w4, wres, transposed) in reqs in ONE launch (wc_pack_wino_batch): the same
+    pieces and scales, bit for bit, as one wc_pack_wino_raw each."""
+    if not reqs:
+        return []
+    outs, rows, wg, max_c0 = [], [], 0, 0
+    dev = reqs[0][0].device
+    for w4, wres, transposed in reqs:
+        _req(w4.is_cuda and w4.dtype == torch.float32 and w4.is_contiguous() and w4.dim() == 4
+             and w4.shape[2:] == (3, 3), 'pack_wino_raw: contiguous fp32 [Co][Ci][3][3] device weight')
+        Co, Ci = w4.shape[:2]
+        N, C0 = (Ci, Co) if transposed else (Co, Ci)
+        C1 = 0
+        if wres is not None:
+            _req(not transposed and wres.is_cuda and wres.dtype == torch.float32 and wres.is_contiguous()
+                 and wres.shape[0] == Co, 'pack_wino_raw residual: contiguous fp32 [Co][C1]')
+            C1 = wres.shape[1]
+        _req(C0 % 16 == 0 and C1 % 16 == 0 and 9 * C0 * 4 <= 64 * 1024, 'wino weight shape')
+        _, BN = wino_tile(N)
+        Np = -(-N // BN) * BN
+        data = torch.empty((Np // BN, (12 * C0 + C1) // 16 * 2 * 2 * BN * 8), dtype=torch.int16, device=dev)
+        wsinv = torch.empty(Np, dtype=torch.float32, device=dev)
+        outs.append(X6Weight(data, N, BN, C0, C1, 'wino', wsinv, bool(C1)))
+        rows.append([w4.data_ptr(), _ptr(wres) or 0, data.data_ptr(), wsinv.data_ptr(),
+                     N | (C0 << 32), C1 | (int(transposed) << 32), BN | (wg << 32), 0])
+        wg += Np
+        max_c0 = max(max_c0, C0)
+    _req(wg < 2**31, 'pack batch too large')
+    tab = torch.empty((len(rows), 8), dtype=torch.int64, pin_memory=True)
+    tab.copy_(torch.tensor(rows, dtype=torch.int64))
+    dtab = tab.to(dev, non_blocking=True)
+    _timed('pack_wino_batch_kernel', 'wc_pack_wino_batch', 0.0, dtab.data_ptr(), len(rows), wg, max_c0, _stream())
+    return outs
+
+
 def pack_wino(w: torch.Tensor, C0: int, C1: int = 0, *, device: Optional[bool] = None) -> X6Weight:
     """Pack a [N][9*C0 + C1] ResBlock conv weight (3x3 taps then the 1x1 residual columns, as
     engine.pack_conv) for wc_conv3x3_wino_f16x3: the F(2,3) filter transform in float64, a per-channel

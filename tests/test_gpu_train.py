@@ -345,6 +345,19 @@ def test_attention_backward(C, heads, N):
     assert rel_l2(dqkv.cpu(), q_.grad.reshape(B * N, 3 * C)) < 1e-5
 
 
+@pytest.mark.parametrize('Ci,N', [(64, 128), (256, 128), (128, 64), (512, 256)])
+def test_pack_f16x3_convT_device_equals_cpu_definition(Ci, N):
+    """The ConvT f16x3 pack in one device launch (the four parities side by side under their common
+    scale) equals the torch definition evaluated on the CPU, bit for bit."""
+    from weatherconverter_amd import kernels as K
+    g = _gen(13)
+    wt = torch.randn((Ci, N, 4, 4), generator=g) * torch.rand((1, N, 1, 1), generator=g) * 2
+    dev = K.pack_f16x3_convT(wt.cuda())
+    cpu = K.pack_f16x3_convT(wt)
+    assert dev.order == cpu.order == 'f16x3t' and (dev.N, dev.BN, dev.C0) == (cpu.N, cpu.BN, cpu.C0)
+    assert torch.equal(dev.data.cpu(), cpu.data.reshape(dev.data.shape)) and torch.equal(dev.wsinv.cpu(), cpu.wsinv)
+
+
 @pytest.mark.parametrize('Co,Ci,res', [(128, 64, True), (256, 256, False), (64, 768, True), (48, 32, False)])
 def test_pack_wino_raw_bit_identical_to_relayout(Co, Ci, res):
     """wc_pack_wino_raw from the module's [Co][Ci][3][3] weight (conv + residual, and the data gradient's

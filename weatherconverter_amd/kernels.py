@@ -723,6 +723,13 @@ def pack_f16x3_convT(wt: torch.Tensor) -> X6Weight:
     Ci, N = wt.shape[0], wt.shape[1]
     _req(Ci % 16 == 0, 'ConvT input channels % 16')
     parts = [pack_convT(wt, py, px)[1].to(wt.device) for py in (0, 1) for px in (0, 1)]
+    if pack_device_enabled() and wt.is_cuda and os.environ.get('WC_PACK_DEVICE_CONVT', '1') != '0':
+        # one device pack of the four parities side by side, columns ordered (parity, chunk, tap, c%16):
+        # its natural step order is then the stacked per-parity halo order below, and its per-row scale
+        # the common one (the row max over all four parities) -- one launch instead of ~60 torch ops
+        wcat = torch.stack(parts, 1).view(N, 4, 4, Ci // 16, 16).permute(0, 1, 3, 2, 4).reshape(N, 16 * Ci)
+        data, wsinv = _pack_dev(wcat, 16 * Ci, 0, 1, 'natural', 1, False)
+        return X6Weight(data, N, x6_tile(N)[1], Ci, 0, 'f16x3t', wsinv)
     amax = torch.stack([p.abs().amax(1) for p in parts]).amax(0)
     packs = [pack_f16x3(p, Ci, ntaps=4, order='halo', amax=amax) for p in parts]
     T = packs[0].data.shape[0]

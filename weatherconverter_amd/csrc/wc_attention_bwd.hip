@@ -246,25 +246,35 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
     }
 }
 
-// Dv[b][h][q] = sum_d dO[b, q, h*D + d] * O[b, q, h*D + d]
+// Dv[b][h][q] = sum_d dO[b, q, h*D + d] * O[b, q, h*D + d].  16 lanes per (b, q, h) row, rows in
+// memory order (b, q, h): a wave reads four heads' rows of one pixel, consecutive 16-byte pieces across
+// the lanes (a thread per row striding through its own row touched 64 cache lines per load); each lane
+// sums d = 4 l + 64 k in order, then a fixed xor butterfly over the 16 lanes (deterministic).
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ O, int ldo,
                                                             const float* __restrict__ dO, int lddo, int B, int N,
                                                             int H, int D, float* __restrict__ Dv) {
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (long)B * H * N) return;
-    const int q = (int)(i % N);
-    const long bh = i / N;
-    const int h = (int)(bh % H);
-    const int b = (int)(bh / H);
-    const float* o = O + ((long)b * N + q) * ldo + h * D;
-    const float* g = dO + ((long)b * N + q) * lddo + h * D;
+    const long r = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int l = threadIdx.x & 15;
+    const bool live = r < (long)B * N * H;
+    const long rr = live ? r : 0;
+    const int h = (int)(rr % H);
+    const long bq = rr / H;
+    const float* o = O + bq * ldo + h * D;
+    const float* g = dO + bq * lddo + h * D;
     float s = 0.f;
-    for (int d = 0; d < D; d += 4) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(o + d);
-        const f32x4 c = *reinterpret_cast<const f32x4*>(g + d);
-        s = fmaf(a.x, c.x, s); s = fmaf(a.y, c.y, s); s = fmaf(a.z, c.z, s); s = fmaf(a.w, c.w, s);
+    if (live)
+        for (int d = 4 * l; d < D; d += 64) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(o + d);
+            const f32x4 c = *reinterpret_cast<const f32x4*>(g + d);
+            s = fmaf(a.x, c.x, s); s = fmaf(a.y, c.y, s); s = fmaf(a.z, c.z, s); s = fmaf(a.w, c.w, s);
+        }
+#pragma unroll
+    for (int m = 8; m > 0; m >>= 1) s += __shfl_xor(s, m, 16);
+    if (live && l == 0) {
+        const int q = (int)(bq % N);
+        const int b = (int)(bq / N);
+        Dv[((long)b * H + h) * N + q] = s;
     }
-    Dv[i] = s;
 }
 
 template <int D>
@@ -313,7 +323,7 @@ extern "C" int wc_attention_bwd(const float* qkv, int ld_qkv, const float* out, 
     if (D % 4) return WC_E_SHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const long n = (long)B * heads * N;
-    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, ld_out, dout,
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, out, ld_out, dout,
                        ld_dout, B, N, heads, D, dv_work);
     WC_CHECK_LAUNCH();
     switch (D) {
@@ -336,7 +346,7 @@ extern "C" int wc_attention_bwd_prep(const float* out, int ld_out, const float* 
     if (!out || !dout || !dv_work) return WC_E_ARG;
     if (B <= 0 || N <= 0 || heads <= 0 || D <= 0 || D % 4 || ld_out % 4 || ld_dout % 4) return WC_E_SHAPE;
     const long n = (long)B * heads * N;
-    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), out, ld_out, dout, ld_dout, B, N, heads, D, dv_work);
     WC_CHECK_LAUNCH();
     return WC_OK;

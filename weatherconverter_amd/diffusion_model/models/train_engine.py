@@ -263,12 +263,13 @@ class TrainEngine:
                 if blk.down_sample:
                     w = blk.down_sample_conv.weight.detach()
                     ci = w.shape[1]
-                    parts = [pack_convT(w, py, px) for py, px in _PARITIES]  # dgrad: ConvT of dY (in = Co)
                     L = _Pack.lazy
                     f3 = self.f3 and ci % 16 == 0 and w.shape[0] % 16 == 0 and K.x6_tile(w.shape[0])[1] == 128
                     self.down_pk.append(_Pack(
                         mod=blk.down_sample_conv, pk=L(lambda w=w, ci=ci: self._pk(pack_conv(w), ci, 16)),
-                        dT=L(lambda parts=parts, w=w: [(taps, self._pk(wp, w.shape[0], len(taps))) for taps, wp in parts]),
+                        # dgrad: ConvT of dY (in = Co), its four parity re-layouts built only if used
+                        dT=L(lambda w=w: [(taps, self._pk(wp, w.shape[0], len(taps)))
+                                          for taps, wp in (pack_convT(w, py, px) for py, px in _PARITIES)]),
                         # f16x3 halo forms: the forward on the space-to-depth kernel, the data gradient (the
                         # ConvT of dY with the same weight) on the one-launch ConvT kernel
                         f3=L(lambda w=w, ci=ci: K.pack_f16x3_s2d(pack_conv(w).float(), ci)) if f3 else None,
@@ -280,13 +281,13 @@ class TrainEngine:
                 if blk.up_sample:
                     wt = blk.up_sample_conv.weight.detach()  # [Cin][Cout][4][4]
                     ci = wt.shape[0]
-                    parts = [pack_convT(wt, py, px) for py, px in _PARITIES]
                     L = _Pack.lazy
                     co = wt.shape[1]
                     f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
                     self.up_pk.append(_Pack(
-                        mod=blk.up_sample_conv, fw=L(lambda parts=parts, ci=ci: [(taps, self._pk(wp, ci, len(taps)))
-                                                                                 for taps, wp in parts]),
+                        mod=blk.up_sample_conv,
+                        fw=L(lambda wt=wt, ci=ci: [(taps, self._pk(wp, ci, len(taps)))
+                                                   for taps, wp in (pack_convT(wt, py, px) for py, px in _PARITIES)]),
                         dT=L(lambda wt=wt, co=co: self._pk(pack_conv(wt), co, 16)),
                         f3=L(lambda wt=wt: K.pack_f16x3_convT(wt.float())) if f3 else None,
                         f3T=L(lambda wt=wt, co=co: K.pack_f16x3_s2d(pack_conv(wt).float(), co))

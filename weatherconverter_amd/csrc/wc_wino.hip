@@ -667,18 +667,26 @@ __device__ double wino_u(const float* row, int C0, int ky, int pos, int c) {
 // at rres[j]; live = n < N (padding rows are zeros).
 __device__ void pack_wino_row(const float* row3, const float* rres, bool live, int n, int C0, int C1, int BN,
                               short* __restrict__ out, float* __restrict__ wsinv) {
-    const int n0 = 12 * C0, nall = n0 + C1;
+    // items of 8 consecutive channels (one 16-byte fragment per piece): 12 (ky, pos) x C0 / 8, then C1 / 8
+    const int c8 = C0 / 8, n0 = 12 * c8, nall = n0 + C1 / 8;
+    auto values = [&](int it, double* v) {
+        if (it < n0) {
+            const int kp = it / c8, c = (it - kp * c8) * 8;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = wino_u(row3, C0, kp / 4, kp % 4, c + e);
+        } else {
+            const int c = (it - n0) * 8;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = rres[c + e];
+        }
+    };
     double m = 0.0;
     if (live) {
-        for (int i = threadIdx.x; i < nall; i += blockDim.x) {
-            double v;
-            if (i < n0) {
-                const int c = i % C0, kp = i / C0;
-                v = wino_u(row3, C0, kp / 4, kp % 4, c);
-            } else {
-                v = rres[i - n0];
-            }
-            m = fmax(m, fabs(v));
+        for (int it = threadIdx.x; it < nall; it += blockDim.x) {
+            double v[8];
+            values(it, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m = fmax(m, fabs(v[e]));
         }
     }
     __shared__ double red[256];
@@ -701,31 +709,38 @@ __device__ void pack_wino_row(const float* row3, const float* rres, bool live, i
     const int T = n / BN, nn = n % BN;
     const long rowlen = (long)(12 * (C0 / 16) + C1 / 16) * 2 * 2 * BN * 8;  // int16 per N tile
     short* trow = out + (long)T * rowlen;
-    for (int i = threadIdx.x; i < nall; i += blockDim.x) {
-        double v = 0.0;
+    const int plane = 2 * BN * 8;  // distance between the two pieces (int16 units)
+    for (int it = threadIdx.x; it < nall; it += blockDim.x) {
+        double v[8];
+        if (live) values(it, v);
+        else
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.0;
         long o;
-        int plane;  // distance between the two pieces (int16 units)
-        if (i < n0) {
-            const int c = i % C0, kp = i / C0, ky = kp / 4, pos = kp % 4;
-            if (live) v = wino_u(row3, C0, ky, pos, c);
-            const int chunk = c / 16, kh = (c % 16) / 8, e = c % 8;
-            o = ((((long)(chunk * 3 + ky) * 4 + pos) * 2 * 2 + kh) * BN + nn) * 8 + e;  // piece 0
-            plane = 2 * BN * 8;
+        if (it < n0) {
+            const int kp = it / c8, c = (it - kp * c8) * 8, ky = kp / 4, pos = kp % 4;
+            const int chunk = c / 16, kh = (c % 16) / 8;
+            o = ((((long)(chunk * 3 + ky) * 4 + pos) * 2 * 2 + kh) * BN + nn) * 8;  // piece 0
         } else {
-            const int c = i - n0;
-            if (live) v = rres[c];
-            const int chunk = c / 16, kh = (c % 16) / 8, e = c % 8;
-            o = (long)(C0 / 16) * 12 * 2 * 2 * BN * 8 + (((long)chunk * 2 * 2 + kh) * BN + nn) * 8 + e;
-            plane = 2 * BN * 8;
+            const int c = (it - n0) * 8;
+            const int chunk = c / 16, kh = (c % 16) / 8;
+            o = (long)(C0 / 16) * 12 * 2 * 2 * BN * 8 + (((long)chunk * 2 * 2 + kh) * BN + nn) * 8;
         }
-        float v32 = (float)(v * scale);
-        // materialize the fp32 value: without this the compiler folds double -> fp32 -> fp16 into one
-        // double -> fp16 rounding, which differs on fp16 ties (the definition rounds twice, fp32 first)
-        asm volatile("" : "+v"(v32));
-        unsigned short h, l;
-        split2_one(v32, h, l);
-        trow[o] = (short)h;
-        trow[o + plane] = (short)l;
+        unsigned hp[4], lp[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            unsigned short h0, l0, h1, l1;
+            float a = (float)(v[e] * scale), b = (float)(v[e + 1] * scale);
+            // materialize the fp32 values: without this the compiler folds double -> fp32 -> fp16 into one
+            // double -> fp16 rounding, which differs on fp16 ties (the definition rounds twice, fp32 first)
+            asm volatile("" : "+v"(a), "+v"(b));
+            split2_one(a, h0, l0);
+            split2_one(b, h1, l1);
+            hp[e / 2] = (unsigned)h0 | ((unsigned)h1 << 16);
+            lp[e / 2] = (unsigned)l0 | ((unsigned)l1 << 16);
+        }
+        *reinterpret_cast<u32x4*>(trow + o) = u32x4{hp[0], hp[1], hp[2], hp[3]};
+        *reinterpret_cast<u32x4*>(trow + o + plane) = u32x4{lp[0], lp[1], lp[2], lp[3]};
     }
 }
 

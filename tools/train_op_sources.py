@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 OPS = ('aten::fill_', 'aten::zero_', 'aten::copy_', 'aten::cat', 'aten::flip', 'aten::add', 'aten::mul', 'aten::sub',
        'aten::div', 'aten::clamp', 'aten::ones_like', 'aten::_to_copy', 'aten::where', 'aten::abs', 'aten::amax',
-       'aten::ldexp', 'aten::stack', 'aten::floor', 'aten::log2')
+       'aten::ldexp', 'aten::stack', 'aten::floor', 'aten::log2', 'aten::zeros', 'aten::zeros_like', 'aten::full',
+       'aten::ones', 'aten::new_zeros', 'aten::fill', 'aten::masked_fill_', 'aten::index_put_', 'aten::scatter_')
 
 
 def main():

@@ -757,6 +757,28 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
 // TRANSPOSED = true, its data gradient (N = Ci, C0 = Co; value (n, tap, c) = w[c][n][8 - tap], the
 // flipped, transposed filter), no residual.  The row goes through LDS in the packed order first, so the
 // values -- and the pieces -- are those of pack_wino_kernel on the host re-layout.
+// Stage output channel n's 3x3 values into LDS in the packed order row3[tap * C0 + c], eight loads in
+// flight per thread (a load-then-store loop waited out one memory latency per element: ~27 latencies a
+// workgroup at C0 = 768).  TRANSPOSED reads the flipped, transposed filter w[c][n][8 - tap].
+__device__ void stage_row3(const float* __restrict__ w, bool transposed, int N, int n, int C0, float* row3) {
+    const int lim = 9 * C0;
+    for (int i0 = threadIdx.x; i0 < lim; i0 += 8 * 256) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * 256;
+            const int c = i / 9, t = i - 9 * c;
+            v[k] = i < lim ? (transposed ? w[((long)c * N + n) * 9 + t] : w[(long)n * lim + i]) : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * 256;
+            const int c = i / 9, t = i - 9 * c;
+            if (i < lim) row3[(transposed ? 8 - t : t) * C0 + c] = v[k];
+        }
+    }
+}
+
 template <bool TRANSPOSED>
 __global__ __launch_bounds__(256) void pack_wino_raw_kernel(const float* __restrict__ w, const float* __restrict__ wres,
                                                             int N, int C0, int C1, int BN, short* __restrict__ out,
@@ -764,14 +786,7 @@ __global__ __launch_bounds__(256) void pack_wino_raw_kernel(const float* __restr
     extern __shared__ float row3[];  // [9][C0]
     const int n = blockIdx.x;
     const bool live = n < N;
-    if (live) {
-        for (int i = threadIdx.x; i < 9 * C0; i += blockDim.x) {
-            // i walks the source in memory order: (c, tap) with the tap fastest
-            const int c = i / 9, t = i - 9 * c;
-            const float v = TRANSPOSED ? w[((long)c * N + n) * 9 + t] : w[(long)n * 9 * C0 + i];
-            row3[(TRANSPOSED ? 8 - t : t) * C0 + c] = v;
-        }
-    }
+    if (live) stage_row3(w, TRANSPOSED, N, n, C0, row3);  // i walks the source in memory order
     __syncthreads();
     pack_wino_row(row3, wres + (long)(live ? n : 0) * C1, live, n, C0, C1, BN, out, wsinv);
 }
@@ -780,24 +795,24 @@ __global__ __launch_bounds__(256) void pack_wino_raw_kernel(const float* __restr
 // output channel g - wg0 of the job with the largest wg0 <= g (binary search over the sorted wg0s).
 __global__ __launch_bounds__(256) void pack_wino_batch_kernel(const wc_wino_pack_job* __restrict__ jobs, int njobs) {
     extern __shared__ float row3[];
+    __shared__ int s_wg0[256];
     const int g = blockIdx.x;
+    // the jobs' first workgroups in LDS in one round of loads, then the search (one dependent global
+    // load per search step cost a memory latency each)
+    const bool lds = njobs <= 256;
+    if (lds && (int)threadIdx.x < njobs) s_wg0[threadIdx.x] = jobs[threadIdx.x].wg0;
+    __syncthreads();
     int lo = 0, hi = njobs - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (jobs[mid].wg0 <= g) lo = mid;
+        if ((lds ? s_wg0[mid] : jobs[mid].wg0) <= g) lo = mid;
         else hi = mid - 1;
     }
     const wc_wino_pack_job jb = jobs[lo];
     const int n = g - jb.wg0;
     const bool live = n < jb.N;
     const int C0 = jb.C0, N = jb.N;
-    if (live) {
-        for (int i = threadIdx.x; i < 9 * C0; i += blockDim.x) {
-            const int c = i / 9, t = i - 9 * c;
-            const float v = jb.transposed ? jb.w[((long)c * N + n) * 9 + t] : jb.w[(long)n * 9 * C0 + i];
-            row3[(jb.transposed ? 8 - t : t) * C0 + c] = v;
-        }
-    }
+    if (live) stage_row3(jb.w, jb.transposed != 0, N, n, C0, row3);
     __syncthreads();
     pack_wino_row(row3, jb.wres + (long)(live ? n : 0) * jb.C1, live, n, C0, jb.C1, jb.BN,
                   reinterpret_cast<short*>(jb.out), jb.wsinv);

@@ -167,12 +167,12 @@ int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, int64_t out_b
 /* wc_pack_wino from the module's own [Co][Ci][3][3] fp32 weight (no host re-layout; bit-identical to
  * wc_pack_wino of engine.pack_conv's layout): transposed = 0, the conv (N = Co, C0 = Ci) with the optional
  * 1x1 residual wres [N][C1]; transposed = 1, its data gradient (N = Ci, C0 = Co: the flipped transposed
- * filter), C1 = 0.  9 * C0 * 4 <= 64 KiB. */
+ * filter), C1 = 0.  9 * (C0 + 4) * 4 <= 64 KiB (the row staged in LDS, padded). */
 int wc_pack_wino_raw(const float* w, const float* wres, int N, int C0, int C1, int transposed, void* out,
                      int64_t out_bytes, float* w_inv_scale, void* stream);
 /* Many wc_pack_wino_raw in one launch.  jobs: a DEVICE array of njobs descriptors sorted by wg0, job j
  * covering workgroups [wg0, wg0 + its N-tile-padded N) of the total_wg; out / wsinv sized as
- * wc_pack_wino_raw's; max_c0 >= every job's C0 (9 * max_c0 * 4 <= 64 KiB).  The caller validates shapes
+ * wc_pack_wino_raw's; max_c0 >= every job's C0 (9 * (max_c0 + 4) * 4 <= 64 KiB).  The caller validates shapes
  * (kernels.pack_wino_raw_batch does, as wc_pack_wino_raw). */
 typedef struct wc_wino_pack_job {
     const float* w;

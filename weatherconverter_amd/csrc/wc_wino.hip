@@ -663,17 +663,37 @@ __device__ double wino_u(const float* row, int C0, int ky, int pos, int c) {
     }
 }
 
+// The same for channels c .. c + 7 of an LDS row with tap stride ld (16-byte aligned): two 16-byte reads
+// per tap instead of eight scalar ones (lanes 8 channels apart hit one bank eight ways).
+__device__ void wino_u8(const float* row, int ld, int ky, int pos, int c, double* v) {
+    f32x4 g[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        g[k][0] = *reinterpret_cast<const f32x4*>(row + (ky * 3 + k) * ld + c);
+        g[k][1] = *reinterpret_cast<const f32x4*>(row + (ky * 3 + k) * ld + c + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const double g0 = g[0][e >> 2][e & 3], g1 = g[1][e >> 2][e & 3], g2 = g[2][e >> 2][e & 3];
+        v[e] = pos == 0 ? g0 : pos == 1 ? ((g0 + g1) + g2) * 0.5 : pos == 2 ? ((g0 - g1) + g2) * 0.5 : g2;
+    }
+}
+
 // The row of output channel n: the 3x3 values at row3[(ky * 3 + kx) * C0 + c], the residual ones (C1)
 // at rres[j]; live = n < N (padding rows are zeros).
-__device__ void pack_wino_row(const float* row3, const float* rres, bool live, int n, int C0, int C1, int BN,
-                              short* __restrict__ out, float* __restrict__ wsinv) {
+__device__ void pack_wino_row(const float* row3, int ld, bool vec, const float* rres, bool live, int n, int C0, int C1,
+                              int BN, short* __restrict__ out, float* __restrict__ wsinv) {
     // items of 8 consecutive channels (one 16-byte fragment per piece): 12 (ky, pos) x C0 / 8, then C1 / 8
     const int c8 = C0 / 8, n0 = 12 * c8, nall = n0 + C1 / 8;
     auto values = [&](int it, double* v) {
         if (it < n0) {
             const int kp = it / c8, c = (it - kp * c8) * 8;
+            if (vec) {
+                wino_u8(row3, ld, kp / 4, kp % 4, c, v);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = wino_u(row3, C0, kp / 4, kp % 4, c + e);
+                for (int e = 0; e < 8; ++e) v[e] = wino_u(row3, ld, kp / 4, kp % 4, c + e);
+            }
         } else {
             const int c = (it - n0) * 8;
 #pragma unroll
@@ -749,7 +769,7 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
     const int n = blockIdx.x;
     const bool live = n < N;
     const float* row = w + (long)(live ? n : 0) * K;
-    pack_wino_row(row, row + 9 * C0, live, n, C0, C1, BN, out, wsinv);
+    pack_wino_row(row, C0, false, row + 9 * C0, live, n, C0, C1, BN, out, wsinv);
 }
 
 // The same from the module's own [Co][Ci][3][3] weight (no host re-layout): TRANSPOSED = false, the conv
@@ -757,11 +777,12 @@ __global__ __launch_bounds__(256) void pack_wino_kernel(const float* __restrict_
 // TRANSPOSED = true, its data gradient (N = Ci, C0 = Co; value (n, tap, c) = w[c][n][8 - tap], the
 // flipped, transposed filter), no residual.  The row goes through LDS in the packed order first, so the
 // values -- and the pieces -- are those of pack_wino_kernel on the host re-layout.
-// Stage output channel n's 3x3 values into LDS in the packed order row3[tap * C0 + c], eight loads in
-// flight per thread (a load-then-store loop waited out one memory latency per element: ~27 latencies a
-// workgroup at C0 = 768).  TRANSPOSED reads the flipped, transposed filter w[c][n][8 - tap].
+// Stage output channel n's 3x3 values into LDS in the packed order row3[tap * (C0 + 4) + c] (the 4-float
+// pad puts the nine taps of one channel, written by neighbouring lanes, in different banks), eight loads
+// in flight per thread (a load-then-store loop waited out one memory latency per element).
+// TRANSPOSED reads the flipped, transposed filter w[c][n][8 - tap].
 __device__ void stage_row3(const float* __restrict__ w, bool transposed, int N, int n, int C0, float* row3) {
-    const int lim = 9 * C0;
+    const int lim = 9 * C0, ld = C0 + 4;
     for (int i0 = threadIdx.x; i0 < lim; i0 += 8 * 256) {
         float v[8];
 #pragma unroll
@@ -774,7 +795,7 @@ __device__ void stage_row3(const float* __restrict__ w, bool transposed, int N, 
         for (int k = 0; k < 8; ++k) {
             const int i = i0 + k * 256;
             const int c = i / 9, t = i - 9 * c;
-            if (i < lim) row3[(transposed ? 8 - t : t) * C0 + c] = v[k];
+            if (i < lim) row3[(transposed ? 8 - t : t) * ld + c] = v[k];
         }
     }
 }
@@ -788,7 +809,7 @@ __global__ __launch_bounds__(256) void pack_wino_raw_kernel(const float* __restr
     const bool live = n < N;
     if (live) stage_row3(w, TRANSPOSED, N, n, C0, row3);  // i walks the source in memory order
     __syncthreads();
-    pack_wino_row(row3, wres + (long)(live ? n : 0) * C1, live, n, C0, C1, BN, out, wsinv);
+    pack_wino_row(row3, C0 + 4, true, wres + (long)(live ? n : 0) * C1, live, n, C0, C1, BN, out, wsinv);
 }
 
 // Many raw packs in one launch (the training step's ~80 per-iteration Winograd packs): workgroup g runs
@@ -814,7 +835,7 @@ __global__ __launch_bounds__(256) void pack_wino_batch_kernel(const wc_wino_pack
     const int C0 = jb.C0, N = jb.N;
     if (live) stage_row3(jb.w, jb.transposed != 0, N, n, C0, row3);
     __syncthreads();
-    pack_wino_row(row3, jb.wres + (long)(live ? n : 0) * jb.C1, live, n, C0, jb.C1, jb.BN,
+    pack_wino_row(row3, C0 + 4, true, jb.wres + (long)(live ? n : 0) * jb.C1, live, n, C0, jb.C1, jb.BN,
                   reinterpret_cast<short*>(jb.out), jb.wsinv);
 }
 
@@ -837,8 +858,8 @@ extern "C" int wc_pack_wino(const float* w, int N, int C0, int C1, void* out, in
 extern "C" int wc_pack_wino_batch(const wc_wino_pack_job* jobs, int njobs, int total_wg, int max_c0, void* stream) {
     if (!jobs || njobs < 0 || total_wg < 0) return WC_E_ARG;
     if (njobs == 0) return WC_OK;
-    if (max_c0 <= 0 || 9L * max_c0 * 4 > 64 * 1024 || total_wg <= 0) return WC_E_SHAPE;
-    hipLaunchKernelGGL(pack_wino_batch_kernel, dim3((unsigned)total_wg), dim3(256), (size_t)9 * max_c0 * sizeof(float),
+    if (max_c0 <= 0 || 9L * (max_c0 + 4) * 4 > 64 * 1024 || total_wg <= 0) return WC_E_SHAPE;
+    hipLaunchKernelGGL(pack_wino_batch_kernel, dim3((unsigned)total_wg), dim3(256), (size_t)9 * (max_c0 + 4) * sizeof(float),
                        reinterpret_cast<hipStream_t>(stream), jobs, njobs);
     wc_last_kernel = "pack_wino_batch_kernel";
     WC_CHECK_LAUNCH();
@@ -848,11 +869,11 @@ extern "C" int wc_pack_wino_batch(const wc_wino_pack_job* jobs, int njobs, int t
 extern "C" int wc_pack_wino_raw(const float* w, const float* wres, int N, int C0, int C1, int transposed, void* out,
                                 int64_t out_bytes, float* w_inv_scale, void* stream) {
     if (!w || !out || !w_inv_scale || (C1 && !wres) || (transposed && C1)) return WC_E_ARG;
-    if (N <= 0 || C0 <= 0 || C0 % 16 || C1 < 0 || C1 % 16 || 9L * C0 * 4 > 64 * 1024) return WC_E_SHAPE;
+    if (N <= 0 || C0 <= 0 || C0 % 16 || C1 < 0 || C1 % 16 || 9L * (C0 + 4) * 4 > 64 * 1024) return WC_E_SHAPE;
     const int BN = wc_conv3x3_wino_tile_n(N);
     const long ntn = (N + BN - 1) / BN;
     if (out_bytes != ntn * (12L * (C0 / 16) + C1 / 16) * BN * 64) return WC_E_SHAPE;
-    const size_t lds = (size_t)9 * C0 * sizeof(float);
+    const size_t lds = (size_t)9 * (C0 + 4) * sizeof(float);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (transposed)
         hipLaunchKernelGGL(pack_wino_raw_kernel<true>, dim3((unsigned)(ntn * BN)), dim3(256), lds, s, w, wres, N, C0, C1,

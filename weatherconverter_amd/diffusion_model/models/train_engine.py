@@ -137,7 +137,7 @@ class TrainEngine:
         f3 = self.f3 and ci % 16 == 0 and co % 16 == 0
         wino = K.wino_enabled()
         raw = all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in (w1, w2)) \
-            and 9 * max(ci, co) * 4 <= 64 * 1024 and os.environ.get('WC_PACK_RAW', '1') != '0'
+            and 9 * (max(ci, co) + 4) * 4 <= 64 * 1024 and os.environ.get('WC_PACK_RAW', '1') != '0'
         L = _Pack.lazy
         # shared re-layouts, each built once and only if a pack that needs it is (the Winograd forms
         # usually replace the direct f16x3 ones, so those are lazy too)

@@ -573,7 +573,7 @@ def pack_wino_raw_batch(reqs: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor
             _req(not transposed and wres.is_cuda and wres.dtype == torch.float32 and wres.is_contiguous()
                  and wres.shape[0] == Co, 'pack_wino_raw residual: contiguous fp32 [Co][C1]')
             C1 = wres.shape[1]
-        _req(C0 % 16 == 0 and C1 % 16 == 0 and 9 * C0 * 4 <= 64 * 1024, 'wino weight shape')
+        _req(C0 % 16 == 0 and C1 % 16 == 0 and 9 * (C0 + 4) * 4 <= 64 * 1024, "wino weight shape")
         _, BN = wino_tile(N)
         Np = -(-N // BN) * BN
         data = torch.empty((Np // BN, (12 * C0 + C1) // 16 * 2 * 2 * BN * 8), dtype=torch.int16, device=dev)

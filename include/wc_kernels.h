@@ -558,7 +558,8 @@ int wc_attention_bwd6(const float* qkv, int ld_qkv, const float* out, int ld_out
  * Q, K, V scaled by 2^eq, 2^ek, 2^ev — the training forward's exponents from the in-projection bounds
  * (|Q| 2^eq <= 2^14 ...); dO by 2^edo from dobound[b] = per-image max |dO| (device, wc_absmax_images);
  * P by 2^14; dS by 2^eds with the bound |dS| <= 2 d max|dO| max|V|.  Head dim in {32, 64, 128}, or 192
- * (dQ on f16x3, dK / dV on fp32 MFMA; dqkv_absmax must then be NULL).
+ * (dQ on f16x3; dK / dV on f16x3 with the V rows in LDS when dqkv_absmax is given, on fp32 MFMA, which
+ * raises no bound, when it is NULL: the caller's choice is the one argument, no environment switch).
  * dqkv_absmax (optional, [B], caller-zeroed): raised to the max |dqkv| written per image. */
 /* The fp32-MFMA dK / dV kernel of wc_attention_bwd alone, head dim 192, after wc_attention_bwd_prep:
  * wc_attention_bwd_f16x3 pairs it with its f16x3 dQ kernel at that width. */
@@ -596,8 +597,12 @@ int wc_nchw_to_nhwc(const float* src, int B, int C, int H, int W, float* dst, in
 int wc_dwconv(const float* x, int ldx, float* out, int ldo, const float* w, const float* bias, int B,
               int H, int W, int C, int K, void* stream);
 
-/* Library identification (for the CPU load test). */
+/* Library identification: "weatherconverter_amd 0.1 gfx950 src:<digest>", where the digest (also alone
+ * from wc_source_hash) is the one weatherconverter_amd/_build.py source_hash() computed over the kernel
+ * sources, this header and the compiler flags the library was built from.  The Python loader refuses a
+ * library whose digest differs from the tree's (no reference counterpart: build provenance). */
 const char* wc_version(void);
+const char* wc_source_hash(void);
 
 /* Instrumentation (no reference counterpart): the exact template instantiation of the kernel the
  * calling host thread launched last through one of the entry points above, in the demangled form

@@ -71,6 +71,31 @@ def test_c_abi_library_exports_every_header_symbol():
     assert sorted(_native.EXPORTS) == names
 
 
+def test_library_refuses_sources_other_than_the_trees(tmp_path, monkeypatch):
+    """The library carries the digest of the sources it was built from; the loader compares it with the
+    tree's and refuses a mismatch (one flipped byte in a copy of csrc/ is enough)."""
+    import shutil
+    from weatherconverter_amd import _build, _native
+    if not os.path.exists(_build.LIB_PATH):
+        pytest.skip('library not built')
+    lib = ctypes.CDLL(_build.LIB_PATH)
+    digest = _native.verify_source_hash(lib, '')  # the in-tree library matches the tree
+    lib.wc_version.restype = ctypes.c_char_p
+    assert lib.wc_version().decode().endswith('src:' + digest)
+    copy = tmp_path / 'csrc'
+    shutil.copytree(_build.CSRC, copy)
+    src = copy / 'wc_wino.hip'
+    data = bytearray(src.read_bytes())
+    data[len(data) // 2] ^= 0x01
+    src.write_bytes(bytes(data))
+    monkeypatch.setattr(_build, 'CSRC', str(copy))
+    monkeypatch.delenv('WC_ALLOW_STALE_LIB', raising=False)
+    with pytest.raises(RuntimeError, match='built from other sources'):
+        _native.verify_source_hash(lib, '')
+    monkeypatch.setenv('WC_ALLOW_STALE_LIB', '1')
+    assert _native.verify_source_hash(lib, '') == digest  # the developer override
+
+
 def test_product_package_never_imports_oracle():
     pkg = os.path.join(ROOT, 'weatherconverter_amd')
     for dp, _, fs in os.walk(pkg):

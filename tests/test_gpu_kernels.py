@@ -241,11 +241,16 @@ def test_conv_in_gn_partials_bit_identical(K, B, H, W, sw):
     K.gn_partials(K.View(ref, 64, 64), gr)
     buf = torch.zeros((B, H, W, 128)).cuda()
     gp = K.GnPart.attach(buf, sw)
-    gp.part.fill_(-7.0)
+    # the partials as the head of a larger buffer whose tail holds a sentinel: a wave past the last pixel
+    # (B*H*W/64 not a multiple of 4) must not write past the partials
+    tail = 4096
+    store = torch.full((gp.part.numel() + tail,), -7.0, device='cuda')
+    gp.part = store[:gp.part.numel()].view(gp.part.shape)
     assert K.conv_in(x, w, b, K.View(buf, 64, 64), gn=gp) is True
     torch.cuda.synchronize()
     assert torch.equal(buf, ref)
     assert torch.equal(gp.part, gr.part)
+    assert bool((store[gp.part.numel():] == -7.0).all()), 'GN partial store past the end of gn.part'
     assert rel_l2(_nchw(buf[..., 64:].cpu()), F.conv2d(x.cpu(), w.cpu(), b.cpu(), padding=1)) < TOL
 
 

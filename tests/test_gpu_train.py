@@ -486,6 +486,25 @@ def test_device_pack_equals_torch_pack(N, C0, C1, ntaps, order, res_f16):
         assert torch.equal(a6.data.cpu(), b6.data), first_diff(a6.data.cpu(), b6.data)
 
 
+@pytest.mark.parametrize('N,C0,C1,ntaps,order,res_f16', [
+    (256, 128, 64, 9, 'halo', True), (96, 48, 0, 9, 'halo', False), (384, 128, 0, 1, 'natural', False)])
+def test_device_pack_equals_torch_pack_bf16_line(N, C0, C1, ntaps, order, res_f16):
+    """The same on the bf16 single-piece library (libwc_kernels_bf16.so): one bf16 piece, the low piece
+    zero on both sides (the device packs write l = 0, and so does the CPU definition)."""
+    from weatherconverter_amd import _native
+    from weatherconverter_amd import kernels as K
+    g = _gen(13)
+    w = torch.randn((N, ntaps * C0 + C1), generator=g) * torch.exp(torch.randn((N, 1), generator=g) * 3)
+    with _native.variant('bf16'):
+        a = K.pack_f16x3(w.cuda(), C0, C1, ntaps=ntaps, order=order, res_f16=res_f16, device=True)
+        b = K.pack_f16x3(w, C0, C1, ntaps=ntaps, order=order, res_f16=res_f16, device=False)
+        torch.cuda.synchronize()
+    assert torch.equal(a.data.cpu(), b.data)
+    assert torch.equal(a.wsinv.cpu(), b.wsinv)
+    # every K-step is [piece 2][k-half 2][BN][8]: the low pieces are all zero
+    assert int(torch.count_nonzero(b.data.view(-1, 2, 2 * b.BN * 8)[:, 1])) == 0
+
+
 # ------------------------------------------------------------------ whole model
 def _model_grads(mc, B, precision, seed=0):
     """(our grads, oracle float64 grads, loss ours, loss ref) for one MSE training iteration;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of an environment switch on the bench line: tools/gpu_ab_env.sh VAR A B [reps]
+# Same-box A/B of an environment switch on the bench line: tools/archive/gpu_ab_env.sh VAR A B [reps]
 # (alternating runs, 20 timed steps each; per-kernel table from the roofline leg).
 mkdir -p gpurun_out
 VAR=$1; A=$2; B=$3; R=${4:-2}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Final-tree bench evidence without the test suite: smoke, the full T=1000 bench (all legs), rocprofv3
-# trace of the timed graph replays -> step table + reconciliation.  usage: TAG=r03m bash tools/gpu_r3_bench_prof.sh
+# trace of the timed graph replays -> step table + reconciliation.  usage: TAG=r03m bash tools/archive/gpu_r3_bench_prof.sh
 TAG=${TAG:-r03x}
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 evidence: quick GPU tests, bench line (20 steps, all legs), rocprofv3 trace of the timed
 # graph replays -> per-step table + reconciliation with the bench's per-kernel table, PMC traffic.
-# usage: TAG=r03a bash tools/gpu_r3_evidence.sh
+# usage: TAG=r03a bash tools/archive/gpu_r3_evidence.sh
 TAG=${TAG:-r03x}
 mkdir -p gpurun_out
 export TMPDIR=/tmp

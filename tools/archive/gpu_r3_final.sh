@@ -2,7 +2,7 @@
 # Round-3 evidence on the final tree: the whole GPU suite, smoke(), the full T=1000 bench (all legs),
 # rocprofv3 trace of the timed replays -> step table + reconciliation, PMC traffic, training lines
 # (fp32-class and the 16-bit line).
-# usage: TAG=r03d bash tools/gpu_r3_final.sh
+# usage: TAG=r03d bash tools/archive/gpu_r3_final.sh
 TAG=${TAG:-r03d}
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC of f16x3 3x3 conv micro-bench cases: SQ stall breakdown, MFMA busy, L1/L2 request traffic.
-# usage: CASES="0 3 4" bash tools/gpu_r3_pmc.sh
+# usage: CASES="0 3 4" bash tools/archive/gpu_r3_pmc.sh
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc3
 for C in ${CASES:-0 3 4}; do

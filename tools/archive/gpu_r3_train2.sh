@@ -2,7 +2,7 @@
 # Training (config 3) iteration: GPU train tests, then the training-step bench with a same-box A/B of
 # env switches (AB_ENV, default: this round's f16x3 wgrad and attention backward off) and an optional
 # rocprofv3 kernel trace.
-# usage: [AB_ENV='A=0 B=0'] [PROF=1] [TAG=x] bash tools/gpu_r3_train2.sh
+# usage: [AB_ENV='A=0 B=0'] [PROF=1] [TAG=x] bash tools/archive/gpu_r3_train2.sh
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-t}

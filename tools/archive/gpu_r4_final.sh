@@ -2,7 +2,7 @@
 # Round-4 evidence on the final tree: the whole GPU suite, smoke(), the full T=1000 bench (all legs),
 # rocprofv3 trace of the timed replays -> step table + reconciliation, PMC traffic, training lines
 # (fp32-class and the f16 / bf16 lines).
-# usage: TAG=r04z bash tools/gpu_r4_final.sh
+# usage: TAG=r04z bash tools/archive/gpu_r4_final.sh
 TAG=${TAG:-r04x}
 mkdir -p gpurun_out
 export TMPDIR=/tmp

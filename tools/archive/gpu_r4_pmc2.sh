@@ -1,6 +1,6 @@
 #!/bin/bash
 # Side-by-side PMC of the direct f16x3 halo conv and the Winograd conv on one micro-bench case:
-# issue / wait breakdown, VALU vs MFMA activity, TA / L1 / L2 load path.  usage: CASE=0 bash tools/gpu_r4_pmc2.sh
+# issue / wait breakdown, VALU vs MFMA activity, TA / L1 / L2 load path.  usage: CASE=0 bash tools/archive/gpu_r4_pmc2.sh
 export TMPDIR=/tmp
 C=${CASE:-0}
 O=gpurun_out/pmc4

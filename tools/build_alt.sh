@@ -1,22 +1,29 @@
 #!/bin/bash
-# Build weatherconverter_amd/lib/alt/libwc_kernels.so for a same-box A/B (tools/gpu_ab_lib.sh,
-# tools/gpu_probe.sh): the named csrc files taken from git revision REV, every other object from
-# this tree's build.  Usage: bash tools/build_alt.sh REV wc_conv6 [wc_igemm6 ...]
+# Build an A/B variant of the default library: the named csrc files taken from git revision REV (or the
+# working tree with REV=WORK) compiled with the extra flags in $EXTRA, every other object from this
+# tree's build, linked into weatherconverter_amd/lib/${ALT:-alt}/libwc_kernels.so.
+# Run it with WC_KERNEL_LIB=<that path> WC_ALLOW_STALE_LIB=1 (tools/ab_lib.sh, tools/wino_ab.py): the
+# variant's compiled-in source digest is the tree's, but it is deliberately not the tree's build.
+# Usage: [ALT=name] [EXTRA="-DX=1"] bash tools/build_alt.sh REV wc_conv6 [wc_igemm6 ...]
 set -e
 REV=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OBJ=$ROOT/weatherconverter_amd/lib/obj
-ALT=$ROOT/weatherconverter_amd/lib/alt
-mkdir -p "$ALT"
+OUT=$ROOT/weatherconverter_amd/lib/${ALT:-alt}
+mkdir -p "$OUT"
 python -c "import sys; sys.path.insert(0, '$ROOT'); from weatherconverter_amd import _build; _build.build()"
 objs=""
 for f in "$@"; do
-  git -C "$ROOT" show "$REV:weatherconverter_amd/csrc/$f.hip" > "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I "$ROOT/include" \
-    -Wno-unused-result -c "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip" -o "$ALT/$f.o"
+  if [ "$REV" = "WORK" ]; then
+    cp "$ROOT/weatherconverter_amd/csrc/$f.hip" "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip"
+  else
+    git -C "$ROOT" show "$REV:weatherconverter_amd/csrc/$f.hip" > "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip"
+  fi
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics $EXTRA -I "$ROOT/include" \
+    -Wno-unused-result -c "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip" -o "$OUT/$f.o"
   rm "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip"
-  objs="$objs $ALT/$f.o"
+  objs="$objs $OUT/$f.o"
 done
-keep=$(ls "$OBJ"/*.o | grep -v -E "/($(echo "$@" | tr ' ' '|'))\.o$")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$ALT/libwc_kernels.so" $keep $objs
-echo "built $ALT/libwc_kernels.so ($REV: $*)"
+keep=$(ls "$OBJ"/*.o | grep -v -E "/($(echo "$@" | tr ' ' '|')|wc_srchash_bf16|wc_srchash_single16)\.o$")
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libwc_kernels.so" $keep $objs
+echo "built $OUT/libwc_kernels.so ($REV $EXTRA: $*)"

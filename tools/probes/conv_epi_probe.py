@@ -1,7 +1,7 @@
 """Probe: f16x3 3x3 conv time on the in-model shapes with and without the epilogue side outputs
 (per-image absmax atomics, GroupNorm tile partials), and on the small-grid 32x32 shapes.
 
-Prints one line per case; run on the GPU box (tools/gpu_probe.sh)."""
+Prints one line per case; run on the GPU box (tools/archive/gpu_probe.sh)."""
 import os
 import sys
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace of 20 graph-replayed sampling steps -> step table (and the bench line).
-# usage: TAG=x bash tools/gpu_steptable.sh
+# usage: TAG=x bash tools/steptable.sh
 TAG=${TAG:-st}
 mkdir -p gpurun_out
 export TMPDIR=/tmp

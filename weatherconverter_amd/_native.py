@@ -23,7 +23,7 @@ EXPORTS = [
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_conv_in_gn', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
     'wc_avgpool2x2', 'wc_upsample2x_bilinear', 'wc_layernorm_channels', 'wc_noise_embed',
-    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version',
+    'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version', 'wc_source_hash',
     'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_f16x3', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_bsum_batch', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
     'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name',
@@ -193,6 +193,7 @@ def load(build_if_missing: bool = True):
                                f'python -c "import __graft_entry__ as g; g.build()"')
         _build.build()
     lib = ctypes.CDLL(path)
+    verify_source_hash(lib, v)
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -205,6 +206,25 @@ def load(build_if_missing: bool = True):
         getattr(lib, name)(value)
     _libs[v] = lib
     return lib
+
+
+_VARIANT_FLAG = {'': '', 'single16': '1', 'bf16': '2'}
+
+
+def verify_source_hash(lib, variant: str = ''):
+    """Refuse a library built from other sources than this tree's: its compiled-in digest
+    (wc_source_hash) must equal _build.source_hash() of the tree's csrc/, header and flags.
+    WC_ALLOW_STALE_LIB=1 lets a developer run a deliberately different build (an A/B variant)."""
+    lib.wc_source_hash.argtypes = []
+    lib.wc_source_hash.restype = ctypes.c_char_p
+    got = lib.wc_source_hash().decode()
+    want = _build.source_hash(_VARIANT_FLAG.get(variant, ''))
+    if got != want and os.environ.get('WC_ALLOW_STALE_LIB', '0') != '1':
+        raise RuntimeError(f'weatherconverter_amd: kernel library {variant or "default"} was built from other sources '
+                           f'(library digest {got}, tree digest {want}); rebuild with '
+                           f'python -c "import __graft_entry__ as g; g.build()" (or set WC_ALLOW_STALE_LIB=1 for a '
+                           f'deliberate A/B build)')
+    return got
 
 
 # Process-wide kernel-form selectors (wc_conv3x3_set_onewave, wc_proj_set_tile): each library variant

@@ -586,15 +586,11 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
         case 192: {
             // f16x3 only: dQ with the output dims in three parts (its own Q / dO rows fit at a third of
             // the accumulators); dK / dV with the V rows in LDS (VL, launch_dkdv192), or
-            // (WC_ATTN_BWD192_FP32=1) on the fp32-MFMA kernel, which raises no bound
+            // (no dqkv_absmax: the caller asked for the fp32-MFMA kernel, which raises no bound) on fp32 MFMA
             if (!f3) return WC_E_SHAPE;
             using Cf = B6Cfg<192, true>;
-            static const bool fp32_dkdv = [] {
-                const char* e = getenv("WC_ATTN_BWD192_FP32");
-                return e && e[0] == '1';
-            }();
+            const bool fp32_dkdv = amx == nullptr;
             if (fp32_dkdv) {
-                if (amx) return WC_E_SHAPE;
                 st = wc_attention_bwd_dkdv192(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
                                               scale, stream);
                 if (st != WC_OK) return st;

@@ -3,6 +3,7 @@
 #include "wc_common.hpp"
 
 #include <math.h>
+#include <stdio.h>
 
 namespace {
 
@@ -192,11 +193,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
             m2 += __shfl_xor(m2, 16, 64);
             m2 += __shfl_xor(m2, 32, 64);
             // after the butterflies every lane of a sub-slot holds its (mean, M2): all of them store it
-            // (the same bytes to one address; no branch)
+            // (the same bytes to one address).  A wave that starts past the last pixel (the grid is
+            // rounded up to 4 waves) has no partial slot: the wave-uniform test skips its store.
             const long bp = pix0 / 64;  // b * np64 + p (HW % 64 == 0)
-            float* o = part + ((bp * ncb + cb_off + cb) * (32 / sw) + q / qw) * 2;
-            o[0] = mean;
-            o[1] = m2;
+            if (pix0 < npix) {
+                float* o = part + ((bp * ncb + cb_off + cb) * (32 / sw) + q / qw) * 2;
+                o[0] = mean;
+                o[1] = m2;
+            }
         }
     }
 }
@@ -659,7 +663,13 @@ extern "C" int wc_sgg_update(const float* grad, const float* mu, const float* si
     return WC_OK;
 }
 
-extern "C" const char* wc_version(void) { return "weatherconverter_amd 0.1 gfx950"; }
+// wc_source_hash: defined in the build's generated object (weatherconverter_amd/_build.py source_hash)
+extern "C" const char* wc_source_hash(void);
+extern "C" const char* wc_version(void) {
+    static char v[96] = {0};
+    if (!v[0]) snprintf(v, sizeof v, "weatherconverter_amd 0.1 gfx950 src:%s", wc_source_hash());
+    return v;
+}
 
 // The instantiation name of the kernel this host thread launched last through a named launcher
 // (rocprofv3's demangled form), then cleared: "" when the last entry point did not name its kernel.

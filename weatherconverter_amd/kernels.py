@@ -8,6 +8,7 @@ RuntimeError.
 import ctypes
 import functools
 import os
+import threading
 from dataclasses import dataclass
 from typing import Dict, List, NamedTuple, Optional, Sequence, Tuple
 
@@ -306,9 +307,13 @@ def _piece_dtype() -> torch.dtype:
 
 
 def _split2(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(h, l) 16-bit pieces of an fp32 tensor: h = piece(v), l = piece(v - h) (round to nearest even)."""
+    """(h, l) 16-bit pieces of an fp32 tensor: h = piece(v), l = piece(v - h) (round to nearest even).
+    On the bf16 single-piece line l = 0, as the device packs write it (wc_x6.hpp split2_one / split2_pair
+    under WC_SINGLE16=2: that line has no correction products)."""
     dt = _piece_dtype()
     h = v.to(dt)
+    if dt == torch.bfloat16:
+        return h, torch.zeros_like(h)
     return h, (v - h.float()).to(dt)
 
 
@@ -1399,7 +1404,13 @@ def channel_sums(g: View) -> torch.Tensor:
     return sums
 
 
-_BSUM_QUEUE: Optional[list] = None
+# WC_ATTN_BWD192_FP32=1 (read once): the d = 192 dK / dV on the fp32-MFMA kernel; the C side follows the
+# dqkv_absmax argument alone (NULL selects the fp32 kernel), so the two sides cannot disagree
+_ATTN_BWD192_FP32 = os.environ.get('WC_ATTN_BWD192_FP32', '0') == '1'
+
+# The bsum deferral queue is per thread: autograd runs each device's backward on its own worker thread
+# (as _native's library selector), so two engines' backwards never share one queue.
+_BSUM = threading.local()
 
 
 def bsum(sums: torch.Tensor, idx: int, out: torch.Tensor, accumulate: bool = False, now: bool = False):
@@ -1409,25 +1420,24 @@ def bsum(sums: torch.Tensor, idx: int, out: torch.Tensor, accumulate: bool = Fal
     the caller reads before the flush)."""
     B, C, _ = sums.shape
     _req(out.is_cuda and out.is_contiguous() and out.numel() == C, 'bsum output')
-    if _BSUM_QUEUE is not None and not now:
-        _req(not _BSUM_QUEUE or _BSUM_QUEUE[0][0].shape[0] == B, 'deferred bsums of one batch size')
-        _BSUM_QUEUE.append((sums, idx, out, accumulate))
+    queue = getattr(_BSUM, 'queue', None)
+    if queue is not None and not now:
+        _req(not queue or queue[0][0].shape[0] == B, 'deferred bsums of one batch size')
+        queue.append((sums, idx, out, accumulate))
         return
     _native.call('wc_bsum', sums.data_ptr(), B, C, idx, out.data_ptr(), int(accumulate), _stream())
 
 
 def bsum_defer():
     """Queue every bsum until bsum_flush() (the training backward: ~200 small sums -> one launch)."""
-    global _BSUM_QUEUE
-    _req(_BSUM_QUEUE is None, 'bsum_defer: already deferring')
-    _BSUM_QUEUE = []
+    _req(getattr(_BSUM, 'queue', None) is None, 'bsum_defer: already deferring (this thread)')
+    _BSUM.queue = []
 
 
 def bsum_flush():
     """Launch the queued bsums (wc_bsum_batch): an output's k-th queued sum goes in launch k, so every
     output accumulates in queue order; ends the deferral."""
-    global _BSUM_QUEUE
-    q, _BSUM_QUEUE = _BSUM_QUEUE, None
+    q, _BSUM.queue = getattr(_BSUM, 'queue', None), None
     if not q:
         return
     launches: List[list] = []
@@ -1541,7 +1551,7 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
         # dQ on f16x3 with the output dims in three parts; dK / dV on f16x3 with the V rows in LDS (or, with
         # WC_ATTN_BWD192_FP32=1, on fp32 MFMA, which raises no bound)
         _req(_bound_ok(dout_bound, B), 'dout_bound: float32 [B] on the device')
-        amx = dqkv_absmax if os.environ.get('WC_ATTN_BWD192_FP32', '0') != '1' else None
+        amx = dqkv_absmax if not _ATTN_BWD192_FP32 else None
         if amx is not None:
             _req(_bound_ok(amx, B), 'dqkv_absmax: float32 [B] on the device')
         _timed(f'attention_bwd<{d}>', 'wc_attention_bwd_f16x3', 10.0 * B * N * N * C, *args, int(exps[0]),

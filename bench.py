@@ -46,6 +46,7 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.m
 BF16X6_PEAK_TFLOPS = round(2516.6 / 6, 1)
 # f16x3 conv: 3 f16 MFMAs (same rate as bf16) per fp32-equivalent block.
 F16X3_PEAK_TFLOPS = round(2516.6 / 3, 1)
+DENSE16_PEAK_TFLOPS = 2516.6  # dense f16 / bf16 MFMA peak (256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz)
 HBM_PEAK_GBS = 8000.0
 GFLOP_PER_IMAGE_STEP_256 = 590.61  # SURVEY.md §8(d) algorithmic FLOPs (probe hook count)
 
@@ -151,14 +152,16 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
     torch.cuda.synchronize()
     kernels.replay_timing(None)
     per, hbm = {}, {}
-    for name, flops, r0, r1, reps, nbytes in rep['events']:
-        d = (hbm if name.startswith(('gn_', 'split_')) else per).setdefault(name, [0, 0.0, 0.0, 0.0])
+    for name, flops, r0, r1, reps, nbytes, mfma in rep['events']:
+        d = (hbm if name.startswith(('gn_', 'split_')) else per).setdefault(name, [0, 0.0, 0.0, 0.0, 0.0])
         d[0] += 1
         d[1] += flops
         d[2] += r0.elapsed_time(r1) * 1e-3 / reps
         d[3] += nbytes
+        # dense 16-bit MFMA FLOPs issued: as stated by the launch, else the algorithmic count x pieces
+        d[4] += mfma if mfma is not None else flops * _pieces(name)
     name = max(per, key=lambda k: per[k][2])
-    n, fl, sec, abytes = per[name]
+    n, fl, sec, abytes, issued = per[name]
     mean_dur = sec / n
     achieved = (fl / n) / mean_dur / 1e12
     peak = _mode_peak(name)
@@ -208,6 +211,11 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
         'peak': peak,
         'unit': 'TFLOP/s',
         'frac': round(achieved / peak, 4),
+        # the matrix pipe's view: dense 16-bit MFMA FLOPs this kernel ISSUES per launch (pieces x, for the
+        # Winograd conv, 2/3 of the direct form's products on its 3x3 segment) / time, against the 2516.6
+        # TF/s dense f16/bf16 peak and against the sustained one-wave stream (frac above can exceed what
+        # the pipe does: it prices the direct conv's FLOPs)
+        'mfma_pipe': _pipe_leg(issued / n, mean_dur, sustained),
         'sustained_mfma_stream': sustained,
         'traffic': traffic,
         'traffic_source': traffic_src,
@@ -223,10 +231,29 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
         'mfma_ms_per_forward': round(total_mfma * 1e3 * groups, 3),
         'mfma_kernels': {k: {'launches': v[0] * groups, 'ms': round(v[2] * 1e3 * groups, 3),
                              'tflops': round(v[1] / v[2] / 1e12, 1), 'peak': _mode_peak(k),
-                             'frac': round(v[1] / v[2] / 1e12 / _mode_peak(k), 4), 'desc': _describe(k)}
+                             'frac': round(v[1] / v[2] / 1e12 / _mode_peak(k), 4),
+                             'mfma_pipe_frac': round(v[4] / v[2] / 1e12 / DENSE16_PEAK_TFLOPS, 4),
+                             'desc': _describe(k)}
                          for k, v in sorted(per.items(), key=lambda kv: -kv[1][2])},
         'hbm_kernels': hbm_leg(hbm, groups),
     }
+
+
+def _pieces(name: str) -> int:
+    """16-bit MFMAs per fp32-equivalent product of an instantiation's arithmetic mode (fp32 MFMA: 0, not
+    on the 16-bit pipe)."""
+    p = _mode_peak(name)
+    return 3 if p == F16X3_PEAK_TFLOPS else (6 if p == BF16X6_PEAK_TFLOPS else 0)
+
+
+def _pipe_leg(issued_per_launch: float, mean_dur: float, sustained) -> dict:
+    rate = issued_per_launch / mean_dur / 1e12
+    out = {'issued_gflop_per_launch': round(issued_per_launch / 1e9, 3), 'issued_tflops': round(rate, 1),
+           'peak': DENSE16_PEAK_TFLOPS, 'mfma_pipe_frac': round(rate / DENSE16_PEAK_TFLOPS, 4)}
+    if sustained:
+        out['vs_sustained_stream'] = round(rate / sustained['f16_mfma_tflops'], 4)
+        out['sustained_stream_tflops'] = sustained['f16_mfma_tflops']
+    return out
 
 
 def _mode_peak(name: str) -> float:

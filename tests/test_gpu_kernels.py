@@ -270,16 +270,18 @@ def _golden_scheduler(gd):
     return s
 
 
-def test_scheduler_tables_within_one_ulp_of_reference_host():
+def test_scheduler_tables_bit_exact_on_this_host():
+    """On the GPU box's host too (host-independent tables, tests/test_scheduler_tables.py): the four
+    linspace / cumprod tables equal the reference host's bit for bit, the square roots are the correctly
+    rounded ones of those, also on the device copies the step kernel reads."""
     from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
     gd = np.load(os.path.join(GOLDEN, 'sched.npz'))
     for T in (50, 1000):
         s = LinearNoiseScheduler(T, 0.0001, 0.02)
-        for n in TABLES:
-            a = getattr(s, n).cpu().numpy()
-            b = gd[f'T{T}_{n}']
-            ulp = np.spacing(np.abs(b).astype(np.float32))
-            assert np.all(np.abs(a - b) <= 4 * ulp), (T, n)
+        for n in ('betas', 'alphas', 'alpha_cum_prod', 'one_minus_cum_prod'):
+            assert np.array_equal(getattr(s, n).cpu().numpy(), gd[f'T{T}_{n}']), (T, n)
+        assert np.array_equal(s.sqrt_alpha_cum_prod.cpu().numpy(), np.sqrt(gd[f'T{T}_alpha_cum_prod']))
+        assert np.array_equal(s.sqrt_one_minus_alpha_cum_prod.cpu().numpy(), np.sqrt(gd[f'T{T}_one_minus_cum_prod']))
 
 
 def test_ddpm_step_bitwise_vs_reference(K):

@@ -50,13 +50,15 @@ CHILD = textwrap.dedent('''
     from weatherconverter_amd.diffusion_model.sample_ddpm import sample_tensor
     from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
     from weatherconverter_amd.synthetic import init_synthetic_
+    from weatherconverter_amd.diffusion_model.config import model_config
+    cfg = sys.argv[1]
     man = json.load(open(os.path.join(GOLDEN, 'manifest.json')))
-    mc = ModelConfig(**man['tiny']['config'])
+    mc = model_config(256) if cfg == '256' else ModelConfig(**man['tiny']['config'])
     net = Unet(mc)
     init_synthetic_(net, seed=0)
     net = net.to(dev).eval()
-    s = LinearNoiseScheduler(6, 0.0001, 0.02)
-    total = 4
+    s = LinearNoiseScheduler(3 if cfg == '256' else 6, 0.0001, 0.02)
+    total = 2 if cfg == '256' else 4
     ref = sample_tensor(net, s, total, mc.im_channels, mc.im_size, noise='philox', seed=77, graph=True)
     x0 = sample_sharded(net, s, total, mc.im_channels, mc.im_size, noise='philox', seed=77, graph=True)
     g = gather_samples(x0, total)
@@ -77,8 +79,11 @@ CHILD = textwrap.dedent('''
 ''')
 
 
-def test_rccl_world1_gathers_bit_identical():
-    r = subprocess.run([sys.executable, '-u', '-c', CHILD], cwd=ROOT, env=_env(), capture_output=True, text=True,
+@pytest.mark.parametrize('cfg', ['tiny', '256'])
+def test_rccl_world1_gathers_bit_identical(cfg):
+    """cfg '256': config 5's per-rank model (the 256-px BASELINE UNet), 2 images, T=3, through the RCCL
+    branch of sample_sharded / gather_samples / bench._gather_x0."""
+    r = subprocess.run([sys.executable, '-u', '-c', CHILD, cfg], cwd=ROOT, env=_env(), capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0, r.stderr[-4000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith('RCCL_RESULT ')]

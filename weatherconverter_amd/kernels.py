@@ -218,16 +218,18 @@ def _conv_args(segs: Sequence[Seg], N: int, bias: Optional[torch.Tensor], out: O
     return a
 
 
-def _timed(name: str, fn_name: str, flops: float, *args, nbytes: float = 0.0):
+def _timed(name: str, fn_name: str, flops: float, *args, nbytes: float = 0.0, mfma: Optional[float] = None):
     """Launch; while profiling, record timing under the launched kernel's exact instantiation name
     (the library reports it, in rocprofv3's form; ``name`` is the fallback for unnamed kernels).
 
     REPLAY with name '*' (or this instantiation's name): an idempotent launch is re-issued
     REPLAY['reps'] times back to back right after itself between one event pair and recorded as
-    (name, flops, e0, e1, reps, nbytes) in REPLAY['events'] — per-launch durations free of event
+    (name, flops, e0, e1, reps, nbytes, mfma) in REPLAY['events'] — per-launch durations free of event
     gaps; a launch that rewrites its own input runs once between its own events (reps 1).  nbytes =
     the launch's algorithmic HBM bytes (each input and output element once) where the wrapper
-    states it."""
+    states it; mfma = the dense 16-bit MFMA FLOPs the launch issues where they are not the
+    algorithmic FLOPs times its arithmetic mode's pieces (the Winograd conv: 2/3 of the direct form's
+    products on its 3x3 segment), else None."""
     if PROFILE is None and REPLAY is None:
         _native.call(fn_name, *args)
         return
@@ -247,9 +249,9 @@ def _timed(name: str, fn_name: str, flops: float, *args, nbytes: float = 0.0):
                 _native.call(fn_name, *args)
             r1.record()
             _native.last_kernel_name()
-            REPLAY['events'].append((exact, flops, r0, r1, reps, nbytes))
+            REPLAY['events'].append((exact, flops, r0, r1, reps, nbytes, mfma))
         else:
-            REPLAY['events'].append((exact, flops, e0, e1, 1, nbytes))
+            REPLAY['events'].append((exact, flops, e0, e1, 1, nbytes, mfma))
 
 
 def _flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int) -> float:
@@ -681,7 +683,19 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
     _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {0 if raw else 2}, {"true" if len(segs) == 2 else "false"}>',
            'wc_conv3x3_wino_f16x3', _flops(segs, Hm, Wm, w.N) if PROFILE is not None or REPLAY is not None else 0.0,
            ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(),
-           _ptr(a_bound) if (len(segs) == 2 or raw) else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res))
+           _ptr(a_bound) if (len(segs) == 2 or raw) else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res),
+           mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
+
+
+def wino_mfma_flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int, pieces: int = 3) -> float:
+    """Dense f16 MFMA FLOPs one wc_conv3x3_wino_f16x3 launch issues: per output pair and 16 input channels
+    12 K-steps on the 3x3 segment (the direct form's 18) and 2 on the 1x1 residual (its 2), each K-step
+    `pieces` MFMAs (f16x3: h*h + h*l + l*h); N counted padded to the kernel's channel tile."""
+    TH, BN = wino_tile(N)
+    Np = -(-N // BN) * BN
+    c0 = segs[0].view.C
+    c1 = segs[1].view.C if len(segs) == 2 else 0
+    return pieces * 2.0 * segs[0].view.B * Hm * Wm * Np * (6 * c0 + c1)
 
 
 def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: Optional[View], *,

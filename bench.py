@@ -281,7 +281,7 @@ def hbm_leg(hbm, groups: int = 1):
     if not hbm:
         return None
     out = {}
-    for k, (n, by, sec, _) in hbm.items():
+    for k, (n, by, sec, *_) in hbm.items():
         out[k] = {'launches': n * groups, 'ms': round(sec * 1e3 * groups, 3), 'gbytes': round(by * groups / 1e9, 3),
                   'achieved': round(by / sec / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                   'frac': round(by / sec / 1e9 / HBM_PEAK_GBS, 4)}

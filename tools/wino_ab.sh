@@ -1,17 +1,23 @@
 #!/bin/bash
-# Same-box A/B of the Winograd conv launches of one 256-px forward (tools/wino_shapes.py): the tree's
-# library against the variant libraries named in $VARS (weatherconverter_amd/lib/<name>, built by
-# tools/build_alt.sh), alternating, $REPS rounds.  Prints each run's total over the 40 launches.
+# Same-box A/B of the Winograd conv launches of one 256-px forward (tools/wino_shapes.py): the arms in
+# $VARS, alternating, $REPS rounds; each arm is LIB[+VAR=VALUE...], LIB = tree (this tree's library) or
+# the name of a variant library under weatherconverter_amd/lib/ (tools/build_alt.sh), e.g.
+#   VARS="tree tree+WC_WINO_ONEWAVE=1 var_head" bash tools/wino_ab.sh
+# Prints each run's total over the 40 launches (the per-launch lines stay in gpurun_out/).
 mkdir -p gpurun_out
 TAG=${TAG:-wab}
+SCRIPT=${SCRIPT:-tools/wino_shapes.py}
 for r in $(seq 1 ${REPS:-2}); do
-  for v in tree $VARS; do
-    if [ "$v" = tree ]; then
-      timeout -k 10 300 python3 -u tools/wino_shapes.py > gpurun_out/${TAG}_${v}_$r.txt 2>&1
-    else
-      WC_KERNEL_LIB=$PWD/weatherconverter_amd/lib/$v/libwc_kernels.so WC_ALLOW_STALE_LIB=1 timeout -k 10 300 python3 -u tools/wino_shapes.py > gpurun_out/${TAG}_${v}_$r.txt 2>&1
+  for arm in ${VARS:-tree}; do
+    lib=${arm%%+*}
+    envs=""
+    [ "$arm" != "$lib" ] && envs=$(echo "${arm#*+}" | tr '+' ' ')
+    if [ "$lib" != tree ]; then
+      envs="$envs WC_KERNEL_LIB=$PWD/weatherconverter_amd/lib/$lib/libwc_kernels.so WC_ALLOW_STALE_LIB=1"
     fi
-    rc=$?; [ $rc -ne 0 ] && { echo "$v rc=$rc"; tail -5 gpurun_out/${TAG}_${v}_$r.txt; exit $rc; }
-    echo "$v $r: $(tail -1 gpurun_out/${TAG}_${v}_$r.txt)"
+    out=gpurun_out/${TAG}_$(echo "$arm" | tr '+=/' '___')_$r.txt
+    env $envs timeout -k 10 300 python3 -u $SCRIPT > $out 2>&1
+    rc=$?; [ $rc -ne 0 ] && { echo "$arm rc=$rc"; tail -5 $out; exit $rc; }
+    echo "$arm $r: $(tail -1 $out)"
   done
 done

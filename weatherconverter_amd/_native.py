@@ -194,7 +194,10 @@ def load(build_if_missing: bool = True):
         _build.build()
     lib = ctypes.CDLL(path)
     verify_source_hash(lib, v)
+    stale_ok = os.environ.get('WC_ALLOW_STALE_LIB', '0') == '1'
     for name, argtypes in _SIGS.items():
+        if stale_ok and not hasattr(lib, name):  # an older A/B build may lack newer entry points
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
@@ -203,7 +206,8 @@ def load(build_if_missing: bool = True):
     lib.wc_last_kernel_name.argtypes = []
     lib.wc_last_kernel_name.restype = ctypes.c_char_p
     for name, value in _selectors.items():  # kernel-form selectors set before this variant was opened
-        getattr(lib, name)(value)
+        if hasattr(lib, name) or not stale_ok:
+            getattr(lib, name)(value)
     _libs[v] = lib
     return lib
 

@@ -45,9 +45,14 @@
 
 #include "wc_x6.hpp"
 
-// VALU instructions placed after each MFMA of a K-step (0: the compiler's own order)
-#ifndef WC_WINO_SGB
-#define WC_WINO_SGB 8
+// Ablation switches for timing experiments only (wrong results; tools/wino_ab.sh): bit 0 no SiLU, 1 no
+// GN/SiLU prologue, 2 no halo transform/split/LDS write in the K loop, 3 no weight loads in the K loop,
+// 4 no barrier in the K loop, 5 no halo loads in the K loop, 6 no A-fragment reads in the K loop.
+#ifndef WC_ABL
+#define WC_ABL 0
+#endif
+#ifndef WC_WINO_SCALAR
+#define WC_WINO_SCALAR 0
 #endif
 
 namespace {
@@ -99,7 +104,6 @@ struct WTile {
     static constexpr int CSTAGE = 8 * CPSTR;     // (piece 2) x (position 0 / 3) x (k-half 2)
     static constexpr int ITEMS = HR * 16;        // (halo row, tile pair, channel quad)
     static constexpr int I_PER_T = (ITEMS + NT - 1) / NT;
-    static_assert(ITEMS % 64 == 32, "a half-full wave repeats its lower half's items (conv3x3_wino_kernel)");
     static constexpr int C_PER_T = TH * 16 * 4 / NT;  // centre float4 items per thread
     static constexpr int BSTEP = BN * 64;        // weight bytes of one K-step: [piece 2][k-half 2][BN][8]
     static constexpr int STEPS = 12;             // (kernel row, position) per chunk
@@ -180,12 +184,8 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
 #pragma unroll
     for (int j = 0; j < T::I_PER_T; ++j) {
         // item tid + NT j: the items fill waves 0 .. in order (spreading them thinner over all four waves
-        // would not shorten any wave's instruction stream, only add wave 3's).  ITEMS = 32 mod 64, so a
-        // wave holds 64, 32 or no items of a slot; in a half-full wave lanes 32-63 repeat lanes 0-31's
-        // items (the same loads, the same LDS bytes to the same addresses): no lane-divergent branch, so
-        // the item VALU sits in the K-step's own basic block, between its MFMAs.
-        int i = tid + NT * j;
-        if (i >= T::ITEMS) i -= 32;
+        // would not shorten any wave's instruction stream, only add wave 3's)
+        const int i = tid + NT * j;
         const int hrow = i >> 4, tp = (i >> 2) & 3;
         const bool valid = i < T::ITEMS;
         const int iy = y0 - 1 + hrow;
@@ -199,15 +199,6 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
         hbase[j] = (((b * p.H + iy) * p.W + x0 - 1 + 4 * tp) * p.ldc0 + 4 * q) * 4;
         hwr[j] = valid ? (q >> 1) * T::PSTR + (hrow * 8 + 2 * tp) * 16 + (q & 1) * 8 : -1;
     }
-    // the slots this wave works on (wave-uniform): bit j = slot j holds items of this wave
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    const int vwork = [&] {
-        int m = 0;
-#pragma unroll
-        for (int j = 0; j < T::I_PER_T; ++j)
-            if (64 * wave_u + NT * j < T::ITEMS) m |= 1 << j;
-        return m;
-    }();
     f32x4 rh[T::I_PER_T][6];
     f32x4 rsc, rsh;
     auto load_ss = [&](int c) {
@@ -228,27 +219,80 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
         load_ss(c);
     };
     // GN + SiLU prologue of pixels k0 .. k1 - 1 of slot j, in place (zero padding after it), x 2^s
+#if WC_WINO_SCALAR
+    // Scalar form (no packed-f32 VALU: v_pk_fma / v_pk_mul cost several times a plain VALU op beside
+    // MFMAs, MI355X_MICROARCH.md): the chunk's GN scale / shift are pre-multiplied by 2^s once, so
+    // a' = x sc' + sh' = (x sc + sh) 2^s exactly, the exp2 argument is a' (-log2 e 2^-s) = a (-log2 e)
+    // exactly, and a' / (1 + 2^u) = SiLU(a) 2^s: the same bits as the vector form, one multiply fewer.
+    const float cu = -1.4426950408889634f * ainv;
+    auto prologue = [&](int j, int k0, int k1) {
+        if constexpr (PRO == 2) {
+            if (j == 0 && k0 == 0) {
+                rsc = rsc * ascale;
+                rsh = rsh * ascale;
+            }
+        }
+        auto act = [&](f32x4 a) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v;
+                if constexpr (PRO == 2) {
+                    const float ap = __builtin_fmaf(a[e], rsc[e], rsh[e]);
+                    const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(ap * cu));
+                    v = ap * r;
+                } else {
+                    v = a[e] * ascale;
+                }
+                a[e] = v;
+            }
+            return a;
+        };
+#pragma unroll
+        for (int k = k0; k < k1; ++k) {
+            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#if WC_WINO_SCALAR == 2
+            // the select over the expression itself: clang branches around each pixel's activation
+            rh[j][k] = ((hin[j] >> k) & 1u) ? act(rh[j][k]) : zero;
+#else
+            const f32x4 a = act(rh[j][k]);
+            rh[j][k] = ((hin[j] >> k) & 1u) ? a : zero;
+#endif
+        }
+    };
+#else
     auto prologue = [&](int j, int k0, int k1) {
 #pragma unroll
         for (int k = k0; k < k1; ++k) {
             f32x4 a = rh[j][k];
-            if constexpr (PRO == 2) {
+            if constexpr (PRO == 2 && !(WC_ABL & 2)) {
                 a = a * rsc + rsh;
-                a.x = silu_fast(a.x); a.y = silu_fast(a.y);
-                a.z = silu_fast(a.z); a.w = silu_fast(a.w);
+                if constexpr (!(WC_ABL & 1)) {
+                    a.x = silu_fast(a.x); a.y = silu_fast(a.y);
+                    a.z = silu_fast(a.z); a.w = silu_fast(a.w);
+                }
             }
-            // both arms computed first: a conditional operator over the vector expression itself made
-            // clang emit a branch around the SiLU of every pixel (and kept it out of the MFMA blocks)
-            const f32x4 av = a * ascale, zero = {0.f, 0.f, 0.f, 0.f};
-            rh[j][k] = ((hin[j] >> k) & 1u) ? av : zero;
+            rh[j][k] = ((hin[j] >> k) & 1u) ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
+#endif
     // Winograd input transform of tile t (0, 1) of slot j, 2-piece fp16 split, 8 fragment writes into
     // halo buffer hs
     auto transform = [&](int j, int t, int hs, int p0 = 0, int p1 = 4) {
+        if (hwr[j] < 0) return;  // idle item slot (ITEMS is not a multiple of NT)
         unsigned char* base = smem + hs * T::HSTAGE + hwr[j] + t * 16;
         const f32x4 d0 = rh[j][2 * t], d1 = rh[j][2 * t + 1], d2 = rh[j][2 * t + 2], d3 = rh[j][2 * t + 3];
+#if WC_WINO_SCALAR
+        f32x4 V[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            V[0][e] = d0[e] - d2[e];
+            V[1][e] = d1[e] + d2[e];
+            V[2][e] = d2[e] - d1[e];
+            V[3][e] = d1[e] - d3[e];
+        }
+#else
         const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
+#endif
 #pragma unroll
         for (int pos = p0; pos < p1; ++pos) {
             u32x2 a0, a1;
@@ -261,7 +305,6 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
     auto write_items = [&](int hs) {
 #pragma unroll
         for (int j = 0; j < T::I_PER_T; ++j) {
-            if (!((vwork >> j) & 1)) continue;
             prologue(j, 0, 6);
             transform(j, 0, hs);
             transform(j, 1, hs);
@@ -407,6 +450,10 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
     auto pro_at = [](int j) { return j == 0 ? 5 : 9; };
     // the slot's VALU at step st (relative step k = st - pro_at(j))
     auto slot_work = [&](int j, int k, int hs) {
+        if constexpr (WC_ABL & 4) {
+            if (k >= 0 && k < 3) prologue(j, 2 * k, 2 * k + 2);
+            return;
+        }
         if constexpr (T::I_PER_T == 1) {
             if (k >= 0 && k < 3) prologue(j, 2 * k, 2 * k + 2);
             if (k >= 3 && k < 7) transform(j, (k - 3) >> 1, hs, ((k - 3) & 1) * 2, ((k - 3) & 1) * 2 + 2);
@@ -415,18 +462,17 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
             if (k == 1 || k == 2) transform(j, k - 1, hs);
         }
     };
-    auto chunk = [&](auto P, auto L, auto VW, int c) __attribute__((always_inline)) {
+    auto chunk = [&](auto P, auto L, int c) {
         constexpr int PV = decltype(P)::value;
         constexpr bool LAST = decltype(L)::value != 0;
-        constexpr int VM = decltype(VW)::value;  // slots this wave works on (loads, prologue, transform)
         read_a(0, PV, 0, 0);  // step 0's fragments (the halo buffer was written before the last barrier)
 #pragma unroll
         for (int st = 0; st < T::STEPS; ++st) {
-            load_w((st + 2) % 3, T::STEPS * c + st + 2);
+            if (!(WC_ABL & 8) || c == 0) load_w((st + 2) % 3, T::STEPS * c + st + 2);
             if constexpr (!LAST) {
 #pragma unroll
                 for (int j = 0; j < T::I_PER_T; ++j)
-                    if (((VM >> j) & 1) && st == load_at(j)) load_slot(j, c + 1);
+                    if (!(WC_ABL & 32) && st == load_at(j)) load_slot(j, c + 1);
                 if (st == HALO_AT) {
                     load_ss(c + 1);
                     if constexpr (RI) load_centre(I0, c + 1, c + 1 < nri);
@@ -439,27 +485,15 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
                 if (st == 9) load_wres(c);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (st + 1 < T::STEPS) read_a((st + 1) & 1, PV, (st + 1) >> 2, (st + 1) & 3);
+            if (st + 1 < T::STEPS && (!(WC_ABL & 64) || c == 0)) read_a((st + 1) & 1, PV, (st + 1) >> 2, (st + 1) & 3);
             mfma_a(st & 1, st % 3, st & 3);
             if constexpr (!LAST) {
 #pragma unroll
-                for (int j = 0; j < T::I_PER_T; ++j)
-                    if ((VM >> j) & 1) slot_work(j, st - pro_at(j), PV ^ 1);
+                for (int j = 0; j < T::I_PER_T; ++j) slot_work(j, st - pro_at(j), PV ^ 1);
                 if constexpr (RI) {
                     if (st == 9) write_centre(I0, PV ^ 1);
                 }
             }
-#if WC_WINO_SGB
-            // the step's order: the next step's A fragment reads, then each MFMA followed by its share of
-            // the item VALU and LDS writes (keeps the live ranges of the interleaved VALU short)
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * MB, 0);
-#pragma unroll
-            for (int m = 0; m < 3 * MB; ++m) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, WC_WINO_SGB, 0);
-                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-            }
-#endif
         }
         if constexpr (RES) {
             if constexpr (RI) {
@@ -469,26 +503,19 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
                 if (ntail > 0) write_centre(I0, 1);  // tail chunk k in centre buffer (k + 1) & 1
             }
         }
-        __syncthreads();
+        if constexpr (!(WC_ABL & 16)) __syncthreads();
     };
     const std::integral_constant<int, 0> NL;
     const std::integral_constant<int, 1> LL;
-    // one straight-line chunk body per slot mask (wave-uniform branch once per K loop, not per step)
-    auto k_loop = [&](auto VW) __attribute__((always_inline)) {
+    {
         int c = 0;
-        if (pv0) chunk(I1, NL, VW, c++);
+        if (pv0) chunk(I1, NL, c++);
         for (; c + 1 < p.nck0 - 1; c += 2) {
-            chunk(I0, NL, VW, c);
-            chunk(I1, NL, VW, c + 1);
+            chunk(I0, NL, c);
+            chunk(I1, NL, c + 1);
         }
-        chunk(I0, LL, VW, p.nck0 - 1);
-    };
-    const std::integral_constant<int, (1 << T::I_PER_T) - 1> VALL;
-    const std::integral_constant<int, 1> VS0;
-    const std::integral_constant<int, 0> VNONE;
-    if (vwork == (1 << T::I_PER_T) - 1) k_loop(VALL);
-    else if (T::I_PER_T > 1 && vwork == 1) k_loop(VS0);
-    else k_loop(VNONE);
+        chunk(I0, LL, p.nck0 - 1);
+    }
     if constexpr (RES) {
         // tail residual chunk nri + k: weights in set k & 1 (the last 3x3 chunk's prefetch put tail steps 0
         // and 1 in sets 0 and 1; from here the load of step k + 2 is issued after step k's MFMAs), centre

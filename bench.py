@@ -270,6 +270,16 @@ def _mode_peak(name: str) -> float:
         return F16X3_PEAK_TFLOPS if targs[1] == 'true' else BF16X6_PEAK_TFLOPS
     if name.startswith(('conv3x3_w1_kernel', 'proj_pa_kernel', 'conv3x3_wino_kernel')):  # f16x3-only forms
         return F16X3_PEAK_TFLOPS
+    # training kernels (tools/bench_train.py): the attention backward <D, F3, ...>, the 3x3 weight gradient
+    # <WM, TH, PRO, F3>, the generic weight gradient <BM, BN, PRO, X6, F3>
+    if name.startswith(('attn_bwd6_dq_kernel', 'attn_bwd6_dkdv_kernel')):
+        return F16X3_PEAK_TFLOPS if len(targs) >= 2 and targs[1] == 'true' else BF16X6_PEAK_TFLOPS
+    if name.startswith('conv_wgrad3_kernel'):
+        return F16X3_PEAK_TFLOPS if len(targs) >= 4 and targs[3] == 'true' else BF16X6_PEAK_TFLOPS
+    if name.startswith('conv_wgrad_kernel'):
+        if len(targs) >= 5 and targs[4] == 'true':
+            return F16X3_PEAK_TFLOPS
+        return BF16X6_PEAK_TFLOPS if len(targs) >= 4 and targs[3] == 'true' else FP32_PEAK_TFLOPS
     return FP32_PEAK_TFLOPS
 
 

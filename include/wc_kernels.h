@@ -158,6 +158,11 @@ int wc_conv3x3_wino_tile_n(int N);
  * per SIMD with 16-row tiles (each weight fragment feeds four MFMA row blocks) where H % 16 == 0.
  * Bit-identical results.  Returns the previous mode (or WC_E_ARG); process-wide. */
 int wc_conv3x3_wino_set_onewave(int mode);
+/* Workgroup form of wc_conv3x3_wino_f16x3 with a GN+SiLU segment and BN = 128 weights: 0 (default) 4-wave
+ * workgroups; 1 8-wave workgroups of 256 output channels x 8 rows where N % 256 == 0 (one halo
+ * transform feeds twice the MFMA work); 2 as 1, else 8-wave 128 channels x 16 rows where H % 16 == 0.
+ * Same weight packing, bit-identical results.  Returns the previous mode (or WC_E_ARG); process-wide. */
+int wc_conv3x3_wino_set_form(int mode);
 /* Device re-pack of a [N][9*C0 + C1] fp32 ResBlock conv weight (K = (ky*3 + kx, c), then the 1x1
  * residual columns) into wc_conv3x3_wino_f16x3's layout and w_inv_scale[ceil(N/BN)*BN]: the F(2,3)
  * filter transform in float64, the per-channel power-of-two scale, one rounding to fp32, two fp16

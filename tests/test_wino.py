@@ -261,6 +261,19 @@ def test_conv3x3_wino_raw_segment_vs_float64(B, H, W, Ci, Co):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('form', [1, 2])
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr', [(2, 16, 32, 64, 128, 0), (1, 32, 16, 48, 256, 48), (1, 16, 16, 32, 128, 96),
+                                            (2, 32, 32, 128, 128, 128), (2, 16, 16, 64, 256, 0), (1, 8, 16, 32, 512, 512),
+                                            (1, 8, 32, 64, 256, 0), (2, 16, 16, 256, 128, 256), (2, 8, 32, 64, 256, 64)])
+def test_conv3x3_wino_eight_wave_forms_bit_identical(B, H, W, Ci, Co, Cr, form):
+    """The 8-wave workgroup forms (wc_conv3x3_wino_set_form 1: 256 channels x 8 rows where N % 256 == 0;
+    2: also 128 channels x 16 rows where H % 16 == 0) against the 4-wave form: bit-identical output,
+    per-image absmax and GroupNorm tile partials (the same products in the same order per output);
+    residual chunks interleaved and as a tail."""
+    _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_form(form if m else 0))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('B,H,W,Ci,Co,Cr,raw', [(2, 16, 32, 64, 128, 0, False), (1, 32, 16, 48, 256, 48, False),
                                                 (1, 16, 16, 32, 128, 96, False), (2, 32, 32, 128, 128, 128, False),
                                                 (1, 16, 32, 64, 128, 0, True)])
@@ -269,6 +282,11 @@ def test_conv3x3_wino_onewave_bit_identical(B, H, W, Ci, Co, Cr, raw):
     bit-identical output (bias, temb), per-image absmax and GroupNorm tile partials — the same products
     in the same order per output; residual chunks interleaved (equal and unequal chunk counts) and the
     raw-segment form."""
+    _compare_forms(B, H, W, Ci, Co, Cr, raw, lambda K, m: K.set_wino_onewave(m))
+
+
+def _compare_forms(B, H, W, Ci, Co, Cr, raw, select):
+    """One conv under select(K, 0) and under select(K, 1): outputs, absmax and GN partials bit-identical."""
     from weatherconverter_amd import kernels as K
     g = torch.Generator().manual_seed(53)
     x = (torch.randn((B, H, W, Ci), generator=g) * 2 + 1).cuda()
@@ -289,18 +307,19 @@ def test_conv3x3_wino_onewave_bit_identical(B, H, W, Ci, Co, Cr, raw):
             segs.append(K.Seg(K.View.full(xr), [(0, 0)], kbase=9 * Ci))
             kw['a_bound'] = xr.abs().reshape(B, -1).amax(1).contiguous() * 1.5
     wp = K.pack_wino(w, Ci, Cr)
-    res = {}
-    prev = K.set_wino_onewave(0)
+    res, names = {}, {}
+    prev = select(K, 0)
     try:
         for mode in (0, 1):
-            K.set_wino_onewave(mode)
+            select(K, mode)
             y = torch.empty((B, H, W, Co), device='cuda')
             gp = K.GnPart.attach(y, 16)
             amax = torch.zeros(B, device='cuda')
             K.conv3x3_wino(segs, wp, None if raw else bias, K.View.full(y), Hm=H, Wm=W, absmax=amax, gn=gp, **kw)
+            names[mode] = K._native.last_kernel_name()
             torch.cuda.synchronize()
             res[mode] = (y.cpu(), amax.cpu(), gp.part.cpu())
     finally:
-        K.set_wino_onewave(prev)
+        select(K, prev)
     for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b), (a - b).abs().max()
+        assert torch.equal(a, b), ((a - b).abs().max(), names)

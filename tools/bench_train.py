@@ -35,6 +35,9 @@ def main():
     ap.add_argument('--seed', type=int, default=3455)
     ap.add_argument('--mode', default='step', choices=['step', 'forward'])
     ap.add_argument('--profile', action='store_true', help='per-kernel-class event times of one step')
+    ap.add_argument('--no-roofline', action='store_true', help='skip the per-kernel roofline leg')
+    ap.add_argument('--no-cpu-baseline', action='store_true', help='skip the CPU reference-iteration leg')
+    ap.add_argument('--cpu-batch', type=int, default=1, help='CPU baseline batch (a bounded sample of B)')
     ap.add_argument('--precision', default='fp32-class', choices=['fp32-class', 'f16', 'bf16'],
                     help="'bf16' / 'f16': the 16-bit training lines (Unet.set_train_precision, single-piece builds)")
     args = ap.parse_args()
@@ -147,6 +150,8 @@ def train_step(args):
     ms = el / args.steps * 1e3
     fwd = sum(e[2].elapsed_time(e[0]) for e in evs) / len(evs)
     bwd = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
+    roof = None if args.no_roofline else roofline_leg(kernels, step, args.precision, ms)
+    cpu = None if args.no_cpu_baseline else cpu_baseline_leg(args)
     prof = None
     if args.profile:
         rec = kernels.profile_conv(True)
@@ -175,8 +180,93 @@ def train_step(args):
                    'backward': True, 'optimizer': 'torch.optim.Adam lr 1e-4', 'precision': args.precision},
         'train_tflops_algorithmic': round(3 * GFLOP_PER_IMAGE_STEP_256 * B / (ms * 1e-3) / 1e3, 1) if S == 256 else None,
         'loss_finite': bool(torch.isfinite(ls).all()), 'loss_first': float(ls[0]), 'loss_last': float(ls[-1]),
+        'roofline': roof,
+        'cpu_baseline': cpu,
         'kernel_classes': prof,
     }))
+
+
+def roofline_leg(kernels, step, precision: str, ms_iter: float):
+    """One training iteration with HIP events around every named launch (kernels.profile_conv): the
+    dominant instantiation by time is the roofline kernel; achieved = its algorithmic FLOPs per launch
+    (fp32-equivalent) / its mean duration, against its arithmetic's ceiling on this line: on the 16-bit
+    lines the split-precision templates compute with ONE 16-bit piece (the dense bf16 / f16 MFMA peak,
+    2516.6 TF/s); on the fp32-class line f16x3 (/3), bf16x6 (/6) or fp32 MFMA (bench.py _mode_peak).
+    Beside it the whole iteration's algorithmic rate (3x the forward's FLOPs) against the same peak."""
+    import bench
+    rec = kernels.profile_conv(True)
+    torch.cuda._sleep(1 << 28)  # the host enqueues the whole iteration ahead of the GPU: events bracket kernels
+    step(0)
+    torch.cuda.synchronize()
+    kernels.profile_conv(False)
+    per = {}
+    for name, flops, e0, e1 in rec:
+        d = per.setdefault(name, [0, 0.0, 0.0])
+        d[0] += 1
+        d[1] += flops
+        d[2] += e0.elapsed_time(e1) * 1e-3
+
+    def peak(name):
+        p = bench._mode_peak(name)
+        return bench.DENSE16_PEAK_TFLOPS if (precision in ('bf16', 'f16') and p == bench.F16X3_PEAK_TFLOPS) else p
+    mfma = {k: v for k, v in per.items() if v[1] > 0 and ('conv' in k or 'attn' in k or 'attention' in k
+                                                          or 'proj' in k or 'wgrad' in k)}
+    name = max(mfma, key=lambda k: mfma[k][2])
+    n, fl, sec = mfma[name]
+    ach = fl / n / (sec / n) / 1e12
+    top = sorted(mfma.items(), key=lambda kv: -kv[1][2])[:12]
+    iter_peak = bench.DENSE16_PEAK_TFLOPS if precision in ('bf16', 'f16') else bench.F16X3_PEAK_TFLOPS
+    it = 3 * GFLOP_PER_IMAGE_STEP_256 * 32 / (ms_iter * 1e-3) / 1e3
+    return {
+        'kernel': name, 'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak(name), 'unit': 'TFLOP/s',
+        'frac': round(ach / peak(name), 4), 'traffic': None, 'launches_per_iter': n,
+        'mean_launch_ms': round(sec / n * 1e3, 4), 'gflop_per_launch': round(fl / n / 1e9, 2),
+        'mean_launch_ms_source': 'HIP events around each launch of one iteration (kernels.profile_conv), host '
+                                 'enqueue ahead of the GPU',
+        'iteration': {'tflops_algorithmic': round(it, 1), 'peak': iter_peak, 'frac': round(it / iter_peak, 4),
+                      'flops': '3 x the forward (590.61 GFLOP per 256-px image, SURVEY.md 8(d)) x 32 images'},
+        'top_kernels': {k: {'launches': v[0], 'ms': round(v[2] * 1e3, 2), 'tflops': round(v[1] / v[2] / 1e12, 1),
+                            'peak': peak(k), 'frac': round(v[1] / v[2] / 1e12 / peak(k), 4)} for k, v in top},
+        'named_launch_ms': round(sum(v[2] for v in per.values()) * 1e3, 2),
+    }
+
+
+def cpu_baseline_leg(args):
+    """The reference training iteration (train_ddpm.py:94-114: add_noise, UNet forward, MSE, backward;
+    Adam excluded) on the CPU: the oracle's op-for-op PyTorch restatement of unet_base.Unet with autograd,
+    fp32, at a bounded sample of the batch (--cpu-batch images at the same size), on the CPUs this process
+    may use, one timed iteration after one warm-up; value = iterations/s scaled to the GPU line's batch."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle.unet_oracle import unet_forward, unet_state_dict_keys
+    from weatherconverter_amd.diffusion_model.config import model_config
+    from weatherconverter_amd.synthetic import synth_tensor
+    share = bench._cpu_share()
+    torch.set_num_threads(share['usable_cpus'])
+    mc = model_config(args.size)
+    sd = {k: synth_tensor(k, s).requires_grad_() for k, s in unet_state_dict_keys(mc).items()}
+    B = args.cpu_batch
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.rand((B, 3, args.size, args.size), generator=g) * 2 - 1
+    nz = torch.randn(x0.shape, generator=g)
+    t = torch.randint(0, 1000, (B, ), generator=g)
+    acp = torch.cumprod(1 - torch.linspace(0.0001, 0.02, 1000), 0)
+
+    def it():
+        noisy = acp[t].sqrt()[:, None, None, None] * x0 + (1 - acp[t]).sqrt()[:, None, None, None] * nz
+        loss = torch.nn.functional.mse_loss(unet_forward(sd, mc, noisy, t), nz)
+        loss.backward()
+        for v in sd.values():
+            v.grad = None
+    it()
+    t0 = time.perf_counter()
+    it()
+    dt = time.perf_counter() - t0
+    return {'value': round(B / args.batch / dt, 6), 'unit': 'iter/s', 'cores': share['usable_cpus'], 'kind': 'port',
+            'ms_per_iter_sample': round(dt * 1e3, 1), 'host': share,
+            'sample': f'oracle PyTorch-CPU restatement of the reference iteration (add_noise + UNet forward + MSE + '
+                      f'autograd backward, no Adam), {args.size}px, B={B} of the line\'s {args.batch}, 1 timed '
+                      f'iteration after 1 warm-up; iterations/s scaled by {B}/{args.batch}'}
 
 
 if __name__ == '__main__':

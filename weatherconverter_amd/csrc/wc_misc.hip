@@ -139,6 +139,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
         }
     }
     const int q = lane & 7, row = lane >> 3;  // (channel quad, pixel row) of the store / GN lane map
+    // the GN partials [npix / 64][ncb][32 / sw][2] as a range-checked buffer (GN only)
+    const __amdgpu_buffer_rsrc_t srd_part = __builtin_amdgcn_make_buffer_rsrc(
+        part, (short)0, GN ? (int)((npix / 64) * ncb * (32 / sw) * 8) : 0, 0x00020000);
     // branch-free stores (a divergent branch around them made the compiler spill the accumulators):
     // a row past the end holds the clamped last pixel's values (lanes past the end computed it), so it
     // is stored to that pixel again, the same bytes
@@ -194,13 +197,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
             m2 += __shfl_xor(m2, 32, 64);
             // after the butterflies every lane of a sub-slot holds its (mean, M2): all of them store it
             // (the same bytes to one address).  A wave that starts past the last pixel (the grid is
-            // rounded up to 4 waves) has no partial slot: the wave-uniform test skips its store.
+            // rounded up to 4 waves) has no partial slot: the stores go through a buffer resource
+            // sized to the partials, whose range check drops them (a branch around them, even a
+            // wave-uniform one, made the compiler spill: 75 -> 150 us per launch)
             const long bp = pix0 / 64;  // b * np64 + p (HW % 64 == 0)
-            if (pix0 < npix) {
-                float* o = part + ((bp * ncb + cb_off + cb) * (32 / sw) + q / qw) * 2;
-                o[0] = mean;
-                o[1] = m2;
-            }
+            const unsigned o = (unsigned)(((bp * ncb + cb_off + cb) * (32 / sw) + q / qw) * 2 * 4);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean), srd_part, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m2), srd_part, o + 4u, 0, 0);
         }
     }
 }

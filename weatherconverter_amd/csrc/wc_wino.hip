@@ -47,7 +47,8 @@
 
 // Ablation switches for timing experiments only (wrong results; tools/wino_ab.sh): bit 0 no SiLU, 1 no
 // GN/SiLU prologue, 2 no halo transform/split/LDS write in the K loop, 3 no weight loads in the K loop,
-// 4 no barrier in the K loop, 5 no halo loads in the K loop, 6 no A-fragment reads in the K loop.
+// 4 no barrier in the K loop, 5 no halo loads in the K loop, 6 no A-fragment reads in the K loop, 7 no
+// output stores.
 #ifndef WC_ABL
 #define WC_ABL 0
 #endif
@@ -90,11 +91,17 @@ struct WDev {
 // MB: 32-tile MFMA row blocks per wave (4 image rows x 8 tiles each): 2 (two waves per SIMD) or 4 (one
 // wave per SIMD, 512 registers: each weight fragment feeds twice the MFMAs, halving the vector-memory
 // traffic per MFMA that the two-wave form is bound by)
-template <int TH, int BN, int MB = 2>
+// NW: waves per workgroup, 4 or 8 (one 8-wave workgroup per CU at two waves per SIMD: its halo's GN+SiLU /
+// transform / split VALU and loads feed twice the MFMA work -- BN = 256 channels over 8 rows, or BN = 128
+// over 16 rows).  The weights stay packed in 128-channel tiles (wc_conv3x3_wino_tile_n): a 256-channel
+// workgroup reads two of them.
+template <int TH, int BN, int MB = 2, int NW = 4>
 struct WTile {
+    static constexpr int NT = 64 * NW;
     static constexpr int WAVES_N = BN / 32;
-    static constexpr int WAVES_M = 4 / WAVES_N;
-    static_assert(WAVES_N * WAVES_M == 4 && WAVES_M * 4 * MB == TH, "each wave owns 4 MB rows x 8 tiles x 32 channels");
+    static constexpr int WAVES_M = NW / WAVES_N;
+    static_assert(WAVES_N * WAVES_M == NW && WAVES_M * 4 * MB == TH, "each wave owns 4 MB rows x 8 tiles x 32 channels");
+    static constexpr int PBN = BN > 128 ? 128 : BN;  // channels per packed weight tile
     static constexpr int HR = TH + 2;            // halo rows
     // one (piece, position, k-half) plane of [halo row][tile] 16-byte fragments; the 16 extra bytes make
     // the k-half stride 16 mod 128 so the item writes of a 16-lane group hit 16 distinct 8-byte slots
@@ -105,7 +112,7 @@ struct WTile {
     static constexpr int ITEMS = HR * 16;        // (halo row, tile pair, channel quad)
     static constexpr int I_PER_T = (ITEMS + NT - 1) / NT;
     static constexpr int C_PER_T = TH * 16 * 4 / NT;  // centre float4 items per thread
-    static constexpr int BSTEP = BN * 64;        // weight bytes of one K-step: [piece 2][k-half 2][BN][8]
+    static constexpr int BSTEP = PBN * 64;       // weight bytes of one K-step: [piece 2][k-half 2][PBN][8]
     static constexpr int STEPS = 12;             // (kernel row, position) per chunk
 };
 
@@ -120,10 +127,12 @@ WC_DEVICE int wg_tile(int r) { return wg_idx(r) & 7; }
 // PRO: 2 = GroupNorm affine + SiLU prologue on segment 0 (static Samuelson bound), 0 = raw segment 0
 // under the per-image bound abound (the training data gradients).  RES: the fused 1x1 residual segment
 // (raw input, f16x3 under the per-image bound abound).
-template <int TH, int BN, int PRO, bool RES, int MB = 2>
-__global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev p) {
+template <int TH, int BN, int PRO, bool RES, int MB = 2, int NW = 4>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(MB == 4 ? 1 : 2, MB == 4 ? 1 : 2)))
+void conv3x3_wino_kernel(WDev p) {
     static_assert((PRO == 2 || PRO == 0) && !(PRO == 0 && RES), "GN+SiLU (+ residual) or one raw segment");
-    using T = WTile<TH, BN, MB>;
+    using T = WTile<TH, BN, MB, NW>;
+    constexpr int NT = T::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* const cbase = smem + 2 * T::HSTAGE;  // residual centre buffers
 
@@ -164,10 +173,11 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
     // residual chunk r < nri rides in 3x3 chunk r as a 13th K-step; the rest (nck1 > nck0) follow as a
     // tail phase, one K-step and one barrier each
     // (TH = 16: the centre staging of four items per thread does not fit beside the halo's; all tail)
-    constexpr bool RI = RES && (TH == 8 || MB == 4);
+    constexpr bool RI = RES && (T::C_PER_T <= 2 || MB == 4);
     const int nri = RI ? min(p.nck0, p.nck1) : 0;
     const int ntail = RES ? p.nck1 - nri : 0;
-    const unsigned wtile = (unsigned)tile_n * (unsigned)(S * T::BSTEP);
+    constexpr int WPT = T::PBN / 32;  // waves per packed weight tile
+    const unsigned wtile = (unsigned)(tile_n * (BN / T::PBN) + wn / WPT) * (unsigned)(S * T::BSTEP);
 
     const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
     const __amdgpu_buffer_rsrc_t srd1 = make_srd(RES ? p.src1 : p.src0);
@@ -313,9 +323,9 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
 
     // ---- residual centre items: item i = tid + NT j = (row i >> 6, pixel (i >> 2) & 15, quad i & 3) ----
     f32x4 rc[2][RES ? T::C_PER_T : 1];
-    const int cpx = (tid >> 2) & 15, crow0 = tid >> 6;  // item j: row crow0 + 4 j
+    const int cpx = (tid >> 2) & 15, crow0 = tid >> 6;  // item j: row crow0 + NW j
     const unsigned coff0 = (unsigned)(((b * p.H + y0 + crow0) * p.W + x0 + cpx) * p.ldc1 + 4 * q);
-    const unsigned cstep = (unsigned)(4 * p.W * p.ldc1);
+    const unsigned cstep = (unsigned)(NW * p.W * p.ldc1);
     // position 0 takes x at even columns, position 3 takes -x at odd columns (plane index 1)
     const int cwr0 = (cpx & 1) * 2 * T::CPSTR + (q >> 1) * T::CPSTR + (crow0 * 8 + (cpx >> 1)) * 16 + (q & 1) * 8;
     // live = false: the same loads at an out-of-range offset (zeros, no traffic): every load is issued
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
         for (int j = 0; j < T::C_PER_T; ++j) {
             u32x2 a0, a1;
             split2_f16(rc[PV][j] * sg, a0, a1);
-            unsigned char* d = base + j * 4 * 8 * 16;  // + 4 rows
+            unsigned char* d = base + j * NW * 8 * 16;  // + NW rows
             *reinterpret_cast<u32x2*>(d) = a0;
             *reinterpret_cast<u32x2*>(d + 4 * T::CPSTR) = a1;
         }
@@ -347,7 +357,7 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
     int abase[MB];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) abase[mb] = ((4 * MB * wm + 4 * mb + wg_row(l32)) * 8 + wg_tile(l32)) * 16;
-    const unsigned wlane = (unsigned)(half * BN * 16 + (wn * 32 + l32) * 16);
+    const unsigned wlane = (unsigned)(half * T::PBN * 16 + ((wn % WPT) * 32 + l32) * 16);
 
     u32x4 wreg[3][2];  // [set][piece]
     // weight fragments of K-step st (past the end: the last step again, unused): issued unconditionally
@@ -358,14 +368,14 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
         s = s < S ? s : S - 1;
         const int off = (int)(wtile + (unsigned)s * T::BSTEP);
 #pragma unroll
-        for (int pc = 0; pc < 2; ++pc) wreg[set][pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * BN * 16), off);
+        for (int pc = 0; pc < 2; ++pc) wreg[set][pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * T::PBN * 16), off);
     };
     u32x4 wres[2];  // the interleaved residual step's weights (their own set: the 3-set cycle stays 12-periodic)
     auto load_wres = [&](int r) {
         const int s = S0 + r < S ? S0 + r : S - 1;
         const int off = (int)(wtile + (unsigned)s * T::BSTEP);
 #pragma unroll
-        for (int pc = 0; pc < 2; ++pc) wres[pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * BN * 16), off);
+        for (int pc = 0; pc < 2; ++pc) wres[pc] = bload_u4s(srdw, wlane + (unsigned)(pc * 2 * T::PBN * 16), off);
     };
 
     f32x16 acc[4][MB];
@@ -584,10 +594,17 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
             vmax = fmaxf(vmax, fmaxf(fabsf(ya), fabsf(yb)));
         }
         if (nok) {
+            if constexpr (WC_ABL & 128) {  // ablation: no output stores (one store only if a sum hits a magic value)
+                float sum = 0.f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                bstore_f1s(srd_out, vo[r >> 2], (r & 3) * 2 * so_px, acc[0][mb][r]);
-                bstore_f1s(srd_out, vo[r >> 2], ((r & 3) * 2 + 1) * so_px, acc[1][mb][r]);
+                for (int r = 0; r < 16; ++r) sum += acc[0][mb][r] + acc[1][mb][r];
+                if (sum == 1234.5678f) bstore_f1s(srd_out, vo[0], 0, sum);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    bstore_f1s(srd_out, vo[r >> 2], (r & 3) * 2 * so_px, acc[0][mb][r]);
+                    bstore_f1s(srd_out, vo[r >> 2], ((r & 3) * 2 + 1) * so_px, acc[1][mb][r]);
+                }
             }
         }
     }
@@ -609,13 +626,13 @@ __global__ __launch_bounds__(NT, MB == 4 ? 1 : 2) void conv3x3_wino_kernel(WDev 
     }
 }
 
-template <int TH, int BN, int PRO, bool RES, int MB = 2>
+template <int TH, int BN, int PRO, bool RES, int MB = 2, int NW = 4>
 int launch_wino(const WDev& d, hipStream_t stream) {
-    using T = WTile<TH, BN, MB>;
+    using T = WTile<TH, BN, MB, NW>;
     constexpr int lds = 2 * T::HSTAGE + (RES ? 2 * T::CSTAGE : 0);
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, PRO, RES, MB>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wino_kernel<TH, BN, PRO, RES, MB, NW>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -625,8 +642,8 @@ int launch_wino(const WDev& d, hipStream_t stream) {
     p.tiles_y = p.H / TH;
     p.ntiles_n = (p.N + BN - 1) / BN;
     dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES), WC_TI(MB)});
-    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, PRO, RES, MB>), grid, dim3(NT), lds, stream, p);
+    WC_SET_NAME("conv3x3_wino_kernel", {WC_TI(TH), WC_TI(BN), WC_TI(PRO), WC_TB(RES), WC_TI(MB), WC_TI(NW)});
+    hipLaunchKernelGGL((conv3x3_wino_kernel<TH, BN, PRO, RES, MB, NW>), grid, dim3(T::NT), lds, stream, p);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -637,10 +654,24 @@ int g_wino_onewave = [] {
     const char* e = getenv("WC_WINO_ONEWAVE");
     return e ? atoi(e) : 0;
 }();
+// 0: 4-wave workgroups; 1: 8-wave workgroups of 256 channels x 8 rows where N % 256 == 0 (GN+SiLU
+// segment), else as 0; 2: as 1, else 8-wave 128 x 16 rows where H % 16 == 0.  Initial value from
+// WC_WINO_FORM (A/B runs).
+int g_wino_form = [] {
+    const char* e = getenv("WC_WINO_FORM");
+    return e ? atoi(e) : 0;
+}();
 
 }  // namespace
 
 extern "C" int wc_conv3x3_wino_tile_n(int N) { return N <= 64 ? 64 : 128; }
+
+extern "C" int wc_conv3x3_wino_set_form(int mode) {
+    if (mode < 0 || mode > 2) return WC_E_ARG;
+    const int prev = g_wino_form;
+    g_wino_form = mode;
+    return prev;
+}
 
 extern "C" int wc_conv3x3_wino_set_onewave(int mode) {
     if (mode < 0 || mode > 1) return WC_E_ARG;
@@ -705,6 +736,10 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     const long ntn = (a->N + BN - 1) / BN;
     if (w_bytes != ntn * (12L * d.nck0 + d.nck1) * BN * 64 || w_bytes >= (1L << 31)) return WC_E_SHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 128 && pro == 2 && g_wino_form >= 1 && d.N % 256 == 0)  // 8 waves: 256 channels x 8 rows
+        return res ? launch_wino<8, 256, 2, true, 2, 8>(d, s) : launch_wino<8, 256, 2, false, 2, 8>(d, s);
+    if (BN == 128 && pro == 2 && g_wino_form == 2 && d.H % 16 == 0)  // 8 waves: 128 channels x 16 rows
+        return res ? launch_wino<16, 128, 2, true, 2, 8>(d, s) : launch_wino<16, 128, 2, false, 2, 8>(d, s);
     if (BN == 128 && g_wino_onewave == 1 && d.H % 16 == 0) {  // the one-wave form (16-row tiles)
         if (pro == 0) return launch_wino<16, 128, 0, false, 4>(d, s);
         return res ? launch_wino<16, 128, 2, true, 4>(d, s) : launch_wino<16, 128, 2, false, 4>(d, s);

@@ -478,6 +478,12 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
     return max(-60, min(60, math.floor(math.log2(2.0**14 / bound))))
 
 
+def set_wino_form(mode: int) -> int:
+    """wc_conv3x3_wino_set_form: 0 the 4-wave Winograd workgroups, 1 8-wave 256-channel ones where
+    N % 256 == 0, 2 also 8-wave 128-channel x 16-row ones; returns the previous mode."""
+    return _native.set_selector('wc_conv3x3_wino_set_form', int(mode), lambda v: v >= 0)
+
+
 def set_conv3_onewave(mode: int) -> int:
     """wc_conv3x3_set_onewave: 0 off (default), 1 forced, -1 where it fills the chip; returns the previous mode."""
     prev = _native.set_selector('wc_conv3x3_set_onewave', int(mode), lambda v: v >= -1)

@@ -153,7 +153,7 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
     kernels.replay_timing(None)
     per, hbm = {}, {}
     for name, flops, r0, r1, reps, nbytes, mfma in rep['events']:
-        d = (hbm if name.startswith(('gn_', 'split_')) else per).setdefault(name, [0, 0.0, 0.0, 0.0, 0.0])
+        d = (hbm if name.startswith(('gn_', 'split_', 'wino_vsplit')) else per).setdefault(name, [0, 0.0, 0.0, 0.0, 0.0])
         d[0] += 1
         d[1] += flops
         d[2] += r0.elapsed_time(r1) * 1e-3 / reps

@@ -163,6 +163,21 @@ int wc_conv3x3_wino_set_onewave(int mode);
  * transform feeds twice the MFMA work); 2 as 1, else 8-wave 128 channels x 16 rows where H % 16 == 0.
  * Same weight packing, bit-identical results.  Returns the previous mode (or WC_E_ARG); process-wide. */
 int wc_conv3x3_wino_set_form(int mode);
+/* The GN + SiLU segment 0 of a wc_conv3x3_wino_f16x3 conv, transformed and split ONCE (instead of once
+ * per output-channel tile inside the conv): segment 0 of `args` (scale / shift / silu set, W % 16 == 0)
+ * GroupNorm-affine'd, SiLU'd, scaled by 2^s (s = a_exp - 1, per image clamped to 13 - e(a_bound[b]) when
+ * args has a residual segment -- the conv's own exponent), Winograd input-transformed (V0..V3 of every
+ * output pair) and split into two fp16 pieces, stored in the conv's LDS image order:
+ * vout[b][C/16][plane 16][H][W/2] x 16 bytes (wc_wino_vsplit_bytes).  Bit for bit what the conv's own
+ * prologue computes. */
+int wc_wino_vsplit_bytes(int B, int C, int H, int W, int64_t* bytes);
+int wc_wino_vsplit_f16x3(const wc_conv_args* args, int a_exp, const float* a_bound, void* vout, int64_t v_bytes,
+                         void* stream);
+/* wc_conv3x3_wino_f16x3 reading segment 0 from wc_wino_vsplit_f16x3's output (same args, a_exp, a_bound):
+ * its halo planes go into LDS by LDS-DMA with no per-item VALU; bit-identical results. */
+int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
+                             const float* w_inv_scale, const float* a_bound, const void* vpre, int64_t v_bytes,
+                             void* stream);
 /* Device re-pack of a [N][9*C0 + C1] fp32 ResBlock conv weight (K = (ky*3 + kx, c), then the 1x1
  * residual columns) into wc_conv3x3_wino_f16x3's layout and w_inv_scale[ceil(N/BN)*BN]: the F(2,3)
  * filter transform in float64, the per-channel power-of-two scale, one rounding to fp32, two fp16

@@ -274,6 +274,19 @@ def test_conv3x3_wino_eight_wave_forms_bit_identical(B, H, W, Ci, Co, Cr, form):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr', [(2, 16, 32, 64, 128, 0), (1, 32, 16, 48, 256, 48), (1, 16, 16, 32, 128, 96),
+                                            (2, 32, 32, 128, 128, 128), (2, 16, 16, 64, 256, 0), (1, 8, 16, 32, 512, 512),
+                                            (3, 8, 32, 64, 768, 0), (2, 16, 16, 256, 128, 256), (2, 16, 48, 32, 64, 0),
+                                            (1, 32, 32, 64, 64, 64)])
+def test_conv3x3_wino_presplit_bit_identical(B, H, W, Ci, Co, Cr):
+    """The pre-split form (wc_wino_vsplit_f16x3 once per input, then wc_conv3x3_wino_f16x3_vp copying the
+    halo planes by LDS-DMA) against the in-conv prologue: bit-identical output, absmax and GroupNorm
+    partials (the same arithmetic in a separate pass); 64- and 128-channel tiles, residual interleaved
+    and as a tail, per-image residual exponents."""
+    _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('B,H,W,Ci,Co,Cr,raw', [(2, 16, 32, 64, 128, 0, False), (1, 32, 16, 48, 256, 48, False),
                                                 (1, 16, 16, 32, 128, 96, False), (2, 32, 32, 128, 128, 128, False),
                                                 (1, 16, 32, 64, 128, 0, True)])

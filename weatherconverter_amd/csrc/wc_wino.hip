@@ -62,6 +62,12 @@ using namespace wcx6;
 
 constexpr int NT = 256;
 
+// 16 bytes per lane from a buffer straight into LDS at the wave-uniform base dst + 16 lane (device-only
+// helper: the target builtin must not appear in a kernel body the host pass parses)
+WC_DEVICE void wino_lds16(__amdgpu_buffer_rsrc_t srd, void* dst, unsigned voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
+
 struct WDev {
     const float* src0;
     int C0, ldc0;
@@ -86,6 +92,8 @@ struct WDev {
     float* gn_part;
     int gn_ncb, gn_sw, gn_c0, gn_np64;
     int tiles_x, tiles_y, ntiles_n;
+    const unsigned char* vpre;  // PRO 3: segment 0 pre-transformed and split (wino_vsplit_kernel layout)
+    long vimg;                  // PRO 3: bytes of one image's V
 };
 
 // MB: 32-tile MFMA row blocks per wave (4 image rows x 8 tiles each): 2 (two waves per SIMD) or 4 (one
@@ -95,7 +103,7 @@ struct WDev {
 // transform / split VALU and loads feed twice the MFMA work -- BN = 256 channels over 8 rows, or BN = 128
 // over 16 rows).  The weights stay packed in 128-channel tiles (wc_conv3x3_wino_tile_n): a 256-channel
 // workgroup reads two of them.
-template <int TH, int BN, int MB = 2, int NW = 4>
+template <int TH, int BN, int MB = 2, int NW = 4, bool VP = false>
 struct WTile {
     static constexpr int NT = 64 * NW;
     static constexpr int WAVES_N = BN / 32;
@@ -105,7 +113,10 @@ struct WTile {
     static constexpr int HR = TH + 2;            // halo rows
     // one (piece, position, k-half) plane of [halo row][tile] 16-byte fragments; the 16 extra bytes make
     // the k-half stride 16 mod 128 so the item writes of a 16-lane group hit 16 distinct 8-byte slots
-    static constexpr int PSTR = HR * 128 + 16;
+    // (VP, PRO 3: the planes arrive by LDS-DMA in 1-KiB pieces, no item writes: no pad, planes contiguous)
+    static constexpr int PSTR = HR * 128 + (VP ? 0 : 16);
+    static constexpr int DPW = 16 * HR * 8 / 64 / NW;  // VP: 1-KiB LDS-DMA pieces per wave per chunk
+    static_assert(!VP || 16 * HR * 8 == DPW * 64 * NW, "VP: the halo stage is a whole number of pieces per wave");
     static constexpr int HSTAGE = 16 * PSTR;     // planes (piece 2) x (position 4) x (k-half 2)
     static constexpr int CPSTR = TH * 128 + 16;  // residual centre plane ([row][tile])
     static constexpr int CSTAGE = 8 * CPSTR;     // (piece 2) x (position 0 / 3) x (k-half 2)
@@ -125,13 +136,17 @@ WC_DEVICE int wg_row(int r) { return 2 * wg_grp(r) + (wg_idx(r) >> 3); }
 WC_DEVICE int wg_tile(int r) { return wg_idx(r) & 7; }
 
 // PRO: 2 = GroupNorm affine + SiLU prologue on segment 0 (static Samuelson bound), 0 = raw segment 0
-// under the per-image bound abound (the training data gradients).  RES: the fused 1x1 residual segment
-// (raw input, f16x3 under the per-image bound abound).
+// under the per-image bound abound (the training data gradients), 3 = segment 0 already GN+SiLU'd,
+// Winograd-transformed and split by wino_vsplit_kernel (the same arithmetic, once per input instead of
+// once per output-channel tile): its halo planes are copied into LDS by LDS-DMA, no item VALU.  RES: the
+// fused 1x1 residual segment (raw input, f16x3 under the per-image bound abound).
 template <int TH, int BN, int PRO, bool RES, int MB = 2, int NW = 4>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(MB == 4 ? 1 : 2, MB == 4 ? 1 : 2)))
 void conv3x3_wino_kernel(WDev p) {
-    static_assert((PRO == 2 || PRO == 0) && !(PRO == 0 && RES), "GN+SiLU (+ residual) or one raw segment");
-    using T = WTile<TH, BN, MB, NW>;
+    static_assert((PRO == 2 || PRO == 0 || PRO == 3) && !(PRO == 0 && RES),
+                  "GN+SiLU (+ residual), pre-split GN+SiLU (+ residual) or one raw segment");
+    constexpr bool VP = PRO == 3;
+    using T = WTile<TH, BN, MB, NW, VP>;
     constexpr int NT = T::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* const cbase = smem + 2 * T::HSTAGE;  // residual centre buffers
@@ -182,8 +197,30 @@ void conv3x3_wino_kernel(WDev p) {
     const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
     const __amdgpu_buffer_rsrc_t srd1 = make_srd(RES ? p.src1 : p.src0);
     const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w);
-    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO ? p.scale : p.src0);
-    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO ? p.shift : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO == 2 ? p.scale : p.src0);
+    const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO == 2 ? p.shift : p.src0);
+    // VP: this image's pre-split planes [chunk][plane 16][row H][tile W/2] x 16 B; per-lane byte offsets
+    // of this wave's LDS-DMA pieces (chunk 0; a chunk is a scalar offset), OOB for halo rows outside
+    // the image (the load returns zeros: the padding rows' V)
+    const __amdgpu_buffer_rsrc_t srdv = make_srd(VP ? (const void*)(p.vpre + (long)b * p.vimg) : (const void*)p.src0);
+    unsigned voff[VP ? T::DPW : 1];
+    if constexpr (VP) {
+#pragma unroll
+        for (int i = 0; i < T::DPW; ++i) {
+            const int f = (wave * T::DPW + i) * 64 + lane;  // 16-byte fragment of the stage
+            const int P = f / (T::HR * 8), r = (f >> 3) % T::HR, tl = f & 7;
+            const int y = y0 - 1 + r;
+            voff[i] = (unsigned)y < (unsigned)p.H ? (unsigned)(((P * p.H + y) * (p.W / 2) + (x0 >> 1) + tl) * 16) : OOB;
+        }
+    }
+    const int vchunk = 16 * p.H * (p.W / 2) * 16;  // bytes of one 16-channel chunk's planes
+    auto dma_halo = [&](int c, int hs) {
+        if constexpr (VP) {
+            unsigned char* dst = smem + hs * T::HSTAGE + wave * T::DPW * 1024;
+#pragma unroll
+            for (int i = 0; i < T::DPW; ++i) wino_lds16(srdv, dst + i * 1024, voff[i], c * vchunk);
+        }
+    };
 
     // ---- halo items: item i = tid + NT j = (halo row i >> 4, tile pair (i >> 2) & 3, quad i & 3) ----
     const int q = tid & 3;
@@ -212,7 +249,7 @@ void conv3x3_wino_kernel(WDev p) {
     f32x4 rh[T::I_PER_T][6];
     f32x4 rsc, rsh;
     auto load_ss = [&](int c) {
-        if constexpr (PRO != 0) {
+        if constexpr (PRO == 2) {
             const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
             rsc = bload_f4(srdsc, o);
             rsh = bload_f4(srdsh, o);
@@ -224,6 +261,7 @@ void conv3x3_wino_kernel(WDev p) {
             rh[j][k] = bload_f4s(srd0, ((hin[j] >> k) & 1u) ? (unsigned)(hbase[j] + k * hpx) : OOB, c * 64);
     };
     auto load_halo = [&](int c) {
+        if constexpr (VP) return;
 #pragma unroll
         for (int j = 0; j < T::I_PER_T; ++j) load_slot(j, c);
         load_ss(c);
@@ -313,6 +351,7 @@ void conv3x3_wino_kernel(WDev p) {
         }
     };
     auto write_items = [&](int hs) {
+        if constexpr (VP) return;
 #pragma unroll
         for (int j = 0; j < T::I_PER_T; ++j) {
             prologue(j, 0, 6);
@@ -438,11 +477,13 @@ void conv3x3_wino_kernel(WDev p) {
     // allocator spill, as in wc_conv6.hip)
     const int pv0 = (p.nck0 - 1) & 1;
     load_halo(0);
+    dma_halo(0, pv0);
     if constexpr (RI) load_centre(I0, 0, nri > 0);
     load_w(0, 0);
     load_w(1, 1);
     write_items(pv0);
     if constexpr (RI) write_centre(I0, pv0);
+    if constexpr (VP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
     __syncthreads();
     // The next chunk's halo item slot j goes out at step load_at(j) (after that step's weight loads:
     // vmcnt drains in issue order, so the weight waits of the following steps wait for it only from
@@ -460,6 +501,7 @@ void conv3x3_wino_kernel(WDev p) {
     auto pro_at = [](int j) { return j == 0 ? 5 : 9; };
     // the slot's VALU at step st (relative step k = st - pro_at(j))
     auto slot_work = [&](int j, int k, int hs) {
+        if constexpr (VP) return;
         if constexpr (WC_ABL & 4) {
             if (k >= 0 && k < 3) prologue(j, 2 * k, 2 * k + 2);
             return;
@@ -484,6 +526,7 @@ void conv3x3_wino_kernel(WDev p) {
                 for (int j = 0; j < T::I_PER_T; ++j)
                     if (!(WC_ABL & 32) && st == load_at(j)) load_slot(j, c + 1);
                 if (st == HALO_AT) {
+                    dma_halo(c + 1, PV ^ 1);
                     load_ss(c + 1);
                     if constexpr (RI) load_centre(I0, c + 1, c + 1 < nri);
                 }
@@ -513,6 +556,10 @@ void conv3x3_wino_kernel(WDev p) {
                 if (ntail > 0) write_centre(I0, 1);  // tail chunk k in centre buffer (k + 1) & 1
             }
         }
+        // VP: this wave's LDS-DMA pieces of the next chunk (issued at step HALO_AT, followed by at least
+        // 18 weight loads) have landed once at most the last 4 vector-memory ops (the next chunk's first
+        // two weight steps) are outstanding: vmcnt counts loads in issue order
+        if constexpr (VP && !LAST) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         if constexpr (!(WC_ABL & 16)) __syncthreads();
     };
     const std::integral_constant<int, 0> NL;
@@ -680,19 +727,22 @@ extern "C" int wc_conv3x3_wino_set_onewave(int mode) {
     return prev;
 }
 
-extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
-                                     const float* w_inv_scale, const float* a_bound, void* stream) {
+namespace {
+
+// Argument checks and the kernel parameters shared by wc_conv3x3_wino_f16x3 and its pre-split form.
+int wino_setup(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp, const float* w_inv_scale,
+               const float* a_bound, WDev& d, int& pro, bool& res, int& BN) {
     if (!a || !w || !a->out || !w_inv_scale) return WC_E_ARG;
     if (a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
     const wc_conv_seg& s0 = a->seg[0];
     if (!s0.src || (s0.scale == nullptr) != (s0.shift == nullptr)) return WC_E_ARG;
     // segment 0: the GN + SiLU prologue (its static bound), or one raw segment under a_bound
-    const int pro = s0.scale ? 2 : 0;
+    pro = s0.scale ? 2 : 0;
     if (pro == 2 && !s0.silu) return WC_E_ARG;
     if (pro == 0 && (!a_bound || a->nseg != 1)) return WC_E_ARG;
     if (a->act != WC_ACT_NONE) return WC_E_ARG;
     if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
-    const int BN = wc_conv3x3_wino_tile_n(a->N);
+    BN = wc_conv3x3_wino_tile_n(a->N);
     const int TH = BN == 64 ? 16 : 8;
     if (s0.ntaps != 9 || s0.sy != 1 || s0.sx != 1 || s0.kbase != 0) return WC_E_SHAPE;
     for (int t = 0; t < 9; ++t)
@@ -701,10 +751,10 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     if (a->B <= 0 || a->N <= 0 || s0.H != a->Hm || s0.W != a->Wm || a->Hm % TH || a->Wm % 16) return WC_E_SHAPE;
     if ((long)a->B * s0.H * s0.W * s0.ldc * 4 >= (1L << 31)) return WC_E_SHAPE;
     if (reinterpret_cast<uintptr_t>(w) & 15) return WC_E_SHAPE;
-    WDev d{};
+    d = WDev{};
     d.src0 = s0.src; d.C0 = s0.C; d.ldc0 = s0.ldc; d.scale = s0.scale; d.shift = s0.shift;
     d.nck0 = s0.C / 16;
-    const bool res = a->nseg == 2;
+    res = a->nseg == 2;
     if (res) {
         const wc_conv_seg& s1 = a->seg[1];
         if (!s1.src || s1.scale || !a_bound) return WC_E_ARG;  // the residual runs on f16x3 under a_bound
@@ -735,6 +785,96 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     }
     const long ntn = (a->N + BN - 1) / BN;
     if (w_bytes != ntn * (12L * d.nck0 + d.nck1) * BN * 64 || w_bytes >= (1L << 31)) return WC_E_SHAPE;
+    return WC_OK;
+}
+
+// bytes of one image's pre-split planes: [chunk C/16][plane 16][row H][tile W/2] x 16 B
+long wino_vimg(int C, int H, int W) { return (long)(C / 16) * 16 * H * (W / 2) * 16; }
+
+// ---- wino_vsplit_kernel: segment 0 of a GN+SiLU Winograd conv, transformed and split once ----
+// Thread = (image b, row y, channel octet o, tile pair tp): the six input pixels 4 tp - 1 .. 4 tp + 4
+// of 8 channels, GN affine + SiLU + 2^s with zero padding, the input transform of tiles 2 tp and
+// 2 tp + 1 and the two-piece fp16 split -- the same operations in the same order as the conv kernel's
+// items (prologue / transform, PRO 2), so the planes are bit for bit the LDS image those items write --
+// stored as 16-byte fragments at [b][o / 2][plane = piece 8 + position 2 + o % 2][y][tile].
+// s per image as the conv: a_exp - 1, clamped to 13 - e(res_bound[b]) under a residual segment.
+__global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restrict__ src, int ldc, int B, int H,
+                                                          int W, int C, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int a_exp1,
+                                                          const float* __restrict__ res_bound,
+                                                          unsigned char* __restrict__ vout, long vimg) {
+    const int ntp = W / 4, noct = C / 8;
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const long total = (long)B * H * noct * ntp;
+    if (gid >= total) return;
+    const int tp = (int)(gid % ntp);
+    long r = gid / ntp;
+    const int o = (int)(r % noct);
+    r /= noct;
+    const int y = (int)(r % H);
+    const int b = (int)(r / H);
+    int s_exp = a_exp1;
+    if (res_bound) {
+        const float bnd = res_bound[b];
+        const int e = (int)((__float_as_uint(bnd) >> 23) & 0xffu) - 127;
+        if (bnd > 0.f) s_exp = min(s_exp, 13 - e);
+        s_exp = max(s_exp, -100);
+    }
+    const float ascale = ldexpf(1.0f, s_exp);
+    f32x4 rsc[2], rsh[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        rsc[h] = *reinterpret_cast<const f32x4*>(scale + (long)b * C + 8 * o + 4 * h);
+        rsh[h] = *reinterpret_cast<const f32x4*>(shift + (long)b * C + 8 * o + 4 * h);
+    }
+    f32x4 d[2][6];  // [quad][pixel]
+    const float* row = src + ((long)(b * H + y) * W) * ldc + 8 * o;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int ix = 4 * tp - 1 + k;
+        const bool inb = (unsigned)ix < (unsigned)W;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 v = inb ? *reinterpret_cast<const f32x4*>(row + (long)ix * ldc + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 a = v * rsc[h] + rsh[h];
+            a.x = silu_fast(a.x); a.y = silu_fast(a.y);
+            a.z = silu_fast(a.z); a.w = silu_fast(a.w);
+            d[h][k] = inb ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    unsigned char* vb = vout + (long)b * vimg;
+    const long plane = (long)H * (W / 2) * 16;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        u32x2 pc[2][4][2];  // [quad][position][piece]
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 d0 = d[h][2 * t], d1 = d[h][2 * t + 1], d2 = d[h][2 * t + 2], d3 = d[h][2 * t + 3];
+            const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) split2_f16(V[pos], pc[h][pos][0], pc[h][pos][1]);
+        }
+        const long tile_off = ((long)y * (W / 2) + 2 * tp + t) * 16;
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos)
+#pragma unroll
+            for (int piece = 0; piece < 2; ++piece) {
+                const int P = piece * 8 + pos * 2 + (o & 1);
+                *reinterpret_cast<u32x4*>(vb + ((long)(o >> 1) * 16 + P) * plane + tile_off) =
+                    u32x4{pc[0][pos][piece].x, pc[0][pos][piece].y, pc[1][pos][piece].x, pc[1][pos][piece].y};
+            }
+    }
+}
+
+}  // namespace
+
+extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
+                                     const float* w_inv_scale, const float* a_bound, void* stream) {
+    WDev d;
+    int pro, BN;
+    bool res;
+    const int st = wino_setup(a, w, w_bytes, a_exp, w_inv_scale, a_bound, d, pro, res, BN);
+    if (st != WC_OK) return st;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (BN == 128 && pro == 2 && g_wino_form >= 1 && d.N % 256 == 0)  // 8 waves: 256 channels x 8 rows
         return res ? launch_wino<8, 256, 2, true, 2, 8>(d, s) : launch_wino<8, 256, 2, false, 2, 8>(d, s);
@@ -747,6 +887,50 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     if (pro == 0) return BN == 64 ? launch_wino<16, 64, 0, false>(d, s) : launch_wino<8, 128, 0, false>(d, s);
     if (BN == 64) return res ? launch_wino<16, 64, 2, true>(d, s) : launch_wino<16, 64, 2, false>(d, s);
     return res ? launch_wino<8, 128, 2, true>(d, s) : launch_wino<8, 128, 2, false>(d, s);
+}
+
+extern "C" int wc_wino_vsplit_bytes(int B, int C, int H, int W, int64_t* bytes) {
+    if (!bytes || B <= 0 || C <= 0 || C % 16 || H <= 0 || W <= 0 || W % 16) return WC_E_SHAPE;
+    *bytes = (int64_t)B * wino_vimg(C, H, W);
+    return WC_OK;
+}
+
+extern "C" int wc_wino_vsplit_f16x3(const wc_conv_args* a, int a_exp, const float* a_bound, void* vout, int64_t v_bytes,
+                                    void* stream) {
+    if (!a || !vout || a->nseg < 1 || a->nseg > 2) return WC_E_ARG;
+    const wc_conv_seg& s0 = a->seg[0];
+    if (!s0.src || !s0.scale || !s0.shift || !s0.silu) return WC_E_ARG;  // the GN + SiLU segment only
+    if (a->nseg == 2 && !a_bound) return WC_E_ARG;
+    if (a_exp < -60 || a_exp > 60) return WC_E_ARG;
+    if (s0.C <= 0 || s0.C % 16 || s0.ldc % 4 || (reinterpret_cast<uintptr_t>(s0.src) & 15) || s0.W % 16)
+        return WC_E_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(vout) & 15) || v_bytes != (int64_t)a->B * wino_vimg(s0.C, s0.H, s0.W))
+        return WC_E_SHAPE;
+    const long total = (long)a->B * s0.H * (s0.C / 8) * (s0.W / 4);
+    wc_last_kernel = "wino_vsplit_kernel";
+    hipLaunchKernelGGL(wino_vsplit_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), s0.src, s0.ldc, a->B, s0.H, s0.W, s0.C, s0.scale,
+                       s0.shift, a_exp - 1, a->nseg == 2 ? a_bound : nullptr,
+                       reinterpret_cast<unsigned char*>(vout), wino_vimg(s0.C, s0.H, s0.W));
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
+                                        const float* w_inv_scale, const float* a_bound, const void* vpre,
+                                        int64_t v_bytes, void* stream) {
+    WDev d;
+    int pro, BN;
+    bool res;
+    const int st = wino_setup(a, w, w_bytes, a_exp, w_inv_scale, a_bound, d, pro, res, BN);
+    if (st != WC_OK) return st;
+    if (pro != 2 || !vpre || (reinterpret_cast<uintptr_t>(vpre) & 15)) return WC_E_ARG;
+    d.vimg = wino_vimg(d.C0, d.H, d.W);
+    if (v_bytes != (int64_t)d.B * d.vimg || d.vimg >= (1L << 31)) return WC_E_SHAPE;
+    d.vpre = reinterpret_cast<const unsigned char*>(vpre);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 64) return res ? launch_wino<16, 64, 3, true>(d, s) : launch_wino<16, 64, 3, false>(d, s);
+    return res ? launch_wino<8, 128, 3, true>(d, s) : launch_wino<8, 128, 3, false>(d, s);
 }
 
 // ---- device re-pack for wc_conv3x3_wino_f16x3 (training: the weights change every step) ----

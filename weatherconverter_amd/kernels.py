@@ -49,7 +49,7 @@ def replay_timing(name: Optional[str], reps: int = 5):
 def _idempotent(fn_name: str, args) -> bool:
     """A conv launch can be re-run without changing its own inputs (output not aliased)."""
     if not fn_name.startswith('wc_conv'):
-        return fn_name.startswith('wc_attention')
+        return fn_name.startswith(('wc_attention', 'wc_wino_vsplit'))
     a = args[0]._obj
     ins = {a.seg[i].src for i in range(a.nseg)} | {a.res}
     return a.out not in ins
@@ -686,11 +686,48 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     a = _conv_args(segs, w.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     TH, BN = wino_tile(w.N)
+    prof = PROFILE is not None or REPLAY is not None
+    ab = _ptr(a_bound) if (len(segs) == 2 or raw) else None
+    if not raw and wino_vsplit_wanted(segs, w.N, Hm, Wm):
+        # segment 0 GN+SiLU'd, transformed and split once (not once per output-channel tile), then the
+        # conv copies its halo planes by LDS-DMA (wc_wino_vsplit_f16x3 + wc_conv3x3_wino_f16x3_vp)
+        v = segs[0].view
+        nb = ctypes.c_int64()
+        _native.call('wc_wino_vsplit_bytes', v.B, v.C, Hm, Wm, ctypes.byref(nb))
+        vbuf = torch.empty(nb.value, dtype=torch.uint8, device=v.t.device)
+        _timed('wino_vsplit_kernel', 'wc_wino_vsplit_f16x3', 0.0, ctypes.byref(a), int(a_exp), ab,
+               vbuf.data_ptr(), nb.value, _stream(), nbytes=4.0 * v.B * Hm * Wm * v.C + nb.value)
+        _timed(f'conv3x3_wino_kernel<{TH}, {BN}, 3, {"true" if len(segs) == 2 else "false"}>',
+               'wc_conv3x3_wino_f16x3_vp', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
+               ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(), ab,
+               vbuf.data_ptr(), nb.value, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res),
+               mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
+        return
     _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {0 if raw else 2}, {"true" if len(segs) == 2 else "false"}>',
-           'wc_conv3x3_wino_f16x3', _flops(segs, Hm, Wm, w.N) if PROFILE is not None or REPLAY is not None else 0.0,
+           'wc_conv3x3_wino_f16x3', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
            ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(),
-           _ptr(a_bound) if (len(segs) == 2 or raw) else None, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res),
+           ab, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res),
            mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
+
+
+# Pre-split Winograd segment 0 (wc_wino_vsplit_f16x3) for convs with at least this many 128-channel
+# output tiles (the redundancy the in-conv prologue pays: every output tile re-transforms the halo);
+# 0 = never.  WC_WINO_VP sets it (A/B runs); set_wino_vsplit at run time.
+_WINO_VP_MIN_TILES = int(os.environ.get('WC_WINO_VP', '4'))
+
+
+def set_wino_vsplit(min_tiles: int) -> int:
+    """Use the pre-split Winograd form for GN+SiLU convs with >= min_tiles output-channel tiles of 128
+    (0 = never); returns the previous setting."""
+    global _WINO_VP_MIN_TILES
+    prev, _WINO_VP_MIN_TILES = _WINO_VP_MIN_TILES, int(min_tiles)
+    return prev
+
+
+def wino_vsplit_wanted(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
+    s0 = segs[0]
+    return (_WINO_VP_MIN_TILES > 0 and N > 64 and -(-N // 128) >= _WINO_VP_MIN_TILES and s0.silu
+            and s0.scale is not None and Wm % 16 == 0)
 
 
 def wino_mfma_flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int, pieces: int = 3) -> float:

@@ -1,13 +1,16 @@
 #!/bin/bash
 # PMC passes (each its own run, kernel-trace only) over one Winograd conv shape, for the tree's library and
 # the variant libraries in $VARS: MFMA busy, issue/wait breakdown, VALU / LDS / VMEM activity, TA / TD busy.
-# usage: VARS="abl38" SHAPE="256 128 128 16" bash tools/pmc_wino.sh ; tables in gpurun_out/pmcw_<arm>_table.txt
+# usage: VARS="abl38 tree+WC_WINO_VP=1" SHAPE="256 128 128 16" bash tools/pmc_wino.sh ; tables in gpurun_out/pmcw_<arm>_table.txt
 export TMPDIR=/tmp
 SHAPE=${SHAPE:-256 128 128 16}
 O=gpurun_out/pmcw
 mkdir -p $O
 for arm in tree $VARS; do
-  if [ $arm = tree ]; then e=""; else e="WC_KERNEL_LIB=$PWD/weatherconverter_amd/lib/$arm/libwc_kernels.so WC_ALLOW_STALE_LIB=1"; fi
+  lib=${arm%%+*}; e=""
+  [ "$arm" != "$lib" ] && e=$(echo "${arm#*+}" | tr '+' ' ')
+  [ "$lib" != tree ] && e="$e WC_KERNEL_LIB=$PWD/weatherconverter_amd/lib/$lib/libwc_kernels.so WC_ALLOW_STALE_LIB=1"
+  arm=$(echo "$arm" | tr '+=' '__')
   i=0
   for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_SALU TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum" \

@@ -792,27 +792,26 @@ int wino_setup(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
 long wino_vimg(int C, int H, int W) { return (long)(C / 16) * 16 * H * (W / 2) * 16; }
 
 // ---- wino_vsplit_kernel: segment 0 of a GN+SiLU Winograd conv, transformed and split once ----
-// Thread = (image b, row y, channel octet o, tile pair tp): the six input pixels 4 tp - 1 .. 4 tp + 4
-// of 8 channels, GN affine + SiLU + 2^s with zero padding, the input transform of tiles 2 tp and
-// 2 tp + 1 and the two-piece fp16 split -- the same operations in the same order as the conv kernel's
-// items (prologue / transform, PRO 2), so the planes are bit for bit the LDS image those items write --
-// stored as 16-byte fragments at [b][o / 2][plane = piece 8 + position 2 + o % 2][y][tile].
-// s per image as the conv: a_exp - 1, clamped to 13 - e(res_bound[b]) under a residual segment.
+// Workgroup = R = 256 / W image rows of one image and one 16-channel chunk.  Stage 1: the rows' pixels
+// -1 .. W (4 lanes per pixel, 16 B each: 16 pixels per load instruction) through GN affine + SiLU + 2^s
+// with zero padding, once per element, into LDS as fp32.  Stage 2: thread = (row, tile t, channel octet
+// h): the tile's four pixels 2t - 1 .. 2t + 2 from LDS, the input transform V0..V3 and the two-piece
+// fp16 split, stored as 16-byte fragments at [b][chunk][plane = piece 8 + position 2 + h][y][t] -- for
+// fixed (plane, row) consecutive lanes write consecutive tiles.  The same operations in the same order as
+// the conv kernel's items (prologue / transform, PRO 2): the planes are bit for bit the LDS image those
+// items write.  s per image as the conv: a_exp - 1, clamped to 13 - e(res_bound[b]) under a residual.
 __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restrict__ src, int ldc, int B, int H,
                                                           int W, int C, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, int a_exp1,
                                                           const float* __restrict__ res_bound,
                                                           unsigned char* __restrict__ vout, long vimg) {
-    const int ntp = W / 4, noct = C / 8;
-    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-    const long total = (long)B * H * noct * ntp;
-    if (gid >= total) return;
-    const int tp = (int)(gid % ntp);
-    long r = gid / ntp;
-    const int o = (int)(r % noct);
-    r /= noct;
-    const int y = (int)(r % H);
-    const int b = (int)(r / H);
+    extern __shared__ __attribute__((aligned(16))) f32x4 act[];  // [R][W + 2][4 quads + 1 pad]
+    const int R = 256 / W, nck = C / 16, nyb = (H + R - 1) / R;
+    const int k = blockIdx.x % nck;
+    const int yb = (blockIdx.x / nck) % nyb;
+    const int b = blockIdx.x / (nck * nyb);
+    const int y0 = yb * R;
+    const int tid = threadIdx.x;
     int s_exp = a_exp1;
     if (res_bound) {
         const float bnd = res_bound[b];
@@ -821,49 +820,47 @@ __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restric
         s_exp = max(s_exp, -100);
     }
     const float ascale = ldexpf(1.0f, s_exp);
-    f32x4 rsc[2], rsh[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        rsc[h] = *reinterpret_cast<const f32x4*>(scale + (long)b * C + 8 * o + 4 * h);
-        rsh[h] = *reinterpret_cast<const f32x4*>(shift + (long)b * C + 8 * o + 4 * h);
+    // stage 1
+    const int W2 = W + 2, items = R * W2 * 4;
+    for (int i = tid; i < items; i += 256) {
+        const int q = i & 3, px = (i >> 2) % W2 - 1, r = (i >> 2) / W2;
+        const int y = y0 + r;
+        const bool inb = (unsigned)px < (unsigned)W && y < H;
+        const int c = k * 16 + 4 * q;
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
+        const f32x4 v = inb ? *reinterpret_cast<const f32x4*>(src + ((long)(b * H + y) * W + px) * ldc + c)
+                            : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 a = v * sc + sh;
+        a.x = silu_fast(a.x); a.y = silu_fast(a.y);
+        a.z = silu_fast(a.z); a.w = silu_fast(a.w);
+        // a pixel is 5 slots (4 quads + pad): stage 2's lanes, two pixels apart, then read distinct banks
+        act[(r * W2 + px + 1) * 5 + q] = inb ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    f32x4 d[2][6];  // [quad][pixel]
-    const float* row = src + ((long)(b * H + y) * W) * ldc + 8 * o;
+    __syncthreads();
+    // stage 2
+    const int T2 = W / 2;
+    const int t = tid % T2, h = (tid / T2) & 1, r = tid / W;
+    const int y = y0 + r;
+    if (y >= H) return;
+    unsigned char* vb = vout + (long)b * vimg + (long)k * 16 * H * T2 * 16;
+    const long plane = (long)H * T2 * 16;
+    const long frag = ((long)y * T2 + t) * 16;
+    u32x2 pc[2][4][2];  // [quad of the octet][position][piece]
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const int ix = 4 * tp - 1 + k;
-        const bool inb = (unsigned)ix < (unsigned)W;
+    for (int qq = 0; qq < 2; ++qq) {
+        const f32x4* ar = act + (r * W2 + 2 * t) * 5 + 2 * h + qq;  // pixel 2t - 1 is padded index 2t
+        const f32x4 d0 = ar[0], d1 = ar[5], d2 = ar[10], d3 = ar[15];
+        const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const f32x4 v = inb ? *reinterpret_cast<const f32x4*>(row + (long)ix * ldc + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
-            f32x4 a = v * rsc[h] + rsh[h];
-            a.x = silu_fast(a.x); a.y = silu_fast(a.y);
-            a.z = silu_fast(a.z); a.w = silu_fast(a.w);
-            d[h][k] = inb ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int pos = 0; pos < 4; ++pos) split2_f16(V[pos], pc[qq][pos][0], pc[qq][pos][1]);
     }
-    unsigned char* vb = vout + (long)b * vimg;
-    const long plane = (long)H * (W / 2) * 16;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        u32x2 pc[2][4][2];  // [quad][position][piece]
+    for (int pos = 0; pos < 4; ++pos)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const f32x4 d0 = d[h][2 * t], d1 = d[h][2 * t + 1], d2 = d[h][2 * t + 2], d3 = d[h][2 * t + 3];
-            const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
-#pragma unroll
-            for (int pos = 0; pos < 4; ++pos) split2_f16(V[pos], pc[h][pos][0], pc[h][pos][1]);
-        }
-        const long tile_off = ((long)y * (W / 2) + 2 * tp + t) * 16;
-#pragma unroll
-        for (int pos = 0; pos < 4; ++pos)
-#pragma unroll
-            for (int piece = 0; piece < 2; ++piece) {
-                const int P = piece * 8 + pos * 2 + (o & 1);
-                *reinterpret_cast<u32x4*>(vb + ((long)(o >> 1) * 16 + P) * plane + tile_off) =
-                    u32x4{pc[0][pos][piece].x, pc[0][pos][piece].y, pc[1][pos][piece].x, pc[1][pos][piece].y};
-            }
-    }
+        for (int piece = 0; piece < 2; ++piece)
+            *reinterpret_cast<u32x4*>(vb + (piece * 8 + pos * 2 + h) * plane + frag) =
+                u32x4{pc[0][pos][piece].x, pc[0][pos][piece].y, pc[1][pos][piece].x, pc[1][pos][piece].y};
 }
 
 }  // namespace
@@ -906,9 +903,12 @@ extern "C" int wc_wino_vsplit_f16x3(const wc_conv_args* a, int a_exp, const floa
         return WC_E_SHAPE;
     if ((reinterpret_cast<uintptr_t>(vout) & 15) || v_bytes != (int64_t)a->B * wino_vimg(s0.C, s0.H, s0.W))
         return WC_E_SHAPE;
-    const long total = (long)a->B * s0.H * (s0.C / 8) * (s0.W / 4);
+    if (s0.W > 256) return WC_E_SHAPE;  // R = 256 / W rows per workgroup
+    const int R = 256 / s0.W;
+    const long nblk = (long)a->B * ((s0.H + R - 1) / R) * (s0.C / 16);
+    const size_t lds = (size_t)R * (s0.W + 2) * 5 * sizeof(f32x4);
     wc_last_kernel = "wino_vsplit_kernel";
-    hipLaunchKernelGGL(wino_vsplit_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(wino_vsplit_kernel, dim3((unsigned)nblk), dim3(256), lds,
                        reinterpret_cast<hipStream_t>(stream), s0.src, s0.ldc, a->B, s0.H, s0.W, s0.C, s0.scale,
                        s0.shift, a_exp - 1, a->nseg == 2 ? a_bound : nullptr,
                        reinterpret_cast<unsigned char*>(vout), wino_vimg(s0.C, s0.H, s0.W));
@@ -929,6 +929,8 @@ extern "C" int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* a, const void* w, in
     if (v_bytes != (int64_t)d.B * d.vimg || d.vimg >= (1L << 31)) return WC_E_SHAPE;
     d.vpre = reinterpret_cast<const unsigned char*>(vpre);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (BN == 128 && g_wino_onewave == 1 && d.H % 16 == 0)  // the one-wave form (16-row tiles)
+        return res ? launch_wino<16, 128, 3, true, 4>(d, s) : launch_wino<16, 128, 3, false, 4>(d, s);
     if (BN == 64) return res ? launch_wino<16, 64, 3, true>(d, s) : launch_wino<16, 64, 3, false>(d, s);
     return res ? launch_wino<8, 128, 3, true>(d, s) : launch_wino<8, 128, 3, false>(d, s);
 }

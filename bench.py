@@ -287,11 +287,13 @@ def hbm_leg(hbm, groups: int = 1):
     """The HBM-bound kernels of the forward: GroupNorm+SiLU are applied in the convs' prologues, so
     what stays on HBM is the statistics pass (one read of the activation, 4 B/element) and the
     pre-split of the projection operand (read 4 + write 4 B/element); achieved GB/s over every
-    launch of one forward against the 8 TB/s HBM peak."""
+    launch of one forward against the 8 TB/s HBM peak.  The byte count is the launch's stated nbytes,
+    else its 'flops' field (the HBM wrappers state bytes there)."""
     if not hbm:
         return None
     out = {}
-    for k, (n, by, sec, *_) in hbm.items():
+    for k, (n, fl, sec, nb, *_) in hbm.items():
+        by = nb or fl
         out[k] = {'launches': n * groups, 'ms': round(sec * 1e3 * groups, 3), 'gbytes': round(by * groups / 1e9, 3),
                   'achieved': round(by / sec / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                   'frac': round(by / sec / 1e9 / HBM_PEAK_GBS, 4)}

@@ -84,3 +84,12 @@ def test_self_launch_refused_under_profiler(monkeypatch):
     assert bench._profiler_preloaded()
     with pytest.raises(SystemExit):
         bench._self_launch(bench.parse(['--gpus', '2']))
+
+
+def test_hbm_leg_bytes_from_nbytes_or_flops_field():
+    """hbm_leg reads a launch's stated nbytes (wino_vsplit) and falls back to the 'flops' field, where the
+    GroupNorm / split wrappers state their bytes."""
+    hbm = {'wino_vsplit_kernel': [2, 0.0, 2e-4, 1.6e9, 0.0], 'split_tiled_kernel': [1, 4e8, 1e-4, 0.0, 0.0]}
+    out = bench.hbm_leg(hbm)
+    assert out['wino_vsplit_kernel']['gbytes'] == 1.6 and out['wino_vsplit_kernel']['achieved'] == 8000.0
+    assert out['split_tiled_kernel']['gbytes'] == 0.4 and out['split_tiled_kernel']['frac'] == 0.5

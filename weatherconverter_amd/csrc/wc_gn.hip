@@ -230,11 +230,17 @@ __global__ __launch_bounds__(256) void gn_partials_kernel(const float* __restric
 
 // Per (b, group) merge of the tile partials of the view's channels [c0, c0 + C): one wave per group
 // (workgroup = image).  Every partial covers the same n0 = 64*sw values, so the merge is the exact
-// equal-count identity  mean = avg(m_i),  M2 = sum(M2_i) + n0 * sum((m_i - mean)^2)  in two
-// division-free passes over the partials, lane butterflies in a fixed order (deterministic); then
-// the same per-(b, c) affine (and optional bound) as gn_finalize.
+// equal-count identity  mean = avg(m_i),  M2 = sum(M2_i) + n0 * sum((m_i - mean)^2): up to
+// 64 * GNF_KC partials per group in one round of loads kept in registers for both passes (the launch is
+// latency-bound: 57 per sampling step), larger groups in two streaming passes; lane butterflies in a
+// fixed order (deterministic, per image); then the same per-(b, c) affine (and optional bound) as
+// gn_finalize.
 constexpr int GNF_THREADS = 512;
+constexpr int GNF_KC = 32;  // register-cached partials per lane (groups of up to 2048 items)
 
+// KC: rounds of 64 partials per group kept in registers (the power of two >= items / 64, chosen on the
+// host), 0 = the streaming form for larger groups
+template <int KC>
 __global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
     const float* __restrict__ part, int np64, int ncb, int sw, int c0, int C, int G,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* __restrict__ scale,
@@ -248,54 +254,95 @@ __global__ __launch_bounds__(GNF_THREADS) void gn_finalize_part_kernel(
     const int j = threadIdx.x & 63;
     const float n0 = 64.0f * (float)sw;
     if (g < G) {
-        // sub-slot (pixel block pp, global slot gs) sits at ((b * np64 + pp) * NS + gs) * 2, and a
-        // group's spg slots are contiguous: stream each slot's np64 partials with a fixed lane
-        // stride, four loads in flight per lane, no index division
         const int NS = ncb * spb;
-        const long pstride = 2L * NS * 64;  // one lane step (64 pixel blocks)
-        const float* base = part + ((long)b * np64 * NS + (c0 + g * cpg) / sw) * 2 + (long)j * NS * 2;
         const int items = np64 * spg;
-        float sm = 0.f;
-        for (int s = 0; s < spg; ++s) {
-            const float* ps = base + 2 * s;
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-            int pp = j;
-            for (; pp + 192 < np64; pp += 256, ps += 4 * pstride) {
-                a0 += ps[0];
-                a1 += ps[pstride];
-                a2 += ps[2 * pstride];
-                a3 += ps[3 * pstride];
-            }
-            for (; pp < np64; pp += 64, ps += pstride) a0 += ps[0];
-            sm += (a0 + a1) + (a2 + a3);
-        }
+        float mean, q;
+        if constexpr (KC > 0) {
+            // the group's (slot, pixel block) partials flattened, item i = j + 64 k -> slot i / np64,
+            // block i % np64: every load of the lane issued at once (no dependent rounds), and the
+            // values kept in registers for the M2 pass
+            const float* gbase = part + ((long)b * np64 * NS + (c0 + g * cpg) / sw) * 2;
+            float mk[KC > 0 ? KC : 1], qk[KC > 0 ? KC : 1];
+            // (slot, block) of item j + 64 k stepped without division: 64 = ds * np64 + dr, dr < np64
+            const int ds = 64 / np64, dr = 64 - ds * np64;
+            int sl = j / np64, pp = j - sl * np64;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
-        const float mean = sm / (float)items;
-        float q = 0.f;
-        for (int s = 0; s < spg; ++s) {
-            const float* ps = base + 2 * s;
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-            int pp = j;
-            for (; pp + 192 < np64; pp += 256, ps += 4 * pstride) {
-                float d;
-                d = ps[0] - mean;
-                a0 += fmaf(n0 * d, d, ps[1]);
-                d = ps[pstride] - mean;
-                a1 += fmaf(n0 * d, d, ps[pstride + 1]);
-                d = ps[2 * pstride] - mean;
-                a2 += fmaf(n0 * d, d, ps[2 * pstride + 1]);
-                d = ps[3 * pstride] - mean;
-                a3 += fmaf(n0 * d, d, ps[3 * pstride + 1]);
+            for (int k = 0; k < KC; ++k) {
+                // KC = the rounds the group's items need (host); in the last one, lanes past the end
+                // load the group's first partial and contribute 0 (no branch)
+                const bool ok = j + 64 * k < items;
+                const float2 v = *reinterpret_cast<const float2*>(gbase + (ok ? 2 * sl + 2 * NS * pp : 0));
+                mk[k] = ok ? v.x : 0.f;
+                qk[k] = ok ? v.y : 0.f;
+                pp += dr;
+                const int wrap = pp >= np64;
+                pp -= wrap ? np64 : 0;
+                sl += ds + wrap;
             }
-            for (; pp < np64; pp += 64, ps += pstride) {
-                const float d = ps[0] - mean;
-                a0 += fmaf(n0 * d, d, ps[1]);
-            }
-            q += (a0 + a1) + (a2 + a3);
-        }
+            float sm = 0.f;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+            for (int k = 0; k < KC; ++k) sm += mk[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+            mean = sm / (float)items;
+            q = 0.f;
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                if (j + 64 * k < items) {
+                    const float d = mk[k] - mean;
+                    q += fmaf(n0 * d, d, qk[k]);
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        } else {
+            // sub-slot (pixel block pp, global slot gs) sits at ((b * np64 + pp) * NS + gs) * 2, and a
+            // group's spg slots are contiguous: stream each slot's np64 partials with a fixed lane
+            // stride, four loads in flight per lane, no index division
+            const long pstride = 2L * NS * 64;  // one lane step (64 pixel blocks)
+            const float* base = part + ((long)b * np64 * NS + (c0 + g * cpg) / sw) * 2 + (long)j * NS * 2;
+            float sm = 0.f;
+            for (int s = 0; s < spg; ++s) {
+                const float* ps = base + 2 * s;
+                float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+                int pp = j;
+                for (; pp + 192 < np64; pp += 256, ps += 4 * pstride) {
+                    a0 += ps[0];
+                    a1 += ps[pstride];
+                    a2 += ps[2 * pstride];
+                    a3 += ps[3 * pstride];
+                }
+                for (; pp < np64; pp += 64, ps += pstride) a0 += ps[0];
+                sm += (a0 + a1) + (a2 + a3);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+            mean = sm / (float)items;
+            q = 0.f;
+            for (int s = 0; s < spg; ++s) {
+                const float* ps = base + 2 * s;
+                float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+                int pp = j;
+                for (; pp + 192 < np64; pp += 256, ps += 4 * pstride) {
+                    float d;
+                    d = ps[0] - mean;
+                    a0 += fmaf(n0 * d, d, ps[1]);
+                    d = ps[pstride] - mean;
+                    a1 += fmaf(n0 * d, d, ps[pstride + 1]);
+                    d = ps[2 * pstride] - mean;
+                    a2 += fmaf(n0 * d, d, ps[2 * pstride + 1]);
+                    d = ps[3 * pstride] - mean;
+                    a3 += fmaf(n0 * d, d, ps[3 * pstride + 1]);
+                }
+                for (; pp < np64; pp += 64, ps += pstride) {
+                    const float d = ps[0] - mean;
+                    a0 += fmaf(n0 * d, d, ps[1]);
+                }
+                q += (a0 + a1) + (a2 + a3);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        }
         if (j == 0) {
             const float n = n0 * (float)items;
             const float var = fmaxf(q / n, 0.f);  // biased, as torch
@@ -345,8 +392,24 @@ extern "C" int wc_gn_finalize_part(const float* part, int B, int HW, int ncb, in
     if (groups < 1 || groups > 8 || C % groups || (C / groups) % sw || c0 % sw || HW % 64 || c0 + C > ncb * 32 ||
         (sw != 4 && sw != 8 && sw != 16 && sw != 32))
         return WC_E_SHAPE;
-    hipLaunchKernelGGL(gn_finalize_part_kernel, dim3(B), dim3(GNF_THREADS), 0, reinterpret_cast<hipStream_t>(stream),
-                       part, HW / 64, ncb, sw, c0, C, groups, gamma, beta, eps, scale, shift, bound);
+    const int items = (HW / 64) * (C / groups / sw), rounds = (items + 63) / 64;
+    const int kc = rounds <= 1 ? 1 : rounds <= 2 ? 2 : rounds <= 4 ? 4 : rounds <= 8 ? 8 : rounds <= 16 ? 16
+                 : rounds <= GNF_KC ? GNF_KC : 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int np64 = HW / 64;
+#define WC_GNF(KC)                                                                                              \
+    hipLaunchKernelGGL(gn_finalize_part_kernel<KC>, dim3(B), dim3(GNF_THREADS), 0, st, part, np64, ncb, sw, c0, C, \
+                       groups, gamma, beta, eps, scale, shift, bound)
+    switch (kc) {
+        case 1: WC_GNF(1); break;
+        case 2: WC_GNF(2); break;
+        case 4: WC_GNF(4); break;
+        case 8: WC_GNF(8); break;
+        case 16: WC_GNF(16); break;
+        case GNF_KC: WC_GNF(GNF_KC); break;
+        default: WC_GNF(0); break;
+    }
+#undef WC_GNF
     WC_CHECK_LAUNCH();
     return WC_OK;
 }

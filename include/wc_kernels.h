@@ -263,11 +263,6 @@ int wc_conv_igemm_f16x3_qkv(const wc_conv_args* args, const void* w3, int64_t w3
  * B*N*C*4), bit for bit that split of the fp32 output, for wc_proj_f16x3 at a_exp = v_exp. */
 int wc_attention_fwd_f16x3_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B, int N, int C, int heads,
                                        float scale, int q_exp, int k_exp, int v_exp, void* stream);
-// Query blocks per wave of the d = 128 pre-split attention forms (wc_attention_fwd_f16x3_presplit and
-// _a3): 1 = 32 queries per wave at two waves per SIMD, 2 = 64 queries per wave at one wave per SIMD
-// (used where N % 256 == 0, else 1).  Bit-identical results.  Initial value from WC_ATTN_QB (default 1).
-// Returns the previous setting, or WC_E_ARG for any other value.
-int wc_attention_set_qb(int qb);
 /* The attention projections (unet_base.py:110-116 in_proj / out_proj) on an A operand split
  * beforehand: wc_split_f16x3_tiled writes, from the rows of an NHWC view (B images x HW pixels,
  * C channels; HW % 128 == 0, C % 32 == 0, 16-byte aligned, ldc % 4 == 0) optionally through a

@@ -693,34 +693,6 @@ def test_projections_presplit_bit_identical_to_register_staged(monkeypatch):
     assert torch.equal(a3o, a3s)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize('N', [1024, 384])
-def test_attention_two_query_blocks_per_wave_bit_identical(N):
-    """wc_attention_set_qb(2): the d = 128 pre-split attention with 64 queries per wave (one wave per
-    SIMD) computes every query's scores, softmax and PV in the order of the 32-query form: both outputs
-    (fp32 O and the out-projection's pre-split a3) are bit-identical; N % 256 != 0 falls back to qb 1."""
-    from weatherconverter_amd import kernels as K
-    B, C, heads = 2, 512, 4
-    g = torch.Generator().manual_seed(71)
-    q3 = (torch.randn(B * 6 * C * N, generator=g) * 4).half().view(torch.int16).cuda()
-    exps = (0, 0, 0)
-    res = []
-    prev = K.set_attention_qb(1)
-    try:
-        for qb in (1, 2):
-            K.set_attention_qb(qb)
-            o = torch.empty((B * N, C), device='cuda')
-            K.attention_presplit(q3, o, B, N, C, heads, exps)
-            a3 = K.attention_presplit_a3(q3, B, N, C, heads, exps)
-            torch.cuda.synchronize()
-            res.append((o.cpu(), a3.cpu()))
-    finally:
-        K.set_attention_qb(prev)
-    assert torch.isfinite(res[0][0]).all()
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
-
-
 # ---------------------------------------------------------------- producer absmax -> per-image f16x3 scale
 
 def _img_amax(o_bhwc):

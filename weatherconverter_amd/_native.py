@@ -18,7 +18,7 @@ NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 
 EXPORTS = [
     'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_conv3x3_wino_set_onewave', 'wc_conv3x3_wino_set_form', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv3x3_set_onewave', 'wc_conv_igemm_x6',
-    'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_attention_set_qb', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
+    'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
     'wc_temb', 'wc_conv_in', 'wc_conv_in_gn', 'wc_head_conv', 'wc_ddpm_step', 'wc_add_noise', 'wc_philox_normal', 'wc_sgg_update',
@@ -94,7 +94,6 @@ _SIGS = {
     'wc_conv_igemm_f16x3_qkv': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _I, _I, _P, _P],
     'wc_split_f16x3_tiled': [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _L, _P],
     'wc_attention_fwd_f16x3_presplit_a3': [_P, _P, _L, _I, _I, _I, _I, _F, _I, _I, _I, _P],
-    'wc_attention_set_qb': [_I],
     'wc_proj_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _P, _L, _I, _P, _P],
     'wc_proj_f16x3_qkv': [ctypes.POINTER(ConvArgs), _P, _L, _P, _L, _I, _P, _P, _I, _I, _P, _P],
     'wc_attention_fwd_f16x3_presplit': [_P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],

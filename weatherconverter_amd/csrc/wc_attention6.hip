@@ -116,22 +116,15 @@ WC_DEVICE void mfma_split(f32x16& acc, const u32x4 (&a)[F3 ? 2 : 3], const u32x4
 // O3 (PRE only): `out` is the A operand of the out-projection GEMM (wc_proj_f16x3): O x 2^ev split
 // into fp16 pieces in the a3 layout of wc_split_f16x3_tiled (C % 32 == 0, N % 128 == 0), bit for bit
 // what that split pass makes of the fp32 O.
-// QB (PRE only): 32-query blocks per wave.  QB = 2 holds 64 queries per wave at one wave per SIMD: each
-// K fragment read from LDS feeds both blocks' S MFMAs, and one block's softmax VALU has the other
-// block's MFMAs beside it in the same wave (instead of a partner wave's).  Per query the arithmetic
-// and its order are those of QB = 1: bit-identical results.
-template <int D, bool F3, bool PRE = false, bool O3 = false, int QB = 1>
-__global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
+template <int D, bool F3, bool PRE = false, bool O3 = false>
+__global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kernel(const float* __restrict__ qkv, int ldq,
                                                              float* __restrict__ out, int ldo, int N,
                                                              int C, float score_mul, float qs, float ks,
                                                              float vs, float ps, float out_mul,
                                                              float* __restrict__ lse) {
     static_assert(!PRE || F3, "pre-split operands are f16x3");
-    static_assert(QB == 1 || (PRE && QB == 2), "two query blocks per wave: pre-split operands only");
     using A = Ax6<D, F3>;
     constexpr int NP = A::NP;
-    constexpr int QW = 32 * QB;  // queries per wave
-    const int zq = N >> 30;      // 0 (N < 2^30), opaque to the compiler: see the QB = 2 S loop
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -142,7 +135,7 @@ __global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_
     // XCD-aware bijective order: the workgroups of one (batch, head) — which all stream the same
     // K/V — are consecutive logical blocks and land on one XCD, so its L2 holds that K/V once
     // (round-robin placement would pull it into all eight L2s).
-    const int nqb = (N + 4 * QW - 1) / (4 * QW);
+    const int nqb = (N + 127) / 128;
     const int nblk = gridDim.x;
     int bid = blockIdx.x;
     {
@@ -152,7 +145,7 @@ __global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_
     const int heads = C / D;
     const int head = (bid / nqb) % heads;
     const int b = bid / (nqb * heads);
-    const int q0 = (bid % nqb) * 4 * QW + wave * QW;
+    const int q0 = (bid % nqb) * 128 + wave * 32;
     const float* base = qkv + (long)b * N * ldq;
     const int qcol = head * D;
     const int kcol = C + head * D;
@@ -165,25 +158,22 @@ __global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_
     const unsigned short* Kp = q3 + (long)((C / D + head) * 2) * hplane;
     const unsigned short* Vp = q3 + 4L * C * N + (long)(head * 2) * hplane;
 
-    // ---- Q pieces: lane (query l32 of block qb, half) holds Q[q][16 ch + 8 half + j] ----
-    u32x4 qp[QB][A::NCH][NP];
+    // ---- Q pieces: lane (query l32, half) holds Q[q][16 ch + 8 half + j] ----
+    const int qrow = q0 + l32;
+    u32x4 qp[A::NCH][NP];
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-        const int qrow = q0 + 32 * qb + l32;
+    for (int ch = 0; ch < A::NCH; ++ch) {
+        if constexpr (PRE) {
 #pragma unroll
-        for (int ch = 0; ch < A::NCH; ++ch) {
-            if constexpr (PRE) {
-#pragma unroll
-                for (int pc = 0; pc < NP; ++pc) {
-                    const u32x4* src = reinterpret_cast<const u32x4*>(Qp + pc * hplane + ((long)(2 * ch + half) * N + qrow) * 8);
-                    qp[qb][ch][pc] = qrow < N ? *src : u32x4{0u, 0u, 0u, 0u};
-                }
-            } else {
-                const unsigned o = (unsigned)(qrow * ldq + qcol + 16 * ch + 8 * half) * 4u;
-                const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB) * qs;
-                const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB) * qs;
-                pieces8<F3>(v0, v1, qp[qb][ch]);
+            for (int pc = 0; pc < NP; ++pc) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(Qp + pc * hplane + ((long)(2 * ch + half) * N + qrow) * 8);
+                qp[ch][pc] = qrow < N ? *src : u32x4{0u, 0u, 0u, 0u};
             }
+        } else {
+            const unsigned o = (unsigned)(qrow * ldq + qcol + 16 * ch + 8 * half) * 4u;
+            const f32x4 v0 = bload_f4(srd, qrow < N ? o : OOB) * qs;
+            const f32x4 v1 = bload_f4(srd, qrow < N ? o + 16u : OOB) * qs;
+            pieces8<F3>(v0, v1, qp[ch]);
         }
     }
     // LDS-DMA of tile t into buf (PRE): D/16 wave-instructions per wave, half K (plane pairs, key
@@ -318,17 +308,12 @@ __global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_
         }
     };
 
-    f32x16 o[QB][A::NDB];
-    float m_run[QB], l_run[QB];
+    f32x16 o[A::NDB];
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
+    for (int d = 0; d < A::NDB; ++d)
 #pragma unroll
-        for (int d = 0; d < A::NDB; ++d)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[qb][d][r] = 0.f;
-        m_run[qb] = -INFINITY;
-        l_run[qb] = 0.f;
-    }
+        for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
 
     const int ntiles = (N + KT - 1) / KT;
     if constexpr (PRE) {
@@ -349,97 +334,75 @@ __global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_
         }
 
         // ---- S^T = K Q^T ----
-        f32x16 s[QB];
+        f32x16 s;
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb)
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) s[qb][r] = 0.f;
-        if constexpr (QB == 1) {
+        for (int ch = 0; ch < A::NCH; ++ch) {
+            u32x4 kf[NP];
 #pragma unroll
-            for (int ch = 0; ch < A::NCH; ++ch) {
-                u32x4 kf[NP];
-#pragma unroll
-                for (int pc = 0; pc < NP; ++pc)
-                    kf[pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE +
-                                                              (l32 ^ ((ch * 2 + half) & 15)) * 16);
-                mfma_split<F3>(s[0], kf, qp[0][ch]);
-            }
-        } else {
-            // block 0's S, then block 1's from its own reads of the same fragments (the opaque zero zq
-            // keeps the compiler from merging the two reads into one long-lived copy), so that block 0's
-            // softmax can issue between block 1's MFMAs
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-                for (int ch = 0; ch < A::NCH; ++ch) {
-                    u32x4 kf[NP];
-#pragma unroll
-                    for (int pc = 0; pc < NP; ++pc)
-                        kf[pc] = *reinterpret_cast<const u32x4*>(cur + (qb ? zq : 0) + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE +
-                                                                  (l32 ^ ((ch * 2 + half) & 15)) * 16);
-                    mfma_split<F3>(s[qb], kf, qp[qb][ch]);
-                }
+            for (int pc = 0; pc < NP; ++pc)
+                kf[pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE +
+                                                          (l32 ^ ((ch * 2 + half) & 15)) * 16);
+            mfma_split<F3>(s, kf, qp[ch]);
         }
 
+        // ---- online softmax over keys, per query (lane) ----
+        // The running max is kept in the exp2 domain: max(s) * score_mul = max(s * score_mul)
+        // (score_mul > 0, rounding is monotonic), and each probability is one fma + v_exp_f32:
+        // p = 2^(s * score_mul + EP - m) carries the f16x3 prescale 2^EP of P exactly in the
+        // exponent (l carries it too, and out_mul omits it)
+        float mloc = -INFINITY;
+        if (PRE || kv0 + KT <= N) {  // full tile (wave-uniform; PRE needs N % KT == 0): no key mask
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-            // ---- online softmax over keys, per query (lane) ----
-            // The running max is kept in the exp2 domain: max(s) * score_mul = max(s * score_mul)
-            // (score_mul > 0, rounding is monotonic), and each probability is one fma + v_exp_f32:
-            // p = 2^(s * score_mul + EP - m) carries the f16x3 prescale 2^EP of P exactly in the
-            // exponent (l carries it too, and out_mul omits it)
-            float mloc = -INFINITY;
-            if (PRE || kv0 + KT <= N) {  // full tile (wave-uniform; PRE needs N % KT == 0): no key mask
+            for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, s[r]);
+        } else {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, s[qb][r]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                    if (key >= N) s[qb][r] = -INFINITY;
-                    mloc = fmaxf(mloc, s[qb][r]);
-                }
+            for (int r = 0; r < 16; ++r) {
+                const int key = kv0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (key >= N) s[r] = -INFINITY;
+                mloc = fmaxf(mloc, s[r]);
             }
-            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-            const float m_new = fmaxf(m_run[qb], mloc * score_mul);
-            const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - m_new);  // v_exp_f32 (results < 2^-126 flush: negligible)
-            const float nb = (F3 ? 14.0f : 0.0f) - m_new;
+        }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc * score_mul);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // v_exp_f32 (results < 2^-126 flush: negligible)
+        const float nb = (F3 ? 14.0f : 0.0f) - m_new;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) s[qb][r] = __builtin_amdgcn_exp2f(fmaf(s[qb][r], score_mul, nb));
-            // row sum as a packed-add tree (8 instructions, not 16)
-            f32x2 ts[4];
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(fmaf(s[r], score_mul, nb));
+        // row sum as a packed-add tree (8 instructions, not 16)
+        f32x2 ts[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                ts[i] = f32x2{s[qb][4 * i], s[qb][4 * i + 1]} + f32x2{s[qb][4 * i + 2], s[qb][4 * i + 3]};
-            const f32x2 u = (ts[0] + ts[1]) + (ts[2] + ts[3]);
-            float lsum = u.x + u.y;
-            lsum += __shfl_xor(lsum, 32, 64);
-            l_run[qb] = l_run[qb] * alpha + lsum;
-            m_run[qb] = m_new;
-            // alpha == 1 exactly when no lane's running max moved: skipping the multiply is then exact
-            if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
+        for (int i = 0; i < 4; ++i)
+            ts[i] = f32x2{s[4 * i], s[4 * i + 1]} + f32x2{s[4 * i + 2], s[4 * i + 3]};
+        const f32x2 u = (ts[0] + ts[1]) + (ts[2] + ts[3]);
+        float lsum = u.x + u.y;
+        lsum += __shfl_xor(lsum, 32, 64);
+        l_run = l_run * alpha + lsum;
+        m_run = m_new;
+        // alpha == 1 exactly when no lane's running max moved: skipping the multiply is then exact
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
 #pragma unroll
-                for (int d = 0; d < A::NDB; ++d)
+            for (int d = 0; d < A::NDB; ++d)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) o[qb][d][r] *= alpha;
-            }
+                for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        }
 
-            // ---- O^T += V^T P^T: two 16-key chunks ----
+        // ---- O^T += V^T P^T: two 16-key chunks ----
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                u32x4 pp[NP];
-                pieces8<F3>(f32x4{s[qb][8 * c + 0], s[qb][8 * c + 1], s[qb][8 * c + 2], s[qb][8 * c + 3]},
-                            f32x4{s[qb][8 * c + 4], s[qb][8 * c + 5], s[qb][8 * c + 6], s[qb][8 * c + 7]}, pp);
+        for (int c = 0; c < 2; ++c) {
+            u32x4 pp[NP];
+            pieces8<F3>(f32x4{s[8 * c + 0], s[8 * c + 1], s[8 * c + 2], s[8 * c + 3]},
+                        f32x4{s[8 * c + 4], s[8 * c + 5], s[8 * c + 6], s[8 * c + 7]}, pp);
 #pragma unroll
-                for (int db = 0; db < A::NDB; ++db) {
-                    const int d = db * 32 + l32;
-                    const int off = A::KBYTES + d * (KT * 2) + (((2 * c + half) ^ ((d >> 2) & 3)) << 4);
-                    u32x4 vf[NP];
+            for (int db = 0; db < A::NDB; ++db) {
+                const int d = db * 32 + l32;
+                const int off = A::KBYTES + d * (KT * 2) + (((2 * c + half) ^ ((d >> 2) & 3)) << 4);
+                u32x4 vf[NP];
 #pragma unroll
-                    for (int pc = 0; pc < NP; ++pc)
-                        vf[pc] = *reinterpret_cast<const u32x4*>(cur + (qb ? zq : 0) + off + pc * A::VPLANE);
-                    mfma_split<F3>(o[qb][db], vf, pp);
-                }
+                for (int pc = 0; pc < NP; ++pc)
+                    vf[pc] = *reinterpret_cast<const u32x4*>(cur + off + pc * A::VPLANE);
+                mfma_split<F3>(o[db], vf, pp);
             }
         }
 
@@ -452,59 +415,54 @@ __global__ __launch_bounds__(NT, F3 && D * QB <= 128 ? 2 : 1) void attention_x6_
     }
 
     // ---- epilogue: O[q][dv] = O^T[dv][q] / l ----
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-        const int qrow = q0 + 32 * qb + l32;
-        if constexpr (O3) {
-            if (qrow < N) {
-                const float inv = out_mul / l_run[qb];
-                const long m = (long)b * N + qrow;  // GEMM row (pixel of the batch)
-                const long rowbase = ((m >> 7) * (C / 16)) * 4 * 128 * 16 + (m & 127) * 16 + 8 * half;
-                unsigned char* a3 = reinterpret_cast<unsigned char*>(out);
-#pragma unroll
-                for (int d = 0; d < A::NDB; ++d) {
-#pragma unroll
-                    for (int r = 0; r < 16; r += 4) {
-                        const int c = head * D + d * 32 + 8 * (r >> 2) + 4 * half;  // c % 8 == 4 half
-                        const f32x4 v =
-                            f32x4{o[qb][d][r] * inv, o[qb][d][r + 1] * inv, o[qb][d][r + 2] * inv, o[qb][d][r + 3] * inv} * vs;
-                        u32x2 ph, pl;
-                        split2_f16(v, ph, pl);
-                        unsigned char* dst = a3 + rowbase + ((long)(c >> 4) * 4 + ((c >> 3) & 1)) * 128 * 16;
-                        *reinterpret_cast<u32x2*>(dst) = ph;                 // piece 0
-                        *reinterpret_cast<u32x2*>(dst + 2 * 128 * 16) = pl;  // piece 1
-                    }
-                }
-            }
-            continue;
-        }
-        // log-sum-exp of the scaled scores for the backward (wc_attention_bwd's contract):
-        // lse = log2 sum_k 2^(s_k * scale * log2 e) = m + log2(l) - EP, EP the f16x3 P prescale
-        if (lse != nullptr && half == 0 && qrow < N)
-            lse[((long)b * heads + head) * N + qrow] = m_run[qb] + log2f(l_run[qb]) - (F3 ? 14.0f : 0.0f);
+    if constexpr (O3) {
         if (qrow < N) {
-            const float inv = out_mul / l_run[qb];
-            float* orow = out + ((long)b * N + qrow) * ldo + head * D;
+            const float inv = out_mul / l_run;
+            const long m = (long)b * N + qrow;  // GEMM row (pixel of the batch)
+            const long rowbase = ((m >> 7) * (C / 16)) * 4 * 128 * 16 + (m & 127) * 16 + 8 * half;
+            unsigned char* a3 = reinterpret_cast<unsigned char*>(out);
 #pragma unroll
             for (int d = 0; d < A::NDB; ++d) {
 #pragma unroll
                 for (int r = 0; r < 16; r += 4) {
-                    const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
-                    *reinterpret_cast<f32x4*>(orow + dv) =
-                        f32x4{o[qb][d][r] * inv, o[qb][d][r + 1] * inv, o[qb][d][r + 2] * inv, o[qb][d][r + 3] * inv};
+                    const int c = head * D + d * 32 + 8 * (r >> 2) + 4 * half;  // c % 8 == 4 half
+                    const f32x4 v = f32x4{o[d][r] * inv, o[d][r + 1] * inv, o[d][r + 2] * inv, o[d][r + 3] * inv} * vs;
+                    u32x2 ph, pl;
+                    split2_f16(v, ph, pl);
+                    unsigned char* dst = a3 + rowbase + ((long)(c >> 4) * 4 + ((c >> 3) & 1)) * 128 * 16;
+                    *reinterpret_cast<u32x2*>(dst) = ph;                 // piece 0
+                    *reinterpret_cast<u32x2*>(dst + 2 * 128 * 16) = pl;  // piece 1
                 }
+            }
+        }
+        return;
+    }
+    // log-sum-exp of the scaled scores for the backward (wc_attention_bwd's contract):
+    // lse = log2 sum_k 2^(s_k * scale * log2 e) = m + log2(l) - EP, EP the f16x3 P prescale
+    if (lse != nullptr && half == 0 && qrow < N)
+        lse[((long)b * heads + head) * N + qrow] = m_run + log2f(l_run) - (F3 ? 14.0f : 0.0f);
+    if (qrow < N) {
+        const float inv = out_mul / l_run;
+        float* orow = out + ((long)b * N + qrow) * ldo + head * D;
+#pragma unroll
+        for (int d = 0; d < A::NDB; ++d) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 4) {
+                const int dv = d * 32 + 8 * (r >> 2) + 4 * half;
+                *reinterpret_cast<f32x4*>(orow + dv) =
+                    f32x4{o[d][r] * inv, o[d][r + 1] * inv, o[d][r + 2] * inv, o[d][r + 3] * inv};
             }
         }
     }
 }
 
-template <int D, bool F3, bool PRE = false, bool O3 = false, int QB = 1>
+template <int D, bool F3, bool PRE = false, bool O3 = false>
 int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, int C, int heads,
                 float scale, int eq, int ek, int ev, hipStream_t stream, float* lse = nullptr) {
     using A = Ax6<D, F3>;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3, PRE, O3, QB>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x6_kernel<D, F3, PRE, O3>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, A::LDS);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -512,23 +470,13 @@ int launch_att6(const float* qkv, int ldq, float* out, int ldo, int B, int N, in
     // P carries 2^14 under f16x3 (small probabilities stay in the fp16 normal range); it is added
     // in the exp2 argument inside the kernel and cancels in O / l
     const float score_mul = scale * 1.4426950408889634f * ldexpf(1.f, -(eq + ek));
-    dim3 grid(((N + 128 * QB - 1) / (128 * QB)) * heads * B);
-    if constexpr (QB == 1)
-        WC_SET_NAME("attention_x6_kernel", {WC_TI(D), WC_TB(F3), WC_TB(PRE), WC_TB(O3)});
-    else
-        WC_SET_NAME("attention_x6_kernel", {WC_TI(D), WC_TB(F3), WC_TB(PRE), WC_TB(O3), WC_TI(QB)});
-    hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE, O3, QB>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
+    dim3 grid(((N + 127) / 128) * heads * B);
+    WC_SET_NAME("attention_x6_kernel", {WC_TI(D), WC_TB(F3), WC_TB(PRE), WC_TB(O3)});
+    hipLaunchKernelGGL((attention_x6_kernel<D, F3, PRE, O3>), grid, dim3(NT), A::LDS, stream, qkv, ldq, out, ldo, N, C,
                        score_mul, ldexpf(1.f, eq), ldexpf(1.f, ek), ldexpf(1.f, ev), 1.0f, ldexpf(1.f, -ev), lse);
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
-
-// Query blocks per wave of the d = 128 pre-split forms: 1 (two waves per SIMD, 32 queries each) or 2
-// (one wave per SIMD, 64 queries; needs N % 256 == 0).  Initial value from WC_ATTN_QB (A/B runs).
-int g_attn_qb = [] {
-    const char* e = getenv("WC_ATTN_QB");
-    return e ? atoi(e) : 1;
-}();
 
 template <bool F3>
 int dispatch_att6(const float* qkv, int ld_qkv, float* out, int ld_out, int B, int N, int C, int heads,
@@ -561,10 +509,7 @@ int dispatch_att_presplit(const void* qkv3, float* out, int ld_out, int B, int N
         case 32: return launch_att6<32, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
         case 64: return launch_att6<64, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
         case 96: return launch_att6<96, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-        case 128:
-            if (g_attn_qb == 2 && N % 256 == 0)
-                return launch_att6<128, true, true, false, 2>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
-            return launch_att6<128, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
+        case 128: return launch_att6<128, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
         case 160: return launch_att6<160, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
         case 192: return launch_att6<192, true, true>(q, 0, out, ld_out, B, N, C, heads, scale, eq, ek, ev, s);
         default: return WC_E_SHAPE;
@@ -584,10 +529,7 @@ int dispatch_att_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B
         case 32: return launch_att6<32, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
         case 64: return launch_att6<64, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
         case 96: return launch_att6<96, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
-        case 128:
-            if (g_attn_qb == 2 && N % 256 == 0)
-                return launch_att6<128, true, true, true, 2>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
-            return launch_att6<128, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
+        case 128: return launch_att6<128, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
         case 160: return launch_att6<160, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
         case 192: return launch_att6<192, true, true, true>(q, 0, o, C, B, N, C, heads, scale, eq, ek, ev, s);
         default: return WC_E_SHAPE;
@@ -595,13 +537,6 @@ int dispatch_att_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B
 }
 
 }  // namespace
-
-extern "C" int wc_attention_set_qb(int qb) {
-    if (qb != 1 && qb != 2) return WC_E_ARG;
-    const int prev = g_attn_qb;
-    g_attn_qb = qb;
-    return prev;
-}
 
 extern "C" int wc_attention_fwd_f16x3_presplit_a3(const void* qkv3, void* a3, int64_t a3_bytes, int B, int N, int C,
                                                   int heads, float scale, int q_exp, int k_exp, int v_exp,

@@ -484,12 +484,6 @@ def set_wino_form(mode: int) -> int:
     return _native.set_selector('wc_conv3x3_wino_set_form', int(mode), lambda v: v >= 0)
 
 
-def set_attention_qb(qb: int) -> int:
-    """wc_attention_set_qb: 32-query blocks per wave of the d = 128 pre-split attention (1 or 2);
-    returns the previous setting."""
-    return _native.set_selector('wc_attention_set_qb', int(qb), lambda v: v in (1, 2))
-
-
 def set_conv3_onewave(mode: int) -> int:
     """wc_conv3x3_set_onewave: 0 off (default), 1 forced, -1 where it fills the chip; returns the previous mode."""
     prev = _native.set_selector('wc_conv3x3_set_onewave', int(mode), lambda v: v >= -1)

@@ -157,12 +157,13 @@ _active = threading.local()
 
 
 def lib_path(variant: str = '') -> str:
-    """The in-tree library (variant 'single16': the single-piece build); WC_KERNEL_LIB points at
-    another build of the default one (developer experiments only)."""
+    """The in-tree library (variant 'single16' / 'bf16': the single-piece builds); WC_KERNEL_LIB
+    (WC_KERNEL_LIB_SINGLE16, WC_KERNEL_LIB_BF16) points at another build of it (developer A/B runs only,
+    with WC_ALLOW_STALE_LIB=1)."""
     if variant == 'single16':
-        return _build.SINGLE16_LIB_PATH
+        return os.environ.get('WC_KERNEL_LIB_SINGLE16', _build.SINGLE16_LIB_PATH)
     if variant == 'bf16':
-        return _build.BF16_LIB_PATH
+        return os.environ.get('WC_KERNEL_LIB_BF16', _build.BF16_LIB_PATH)
     return os.environ.get('WC_KERNEL_LIB', _build.LIB_PATH)
 
 

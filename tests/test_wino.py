@@ -270,7 +270,8 @@ def test_conv3x3_wino_eight_wave_forms_bit_identical(B, H, W, Ci, Co, Cr, form):
     2: also 128 channels x 16 rows where H % 16 == 0) against the 4-wave form: bit-identical output,
     per-image absmax and GroupNorm tile partials (the same products in the same order per output);
     residual chunks interleaved and as a tail."""
-    _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_form(form if m else 0))
+    _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_form(form if m else 0),
+                   lambda K, v: K.set_wino_form(v))
 
 
 @pytest.mark.gpu
@@ -283,7 +284,8 @@ def test_conv3x3_wino_presplit_bit_identical(B, H, W, Ci, Co, Cr):
     halo planes by LDS-DMA) against the in-conv prologue: bit-identical output, absmax and GroupNorm
     partials (the same arithmetic in a separate pass); 64- and 128-channel tiles, residual interleaved
     and as a tail, per-image residual exponents."""
-    _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0))
+    _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0),
+                   lambda K, v: K.set_wino_vsplit(v))
 
 
 @pytest.mark.gpu
@@ -295,11 +297,12 @@ def test_conv3x3_wino_onewave_bit_identical(B, H, W, Ci, Co, Cr, raw):
     bit-identical output (bias, temb), per-image absmax and GroupNorm tile partials — the same products
     in the same order per output; residual chunks interleaved (equal and unequal chunk counts) and the
     raw-segment form."""
-    _compare_forms(B, H, W, Ci, Co, Cr, raw, lambda K, m: K.set_wino_onewave(m))
+    _compare_forms(B, H, W, Ci, Co, Cr, raw, lambda K, m: K.set_wino_onewave(m), lambda K, v: K.set_wino_onewave(v))
 
 
-def _compare_forms(B, H, W, Ci, Co, Cr, raw, select):
-    """One conv under select(K, 0) and under select(K, 1): outputs, absmax and GN partials bit-identical."""
+def _compare_forms(B, H, W, Ci, Co, Cr, raw, select, restore):
+    """One conv under select(K, 0) and under select(K, 1): outputs, absmax and GN partials bit-identical;
+    restore(K, v) puts back the setting select(K, 0) returned."""
     from weatherconverter_amd import kernels as K
     g = torch.Generator().manual_seed(53)
     x = (torch.randn((B, H, W, Ci), generator=g) * 2 + 1).cuda()
@@ -333,6 +336,6 @@ def _compare_forms(B, H, W, Ci, Co, Cr, raw, select):
             torch.cuda.synchronize()
             res[mode] = (y.cpu(), amax.cpu(), gp.part.cpu())
     finally:
-        select(K, prev)
+        restore(K, prev)
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b), ((a - b).abs().max(), names)

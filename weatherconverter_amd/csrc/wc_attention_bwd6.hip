@@ -39,16 +39,19 @@ template <int D, bool F3 = false>
 struct B6Cfg {
     static_assert(D % 32 == 0, "split-precision attention backward: D % 32 == 0");
     static constexpr int NP = F3 ? 2 : 3;   // operand pieces
+    // pieces kept in LDS: the single-piece builds (WC_SINGLE16) never read the f16x3 low piece, so their
+    // tiles hold the high piece only (half the LDS: two workgroups per CU at D = 128)
+    static constexpr int NPS = F3 && WC_SINGLE16 ? 1 : NP;
     static constexpr int NCH = D / 16;      // 16-dim K-steps of S / dP
     static constexpr int NDB = D / 32;      // 32-dim output blocks
     static constexpr int RSB = 2 * D + 80;  // tile row bytes (odd multiple of 16: conflict-free b128 reads)
     static constexpr int PLANE = 32 * RSB;  // one piece of one 32-row tile
-    static constexpr int TILE = NP * PLANE; // the pieces
+    static constexpr int TILE = NPS * PLANE; // the pieces
     static constexpr int STAGE = 2 * TILE + 2 * 32 * 4;  // two tiles (Q, dO or K, V) + lse / Dv
     static constexpr int LDS = 2 * STAGE;                // double-buffered: tile t + 1 staged under tile t
     static constexpr int IPT = D / 32;                   // float4 items per thread of one 32 x D tile
     static constexpr bool PRESPLIT = D <= 128;   // own rows kept as pieces (else fp32, split per use)
-    static constexpr int VROWB = NCH * NP * 64 * 16;  // one wave's own rows as pieces in get() order (VL)
+    static constexpr int VROWB = NCH * NPS * 64 * 16;  // one wave's own rows as pieces in get() order (VL)
     static constexpr int LDS_VL = STAGE + 4 * VROWB;  // VL: one Q / dO stage + the four waves' V rows
 };
 
@@ -160,7 +163,7 @@ struct TileStage {
                 u32x2 h, l;
                 split2_f16(v[j] * sc, h, l);
                 *reinterpret_cast<u32x2*>(d) = h;
-                *reinterpret_cast<u32x2*>(d + Cf::PLANE) = l;
+                if constexpr (Cf::NPS > 1) *reinterpret_cast<u32x2*>(d + Cf::PLANE) = l;
             } else {
                 u32x2 p0, p1, p2;
                 split3(v[j], p0, p1, p2);
@@ -178,7 +181,8 @@ WC_DEVICE void tile_rows(const unsigned char* tile, int l32, int half, int ch, u
     using Cf = B6Cfg<D, F3>;
     const unsigned char* p = tile + l32 * Cf::RSB + (16 * ch + 8 * half) * 2;
 #pragma unroll
-    for (int pc = 0; pc < Cf::NP; ++pc) out[pc] = *reinterpret_cast<const u32x4*>(p + pc * Cf::PLANE);
+    for (int pc = 0; pc < Cf::NP; ++pc)
+        out[pc] = pc < Cf::NPS ? *reinterpret_cast<const u32x4*>(p + pc * Cf::PLANE) : u32x4{0u, 0u, 0u, 0u};
 }
 
 // A operand = tile^T (rows = the 32 dims of block db, K = 16 tile rows of chunk c) in the row order
@@ -194,6 +198,10 @@ WC_DEVICE void tile_cols(const unsigned char* tile, int lane, int db, int c, u32
     typedef short v4s __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int pc = 0; pc < Cf::NP; ++pc) {
+        if (pc >= Cf::NPS) {
+            out[pc] = u32x4{0u, 0u, 0u, 0u};
+            continue;
+        }
         const unsigned char* a = base + pc * Cf::PLANE;
         const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a));
         const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a + 8 * Cf::RSB));
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
             u32x4 pc[NP];
             pieces8<F3>(v, sc.sv, pc);
 #pragma unroll
-            for (int pp = 0; pp < NP; ++pp) *reinterpret_cast<u32x4*>(vls + ((ch * NP + pp) * 64 + lane) * 16) = pc[pp];
+            for (int pp = 0; pp < Cf::NPS; ++pp) *reinterpret_cast<u32x4*>(vls + ((ch * Cf::NPS + pp) * 64 + lane) * 16) = pc[pp];
         }
     } else {
         vr.load(base + (long)key * ldq + vcol, key < N, half, sc.sv);
@@ -329,7 +337,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
             tile_rows<D, F3>(Os, l32, half, ch, a);
             if constexpr (VL) {
 #pragma unroll
-                for (int pp = 0; pp < NP; ++pp) bk[pp] = *reinterpret_cast<const u32x4*>(vls + ((ch * NP + pp) * 64 + lane) * 16);
+                for (int pp = 0; pp < NP; ++pp)
+                    bk[pp] = pp < Cf::NPS ? *reinterpret_cast<const u32x4*>(vls + ((ch * Cf::NPS + pp) * 64 + lane) * 16)
+                                          : u32x4{0u, 0u, 0u, 0u};
             } else {
                 vr.get(ch, bk);
             }
@@ -391,7 +401,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
 }
 
 template <int D, bool F3, int DS = 1>
-__global__ __launch_bounds__(256, 1) void attn_bwd6_dq_kernel(
+__global__ __launch_bounds__(256, F3 && WC_SINGLE16 && D <= 128 ? 2 : 1) void attn_bwd6_dq_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
     int eq, int ek, int ev, const float* __restrict__ dobound, float* __restrict__ amx) {

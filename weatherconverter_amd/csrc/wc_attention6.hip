@@ -29,6 +29,12 @@ using namespace wcx6;
 
 constexpr int NT = 256;
 constexpr int KT = 32;  // keys per tile
+// 1 (default): the pre-split d = 128 forms read a tile's K fragments all at once and its V fragments
+// before the softmax (one LDS latency per phase, the V reads under the softmax VALU; 252 VGPRs, still
+// two waves per SIMD): 1549 -> 1514 us on the 64 x 64 attention, same box.  0 for A/B builds.
+#ifndef WC_ATT_PREF
+#define WC_ATT_PREF 1
+#endif
 
 template <int D, bool F3>
 struct Ax6 {
@@ -337,6 +343,22 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
         f32x16 s;
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#if WC_ATT_PREF
+        if constexpr (PRE && D == 128) {
+            // all of the tile's K fragments first (one LDS latency for the whole S, not one per chunk)
+            u32x4 kf[A::NCH][NP];
+#pragma unroll
+            for (int ch = 0; ch < A::NCH; ++ch)
+#pragma unroll
+                for (int pc = 0; pc < NP; ++pc)
+                    kf[ch][pc] = *reinterpret_cast<const u32x4*>(cur + ((pc * A::NCH + ch) * 2 + half) * A::KPLANE +
+                                                                  (l32 ^ ((ch * 2 + half) & 15)) * 16);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int ch = 0; ch < A::NCH; ++ch) mfma_split<F3>(s, kf[ch], qp[ch]);
+        } else
+#endif
+        {
 #pragma unroll
         for (int ch = 0; ch < A::NCH; ++ch) {
             u32x4 kf[NP];
@@ -346,6 +368,23 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
                                                           (l32 ^ ((ch * 2 + half) & 15)) * 16);
             mfma_split<F3>(s, kf, qp[ch]);
         }
+        }
+#if WC_ATT_PREF
+        // the tile's V fragments issued before the softmax, whose VALU covers their latency
+        u32x4 vpre[(PRE && D == 128) ? 2 : 1][(PRE && D == 128) ? A::NDB : 1][NP];
+        if constexpr (PRE && D == 128) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int db = 0; db < A::NDB; ++db) {
+                    const int d = db * 32 + l32;
+                    const int off = A::KBYTES + d * (KT * 2) + (((2 * c + half) ^ ((d >> 2) & 3)) << 4);
+#pragma unroll
+                    for (int pc = 0; pc < NP; ++pc)
+                        vpre[c][db][pc] = *reinterpret_cast<const u32x4*>(cur + off + pc * A::VPLANE);
+                }
+        }
+#endif
 
         // ---- online softmax over keys, per query (lane) ----
         // The running max is kept in the exp2 domain: max(s) * score_mul = max(s * score_mul)
@@ -398,6 +437,13 @@ __global__ __launch_bounds__(NT, F3 && D <= 128 ? 2 : 1) void attention_x6_kerne
             for (int db = 0; db < A::NDB; ++db) {
                 const int d = db * 32 + l32;
                 const int off = A::KBYTES + d * (KT * 2) + (((2 * c + half) ^ ((d >> 2) & 3)) << 4);
+#if WC_ATT_PREF
+                if constexpr (PRE && D == 128) {
+                    (void)off;
+                    mfma_split<F3>(o[db], vpre[c][db], pp);
+                    continue;
+                }
+#endif
                 u32x4 vf[NP];
 #pragma unroll
                 for (int pc = 0; pc < NP; ++pc)

@@ -285,8 +285,9 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
     const int grp = ((l32 >= 4 && l32 < 12) || (l32 >= 16 && l32 < 20) || l32 >= 28) ? 1 : 0;
     const int px = l32 < 4 ? l32 : l32 < 12 ? l32 - 4 : l32 < 20 ? l32 - 8 : l32 < 28 ? l32 - 12 : l32 - 16;
     const int py = (threadIdx.x >> 6) * 4 + (lane >> 5) * 2 + grp;
-    float acc0 = bias[0], acc1 = NO > 1 ? bias[1] : 0.f, acc2 = NO > 2 ? bias[2] : 0.f,
-          acc3 = (NOC > 3 && NO > 3) ? bias[3] : 0.f;
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    f32x2v acc01 = {bias[0], NO > 1 ? bias[1] : 0.f};
+    float acc2 = NO > 2 ? bias[2] : 0.f, acc3 = (NOC > 3 && NO > 3) ? bias[3] : 0.f;
     // halo item i = threadIdx.x + 256 k: pixel i >> 2, channels 4 (i & 3) ..
     long goff[HD_PER_T];
     unsigned inb = 0, val = 0;
@@ -320,7 +321,12 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if ((inb >> k) & 1u) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = wc_silu(fmaf(ra[k][e], rs[e], rh[e]));
+                for (int e = 0; e < 4; ++e) {
+                    // SiLU with v_rcp_f32 (as the conv prologues' silu_fast) instead of an IEEE division:
+                    // the division's ten instructions per value were a quarter of this kernel's VALU
+                    const float y = fmaf(ra[k][e], rs[e], rh[e]);
+                    v[e] = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                }
             }
             const int i = threadIdx.x + 256 * k;
             halo[(i & 3) * HPIX + (i >> 2)] = v;  // zero padding after the prologue, as the reference pads
@@ -337,8 +343,8 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const f32x4 wv = *reinterpret_cast<const f32x4*>(wc + ((tap * 16) + 4 * q + e) * 4);
-                    acc0 = fmaf(a[e], wv.x, acc0);
-                    acc1 = fmaf(a[e], wv.y, acc1);
+                    // outputs 0 and 1 as one packed FMA (v_pk_fma_f32, the same fused products)
+                    acc01 = __builtin_elementwise_fma(f32x2v{a[e], a[e]}, f32x2v{wv.x, wv.y}, acc01);
                     acc2 = fmaf(a[e], wv.z, acc2);
                     if constexpr (NOC > 3) acc3 = fmaf(a[e], wv.w, acc3);
                 }
@@ -349,8 +355,8 @@ __global__ __launch_bounds__(256) void head_conv_kernel(const float* __restrict_
     if (gx < W && gy < H) {
         const long o = ((long)b * NO * H + gy) * W + gx;
         const long ps = (long)H * W;
-        out[o] = acc0;
-        if (NO > 1) out[o + ps] = acc1;
+        out[o] = acc01.x;
+        if (NO > 1) out[o + ps] = acc01.y;
         if (NO > 2) out[o + 2 * ps] = acc2;
         if (NOC > 3 && NO > 3) out[o + 3 * ps] = acc3;
     }

@@ -116,50 +116,124 @@ def _describe(name: str) -> str:
     return f'{mode}: {d}'
 
 
-def roofline_leg(model, x, t_dev, groups: int = 1):
-    """Per-kernel timing of one UNet forward (eager, same kernels and arguments as the graph).
+def _is_hbm(name: str) -> bool:
+    return name.startswith(('gn_', 'split_', 'wino_vsplit'))
 
-    Every conv / projection / attention launch is re-issued 5x back to back right after itself
-    between one HIP event pair (kernels.replay_timing('*')): per-launch durations without event
-    gaps, as rocprofv3's kernel trace times them.  Launches are keyed by the exact instantiation the
-    library reports (rocprofv3's name), so this table lines up with the trace of the timed graph
-    replays (tools/step_table.py).  The dominant kernel = the instantiation with the most time per
-    forward; achieved = its algorithmic (fp32-equivalent) FLOPs per launch / its mean duration,
-    against its arithmetic mode's ceiling."""
+
+def _stamp_overhead(slots, n: int = 65) -> float:
+    """Seconds one wc_stamp node adds to a replayed graph: n stamps captured back to back, the median
+    interval between consecutive ones."""
+    from weatherconverter_amd import _native, kernels
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(n):
+            _native.call('wc_stamp', slots.data_ptr(), i, kernels._stream())
+    g.replay()
+    torch.cuda.synchronize()
+    v = slots[:n].cpu().tolist()
+    del g
+    d = sorted(b - a for a, b in zip(v, v[1:]))
+    return d[len(d) // 2] / kernels.wall_clock_hz()
+
+
+def ingraph_timing(model, x, t_dev, reps: int = 3):
+    """Per-launch durations INSIDE a replayed HIP graph, as the timed steps run them.  One UNet forward is
+    captured with a wc_stamp node (a one-wave kernel writing the GPU wall clock, kernels.stamp_timing) on
+    each side of every named launch and replayed `reps` times; a launch's duration = the clock
+    difference of its two stamps minus one stamp node's own share of the graph (measured by
+    _stamp_overhead), averaged over the replays.  (torch refuses timed event-record nodes in ROCm graph
+    capture, so the clock is read by the graph itself.)  Returns ({instantiation: [launches, flops, sec,
+    bytes, issued mfma flops]} per forward, the stamped graph's wall per replay, the sum of the
+    per-launch durations, the stamp overhead)."""
     from weatherconverter_amd import kernels
-    with torch.no_grad():
-        model(x, t_dev)  # packs / allocations outside the measured forward
-    torch.cuda.synchronize()
-    # pass 1: per-launch events around single launches (kept beside the re-issue means)
-    prof = kernels.profile_conv(True)
-    # Park the GPU first so the host enqueues the whole forward ahead of it: the kernels then run
-    # back to back and each event pair brackets one kernel, not a host launch gap.
-    torch.cuda._sleep(1 << 28)
-    with torch.no_grad():
-        model(x, t_dev)
-    torch.cuda.synchronize()
-    kernels.profile_conv(False)
-    ev = {}
-    for name, flops, e0, e1 in prof:
-        d = ev.setdefault(name, [0, 0.0])
+    hz = kernels.wall_clock_hz()
+    x_in, t_in = x.clone(), t_dev.clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        model(x_in, t_in)  # allocations / packs outside the capture
+    torch.cuda.current_stream().wait_stream(side)
+    slots = torch.zeros(16384, dtype=torch.int64, device=x.device)
+    over = _stamp_overhead(slots)
+    g = torch.cuda.CUDAGraph()
+    st = kernels.stamp_timing(slots)
+    try:
+        with torch.cuda.graph(g):
+            model(x_in, t_in)
+    finally:
+        kernels.stamp_timing(None)
+    launches = st['launches']
+    per, walls = {}, []
+    for name, flops, nbytes, mfma in launches:
+        d = per.setdefault(name, [0, 0.0, 0.0, 0.0, 0.0])
         d[0] += 1
-        d[1] += e0.elapsed_time(e1) * 1e-3
-    # pass 2: every launch re-issued 5x between one event pair
+        d[1] += flops
+        d[3] += nbytes
+        d[4] += mfma if mfma is not None else flops * _pieces(name)
+    for _ in range(reps):
+        w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        w0.record()
+        g.replay()
+        w1.record()
+        torch.cuda.synchronize()
+        walls.append(w0.elapsed_time(w1) * 1e-3)
+        v = slots[:2 * len(launches)].cpu().tolist()
+        for i, (name, *_) in enumerate(launches):
+            per[name][2] += ((v[2 * i + 1] - v[2 * i]) / hz - over) / reps
+    del g
+    total = sum(v[2] for v in per.values())
+    return per, sum(walls) / len(walls), total, over
+
+
+def reissue_timing(model, x, t_dev):
+    """Every conv / projection / attention launch of one eager forward re-issued 5x back to back right
+    after itself between one HIP event pair (kernels.replay_timing('*')): the per-instantiation table
+    of rounds 3-5, kept beside the in-graph one."""
+    from weatherconverter_amd import kernels
     rep = kernels.replay_timing('*', reps=5)
     torch.cuda._sleep(1 << 28)
     with torch.no_grad():
         model(x, t_dev)
     torch.cuda.synchronize()
     kernels.replay_timing(None)
-    per, hbm = {}, {}
+    per = {}
     for name, flops, r0, r1, reps, nbytes, mfma in rep['events']:
-        d = (hbm if name.startswith(('gn_', 'split_', 'wino_vsplit')) else per).setdefault(name, [0, 0.0, 0.0, 0.0, 0.0])
+        d = per.setdefault(name, [0, 0.0, 0.0, 0.0, 0.0])
         d[0] += 1
         d[1] += flops
         d[2] += r0.elapsed_time(r1) * 1e-3 / reps
         d[3] += nbytes
-        # dense 16-bit MFMA FLOPs issued: as stated by the launch, else the algorithmic count x pieces
         d[4] += mfma if mfma is not None else flops * _pieces(name)
+    return per
+
+
+def roofline_leg(model, x, t_dev, groups: int = 1):
+    """Per-kernel timing of one UNet forward as the timed graph runs it.
+
+    Primary: ingraph_timing -- a HIP event pair around every named launch inside a replayed graph of
+    the forward (same kernels, arguments and order as the timed steps), keyed by the exact
+    instantiation the library reports (rocprofv3's name), so the table lines up with the rocprofv3
+    trace of the timed replays (tools/step_table.py).  The dominant kernel = the MFMA instantiation
+    with the most in-graph time per forward; achieved = its algorithmic (fp32-equivalent) FLOPs per
+    launch / its in-graph mean duration, against its arithmetic mode's ceiling.  The round-3..5
+    re-issue table (reissue_timing) rides along as mean_launch_ms_reissue."""
+    with torch.no_grad():
+        model(x, t_dev)  # packs / allocations outside the measured forward
+    torch.cuda.synchronize()
+    src = ('in-graph: GPU wall-clock stamps (wc_stamp nodes) around each launch inside a replayed HIP graph of '
+           'the forward, minus one stamp node; mean of 3 replays')
+    graph_wall = graph_sum = over = None
+    try:
+        with torch.no_grad():
+            per_all, graph_wall, graph_sum, over = ingraph_timing(model, x, t_dev)
+    except Exception as e:  # noqa: BLE001 -- report the fallback in the line instead of failing the bench
+        per_all = None
+        src = f'in-graph stamps failed ({type(e).__name__}: {e}); each launch re-issued 5x between one event pair'
+    rei = reissue_timing(model, x, t_dev)
+    if per_all is None:
+        per_all = rei
+    per = {k: v for k, v in per_all.items() if not _is_hbm(k)}
+    hbm = {k: v for k, v in per_all.items() if _is_hbm(k)}
     name = max(per, key=lambda k: per[k][2])
     n, fl, sec, abytes, issued = per[name]
     mean_dur = sec / n
@@ -180,7 +254,7 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
                            f'mean over {rec["launches"]} launches'
                            + (f'; algorithmic {rec["algorithmic_bytes"] / 1e9:.3f}' if 'algorithmic_bytes' in rec
                               else ''))
-    ev_n, ev_sec = ev.get(name, (0, 0.0))
+    rn = rei.get(name)
     # what a bare f16 MFMA stream sustains on this power-capped chip: the MAXIMUM over the committed
     # waves-per-SIMD sweep (tools/probes/mfma_peak.hip, median of each point's three launches; the
     # best point is one wave per SIMD issuing back to back), the split-precision kernels' work
@@ -222,8 +296,11 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
         'launches_per_step': n * groups,
         'images_per_launch': int(x.shape[0]),
         'mean_launch_ms': round(mean_dur * 1e3, 4),
-        'mean_launch_ms_source': 'each launch re-issued 5x back to back between one HIP event pair',
-        'mean_launch_ms_events': round(ev_sec / ev_n * 1e3, 4) if ev_n else None,
+        'mean_launch_ms_source': src,
+        'mean_launch_ms_reissue': round(rn[2] / rn[0] * 1e3, 4) if rn else None,
+        'ingraph_stamped_forward_ms': round(graph_wall * 1e3, 3) if graph_wall else None,
+        'ingraph_launch_sum_ms': round(graph_sum * 1e3, 3) if graph_sum else None,
+        'ingraph_stamp_node_us': round(over * 1e6, 3) if over is not None else None,
         'gflop_per_launch': round(fl / n / 1e9, 3),
         'algorithmic_gb_per_launch': round(abytes / n / 1e9, 4) if abytes else None,
         'traffic_over_algorithmic': round(traffic / (abytes / n / 1e9), 3) if (traffic and abytes) else None,

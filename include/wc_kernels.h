@@ -132,12 +132,6 @@ int wc_conv3x3_f16x3(const wc_conv_args* args, const void* w3, int64_t w3_bytes,
  * wc_absmax_images — the 3x3 data gradients of the training backward, unet_base.py:92,106.) */
 /* The output-channel tile (BN) wc_conv3x3_x6 and wc_conv_igemm_x6 use for N output channels. */
 int wc_conv3x3_x6_tile_n(int N);
-/* Selects the kernel form of wc_conv3x3_f16x3's GN(+SiLU) 3x3 conv without residual segment
- * (N % 128 == 0, Hm % 16 == 0): 0 (default) the three-wave halo kernel; 1 the one-wave-per-SIMD
- * 16 x 16-pixel form wherever it applies; -1 that form where its tiles fill the chip (>= 1024
- * workgroups).  Both forms give bit-identical results.  Returns the previous mode (or WC_E_ARG).
- * Process-wide, not thread-safe against concurrent launches. */
-int wc_conv3x3_set_onewave(int mode);
 /* The ResBlock 3x3 conv (GN+SiLU prologue on segment 0, optional fused 1x1 residual segment 1; or
  * one raw segment 0 under the per-image bound a_bound, s = min(a_exp - 1, 12 - floor(log2 a_bound[b])))
  * through a Winograd F(2,3) transform along x on f16x3 (csrc/wc_wino.hip): per output pair and
@@ -154,15 +148,6 @@ int wc_conv3x3_set_onewave(int mode);
 int wc_conv3x3_wino_f16x3(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
                           const float* w_inv_scale, const float* a_bound, void* stream);
 int wc_conv3x3_wino_tile_n(int N);
-/* Form of wc_conv3x3_wino_f16x3 for BN = 128: 0 (default) two waves per SIMD, 8-row tiles; 1 one wave
- * per SIMD with 16-row tiles (each weight fragment feeds four MFMA row blocks) where H % 16 == 0.
- * Bit-identical results.  Returns the previous mode (or WC_E_ARG); process-wide. */
-int wc_conv3x3_wino_set_onewave(int mode);
-/* Workgroup form of wc_conv3x3_wino_f16x3 with a GN+SiLU segment and BN = 128 weights: 0 (default) 4-wave
- * workgroups; 1 8-wave workgroups of 256 output channels x 8 rows where N % 256 == 0 (one halo
- * transform feeds twice the MFMA work); 2 as 1, else 8-wave 128 channels x 16 rows where H % 16 == 0.
- * Same weight packing, bit-identical results.  Returns the previous mode (or WC_E_ARG); process-wide. */
-int wc_conv3x3_wino_set_form(int mode);
 /* The GN + SiLU segment 0 of a wc_conv3x3_wino_f16x3 conv, transformed and split ONCE (instead of once
  * per output-channel tile inside the conv): segment 0 of `args` (scale / shift / silu set, W % 16 == 0)
  * GroupNorm-affine'd, SiLU'd, scaled by 2^s (s = a_exp - 1, per image clamped to 13 - e(a_bound[b]) when
@@ -283,10 +268,9 @@ int wc_proj_f16x3_qkv(const wc_conv_args* args, const void* a3, int64_t a3_bytes
                       void* stream);
 /* Form of the two pre-split projection GEMMs above: 0 (default) the measured choice (256 x 128
  * tiles for wc_proj_f16x3_qkv at >= 2048 of them, else 128 x 128), 256 (wherever the pixels per
- * image are a multiple of 256), 128 (the 128 x 128 LDS-DMA form), -128 (128 x 128 tiles with the
- * B fragments from L2 in registers) or -129 (A and B in registers, no LDS).  All forms give
- * bit-identical results.  Returns the previous
- * setting (or WC_E_ARG).  Process-wide, not thread-safe against concurrent launches. */
+ * image are a multiple of 256) or 128 (the 128 x 128 LDS-DMA form).  Both forms give bit-identical
+ * results.  Returns the previous setting (or WC_E_ARG).  Process-wide, not thread-safe against
+ * concurrent launches. */
 int wc_proj_set_tile(int rows);
 
 /* ------------------------------------------------------------------------------------------ */
@@ -630,6 +614,13 @@ const char* wc_source_hash(void);
  * when that entry point does not name its kernel.  Reading it clears it.  bench.py keys its
  * per-launch HIP-event timings by this name so they line up with the rocprofv3 kernel trace. */
 const char* wc_last_kernel_name(void);
+/* Instrumentation (no reference counterpart): a one-wave kernel that writes the GPU's constant-rate
+ * wall clock (wall_clock64) to slots[index].  Captured into a HIP graph around each named launch
+ * (kernels.stamp_timing), the stamps time every launch as the replayed graph runs it -- bench.py's
+ * roofline duration (torch refuses timed event-record nodes in ROCm graph capture). */
+int wc_stamp(unsigned long long* slots, int index, void* stream);
+/* The wall clock's rate in kHz (hipDeviceAttributeWallClockRate of the current device). */
+int wc_wall_clock_khz(int* khz);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,41 @@ def default_model(ref_models, im_size):
     return ref_models.ModelConfig(**m)
 
 
+# Reverse-step t: the ends and the middle, plus every t whose step scalars the reference host's MKL sqrt
+# rounds 1 ulp below the correctly rounded root: sqrt(1 - acp) at 14, 308, 611, 867 (and 310), sqrt(alpha)
+# at 710, the posterior sigma at 85, 490 (weatherconverter_amd/diffusion_model/scheduler/vml_sqrt.py).
+STEP_T = (0, 1, 37, 500, 999, 14, 308, 310, 611, 867, 710, 85, 490)
+# sample_prev_timestep2 (beta variance): t = 3, and the beta sigmas MKL rounds down (190, 222)
+STEP2_T = (3, 190, 222)
+
+
+def sched_steps(s, sched):
+    """Reverse-step vectors of the reference scheduler s (T = 1000) into sched."""
+    g = torch.Generator().manual_seed(11)
+    xt = torch.randn((2, 3, 16, 16), generator=g) * 3
+    eps = torch.randn((2, 3, 16, 16), generator=g)
+    sched['step_xt'] = xt.numpy()
+    sched['step_eps'] = eps.numpy()
+    for t in STEP_T:
+        torch.manual_seed(1000 + t)
+        mean, sz, _ = s.sample_prev_timestep(xt, eps, torch.as_tensor(t))
+        sched[f'step{t}_mean'] = mean.numpy()
+        if sz is not None:
+            sched[f'step{t}_sigz'] = sz.numpy()
+            torch.manual_seed(1000 + t)
+            sched[f'step{t}_z'] = torch.randn(xt.shape).numpy()
+    for t in STEP2_T:
+        tb = torch.tensor([t, t])
+        torch.manual_seed(77 + (t if t != 3 else 0))
+        mean2, sz2, _ = s.sample_prev_timestep2(xt, eps, tb)
+        key = 'step2' if t == 3 else f'step2_{t}'
+        sched[f'{key}_t'] = tb.numpy()
+        sched[f'{key}_mean'] = mean2.numpy()
+        sched[f'{key}_sigz'] = sz2.numpy()
+        torch.manual_seed(77 + (t if t != 3 else 0))
+        sched[f'{key}_z'] = torch.randn(xt.shape).numpy()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reference', default='/root/reference')
@@ -52,6 +87,8 @@ def main():
     ap.add_argument('--only-guided', action='store_true')
     ap.add_argument('--only-old', action='store_true')
     ap.add_argument('--only-traj1000', action='store_true')
+    ap.add_argument('--only-sched-steps', action='store_true',
+                    help='add the reverse-step vectors at STEP_T / STEP2_T to the existing sched.npz')
     args = ap.parse_args()
     sys.path.insert(0, args.reference)
     torch.Tensor.cuda = lambda self, *a, **k: self  # harness shim for unet_base.py:461
@@ -62,6 +99,14 @@ def main():
         return old_unet(args)
     if args.only_traj1000:
         return traj1000(args)
+    if args.only_sched_steps:
+        from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
+        path = os.path.join(HERE, 'sched.npz')
+        with np.load(path, allow_pickle=False) as z:
+            sched = dict(z)
+        sched_steps(LinearNoiseScheduler(1000, 0.0001, 0.02), sched)
+        np.savez(path, **sched)
+        return
     from diffusion_model.config import models as ref_models
     from diffusion_model.models.unet_base import Unet, get_time_embedding
     from diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
@@ -87,27 +132,8 @@ def main():
                   'sqrt_one_minus_alpha_cum_prod'):
             sched[f'T{T}_{n}'] = getattr(s, n).numpy()
     s = LinearNoiseScheduler(1000, 0.0001, 0.02)
-    g = torch.Generator().manual_seed(11)
-    xt = torch.randn((2, 3, 16, 16), generator=g) * 3
-    eps = torch.randn((2, 3, 16, 16), generator=g)
-    sched['step_xt'] = xt.numpy()
-    sched['step_eps'] = eps.numpy()
-    for t in (0, 1, 37, 500, 999):
-        torch.manual_seed(1000 + t)
-        mean, sz, _ = s.sample_prev_timestep(xt, eps, torch.as_tensor(t))
-        sched[f'step{t}_mean'] = mean.numpy()
-        if sz is not None:
-            sched[f'step{t}_sigz'] = sz.numpy()
-            torch.manual_seed(1000 + t)
-            sched[f'step{t}_z'] = torch.randn(xt.shape).numpy()
-    tb = torch.tensor([3, 3])
-    torch.manual_seed(77)
-    mean2, sz2, _ = s.sample_prev_timestep2(xt, eps, tb)
-    sched['step2_t'] = tb.numpy()
-    sched['step2_mean'] = mean2.numpy()
-    sched['step2_sigz'] = sz2.numpy()
-    torch.manual_seed(77)
-    sched['step2_z'] = torch.randn(xt.shape).numpy()
+    sched_steps(s, sched)
+    xt, eps = torch.from_numpy(sched['step_xt']), torch.from_numpy(sched['step_eps'])
     tn = torch.tensor([5, 880])
     sched['addnoise_t'] = tn.numpy()
     sched['addnoise_out'] = s.add_noise(xt, eps, tn).numpy()

@@ -106,18 +106,17 @@ def test_product_package_never_imports_oracle():
 
 
 def test_kernel_form_selectors_reach_every_library_variant():
-    """wc_conv3x3_set_onewave / wc_proj_set_tile keep static state per library: a setting made before
+    """wc_proj_set_tile keeps static state per library: a setting made before
     the single16 variant is opened is replayed into it, and one made after reaches both (no GPU call)."""
     from weatherconverter_amd import _build, _native
     from weatherconverter_amd import kernels as K
     if not (os.path.exists(_build.LIB_PATH) and os.path.exists(_build.SINGLE16_LIB_PATH)):
         pytest.skip('kernel libraries not built')
     p_tile = K.set_proj_tile(128)
-    p_w1 = K.set_conv3_onewave(1)
     try:
         with _native.variant('single16'):
             lib16 = _native.load()
-        assert lib16.wc_proj_set_tile(128) == 128 and lib16.wc_conv3x3_set_onewave(1) == 1  # replayed
+        assert lib16.wc_proj_set_tile(128) == 128  # replayed
         K.set_proj_tile(256)
         assert lib16.wc_proj_set_tile(256) == 256  # applied to the already-open variant too
         with pytest.raises(RuntimeError):
@@ -125,4 +124,3 @@ def test_kernel_form_selectors_reach_every_library_variant():
         assert _native.load().wc_proj_set_tile(256) == 256  # a rejected value changes nothing
     finally:
         K.set_proj_tile(p_tile)
-        K.set_conv3_onewave(p_w1)

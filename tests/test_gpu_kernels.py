@@ -259,36 +259,37 @@ TABLES = ('betas', 'alphas', 'alpha_cum_prod', 'sqrt_alpha_cum_prod', 'one_minus
 
 
 def _golden_scheduler(gd):
-    """Scheduler whose tables are the golden host's.  torch.linspace's CPU kernel groups its FMAs by the
-    host's SIMD width, so the reference's own beta table differs in the last bit between machines; the
-    bitwise kernel checks therefore run on the golden host's tables."""
+    """The product scheduler (host-independent tables, equal to the reference host's: the tables test
+    below), checked against the golden host's tables before it is used."""
     from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
     s = LinearNoiseScheduler(1000, 0.0001, 0.02)
     for n in TABLES:
-        s._cpu[n] = torch.from_numpy(gd[f'T1000_{n}'])
-        setattr(s, n, s._cpu[n].to(s.device))
+        assert np.array_equal(s._cpu[n].numpy(), gd[f'T1000_{n}']), n
     return s
 
 
+# t of the golden reverse-step vectors (tests/golden/make_golden.py STEP_T / STEP2_T): the ends, the
+# middle, and every t whose scalars the reference host's MKL sqrt rounds 1 ulp below the exact rounding
+STEP_T = (0, 1, 37, 500, 999, 14, 308, 310, 611, 867, 710, 85, 490)
+STEP2_KEYS = ('step2', 'step2_190', 'step2_222')
+
+
 def test_scheduler_tables_bit_exact_on_this_host():
-    """On the GPU box's host too (host-independent tables, tests/test_scheduler_tables.py): the four
-    linspace / cumprod tables equal the reference host's bit for bit, the square roots are the correctly
-    rounded ones of those, also on the device copies the step kernel reads."""
+    """On the GPU box's host too (host-independent tables, tests/test_scheduler_tables.py): all six tables
+    equal the reference host's bit for bit, also on the device copies the step kernel reads."""
     from weatherconverter_amd.diffusion_model.scheduler.linear_noise_scheduler import LinearNoiseScheduler
     gd = np.load(os.path.join(GOLDEN, 'sched.npz'))
     for T in (50, 1000):
         s = LinearNoiseScheduler(T, 0.0001, 0.02)
-        for n in ('betas', 'alphas', 'alpha_cum_prod', 'one_minus_cum_prod'):
+        for n in TABLES:
             assert np.array_equal(getattr(s, n).cpu().numpy(), gd[f'T{T}_{n}']), (T, n)
-        assert np.array_equal(s.sqrt_alpha_cum_prod.cpu().numpy(), np.sqrt(gd[f'T{T}_alpha_cum_prod']))
-        assert np.array_equal(s.sqrt_one_minus_alpha_cum_prod.cpu().numpy(), np.sqrt(gd[f'T{T}_one_minus_cum_prod']))
 
 
 def test_ddpm_step_bitwise_vs_reference(K):
     gd = np.load(os.path.join(GOLDEN, 'sched.npz'))
     s = _golden_scheduler(gd)
     xt, eps = torch.from_numpy(gd['step_xt']).cuda(), torch.from_numpy(gd['step_eps']).cuda()
-    for t in (0, 1, 37, 500, 999):
+    for t in STEP_T:
         z = torch.from_numpy(gd[f'step{t}_z']) if t else None
         mean, sz, none = s.sample_prev_timestep(xt, eps, torch.as_tensor(t), z=z)
         assert none is None
@@ -299,10 +300,11 @@ def test_ddpm_step_bitwise_vs_reference(K):
             assert np.array_equal(fused.cpu().numpy(), gd[f'step{t}_mean'] + gd[f'step{t}_sigz'])
         else:
             assert sz is None
-    mean2, sz2, _ = s.sample_prev_timestep2(xt, eps, torch.from_numpy(gd['step2_t']),
-                                            z=torch.from_numpy(gd['step2_z']))
-    assert np.array_equal(mean2.cpu().numpy(), gd['step2_mean'])
-    assert np.array_equal(sz2.cpu().numpy(), gd['step2_sigz'])
+    for key in STEP2_KEYS:
+        mean2, sz2, _ = s.sample_prev_timestep2(xt, eps, torch.from_numpy(gd[f'{key}_t']),
+                                                z=torch.from_numpy(gd[f'{key}_z']))
+        assert np.array_equal(mean2.cpu().numpy(), gd[f'{key}_mean']), key
+        assert np.array_equal(sz2.cpu().numpy(), gd[f'{key}_sigz']), key
     tn = torch.from_numpy(gd['addnoise_t'])
     assert np.array_equal(s.add_noise(xt, eps, tn).cpu().numpy(), gd['addnoise_out'])
     assert np.array_equal(s.add_noise2(xt, eps, tn).cpu().numpy(), gd['addnoise2_out'])
@@ -400,3 +402,27 @@ def test_head_conv_vs_float64(B, H, W, C, NO):
     out = torch.empty((B, NO, H, W), device='cuda')
     K.head_conv(K.View(buf.cuda(), 16, C), sc.cuda(), sh.cuda(), K.pack_head(w.cuda()), b.cuda(), out)
     assert rel_l2(out.cpu(), ref) < 1e-6
+
+
+def test_stamp_timing_in_graph(K):
+    """The in-graph timing bench.py's roofline reads: a tiny UNet forward captured with wc_stamp nodes
+    around every named launch; each launch gets a positive duration, the stamps are in order, and the
+    per-launch durations fit inside the stamped graph's own wall time."""
+    import bench
+    from weatherconverter_amd.diffusion_model.config import ModelConfig
+    from weatherconverter_amd.diffusion_model.models.unet_base import Unet
+    from weatherconverter_amd.synthetic import init_synthetic_
+    import json
+    man = json.load(open(os.path.join(GOLDEN, 'manifest.json')))
+    net = Unet(ModelConfig(**man['tiny']['config']))
+    init_synthetic_(net, seed=0)
+    net = net.cuda().eval()
+    assert K.wall_clock_hz() > 1e6
+    x = torch.randn((2, 3, 32, 32), device='cuda')
+    t = torch.tensor([5], device='cuda')
+    with torch.no_grad():
+        per, wall, total, over = bench.ingraph_timing(net, x, t)
+    assert K.STAMPS is None
+    assert len(per) >= 5 and all(v[0] > 0 and v[2] > 0 for v in per.values()), per
+    assert 0 < over < 50e-6
+    assert total < wall

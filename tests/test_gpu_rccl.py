@@ -58,7 +58,7 @@ CHILD = textwrap.dedent('''
     init_synthetic_(net, seed=0)
     net = net.to(dev).eval()
     s = LinearNoiseScheduler(3 if cfg == '256' else 6, 0.0001, 0.02)
-    total = 2 if cfg == '256' else 4
+    total = 16 if cfg == '256' else 4  # '256': config 5's per-rank batch (128 images / 8 GPUs)
     ref = sample_tensor(net, s, total, mc.im_channels, mc.im_size, noise='philox', seed=77, graph=True)
     x0 = sample_sharded(net, s, total, mc.im_channels, mc.im_size, noise='philox', seed=77, graph=True)
     g = gather_samples(x0, total)
@@ -81,10 +81,10 @@ CHILD = textwrap.dedent('''
 
 @pytest.mark.parametrize('cfg', ['tiny', '256'])
 def test_rccl_world1_gathers_bit_identical(cfg):
-    """cfg '256': config 5's per-rank model (the 256-px BASELINE UNet), 2 images, T=3, through the RCCL
+    """cfg '256': config 5's per-rank workload (the 256-px BASELINE UNet, 16 images, T=3) through the RCCL
     branch of sample_sharded / gather_samples / bench._gather_x0."""
     r = subprocess.run([sys.executable, '-u', '-c', CHILD, cfg], cwd=ROOT, env=_env(), capture_output=True, text=True,
-                       timeout=110)
+                       timeout=200)
     assert r.returncode == 0, r.stderr[-4000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith('RCCL_RESULT ')]
     assert len(line) == 1, r.stdout[-2000:]

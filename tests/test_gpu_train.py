@@ -672,48 +672,6 @@ def test_two_forwards_then_two_backwards_accumulate():
         net(xa.clone().requires_grad_(True), ta)
 
 
-_DKDV192_CHILD = r'''
-import sys, torch
-sys.path.insert(0, sys.argv[1])
-from weatherconverter_amd import kernels as K
-g = torch.Generator().manual_seed(8)
-B, N, C, heads = 2, 96, 768, 4
-qkv = torch.randn((B * N, 3 * C), generator=g).cuda()
-do = torch.randn((B * N, C), generator=g).cuda()
-o = torch.empty((B * N, C), device='cuda')
-lse = torch.empty((B, heads, N), device='cuda')
-K.attention_fwd_lse(qkv, o, lse, B, N, C, heads, precision='f16x3', exps=(10, 10, 10))
-dqkv = torch.empty((B * N, 3 * C), device='cuda')
-amx = torch.zeros(B, device='cuda')
-K.attention_bwd(qkv, o, do, lse, dqkv, B, N, C, heads, precision='f16x3', exps=(10, 10, 10),
-                dout_bound=do.abs().reshape(B, -1).amax(1).contiguous(), dqkv_absmax=amx)
-torch.cuda.synchronize()
-torch.save({'dqkv': dqkv.cpu(), 'amx': amx.cpu()}, sys.argv[2])
-'''
-
-
-def test_attention_bwd_d192_dkdv_splits_bit_identical(tmp_path):
-    """The d = 192 dK/dV kernel with its V rows in LDS computes each output from the same products in the
-    same order whether the output dims are split in two workgroups (default) or not (WC_DKDV192_DS=1):
-    bit-identical dqkv and raised bound.  Each setting runs in its own child process (the split is read
-    once per process)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for ds in ('2', '1'):
-        out = tmp_path / f'ds{ds}.pt'
-        env = dict(os.environ, WC_DKDV192_DS=ds)
-        r = subprocess.run([sys.executable, '-c', _DKDV192_CHILD, root, str(out)], env=env, capture_output=True,
-                           text=True, timeout=180)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res[ds] = torch.load(out, weights_only=True)
-    assert torch.equal(res['1']['dqkv'], res['2']['dqkv'])
-    assert torch.equal(res['1']['amx'], res['2']['amx'])
-    assert float(res['2']['amx'].min()) > 0
-
-
 @pytest.mark.parametrize('B,H,W,C,ld', [(3, 17, 9, 4, 4), (2, 16, 16, 64, 128), (2, 8, 12, 768, 768), (1, 5, 7, 1536, 1600),
                                         (2, 32, 33, 96, 96)])
 def test_absmax_images_vs_torch(B, H, W, C, ld):

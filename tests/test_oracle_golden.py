@@ -47,15 +47,16 @@ def test_scheduler_steps_bitwise():
     g = np.load(os.path.join(GOLDEN, 'sched.npz'))
     s = OracleScheduler(1000, 0.0001, 0.02)
     xt, eps = torch.from_numpy(g['step_xt']), torch.from_numpy(g['step_eps'])
-    for t in (0, 1, 37, 500, 999):
+    for t in (0, 1, 37, 500, 999, 14, 308, 310, 611, 867, 710, 85, 490):  # make_golden.py STEP_T
         z = torch.from_numpy(g[f'step{t}_z']) if t else None
         mean, sz = s.sample_prev_timestep(xt, eps, t, z=z)
         assert np.array_equal(mean.numpy(), g[f'step{t}_mean'])
         if t:
             assert np.array_equal(sz.numpy(), g[f'step{t}_sigz'])
-    mean2, sz2 = s.sample_prev_timestep2(xt, eps, torch.from_numpy(g['step2_t']), z=torch.from_numpy(g['step2_z']))
-    assert np.array_equal(mean2.numpy(), g['step2_mean'])
-    assert np.array_equal(sz2.numpy(), g['step2_sigz'])
+    for key in ('step2', 'step2_190', 'step2_222'):
+        mean2, sz2 = s.sample_prev_timestep2(xt, eps, torch.from_numpy(g[f'{key}_t']), z=torch.from_numpy(g[f'{key}_z']))
+        assert np.array_equal(mean2.numpy(), g[f'{key}_mean']), key
+        assert np.array_equal(sz2.numpy(), g[f'{key}_sigz']), key
     assert np.array_equal(s.add_noise(xt, eps, torch.from_numpy(g['addnoise_t'])).numpy(), g['addnoise_out'])
 
 

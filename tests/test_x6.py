@@ -475,51 +475,6 @@ def test_conv3x3_f16x3_vs_float64(B, H, W, Ci, Co, Cr, silu, gs, outlier, bounde
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('B,H,W,Ci,Co,silu,sw', [(2, 32, 32, 48, 128, True, 16), (1, 48, 16, 128, 256, False, 8),
-                                                 (3, 16, 32, 80, 128, True, 32), (1, 64, 64, 256, 384, True, 4)])
-def test_conv3x3_f16x3_onewave_bit_identical(B, H, W, Ci, Co, silu, sw):
-    """The one-wave-per-SIMD 16 x 16-pixel form (conv3x3_w1_kernel, forced on) against the
-    three-wave halo kernel (forced off): bit-identical output (with bias + temb), per-image absmax
-    and GroupNorm tile partials; and within the f16x3 tolerance of float64.  Odd and even chunk
-    counts (Ci / 16 = 3, 8, 5, 16), non-square images, several N tiles."""
-    from weatherconverter_amd import kernels as K
-    g = torch.Generator().manual_seed(77)
-    h = torch.randn((B, Ci, H, W), generator=g) * 2 + 0.3
-    gamma = 1 + 0.3 * torch.randn(Ci, generator=g)
-    beta = 0.5 * torch.randn(Ci, generator=g)
-    sc, sh = _gn_affine(h, gamma, beta)
-    w = torch.randn((Co, Ci, 3, 3), generator=g) / (Ci * 9)**0.5
-    b = torch.randn(Co, generator=g) * 0.1
-    temb = torch.randn((B, Co + 32), generator=g)
-    a = h.double() * sc[:, :, None, None] + sh[:, :, None, None]
-    if silu:
-        a = F.silu(a)
-    ref = F.conv2d(a, w.double(), b.double(), padding=1) + temb[:, :Co].double()[:, :, None, None]
-    segs = [K.Seg(K.View.full(_nhwc(h).cuda()), TAPS3, scale=sc.float().cuda(), shift=sh.float().cuda(), silu=silu)]
-    w3 = K.pack_f16x3(_pack(w).contiguous().cuda(), Ci, 0)
-    e = K.f16x3_a_exp(float(gamma.abs().max()), float(beta.abs().max()), H * W * Ci // 8)
-    res = {}
-    prev = K.set_conv3_onewave(1)
-    try:
-        for mode in (1, 0):
-            K.set_conv3_onewave(mode)
-            out = torch.full((B, H, W, Co), 7.0, device='cuda')
-            gp = K.GnPart.attach(out, sw)
-            am = torch.zeros(B, device='cuda')
-            K.conv3x3_f16x3(segs, w3, b.cuda(), K.View.full(out), Hm=H, Wm=W, a_exp=e, temb=temb.cuda(),
-                            temb_ld=Co + 32, absmax=am, gn=gp)
-            torch.cuda.synchronize()
-            res[mode] = (out.cpu(), am.cpu(), gp.part.cpu(), K._native.last_kernel_name())
-    finally:
-        K.set_conv3_onewave(prev)
-    assert res[1][3].startswith('conv3x3_w1_kernel') and res[0][3].startswith('conv3x3_x6_kernel'), (res[1][3], res[0][3])
-    for u, v in zip(res[1][:3], res[0][:3]):
-        assert torch.equal(u, v), (u - v).abs().max()
-    assert rel_l2(_nchw(res[1][0]).double(), ref) < 1e-5
-    assert torch.equal(res[1][1], res[1][0].reshape(B, -1).abs().amax(1))
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize('B,N,C,heads,gs', [(2, 300, 128, 4, 1.0), (1, 1024, 256, 4, 1.0), (2, 257, 512, 4, 3.0),
                                             (1, 200, 768, 4, 1.0), (1, 96, 384, 4, 1.0), (1, 64, 640, 4, 0.5)])
 def test_attention_f16x3_vs_float64(B, N, C, heads, gs):
@@ -1087,8 +1042,8 @@ def test_qkv_presplit_attention_bit_identical(B, H, C, heads):
 @pytest.mark.parametrize('B,H,W,C,heads', [(2, 16, 16, 128, 4), (1, 32, 32, 512, 4), (2, 16, 32, 768, 4),
                                            (1, 64, 64, 256, 4), (3, 16, 24, 256, 2)])
 def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
-    """The pre-split projection GEMM on 256 x 128 tiles and on 128 x 128 tiles with B in registers
-    (proj_pa_kernel<QKV, 2, false> / <QKV, 1, true>) against the 128 x 128 LDS-DMA form: the out-projection form (in-place residual, bias, per-image absmax, GroupNorm tile
+    """The pre-split projection GEMM on 256 x 128 tiles (proj_pa_kernel<QKV, 2, false>) against the
+    128 x 128 LDS-DMA form: the out-projection form (in-place residual, bias, per-image absmax, GroupNorm tile
     partials) and the pre-split qkv form give bit-identical results; 16 x 24 images (HW % 256 != 0)
     fall back to 128 rows.  And the out-projection within the f16x3 tolerance of float64."""
     from weatherconverter_amd import kernels as K
@@ -1108,7 +1063,7 @@ def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
     res = {}
     prev = K.set_proj_tile(256)
     try:
-        for rows in (256, -128, -129, 128):  # 256 x 128; 128 x 128 with B / A and B in registers; LDS-DMA
+        for rows in (256, 128):  # 256 x 128; the 128 x 128 LDS-DMA form
             K.set_proj_tile(rows)
             y = y0.cuda()
             yv = K.View.full(y)
@@ -1124,12 +1079,35 @@ def test_proj_pa256_bit_identical_to_128_rows(B, H, W, C, heads):
         K.set_proj_tile(prev)
     big = HW % 256 == 0
     assert res[256][4].startswith('proj_pa_kernel<false, 2' if big else 'conv_igemm_x6_kernel'), res[256][4]
-    assert res[-128][4].startswith('proj_pa_kernel<false, 1, true, false>'), res[-128][4]
-    assert res[-129][4].startswith('proj_pa_kernel<false, 1, true, true>'), res[-129][4]
     assert res[128][4].startswith('conv_igemm_x6_kernel'), res[128][4]
-    for form in (256, -128, -129):
-        for u, v in zip(res[form][:4], res[128][:4]):
-            assert torch.equal(u, v), form
+    for u, v in zip(res[256][:4], res[128][:4]):
+        assert torch.equal(u, v)
     ref = o.double() @ w.double().t() + b.double() + y0.double()
     assert rel_l2(res[256][0].double(), ref) < 2e-6
     assert torch.equal(res[256][1], res[256][0].reshape(B, -1).abs().amax(1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,C,ld,gn', [(2, 16, 16, 64, 64, True), (1, 32, 32, 512, 512, False),
+                                         (2, 8, 32, 96, 160, True), (3, 16, 8, 32, 32, False)])
+def test_split_tiled_layout_vs_torch(B, H, W, C, ld, gn):
+    """wc_split_f16x3_tiled: every value lands at its [mt][k-step][piece][k-half][row][8] slot of the GEMM's
+    LDS stage order, the two fp16 pieces sum to (x sc + sh) 2^e within the split's 2^-22 relative, the
+    high piece is the round-to-nearest fp16 of the value; strided channel views (ld > C)."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(3)
+    t = torch.randn((B, H, W, ld), generator=g) * 3
+    sc = (1 + 0.2 * torch.randn((B, C), generator=g)) if gn else None
+    sh = (0.3 * torch.randn((B, C), generator=g)) if gn else None
+    e = 5
+    v = K.View(t.cuda(), 0, C)
+    a3 = K.split_f16x3_tiled(v, e, sc.cuda() if gn else None, sh.cuda() if gn else None)
+    torch.cuda.synchronize()
+    M = B * H * W
+    raw = a3.cpu().view(torch.float16).reshape(M // 128, C // 16, 2, 2, 128, 8)  # [mt][ks][piece][kh][row][8]
+    pieces = raw.permute(2, 0, 4, 1, 3, 5).reshape(2, M, C).double()  # [piece][row][channel]
+    x = t[..., :C].reshape(M, C).double()
+    if gn:
+        x = (x.reshape(B, H * W, C) * sc.double()[:, None] + sh.double()[:, None]).reshape(M, C)
+    ref = x * 2.0**e
+    assert torch.allclose(pieces[0] + pieces[1], ref, rtol=2e-6, atol=1e-6)

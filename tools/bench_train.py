@@ -159,7 +159,7 @@ def train_step(args):
         torch.cuda.synchronize()
         kernels.profile_conv(False)
         per = {}
-        for name, flops, e0, e1 in rec:
+        for name, flops, e0, e1, *_ in rec:
             key = name.split('<')[0].split(' ')[0]
             d = per.setdefault(key, [0, 0.0, 0.0])
             d[0] += 1
@@ -200,7 +200,7 @@ def roofline_leg(kernels, step, precision: str, ms_iter: float):
     torch.cuda.synchronize()
     kernels.profile_conv(False)
     per = {}
-    for name, flops, e0, e1 in rec:
+    for name, flops, e0, e1, *_ in rec:
         d = per.setdefault(name, [0, 0.0, 0.0])
         d[0] += 1
         d[1] += flops

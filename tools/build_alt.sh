@@ -3,7 +3,7 @@
 # working tree with REV=WORK) compiled with the extra flags in $EXTRA, every other object from this
 # tree's build, linked into weatherconverter_amd/lib/${ALT:-alt}/libwc_kernels.so.
 # Run it with WC_KERNEL_LIB=<that path> WC_ALLOW_STALE_LIB=1 (tools/ab_lib.sh, tools/wino_ab.py): the
-# variant's compiled-in source digest is the tree's, but it is deliberately not the tree's build.
+# variant carries its own "alt:" digest, so the loader refuses it without that override.
 # Usage: [ALT=name] [EXTRA="-DX=1"] bash tools/build_alt.sh REV wc_conv6 [wc_igemm6 ...]
 set -e
 REV=$1; shift
@@ -24,6 +24,11 @@ for f in "$@"; do
   rm "$ROOT/weatherconverter_amd/csrc/_alt_$f.hip"
   objs="$objs $OUT/$f.o"
 done
-keep=$(ls "$OBJ"/*.o | grep -v -E "/($(echo "$@" | tr ' ' '|')|wc_srchash_bf16|wc_srchash_single16)\.o$")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libwc_kernels.so" $keep $objs
+# the variant's own digest ("alt:" + a hash of REV, EXTRA and the files): the loader refuses it unless
+# WC_ALLOW_STALE_LIB=1, so an A/B or ablation build can never pass for the tree's library
+ALTHASH="alt:$(echo "$REV $EXTRA $*" | sha256sum | cut -c1-16)"
+printf 'extern "C" const char* wc_source_hash(void) { return "%s"; }\n' "$ALTHASH" > "$OUT/wc_srchash_alt.cpp"
+/opt/rocm/bin/hipcc -x c++ -O2 -fPIC -c "$OUT/wc_srchash_alt.cpp" -o "$OUT/wc_srchash_alt.o"
+keep=$(ls "$OBJ"/*.o | grep -v -E "/($(echo "$@" | tr ' ' '|')|wc_srchash_bf16|wc_srchash_single16|wc_srchash_default)\.o$")
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libwc_kernels.so" $keep $objs "$OUT/wc_srchash_alt.o"
 echo "built $OUT/libwc_kernels.so ($REV $EXTRA: $*)"

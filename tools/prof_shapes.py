@@ -29,7 +29,7 @@ def main():
         torch.cuda.synchronize()
         kernels.profile_conv(False)
     agg = defaultdict(lambda: [0, 0.0])
-    for name, work, e0, e1 in prof:
+    for name, work, e0, e1, *_ in prof:
         a = agg[(name, work)]
         a[0] += 1
         a[1] += e0.elapsed_time(e1)

@@ -17,7 +17,7 @@ MAX_TAPS = 16
 NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 
 EXPORTS = [
-    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_conv3x3_wino_set_onewave', 'wc_conv3x3_wino_set_form', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv3x3_set_onewave', 'wc_conv_igemm_x6',
+    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
     'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
@@ -26,7 +26,7 @@ EXPORTS = [
     'wc_mse_workspace_doubles', 'wc_mse_loss', 'wc_dwconv', 'wc_version', 'wc_source_hash',
     'wc_conv_wgrad', 'wc_conv_wgrad_x6', 'wc_conv_wgrad_f16x3', 'wc_conv_wgrad_splits', 'wc_wgrad_reduce', 'wc_gn_bwd_splits', 'wc_gn_bwd_reduce',
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_bsum_batch', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
-    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name',
+    'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name', 'wc_stamp', 'wc_wall_clock_khz',
     'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse',
     'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_dkdv192', 'wc_attention_bwd_prep', 'wc_pack_split'
 ]
@@ -74,7 +74,6 @@ _SIGS = {
     'wc_conv_igemm': [ctypes.POINTER(ConvArgs), _P],
     'wc_conv3x3_x6': [ctypes.POINTER(ConvArgs), _P, _L, _P],
     'wc_conv3x3_x6_tile_n': [_I],
-    'wc_conv3x3_set_onewave': [_I],
     'wc_proj_set_tile': [_I],
     'wc_conv3x3_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
     'wc_conv3x3_wino_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P],
@@ -82,8 +81,6 @@ _SIGS = {
     'wc_wino_vsplit_f16x3': [ctypes.POINTER(ConvArgs), _I, _P, _P, _L, _P],
     'wc_conv3x3_wino_f16x3_vp': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P, _L, _P],
     'wc_conv3x3_wino_tile_n': [_I],
-    'wc_conv3x3_wino_set_onewave': [_I],
-    'wc_conv3x3_wino_set_form': [_I],
     'wc_pack_wino': [_P, _I, _I, _I, _P, _L, _P, _P],
     'wc_pack_wino_raw': [_P, _P, _I, _I, _I, _I, _P, _L, _P, _P],
     'wc_pack_wino_batch': [_P, _I, _I, _I, _P],
@@ -98,6 +95,8 @@ _SIGS = {
     'wc_proj_f16x3_qkv': [ctypes.POINTER(ConvArgs), _P, _L, _P, _L, _I, _P, _P, _I, _I, _P, _P],
     'wc_attention_fwd_f16x3_presplit': [_P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _I, _P],
     'wc_gn_num_splits': [_I, _I, _I],
+    'wc_stamp': [_P, _I, _P],
+    'wc_wall_clock_khz': [_P],
     'wc_gn_stats': [_P, _I, _I, _I, _I, _I, _P, _P],
     'wc_gn_finalize': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P],
     'wc_gn_finalize_bound': [_P, _I, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P],
@@ -224,11 +223,16 @@ def verify_source_hash(lib, variant: str = ''):
     """Refuse a library built from other sources than this tree's: its compiled-in digest
     (wc_source_hash) must equal _build.source_hash() of the tree's csrc/, header and flags.
     WC_ALLOW_STALE_LIB=1 lets a developer run a deliberately different build (an A/B variant)."""
+    stale_ok = os.environ.get('WC_ALLOW_STALE_LIB', '0') == '1'
+    if not hasattr(lib, 'wc_source_hash'):
+        if stale_ok:  # an older A/B build from before the digest existed
+            return None
+        raise RuntimeError('weatherconverter_amd: kernel library has no wc_source_hash (built from other sources)')
     lib.wc_source_hash.argtypes = []
     lib.wc_source_hash.restype = ctypes.c_char_p
     got = lib.wc_source_hash().decode()
     want = _build.source_hash(_VARIANT_FLAG.get(variant, ''))
-    if got != want and os.environ.get('WC_ALLOW_STALE_LIB', '0') != '1':
+    if got != want and not stale_ok:
         raise RuntimeError(f'weatherconverter_amd: kernel library {variant or "default"} was built from other sources '
                            f'(library digest {got}, tree digest {want}); rebuild with '
                            f'python -c "import __graft_entry__ as g; g.build()" (or set WC_ALLOW_STALE_LIB=1 for a '
@@ -236,7 +240,7 @@ def verify_source_hash(lib, variant: str = ''):
     return got
 
 
-# Process-wide kernel-form selectors (wc_conv3x3_set_onewave, wc_proj_set_tile): each library variant
+# Process-wide kernel-form selectors (wc_proj_set_tile): each library variant
 # keeps its own static state, so a setting is applied to every loaded variant and replayed into any
 # variant opened later (the single16 training line included).
 _selectors = {}

@@ -614,14 +614,10 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
             }
             const float scale_log2 = scale * 1.4426950408889634f;
             if (!fp32_dkdv) {
-                static const int ds = [] {
-                    const char* e = getenv("WC_DKDV192_DS");
-                    return e && e[0] == '1' ? 1 : 2;
-                }();
-                st = ds == 1 ? launch_dkdv192<1>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
-                                                 scale, eq, ek, ev, dobound, amx, s)
-                             : launch_dkdv192<2>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
-                                                 scale, eq, ek, ev, dobound, amx, s);
+                // output dims in two workgroups (DS = 2: no scratch; one workgroup spilled 216 B/lane and
+                // was no faster, removed)
+                st = launch_dkdv192<2>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale,
+                                       eq, ek, ev, dobound, amx, s);
                 if (st != WC_OK) return st;
             }
             WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(192), WC_TB(true), WC_TI(3)});

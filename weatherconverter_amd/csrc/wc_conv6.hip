@@ -831,315 +831,10 @@ __global__ __launch_bounds__(NT, (TH == 8 && (!RES || (F3 && R16))) ? 3 : 2) voi
     }
 }
 
-// ---- One wave per SIMD: the GN(+SiLU) -> 3x3 conv (no residual segment) software-pipelined ----
-// The halo kernel above runs three waves per SIMD and relies on the other waves to hide each
-// wave's LDS and L2 latency; a bare f16 32x32x16 MFMA stream sustains ~1.8 PF at one wave per SIMD
-// against 1.2-1.3 PF at three (profiles/r03_mfma_peak*).  This form owns a 16 x 16
-// pixel tile x 128 channels per workgroup, 128 pixels x 64 channels per wave (4 x 2 accumulators,
-// 24 MFMAs per tap) with the latencies hidden inside the wave:
-//   * A fragments of tap t + 1 are read from LDS while tap t's MFMAs run (two fragment sets);
-//   * weights come from L2 straight into registers two taps ahead (three sets, set = tap % 3);
-//   * the next chunk's halo is loaded at tap 3 (after that tap's weight loads: vmcnt drains in issue
-//     order, so nothing waits on it before tap 6), GN+SiLU-transformed and split into the other halo
-//     buffer at tap 6 (VALU under tap 6's MFMAs), one barrier per chunk at tap 8, after which tap 8
-//     reads the next chunk's tap-0 fragments.
-// Same operands, pieces, products and accumulation order per output as conv3x3_x6_kernel<8, 128,
-// PRO, false, true, false, false, 0, WR>: the results are bit-identical (tests/test_gpu_kernels.py).
-template <int PRO>
-__global__ __launch_bounds__(NT, 1) void conv3x3_w1_kernel(X6Dev p) {
-    constexpr int TH = 16, BN = 128;
-    constexpr int HPIX = (TH + 2) * HWD;            // 324 halo pixels
-    // one (piece, k-half) plane, sized for the 384 item slots of 6 items per thread: the unused
-    // items write into the plane's tail (never read), so the halo writer has no branch and the
-    // scheduler can interleave it with the MFMAs of its tap
-    constexpr int HPLANE = 384 * 16;
-    constexpr int HSTAGE = 2 * 2 * HPLANE;          // [piece][k-half][pixel][8 x fp16]
-    constexpr int H_ITEMS = HPIX * 4;               // float4 items of one halo chunk
-    constexpr int H_PER_T = (H_ITEMS + NT - 1) / NT;
-    constexpr int BPLANE = BN * 16;
-    constexpr int BSTEP = 2 * 2 * BPLANE;           // weight bytes of one tap (host layout as the halo kernel)
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-
-    const int nblk = gridDim.x;
-    int bid = blockIdx.x;
-    {
-        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    }
-    const int tile_n = bid % p.ntiles_n;
-    int tt = bid / p.ntiles_n;
-    const int txi = tt % p.tiles_x;
-    tt /= p.tiles_x;
-    const int tyi = tt % p.tiles_y;
-    const int b = tt / p.tiles_y;
-    const int y0 = tyi * TH, x0 = txi * 16, n0 = tile_n * BN;
-    int s_exp = p.a_exp;
-    if (p.abound) {
-        const float bnd = p.abound[b];
-        const int e = (int)((__float_as_uint(bnd) >> 23) & 0xffu) - 127;
-        if (bnd > 0.f) s_exp = min(s_exp, 13 - e);
-        s_exp = max(s_exp, -100);
-    }
-    const float ascale = ldexpf(1.0f, s_exp), ainv = ldexpf(1.0f, -s_exp);
-    const int nck = p.nck0;
-    const int S = 9 * nck;
-    const unsigned wtile = (unsigned)tile_n * (unsigned)(S * BSTEP);
-
-    // halo item i = tid + NT j: pixel i >> 2, channels 4 (i & 3) ..; LDS byte hlds0 + 1024 j
-    const int q = tid & 3;
-    const int hlds0 = (q >> 1) * HPLANE + (tid >> 2) * 16 + (q & 1) * 8;
-    int hoff0[H_PER_T];
-    static_assert(H_PER_T * NT <= 4 * 384, "item slots fit the plane");
-    unsigned hin = 0;
-#pragma unroll
-    for (int j = 0; j < H_PER_T; ++j) {
-        const int i = tid + NT * j;
-        const int P = i >> 2;
-        const int hy = P / HWD;
-        const int hx = P - hy * HWD;
-        const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-        const bool valid = i < H_ITEMS;
-        const bool inb = valid && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-        hin |= (inb ? 1u : 0u) << j;
-        hoff0[j] = inb ? (((b * p.H + iy) * p.W + ix) * p.ldc0 + 4 * q) * 4 : (int)OOB;
-    }
-    const __amdgpu_buffer_rsrc_t srd0 = make_srd(p.src0);
-    const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w6);
-    const __amdgpu_buffer_rsrc_t srdsc = make_srd(p.scale);
-    const __amdgpu_buffer_rsrc_t srdsh = make_srd(p.shift);
-
-    f32x4 rh[H_PER_T];
-    f32x4 rsc = {1.f, 1.f, 1.f, 1.f}, rsh = {0.f, 0.f, 0.f, 0.f};
-    auto load_halo = [&](int c) {
-#pragma unroll
-        for (int j = 0; j < H_PER_T; ++j) rh[j] = bload_f4s(srd0, (unsigned)hoff0[j], c * 64);
-        const unsigned o = (unsigned)(b * p.C0 + c * 16 + 4 * q) * 4u;
-        rsc = bload_f4(srdsc, o);
-        rsh = bload_f4(srdsh, o);
-    };
-    auto write_halo = [&](int hs, int j0, int j1) {  // items j0 .. j1 - 1
-        unsigned char* base = smem + hs * HSTAGE;
-#pragma unroll
-        for (int j = j0; j < j1; ++j) {
-            f32x4 v = rh[j] * rsc + rsh;
-            if constexpr (PRO == 2) {
-                v.x = silu_fast(v.x); v.y = silu_fast(v.y);
-                v.z = silu_fast(v.z); v.w = silu_fast(v.w);
-            }
-            if (!((hin >> j) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};  // padding after the prologue
-            v = v * ascale;
-            u32x2 a0, a1;
-            split2_f16(v, a0, a1);
-            *reinterpret_cast<u32x2*>(base + hlds0 + 1024 * j) = a0;
-            *reinterpret_cast<u32x2*>(base + 2 * HPLANE + hlds0 + 1024 * j) = a1;
-        }
-    };
-
-    const int l32 = lane & 31;
-    const int half = lane >> 5;
-    int abase[4];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-        abase[mb] = half * HPLANE + ((8 * wm + 2 * mb + row_dy(l32)) * HWD + row_dx(l32)) * 16;
-    const unsigned wlane = (unsigned)(half * BPLANE + (wn * 64 + l32) * 16);
-
-    u32x4 wreg[3][2][2];  // [set][nb][piece]
-    u32x4 fa[2][4][2];    // [set][mb][piece]
-    f32x16 acc[2][2][2];  // [64-pixel half][mb within the half][nb]
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[h][i][j][r] = 0.f;
-
-    // every load issued unconditionally (a step past the end re-reads the last one, unused)
-    auto load_w = [&](int set, int st) {
-        const int off = (int)(wtile + (unsigned)((st < S ? st : S - 1) * BSTEP));
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int pc = 0; pc < 2; ++pc)
-                wreg[set][nb][pc] = bload_u4s(srdw, wlane + (unsigned)(nb * 32 * 16 + pc * 2 * BPLANE), off);
-    };
-    auto read_a = [&](int fs, int hs, int mt) {
-        const unsigned char* ha = smem + hs * HSTAGE + ((mt / 3) * HWD + mt % 3) * 16;
-#pragma unroll
-        for (int pc = 0; pc < 2; ++pc)
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-                fa[fs][mb][pc] = *reinterpret_cast<const u32x4*>(ha + abase[mb] + pc * 2 * HPLANE);
-    };
-    // the 12 MFMAs of one 64-pixel half h (per accumulator: h*h, then h*l, then l*h)
-    auto mfma_half = [&](int fs, int set, int h) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) acc[h][i][nb] = mfma_f16(fa[fs][2 * h + i][0], wreg[set][nb][0], acc[h][i][nb]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                f32x16& a = acc[h][i][nb];
-                a = mfma_f16c(fa[fs][2 * h + i][0], wreg[set][nb][1], a);
-                a = mfma_f16c(fa[fs][2 * h + i][1], wreg[set][nb][0], a);
-            }
-    };
-
-    // prologue: chunk 0's halo into buffer 0, weights of taps 0 and 1, tap 0's fragments
-    load_halo(0);
-    load_w(0, 0);
-    load_w(1, 1);
-    write_halo(0, 0, H_PER_T);
-    __syncthreads();
-    read_a(0, 0, 0);
-
-    // chunk c in halo buffer PV starts with fragment set PV (9 taps: the parity flips per chunk)
-    auto chunk = [&](auto P0, int c) {
-        constexpr int PV = decltype(P0)::value;
-        // sched_barriers pin the order: loads, then the next tap's fragment reads, then this tap's
-        // MFMAs (left alone, the scheduler sinks the fragment reads to just before their use)
-#pragma unroll
-        for (int mt = 0; mt < 9; ++mt) {
-            load_w((mt + 2) % 3, 9 * c + mt + 2);
-            if (mt == 3) load_halo(c + 1 < nck ? c + 1 : c);  // the last chunk re-reads its own (unused)
-            if (mt < 8) read_a((PV + mt + 1) & 1, PV, mt + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            // VALU under the MFMAs of taps 6 and 7, half of the items each
-            if (mt == 6) write_halo(PV ^ 1, 0, H_PER_T / 2);
-            if (mt == 7) write_halo(PV ^ 1, H_PER_T / 2, H_PER_T);
-            mfma_half((PV + mt) & 1, mt % 3, 0);
-            if (mt == 8) {
-                __builtin_amdgcn_sched_barrier(0);
-                __syncthreads();
-                read_a(PV ^ 1, PV ^ 1, 0);  // the next chunk's tap 0 (garbage after the last chunk, unused)
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            mfma_half((PV + mt) & 1, mt % 3, 1);
-            if (mt == 6 || mt == 7) {  // the halo writer's VALU and LDS writes spread between the MFMAs
-#pragma unroll
-                for (int k = 0; k < 24; ++k) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // VALU
-                    __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    const std::integral_constant<int, 0> I0;
-    const std::integral_constant<int, 1> I1;
-    int c = 0;
-    for (; c + 1 < nck; c += 2) {
-        chunk(I0, c);
-        chunk(I1, c + 1);
-    }
-    if (c < nck) chunk(I0, c);
-
-    // ---- epilogue: x 2^-(sA + sW[n]) + bias + temb, NHWC store, GN partials ----
-    const long img_px = (long)b * p.H * p.W;
-    const __amdgpu_buffer_rsrc_t srd_out = make_srd(p.out + img_px * p.ldo);
-    float vmax = 0.f;
-    float eadd[2], emul[2];
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-        const int n = n0 + wn * 64 + nb * 32 + l32;
-        eadd[nb] = p.bias ? p.bias[n] : 0.f;
-        if (p.temb) eadd[nb] += p.temb[b * p.temb_ld + n];
-        emul[nb] = p.wsinv[n] * ainv;
-    }
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-        const int pix0 = (y0 + 8 * wm + 2 * mb) * p.W + x0;
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            const int n = n0 + wn * 64 + nb * 32 + l32;
-            const unsigned vout = (unsigned)(pix0 * p.ldo + n) * 4u;
-            f32x16& a = acc[mb >> 1][mb & 1][nb];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int dpx = (row_dy(row) ? p.W : 0) + row_dx(row);
-                const float v = a[r] * emul[nb] + eadd[nb];
-                bstore_f1s(srd_out, vout, dpx * p.ldo * 4, v);
-                vmax = fmaxf(vmax, fabsf(v));
-                a[r] = v;
-            }
-        }
-    }
-    if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);
-    if (p.gn_part) {
-        // the wave's rows 8 wm + 4 h .. + 3 are 64-pixel block ((y / 8) tiles_x8 + txi) * 2 + (y % 8) / 4
-        // of the TH = 8 numbering (tiles_x is W / 16 in both forms)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            GnTile g{p.gn_part, p.gn_ncb, p.gn_sw,
-                     (long)b * p.gn_np64 + (long)((2 * tyi + wm) * p.tiles_x + txi) * 2 + h,
-                     (p.gn_c0 + n0 + wn * 64) / 32};
-            gn_tile_partials(acc[h], g, 2);
-        }
-    }
-}
-
-// 0 (default): off; -1: the one-wave form where its tiles fill the chip; 1: wherever it applies.
-// Initial value from WC_CONV3_W1 (A/B runs), settable through wc_conv3x3_set_onewave (tests).
-// Measured off by default: bit-identical results, but no faster in steady state (64^2, 512 -> 512:
-// 425 vs 427 TF/s) and slower where a workgroup runs only a few chunks (256^2, 64 -> 128: 280 vs
-// 296-356 TF/s): one workgroup per CU has nothing to overlap its prologue and epilogue with, and
-// the MFMA stream of either form stops at the same ~1.28 PF of f16 work (tools/w1_probe.py).
-int g_w1_mode = [] {
-    const char* e = getenv("WC_CONV3_W1");
-    return e ? atoi(e) : 0;
-}();
-int conv3_w1_mode() { return g_w1_mode; }
-
-// The one-wave form applies to the GN(+SiLU) 3x3 conv without residual, N a multiple of 128, H and W
-// multiples of 16; in mode -1 only where its 16 x 16 tiles fill the chip at least four times over
-// (one workgroup per CU: a partial last round costs a whole tile time).
-template <int PRO>
-int launch_w1(const X6Dev& d, hipStream_t stream) {
-    constexpr int HSTAGE = 2 * 2 * 384 * 16;  // conv3x3_w1_kernel's halo buffer
-    X6Dev p = d;
-    p.tiles_x = p.W / 16;
-    p.tiles_y = p.H / 16;
-    p.ntiles_n = p.N / 128;
-    dim3 grid(p.B * p.tiles_y * p.tiles_x * p.ntiles_n);
-    WC_SET_NAME("conv3x3_w1_kernel", {WC_TI(PRO)});
-    hipLaunchKernelGGL((conv3x3_w1_kernel<PRO>), grid, dim3(NT), 2 * HSTAGE, stream, p);
-    WC_CHECK_LAUNCH();
-    return WC_OK;
-}
-bool w1_applies(const X6Dev& d, int pro, bool res) {
-    const int mode = conv3_w1_mode();
-    if (mode == 0 || res || pro == 0 || d.act != WC_ACT_NONE || d.N % 128 || d.H % 16 || d.W % 16) return false;
-    if (d.gn_part && d.gn_np64 * 64 != d.H * d.W) return false;
-    const long wgs = (long)d.B * (d.H / 16) * (d.W / 16) * (d.N / 128);
-    return mode == 1 || wgs >= 1024;
-}
-
-// A/B knob (WC_CONV3_WGS_PER_CU=n, 1..2): pad each workgroup's dynamic LDS so that at most n
-// workgroups (n waves per SIMD) share a CU; 0 = the kernel's own occupancy.
-int conv3_lds_for(int lds) {
-    static const int n = [] {
-        const char* e = getenv("WC_CONV3_WGS_PER_CU");
-        return e ? atoi(e) : 0;
-    }();
-    if (n < 1 || n > 2) return lds;
-    const int need = (160 * 1024) / (n + 1) + 1024;  // more than 1 / (n + 1) of the CU's 160 KiB
-    return lds > need ? lds : need;
-}
-
 template <int TH, int BN, int PRO, bool RES, bool F3, bool R16 = false, bool GL = false, int MAP = 0, int WR = 0>
 int launch6(const X6Dev& d, hipStream_t stream) {
     using T = X6Tile<TH, BN, RES, F3, R16, GL, MAP, WR>;
-    static const int lds = conv3_lds_for(T::LDS);
+    static const int lds = T::LDS;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_x6_kernel<TH, BN, PRO, RES, F3, R16, GL, MAP, WR>),
@@ -1159,104 +854,26 @@ int launch6(const X6Dev& d, hipStream_t stream) {
     return WC_OK;
 }
 
-// f16x3 weight staging: registers at one tap per K-step (default) or LDS-DMA at three taps
-// (WC_CONV3_GL=1, kept for A/B measurement: 292 vs 318 TF/s aggregate, tools/gpu_ab_conv.sh)
-bool conv3_glds() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_GL");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return v != 0;
-}
-
-// f16x3 weight fragments straight from L2 into registers, one barrier per 16-channel chunk instead of
-// one per tap (WC_CONV3_WR=0: the LDS-staged form, kept for A/B measurement)
-bool conv3_wr() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_WR");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v != 0;
-}
-
-// the fp16-residual forms on weights in registers too (WC_CONV3_WR_RES=0: LDS-staged, for A/B)
-bool conv3_wr_res() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_WR_RES");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v != 0;
-}
-
-// WC_CONV3_LA2=1 (A/B only): the plain (no residual) GN+SiLU form with the last tap's weights two
-// taps ahead and the next chunk's halo issued before them.  Alone each launch gains (359 -> 368 TF/s
-// at 256^2, 316 -> 332 at 64^2 / 512 channels) but the whole step does not (same box 27.06 / 27.09
-// vs 27.09 / 27.22 ms: the power-capped clock takes the saved cycles back).  =1r: the residual form
-// too, which needs 2 waves/SIMD or spills at 3, and loses (334 -> 297 TF/s).
-bool conv3_la2() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_LA2");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return v != 0;
-}
-bool conv3_wr16() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_WR16");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v != 0;
-}
-// residual 1x1 chunks interleaved with the 3x3 chunks when the two segments have as many chunks
-// (WC_CONV3_FUSE=0: the separate residual phase, one barrier per 1x1 step; for A/B)
-bool conv3_fuse() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_FUSE");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v != 0;
-}
-bool conv3_la2_res() {
-    static const int v = [] {
-        const char* e = getenv("WC_CONV3_LA2");
-        return (e && e[0] == '1' && e[1] == 'r') ? 1 : 0;
-    }();
-    return v != 0;
-}
-
 template <int TH, int BN>
 int dispatch6(const X6Dev& d, int pro, bool res, bool f3, hipStream_t s) {
-    if (f3 && conv3_glds()) {
-        const bool r16 = res && d.abound != nullptr;
-        switch ((pro - 1) * 3 + (res ? (r16 ? 2 : 1) : 0)) {
-            case 0: return launch6<TH, BN, 1, false, true, false, true>(d, s);
-            case 1: return launch6<TH, BN, 1, true, true, false, true>(d, s);
-            case 2: return launch6<TH, BN, 1, true, true, true, true>(d, s);
-            case 3: return launch6<TH, BN, 2, false, true, false, true>(d, s);
-            case 4: return launch6<TH, BN, 2, true, true, false, true>(d, s);
-            default: return launch6<TH, BN, 2, true, true, true, true>(d, s);
-        }
-    }
-    // weights in registers: the TH = 8 forms without the residual segment only (same-box A/B: conv1
-    // 338 -> 356 TF/s; the TH = 16 / BN = 64 form drops to 2 waves/SIMD and loses, 312 -> 292; with
-    // the residual the register sets exceed the 3-wave budget and spill)
-    if constexpr (TH == 16) {  // the 64-channel forms on weights in registers too (WC_CONV3_WR16=0: LDS-staged,
-                               // for A/B; same box 27.10 -> 27.00 ms/step)
-        if (f3 && conv3_wr16() && pro == 2 && (!res || d.abound != nullptr))
+    // f16x3 weight fragments straight from L2 into registers one K-step ahead, one barrier per 16-channel
+    // chunk (same-box A/Bs against LDS-staged weights: conv1 338 -> 356 TF/s; 64-channel forms 27.10 ->
+    // 27.00 ms/step); the residual 1x1 chunks interleaved with the 3x3 chunks when the two segments have
+    // as many chunks (WR 3).  Measured and removed: LDS-DMA weight staging (292 vs 318
+    // TF/s), the last tap's weights two taps ahead (the step did not gain), the one-wave-per-SIMD
+    // software-pipelined form (no faster: 425 vs 427 TF/s at 64^2, slower at 256^2).
+    if constexpr (TH == 16) {
+        if (f3 && pro == 2 && (!res || d.abound != nullptr))
             return res ? launch6<TH, BN, 2, true, true, true, false, 0, 1>(d, s)
                        : launch6<TH, BN, 2, false, true, false, false, 0, 1>(d, s);
     }
     if constexpr (TH == 8) {
-        if (f3 && w1_applies(d, pro, res)) return pro == 1 ? launch_w1<1>(d, s) : launch_w1<2>(d, s);
-        if (f3 && conv3_la2() && pro == 2 && (!res || (conv3_la2_res() && d.abound != nullptr)))
-            return res ? launch6<TH, BN, 2, true, true, true, false, 0, 2>(d, s)
-                       : launch6<TH, BN, 2, false, true, false, false, 0, 2>(d, s);
-        if (f3 && conv3_wr() && !res) {
+        if (f3 && !res) {
             return pro == 1 ? launch6<TH, BN, 1, false, true, false, false, 0, true>(d, s)
                             : launch6<TH, BN, 2, false, true, false, false, 0, true>(d, s);
         }
-        if (f3 && conv3_wr_res() && res && d.abound != nullptr && pro == 2) {
-            if (d.nck1 == d.nck0 && conv3_fuse()) return launch6<TH, BN, 2, true, true, true, false, 0, 3>(d, s);
+        if (f3 && res && d.abound != nullptr && pro == 2) {
+            if (d.nck1 == d.nck0) return launch6<TH, BN, 2, true, true, true, false, 0, 3>(d, s);
             return launch6<TH, BN, 2, true, true, true, false, 0, true>(d, s);
         }
     }
@@ -1340,13 +957,6 @@ int prepare(const wc_conv_args* a, const void* w, X6Dev& d, int& BN, int& TH) {
 }  // namespace
 
 extern "C" int wc_conv3x3_x6_tile_n(int N) { return N <= 64 ? 64 : 128; }
-
-extern "C" int wc_conv3x3_set_onewave(int mode) {
-    if (mode < -1 || mode > 1) return WC_E_ARG;
-    const int prev = g_w1_mode;
-    g_w1_mode = mode;
-    return prev;
-}
 
 extern "C" int wc_conv3x3_x6(const wc_conv_args* a, const void* w6, int64_t w6_bytes, void* stream) {
     X6Dev d;
@@ -1435,8 +1045,7 @@ extern "C" int wc_conv4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64_t
     }
     const long ntn = (a->N + BN - 1) / BN;
     if (w3_bytes != ntn * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
-    if (conv3_wr()) return launch6<8, 128, 0, false, true, false, false, 1, true>(d, reinterpret_cast<hipStream_t>(stream));
-    return launch6<8, 128, 0, false, true, false, false, 1>(d, reinterpret_cast<hipStream_t>(stream));
+    return launch6<8, 128, 0, false, true, false, false, 1, true>(d, reinterpret_cast<hipStream_t>(stream));
 }
 
 // ConvTranspose2d(C, N, 4, stride 2, padding 1) (the UNet up-sampling conv) in one launch: output
@@ -1481,6 +1090,5 @@ extern "C" int wc_convtr4x4s2_f16x3(const wc_conv_args* a, const void* w3, int64
     if (w3_bytes != ntn * 4L * 4L * d.nck0 * BN * 64 || w3_bytes >= (1L << 31)) return WC_E_SHAPE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (BN == 64) return launch6<16, 64, 0, false, true, false, false, 2>(d, st);
-    if (conv3_wr()) return launch6<8, 128, 0, false, true, false, false, 2, true>(d, st);
-    return launch6<8, 128, 0, false, true, false, false, 2>(d, st);
+    return launch6<8, 128, 0, false, true, false, false, 2, true>(d, st);
 }

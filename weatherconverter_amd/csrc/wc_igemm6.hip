@@ -967,45 +967,46 @@ namespace {
 
 // a3[mt][ks][piece][k-half][row 128][8 x fp16] from the fp32 rows of an NHWC view: optional GroupNorm
 // affine (+ SiLU), x 2^a_exp, two-piece round-to-nearest fp16 split (wcx6::split2_f16).  A wave owns
-// 64 rows x 32 channels: 128-byte row reads, 1 KiB contiguous stores per (step, piece, k-half).
+// 64 rows x 32 channels in 8 rounds of 8 rows: lane = (row 8, channel quad 8), so each load instruction
+// reads 8 whole 128-byte row segments (a lane per row read 64 separate lines per instruction: 0.56 of
+// HBM); each lane splits its quad and stores the two 8-byte halves of its fragments, so for a fixed
+// (16-channel step, k-half, piece) the 8 rows' 16-byte fragments land as one contiguous 128 bytes.
 __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restrict__ src, int ldc, int HW, int K,
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift, int silu, float ascale,
                                                           unsigned char* __restrict__ a3) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int row = blockIdx.x * 64 + lane;
     const int g32 = blockIdx.y * 4 + wave;
     if (g32 * 32 >= K) return;
-    const int b = row / HW;
-    const f32x4* s4 = reinterpret_cast<const f32x4*>(src + (long)row * ldc + g32 * 32);
+    const int row0 = blockIdx.x * 64;
+    const int b = row0 / HW;  // HW % 128 == 0: the 64 rows are one image's
+    const int q = lane & 7, rl = lane >> 3;
+    const int c = g32 * 32 + 4 * q;
     f32x4 v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = s4[i];
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(src + (long)(row0 + 8 * i + rl) * ldc + c);
     if (scale) {
-        const f32x4* sc4 = reinterpret_cast<const f32x4*>(scale + (long)b * K + g32 * 32);
-        const f32x4* sh4 = reinterpret_cast<const f32x4*>(shift + (long)b * K + g32 * 32);
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + (long)b * K + c);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + (long)b * K + c);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            v[i] = v[i] * sc4[i] + sh4[i];
+            v[i] = v[i] * sc + sh;
             if (silu) {
                 v[i].x = silu_fast(v[i].x); v[i].y = silu_fast(v[i].y);
                 v[i].z = silu_fast(v[i].z); v[i].w = silu_fast(v[i].w);
             }
         }
     }
-    const int mt = row >> 7, r = row & 127, KS = K / 16;
+    // quad q: channels 4q .. 4q + 3 of the 32 = step 2 g32 + q / 4, k-half (q / 2) % 2, 8-byte half q % 2
+    const int mt = row0 >> 7, KS = K / 16;
+    const long step = (long)mt * KS + 2 * g32 + (q >> 2);
+    unsigned char* base = a3 + ((step * 2 * 2 + ((q >> 1) & 1)) * 128 + (row0 & 127) + rl) * 16 + (q & 1) * 8;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const long step = (long)mt * KS + 2 * g32 + h;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-            u32x2 h0, l0, h1, l1;
-            split2_f16(v[4 * h + 2 * kh] * ascale, h0, l0);
-            split2_f16(v[4 * h + 2 * kh + 1] * ascale, h1, l1);
-            unsigned char* d = a3 + ((step * 2 * 2 + kh) * 128 + r) * 16;
-            *reinterpret_cast<u32x4*>(d) = u32x4{h0.x, h0.y, h1.x, h1.y};
-            *reinterpret_cast<u32x4*>(d + 2 * 128 * 16) = u32x4{l0.x, l0.y, l1.x, l1.y};
-        }
+    for (int i = 0; i < 8; ++i) {
+        u32x2 ph, pl;
+        split2_f16(v[i] * ascale, ph, pl);
+        *reinterpret_cast<u32x2*>(base + i * 8 * 16) = ph;
+        *reinterpret_cast<u32x2*>(base + i * 8 * 16 + 2 * 128 * 16) = pl;
     }
 }
 
@@ -1338,17 +1339,8 @@ __global__ __launch_bounds__(NT, H == 2 || DA ? 2 : 3) void proj_pa_kernel(IgDev
 // 2: the 256 x 128 form wherever the pixels per image are a multiple of 256; 1 (default): the
 // 256 x 128 form for the pre-split qkv epilogue at >= 2048 of its tiles, the one place it measured
 // faster (64^2, C 512 -> 1536: 341 vs 373 us; the out-projections and the smaller qkv grids ran
-// 4-16 % slower at two workgroups per CU, tools/proj_probe.py).  g_pawr -- 1: the 128 x 128 tiles
-// with B in registers (proj_pa_wr_kernel) instead of conv_igemm_x6_kernel's LDS-DMA form.
-// WC_PROJ_BM256 / WC_PROJ_WR for A/B runs, wc_proj_set_tile for tests.
-int g_pa256 = [] {
-    const char* e = getenv("WC_PROJ_BM256");
-    return e ? atoi(e) : 1;
-}();
-int g_pawr = [] {
-    const char* e = getenv("WC_PROJ_WR");
-    return e ? atoi(e) : 0;
-}();
+// 4-16 % slower at two workgroups per CU, tools/proj_probe.py).  wc_proj_set_tile for tests.
+int g_pa256 = 1;
 
 template <bool QKV, int H, bool WR, bool DA = false>
 void launch_pa_form(const IgDev& d, hipStream_t stream) {
@@ -1365,15 +1357,6 @@ int launch_pa(const IgDev& d, hipStream_t stream) {
     if (fits && (g_pa256 == 2 || (g_pa256 == 1 && d.qkv3 && tiles256 >= 2048))) {
         if (d.qkv3) launch_pa_form<true, 2, false>(d, stream);
         else launch_pa_form<false, 2, false>(d, stream);
-        WC_CHECK_LAUNCH();
-        return WC_OK;
-    }
-    if (g_pawr && d.N % 128 == 0 && !d.abound) {
-        if (g_pawr == 2) {
-            if (d.qkv3) launch_pa_form<true, 1, true, true>(d, stream);
-            else launch_pa_form<false, 1, true, true>(d, stream);
-        } else if (d.qkv3) launch_pa_form<true, 1, true>(d, stream);
-        else launch_pa_form<false, 1, true>(d, stream);
         WC_CHECK_LAUNCH();
         return WC_OK;
     }
@@ -1461,11 +1444,9 @@ extern "C" int wc_proj_f16x3_qkv(const wc_conv_args* a, const void* a3, int64_t 
 }
 
 extern "C" int wc_proj_set_tile(int rows) {
-    // 0 the default choice, 128 / 256 the LDS-DMA forms, -128 the 128-row form with B in registers
-    // -129: 128 x 128 tiles with A and B in registers (no LDS)
-    if (rows != 0 && rows != 128 && rows != 256 && rows != -128 && rows != -129) return WC_E_ARG;
-    const int prev = g_pawr == 2 ? -129 : g_pawr ? -128 : g_pa256 == 0 ? 128 : g_pa256 == 2 ? 256 : 0;
-    g_pa256 = rows == 128 || rows < 0 ? 0 : rows == 256 ? 2 : 1;
-    g_pawr = rows == -128 ? 1 : rows == -129 ? 2 : 0;
+    // 0 the default choice, 128 / 256 the LDS-DMA forms
+    if (rows != 0 && rows != 128 && rows != 256) return WC_E_ARG;
+    const int prev = g_pa256 == 0 ? 128 : g_pa256 == 2 ? 256 : 0;
+    g_pa256 = rows == 128 ? 0 : rows == 256 ? 2 : 1;
     return prev;
 }

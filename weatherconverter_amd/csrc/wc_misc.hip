@@ -680,6 +680,29 @@ extern "C" const char* wc_version(void) {
     return v;
 }
 
+// In-graph launch timing: one wave reads the GPU's constant-rate wall clock (wall_clock64, the
+// 100 MHz real-time counter) and lane 0 stores it to slots[index] with an ordinary vector store.  Stamp
+// launches captured around the named launches of a graph give their durations as the graph runs them.
+__global__ __launch_bounds__(64) void stamp_kernel(unsigned long long* __restrict__ slots, int index) {
+    const unsigned long long t = wall_clock64();
+    if (threadIdx.x == 0) slots[index] = t;
+}
+
+extern "C" int wc_stamp(unsigned long long* slots, int index, void* stream) {
+    if (!slots || index < 0) return WC_E_ARG;
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), slots, index);
+    WC_CHECK_LAUNCH();
+    return WC_OK;
+}
+
+extern "C" int wc_wall_clock_khz(int* khz) {
+    if (!khz) return WC_E_ARG;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev);
+    return e == hipSuccess ? WC_OK : (int)e;
+}
+
 // The instantiation name of the kernel this host thread launched last through a named launcher
 // (rocprofv3's demangled form), then cleared: "" when the last entry point did not name its kernel.
 extern "C" const char* wc_last_kernel_name(void) {

@@ -675,7 +675,7 @@ void conv3x3_wino_kernel(WDev p) {
 
 template <int TH, int BN, int PRO, bool RES, int MB = 2, int NW = 4>
 int launch_wino(const WDev& d, hipStream_t stream) {
-    using T = WTile<TH, BN, MB, NW>;
+    using T = WTile<TH, BN, MB, NW, PRO == 3>;  // the layout the kernel itself uses (PRO 3: unpadded planes)
     constexpr int lds = 2 * T::HSTAGE + (RES ? 2 * T::CSTAGE : 0);
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an explicit opt-in
     if (!attr_set) {
@@ -695,37 +695,9 @@ int launch_wino(const WDev& d, hipStream_t stream) {
     return WC_OK;
 }
 
-// 0: the two-waves-per-SIMD form (MB = 2); 1: the one-wave form (MB = 4, 16-row tiles) for BN = 128
-// where H % 16 == 0.  Initial value from WC_WINO_ONEWAVE (A/B runs); wc_conv3x3_wino_set_onewave.
-int g_wino_onewave = [] {
-    const char* e = getenv("WC_WINO_ONEWAVE");
-    return e ? atoi(e) : 0;
-}();
-// 0: 4-wave workgroups; 1: 8-wave workgroups of 256 channels x 8 rows where N % 256 == 0 (GN+SiLU
-// segment), else as 0; 2: as 1, else 8-wave 128 x 16 rows where H % 16 == 0.  Initial value from
-// WC_WINO_FORM (A/B runs).
-int g_wino_form = [] {
-    const char* e = getenv("WC_WINO_FORM");
-    return e ? atoi(e) : 0;
-}();
-
 }  // namespace
 
 extern "C" int wc_conv3x3_wino_tile_n(int N) { return N <= 64 ? 64 : 128; }
-
-extern "C" int wc_conv3x3_wino_set_form(int mode) {
-    if (mode < 0 || mode > 2) return WC_E_ARG;
-    const int prev = g_wino_form;
-    g_wino_form = mode;
-    return prev;
-}
-
-extern "C" int wc_conv3x3_wino_set_onewave(int mode) {
-    if (mode < 0 || mode > 1) return WC_E_ARG;
-    const int prev = g_wino_onewave;
-    g_wino_onewave = mode;
-    return prev;
-}
 
 namespace {
 
@@ -792,24 +764,28 @@ int wino_setup(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
 long wino_vimg(int C, int H, int W) { return (long)(C / 16) * 16 * H * (W / 2) * 16; }
 
 // ---- wino_vsplit_kernel: segment 0 of a GN+SiLU Winograd conv, transformed and split once ----
-// Workgroup = R = 256 / W image rows of one image and one 16-channel chunk.  Stage 1: the rows' pixels
-// -1 .. W (4 lanes per pixel, 16 B each: 16 pixels per load instruction) through GN affine + SiLU + 2^s
-// with zero padding, once per element, into LDS as fp32.  Stage 2: thread = (row, tile t, channel octet
-// h): the tile's four pixels 2t - 1 .. 2t + 2 from LDS, the input transform V0..V3 and the two-piece
-// fp16 split, stored as 16-byte fragments at [b][chunk][plane = piece 8 + position 2 + h][y][t] -- for
-// fixed (plane, row) consecutive lanes write consecutive tiles.  The same operations in the same order as
-// the conv kernel's items (prologue / transform, PRO 2): the planes are bit for bit the LDS image those
-// items write.  s per image as the conv: a_exp - 1, clamped to 13 - e(res_bound[b]) under a residual.
+// Workgroup = R = 256 / W image rows of one image and NCK 16-channel chunks (NCK = 2 where C % 32 == 0:
+// a pixel's 32 channels are one whole 128-byte line, read by one workgroup -- with one chunk per
+// workgroup the two halves of every line went to workgroups on different XCDs and were fetched twice).
+// Stage 1: the rows' pixels -1 .. W (4 NCK lanes per pixel, 16 B each) through GN affine + SiLU + 2^s
+// with zero padding, once per element, into LDS as fp32 [chunk][row][pixel][quad].  Stage 2: thread =
+// (row, tile t, channel octet h), for each chunk: the tile's four pixels 2t - 1 .. 2t + 2 from LDS, the
+// input transform V0..V3 and the two-piece fp16 split, stored as 16-byte fragments at
+// [b][chunk][plane = piece 8 + position 2 + h][y][t] -- for fixed (plane, row) consecutive lanes write
+// consecutive tiles.  The same operations in the same order as the conv kernel's items (prologue /
+// transform, PRO 2): the planes are bit for bit the LDS image those items write.  s per image as the
+// conv: a_exp - 1, clamped to 13 - e(res_bound[b]) under a residual.
+template <int NCK>
 __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restrict__ src, int ldc, int B, int H,
                                                           int W, int C, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, int a_exp1,
                                                           const float* __restrict__ res_bound,
                                                           unsigned char* __restrict__ vout, long vimg) {
-    extern __shared__ __attribute__((aligned(16))) f32x4 act[];  // [R][W + 2][4 quads + 1 pad]
-    const int R = 256 / W, nck = C / 16, nyb = (H + R - 1) / R;
-    const int k = blockIdx.x % nck;
-    const int yb = (blockIdx.x / nck) % nyb;
-    const int b = blockIdx.x / (nck * nyb);
+    extern __shared__ __attribute__((aligned(16))) f32x4 act[];  // [NCK][R][W + 2][4 quads + 1 pad]
+    const int R = 256 / W, ngrp = C / (16 * NCK), nyb = (H + R - 1) / R;
+    const int kg = blockIdx.x % ngrp;
+    const int yb = (blockIdx.x / ngrp) % nyb;
+    const int b = blockIdx.x / (ngrp * nyb);
     const int y0 = yb * R;
     const int tid = threadIdx.x;
     int s_exp = a_exp1;
@@ -820,47 +796,63 @@ __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restric
         s_exp = max(s_exp, -100);
     }
     const float ascale = ldexpf(1.0f, s_exp);
-    // stage 1
-    const int W2 = W + 2, items = R * W2 * 4;
-    for (int i = tid; i < items; i += 256) {
-        const int q = i & 3, px = (i >> 2) % W2 - 1, r = (i >> 2) / W2;
-        const int y = y0 + r;
-        const bool inb = (unsigned)px < (unsigned)W && y < H;
-        const int c = k * 16 + 4 * q;
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
-        const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
-        const f32x4 v = inb ? *reinterpret_cast<const f32x4*>(src + ((long)(b * H + y) * W + px) * ldc + c)
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 a = v * sc + sh;
-        a.x = silu_fast(a.x); a.y = silu_fast(a.y);
-        a.z = silu_fast(a.z); a.w = silu_fast(a.w);
-        // a pixel is 5 slots (4 quads + pad): stage 2's lanes, two pixels apart, then read distinct banks
-        act[(r * W2 + px + 1) * 5 + q] = inb ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
+    // stage 1: item = (row, padded pixel, quad of the NCK x 16 channels); 4 items per thread in flight
+    const int W2 = W + 2, items = R * W2 * 4 * NCK, cstride = R * W2 * 5;
+    for (int i0 = tid; i0 < items; i0 += 4 * 256) {
+        f32x4 v[4], sc[4], sh[4];
+        bool inb[4];
+        int slot[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = min(i0 + u * 256, items - 1);
+            const int q = i % (4 * NCK), px = (i / (4 * NCK)) % W2 - 1, r = (i / (4 * NCK)) / W2;
+            const int y = y0 + r;
+            inb[u] = (unsigned)px < (unsigned)W && y < H;
+            const int c = kg * 16 * NCK + 4 * q;
+            sc[u] = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
+            sh[u] = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
+            v[u] = *reinterpret_cast<const f32x4*>(src + ((long)(b * H + min(y, H - 1)) * W + min(max(px, 0), W - 1)) * ldc + c);
+            // a pixel is 5 slots (4 quads + pad): stage 2's lanes, two pixels apart, then read distinct banks
+            slot[u] = (q >> 2) * cstride + (r * W2 + px + 1) * 5 + (q & 3);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i0 + u * 256 >= items) break;
+            f32x4 a = v[u] * sc[u] + sh[u];
+            a.x = silu_fast(a.x); a.y = silu_fast(a.y);
+            a.z = silu_fast(a.z); a.w = silu_fast(a.w);
+            act[slot[u]] = inb[u] ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
     }
     __syncthreads();
     // stage 2
     const int T2 = W / 2;
     const int t = tid % T2, h = (tid / T2) & 1, r = tid / W;
     const int y = y0 + r;
-    if (y >= H) return;
-    unsigned char* vb = vout + (long)b * vimg + (long)k * 16 * H * T2 * 16;
+    // R * W <= 256 threads own a (row, tile, octet): when W does not divide 256 the trailing threads
+    // (r == R) would read past stage 1's rows and write the next workgroup's first row
+    if (r >= R || y >= H) return;
     const long plane = (long)H * T2 * 16;
     const long frag = ((long)y * T2 + t) * 16;
-    u32x2 pc[2][4][2];  // [quad of the octet][position][piece]
 #pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-        const f32x4* ar = act + (r * W2 + 2 * t) * 5 + 2 * h + qq;  // pixel 2t - 1 is padded index 2t
-        const f32x4 d0 = ar[0], d1 = ar[5], d2 = ar[10], d3 = ar[15];
-        const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
+    for (int ck = 0; ck < NCK; ++ck) {
+        unsigned char* vb = vout + (long)b * vimg + (long)(kg * NCK + ck) * 16 * H * T2 * 16;
+        u32x2 pc[2][4][2];  // [quad of the octet][position][piece]
 #pragma unroll
-        for (int pos = 0; pos < 4; ++pos) split2_f16(V[pos], pc[qq][pos][0], pc[qq][pos][1]);
+        for (int qq = 0; qq < 2; ++qq) {
+            const f32x4* ar = act + ck * cstride + (r * W2 + 2 * t) * 5 + 2 * h + qq;  // pixel 2t - 1 is padded index 2t
+            const f32x4 d0 = ar[0], d1 = ar[5], d2 = ar[10], d3 = ar[15];
+            const f32x4 V[4] = {d0 - d2, d1 + d2, d2 - d1, d1 - d3};
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) split2_f16(V[pos], pc[qq][pos][0], pc[qq][pos][1]);
+        }
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos)
+#pragma unroll
+            for (int piece = 0; piece < 2; ++piece)
+                *reinterpret_cast<u32x4*>(vb + (piece * 8 + pos * 2 + h) * plane + frag) =
+                    u32x4{pc[0][pos][piece].x, pc[0][pos][piece].y, pc[1][pos][piece].x, pc[1][pos][piece].y};
     }
-#pragma unroll
-    for (int pos = 0; pos < 4; ++pos)
-#pragma unroll
-        for (int piece = 0; piece < 2; ++piece)
-            *reinterpret_cast<u32x4*>(vb + (piece * 8 + pos * 2 + h) * plane + frag) =
-                u32x4{pc[0][pos][piece].x, pc[0][pos][piece].y, pc[1][pos][piece].x, pc[1][pos][piece].y};
 }
 
 }  // namespace
@@ -873,14 +865,6 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     const int st = wino_setup(a, w, w_bytes, a_exp, w_inv_scale, a_bound, d, pro, res, BN);
     if (st != WC_OK) return st;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (BN == 128 && pro == 2 && g_wino_form >= 1 && d.N % 256 == 0)  // 8 waves: 256 channels x 8 rows
-        return res ? launch_wino<8, 256, 2, true, 2, 8>(d, s) : launch_wino<8, 256, 2, false, 2, 8>(d, s);
-    if (BN == 128 && pro == 2 && g_wino_form == 2 && d.H % 16 == 0)  // 8 waves: 128 channels x 16 rows
-        return res ? launch_wino<16, 128, 2, true, 2, 8>(d, s) : launch_wino<16, 128, 2, false, 2, 8>(d, s);
-    if (BN == 128 && g_wino_onewave == 1 && d.H % 16 == 0) {  // the one-wave form (16-row tiles)
-        if (pro == 0) return launch_wino<16, 128, 0, false, 4>(d, s);
-        return res ? launch_wino<16, 128, 2, true, 4>(d, s) : launch_wino<16, 128, 2, false, 4>(d, s);
-    }
     if (pro == 0) return BN == 64 ? launch_wino<16, 64, 0, false>(d, s) : launch_wino<8, 128, 0, false>(d, s);
     if (BN == 64) return res ? launch_wino<16, 64, 2, true>(d, s) : launch_wino<16, 64, 2, false>(d, s);
     return res ? launch_wino<8, 128, 2, true>(d, s) : launch_wino<8, 128, 2, false>(d, s);
@@ -905,13 +889,23 @@ extern "C" int wc_wino_vsplit_f16x3(const wc_conv_args* a, int a_exp, const floa
         return WC_E_SHAPE;
     if (s0.W > 256) return WC_E_SHAPE;  // R = 256 / W rows per workgroup
     const int R = 256 / s0.W;
-    const long nblk = (long)a->B * ((s0.H + R - 1) / R) * (s0.C / 16);
-    const size_t lds = (size_t)R * (s0.W + 2) * 5 * sizeof(f32x4);
-    wc_last_kernel = "wino_vsplit_kernel";
-    hipLaunchKernelGGL(wino_vsplit_kernel, dim3((unsigned)nblk), dim3(256), lds,
-                       reinterpret_cast<hipStream_t>(stream), s0.src, s0.ldc, a->B, s0.H, s0.W, s0.C, s0.scale,
-                       s0.shift, a_exp - 1, a->nseg == 2 ? a_bound : nullptr,
-                       reinterpret_cast<unsigned char*>(vout), wino_vimg(s0.C, s0.H, s0.W));
+    const int nck = s0.C % 32 == 0 ? 2 : 1;
+    const long nblk = (long)a->B * ((s0.H + R - 1) / R) * (s0.C / (16 * nck));
+    const size_t lds = (size_t)nck * R * (s0.W + 2) * 5 * sizeof(f32x4);
+    if (lds > 64 * 1024) return WC_E_SHAPE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const float* rb = a->nseg == 2 ? a_bound : nullptr;
+    unsigned char* vo = reinterpret_cast<unsigned char*>(vout);
+    const long vimg = wino_vimg(s0.C, s0.H, s0.W);
+    if (nck == 2) {
+        WC_SET_NAME("wino_vsplit_kernel", {WC_TI(2)});
+        hipLaunchKernelGGL(wino_vsplit_kernel<2>, dim3((unsigned)nblk), dim3(256), lds, st, s0.src, s0.ldc, a->B, s0.H,
+                           s0.W, s0.C, s0.scale, s0.shift, a_exp - 1, rb, vo, vimg);
+    } else {
+        WC_SET_NAME("wino_vsplit_kernel", {WC_TI(1)});
+        hipLaunchKernelGGL(wino_vsplit_kernel<1>, dim3((unsigned)nblk), dim3(256), lds, st, s0.src, s0.ldc, a->B, s0.H,
+                           s0.W, s0.C, s0.scale, s0.shift, a_exp - 1, rb, vo, vimg);
+    }
     WC_CHECK_LAUNCH();
     return WC_OK;
 }
@@ -929,8 +923,6 @@ extern "C" int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* a, const void* w, in
     if (v_bytes != (int64_t)d.B * d.vimg || d.vimg >= (1L << 31)) return WC_E_SHAPE;
     d.vpre = reinterpret_cast<const unsigned char*>(vpre);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (BN == 128 && g_wino_onewave == 1 && d.H % 16 == 0)  // the one-wave form (16-row tiles)
-        return res ? launch_wino<16, 128, 3, true, 4>(d, s) : launch_wino<16, 128, 3, false, 4>(d, s);
     if (BN == 64) return res ? launch_wino<16, 64, 3, true>(d, s) : launch_wino<16, 64, 3, false>(d, s);
     return res ? launch_wino<8, 128, 3, true>(d, s) : launch_wino<8, 128, 3, false>(d, s);
 }

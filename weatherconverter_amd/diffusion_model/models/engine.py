@@ -10,21 +10,40 @@ Data layout in HBM
   stage below when it does not upsample) writes channels ``[0, C_i)``.  The up ResBlock then reads
   ``U[i]`` as one contiguous tensor, which is exactly ``torch.cat([x, out_down], dim=1)`` of
   ``unet_base.py:349``.
-* Weights are repacked once into GEMM form ``[N][K]`` with ``K = (tap, c_in)``; conv2 of every
-  ResBlock carries the 1x1 ``residual_input_conv`` as 32-aligned extra K columns (its bias folded
-  into conv2's), so a ResBlock is GN-stats, conv1, GN-stats, conv2 = 6 launches.
+* Weights are repacked once per ``load_state_dict``: the ResBlock 3x3 convs into the Winograd
+  F(2,3)-along-x operand layout (``U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)`` per kernel row, split
+  into two fp16 pieces under a per-channel power-of-two scale), conv2 carrying the 1x1
+  ``residual_input_conv`` as a 13th K-step per chunk (its bias folded into conv2's); the
+  projections, down convs and ConvT into the pre-split ``[N][K]`` fp16-piece layouts.
 
-Per ResBlock (``unet_base.py:146-150``)::
+Default (f16x3, fp32-class) launches per ResBlock (``unet_base.py:146-150``)::
 
-    sc1, sh1 = GN-stats(X)                           wc_gn_stats + wc_gn_finalize
-    h  = conv3x3(SiLU(X*sc1 + sh1)) + b1 + temb      wc_conv_igemm (prologue + epilogue fused)
-    sc2, sh2 = GN-stats(h)
-    Y  = conv3x3(SiLU(h*sc2 + sh2)) + conv1x1(X) + b2 + b_res     one wc_conv_igemm, 2 K-segments
+    sc1, sh1, |X| = GN-finalize(partials of X)             wc_gn_finalize_part (partials came from
+                                                            X's producer epilogue: no stats pass)
+    h  = conv3x3(SiLU(X*sc1 + sh1)) + b1 + temb            wc_conv3x3_wino_f16x3 (GN+SiLU prologue,
+                                                            transform, split per chunk in the conv;
+                                                            epilogue writes h's GN partials)
+    sc2, sh2 = GN-finalize(partials of h)                  wc_gn_finalize_part
+    Y  = conv3x3(SiLU(h*sc2 + sh2)) + conv1x1(X) + b2      wc_conv3x3_wino_f16x3, residual in the
+                                                            transform domain under |X|
+
+For convs with >= 4 output-channel tiles of 128 the GN+SiLU + transform + split of segment 0 runs
+once per input (``wc_wino_vsplit_f16x3``) and the conv copies its halo planes by LDS-DMA
+(``wc_conv3x3_wino_f16x3_vp``); the 64-channel conv2 + residual stays on the direct halo kernel
+(``wc_conv3x3_f16x3``, measured faster there).
 
 Per attention layer (``unet_base.py:153-161``), in place on Y::
 
-    sc, sh = GN-stats(Y);  qkv = (Y*sc + sh) W_in^T + b_in      (GN-apply fused in the GEMM)
-    O = flash-attention(qkv);  Y = Y + O W_out^T + b_out        (residual fused in the epilogue)
+    sc, sh = GN-finalize(partials of Y)
+    a3 = split(GN(Y))                                     wc_split_f16x3_tiled (once per element)
+    Q, K, V = a3 W_in^T + b_in, written pre-split           wc_proj_f16x3_qkv (fp16 pieces, V in the
+                                                            PV MFMA's key order)
+    O = flash-attention(Q, K, V), written pre-split        wc_attention_fwd_f16x3_presplit_a3
+    Y = Y + O W_out^T + b_out                              wc_proj_f16x3 (residual in place, Y's GN
+                                                            partials from the epilogue)
+
+Modes ``bf16x6`` / ``fp32`` (``set_conv_precision``) run the same structure on the direct halo
+kernels (``wc_conv3x3_x6``) and implicit-GEMM convs (``wc_conv_igemm``).
 """
 import os
 from dataclasses import dataclass

@@ -29,11 +29,38 @@ REPLAY = None  # {'name': instantiation, 'reps': R, 'events': []}: see replay_ti
 
 
 def profile_conv(enable: bool):
-    """Record (name, algorithmic work, start event, end event) for every conv / attention / GN launch
-    until disabled."""
+    """Record (name, algorithmic work, start event, end event, algorithmic bytes, issued MFMA FLOPs or
+    None) for every conv / attention / GN launch until disabled."""
     global PROFILE
     PROFILE = [] if enable else None
     return PROFILE
+STAMPS = None  # {'slots': int64 device tensor, 'launches': [(name, flops, nbytes, mfma)]}: see stamp_timing
+
+
+def stamp_timing(slots: Optional[torch.Tensor]):
+    """While set (an int64 device tensor), every named launch is bracketed by two wc_stamp launches that
+    write the GPU wall clock to slots[2 i], slots[2 i + 1] (launch i in STAMPS['launches'] order).
+    Captured into a HIP graph, the stamps time each launch as the replayed graph runs it.  None ends
+    it; returns the state dict."""
+    global STAMPS
+    if slots is None:
+        STAMPS = None
+    else:
+        _req(slots.is_cuda and slots.dtype == torch.int64 and slots.is_contiguous(), 'stamp slots: int64 device tensor')
+        STAMPS = {'slots': slots, 'launches': []}
+    return STAMPS
+
+
+def _measuring() -> bool:
+    """A timing mode that records the launches' algorithmic work is active."""
+    return PROFILE is not None or REPLAY is not None or STAMPS is not None
+
+
+def wall_clock_hz() -> float:
+    """Rate of the clock wc_stamp reads (hipDeviceAttributeWallClockRate)."""
+    khz = ctypes.c_int()
+    _native.call('wc_wall_clock_khz', ctypes.byref(khz))
+    return khz.value * 1e3
 
 
 def replay_timing(name: Optional[str], reps: int = 5):
@@ -230,6 +257,16 @@ def _timed(name: str, fn_name: str, flops: float, *args, nbytes: float = 0.0, mf
     states it; mfma = the dense 16-bit MFMA FLOPs the launch issues where they are not the
     algorithmic FLOPs times its arithmetic mode's pieces (the Winograd conv: 2/3 of the direct form's
     products on its 3x3 segment), else None."""
+    if STAMPS is not None:
+        i = len(STAMPS['launches'])
+        _req(2 * i + 1 < STAMPS['slots'].numel(), 'stamp slots exhausted')
+        sp = STAMPS['slots'].data_ptr()
+        _native.call('wc_stamp', sp, 2 * i, _stream())
+        _native.call(fn_name, *args)
+        exact = _native.last_kernel_name() or name
+        _native.call('wc_stamp', sp, 2 * i + 1, _stream())
+        STAMPS['launches'].append((exact, flops, nbytes, mfma))
+        return
     if PROFILE is None and REPLAY is None:
         _native.call(fn_name, *args)
         return
@@ -239,7 +276,7 @@ def _timed(name: str, fn_name: str, flops: float, *args, nbytes: float = 0.0, mf
     e1.record()
     exact = _native.last_kernel_name() or name
     if PROFILE is not None:
-        PROFILE.append((exact, flops, e0, e1))
+        PROFILE.append((exact, flops, e0, e1, nbytes, mfma))
     if REPLAY is not None and REPLAY['name'] in ('*', exact):
         reps = REPLAY['reps'] if _idempotent(fn_name, args) else 0
         if reps:
@@ -284,7 +321,7 @@ def conv_igemm(segs: Sequence[Seg], w: torch.Tensor, bias: Optional[torch.Tensor
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
     _timed(f'conv_igemm_kernel<{bm}, {bn}, {pro}, {unib}, {act}>', 'wc_conv_igemm',
-           _flops(segs, Hm, Wm, N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), _stream())
+           _flops(segs, Hm, Wm, N) if _measuring() else 0.0, ctypes.byref(a), _stream())
 
 
 # ---- bf16x6 split-precision 3x3 conv (csrc/wc_conv6.hip) ----
@@ -478,18 +515,6 @@ def f16x3_a_exp(gamma_absmax: float, beta_absmax: float, n_group: int) -> int:
     return max(-60, min(60, math.floor(math.log2(2.0**14 / bound))))
 
 
-def set_wino_form(mode: int) -> int:
-    """wc_conv3x3_wino_set_form: 0 the 4-wave Winograd workgroups, 1 8-wave 256-channel ones where
-    N % 256 == 0, 2 also 8-wave 128-channel x 16-row ones; returns the previous mode."""
-    return _native.set_selector('wc_conv3x3_wino_set_form', int(mode), lambda v: v >= 0)
-
-
-def set_conv3_onewave(mode: int) -> int:
-    """wc_conv3x3_set_onewave: 0 off (default), 1 forced, -1 where it fills the chip; returns the previous mode."""
-    prev = _native.set_selector('wc_conv3x3_set_onewave', int(mode), lambda v: v >= -1)
-    return prev
-
-
 def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                   a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
                   temb_ld: int = 0, res: Optional[View] = None, act: int = 0,
@@ -512,7 +537,7 @@ def conv3x3_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Tensor
     res_seg = 'true' if len(segs) == 2 else 'false'
     r16 = 'true' if a_bound is not None and len(segs) == 2 else 'false'
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, true, {r16}>', 'wc_conv3x3_f16x3',
-           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
+           _flops(segs, Hm, Wm, w3.N) if _measuring() else 0.0, ctypes.byref(a),
            w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream(),
            nbytes=_abytes(segs, w3.N, Hm * Wm, res))
 
@@ -522,12 +547,6 @@ def wino_tile(N: int) -> Tuple[int, int]:
     """(TH, BN) of wc_conv3x3_wino_f16x3 for N output channels."""
     bn = _native.load().wc_conv3x3_wino_tile_n(N)
     return (16 if bn == 64 else 8), bn
-
-
-def set_wino_onewave(mode: int) -> int:
-    """wc_conv3x3_wino_set_onewave: 0 the two-wave form (default), 1 the one-wave 16-row form; returns the
-    previous mode (applied to every library variant)."""
-    return _native.set_selector('wc_conv3x3_wino_set_onewave', int(mode), lambda v: v in (0, 1))
 
 
 def wino_enabled() -> bool:
@@ -686,7 +705,7 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
     a = _conv_args(segs, w.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     TH, BN = wino_tile(w.N)
-    prof = PROFILE is not None or REPLAY is not None
+    prof = _measuring()
     ab = _ptr(a_bound) if (len(segs) == 2 or raw) else None
     if not raw and wino_vsplit_wanted(segs, w.N, Hm, Wm):
         # segment 0 GN+SiLU'd, transformed and split once (not once per output-channel tile), then the
@@ -725,9 +744,13 @@ def set_wino_vsplit(min_tiles: int) -> int:
 
 
 def wino_vsplit_wanted(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
+    """Whether the conv takes the pre-split form: the tile threshold, and every constraint
+    wc_wino_vsplit_f16x3 checks (otherwise the in-conv prologue form runs, which accepts more shapes)."""
     s0 = segs[0]
+    v = s0.view
     return (_WINO_VP_MIN_TILES > 0 and N > 64 and -(-N // 128) >= _WINO_VP_MIN_TILES and s0.silu
-            and s0.scale is not None and Wm % 16 == 0)
+            and s0.scale is not None and Wm % 16 == 0 and Wm <= 256 and v.W == Wm and v.H == Hm
+            and v.C % 16 == 0 and v.ldc % 4 == 0 and v.ptr % 16 == 0)
 
 
 def wino_mfma_flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int, pieces: int = 3) -> float:
@@ -763,7 +786,7 @@ def conv_igemm_f16x3(segs: Sequence[Seg], w3: X6Weight, bias: Optional[torch.Ten
         _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == s0.view.B, 'A bound')
         _req(unib == 'true', 'a per-image A bound needs (Hm*Wm) % BM == 0')
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, 0, true>', 'wc_conv_igemm_f16x3',
-           _flops(segs, Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           _flops(segs, Hm, Wm, w3.N) if _measuring() else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _ptr(a_bound), _stream())
 
 
@@ -818,7 +841,7 @@ def convT4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: 
     a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, res, (2, 2, 0, 0), None, 0, absmax, gn=gn)
     TH, BN = x6_tile(w3.N)
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, 0, false, true, false, false, 2> (ConvT 4x4/s2)', 'wc_convtr4x4s2_f16x3',
-           2.0 * v.B * v.H * v.W * w3.N * 16 * v.C if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a),
+           2.0 * v.B * v.H * v.W * w3.N * 16 * v.C if _measuring() else 0.0, ctypes.byref(a),
            w3.data.data_ptr(), w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream(),
            nbytes=_abytes([seg], w3.N, 4 * v.H * v.W))
 
@@ -841,7 +864,7 @@ def conv4x4s2_f16x3(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], out: V
     _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == seg.view.B, 'A bound')
     a = _conv_args([seg], w3.N, bias, out, Hm, Wm, None, 0, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     _timed('conv3x3_x6_kernel<8, 128, 0, false, true, false, false, true> (s2d 4x4/s2)', 'wc_conv4x4s2_f16x3',
-           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           _flops([seg], Hm, Wm, w3.N) if _measuring() else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, w3.wsinv.data_ptr(), _ptr(a_bound), _stream(), nbytes=_abytes([seg], w3.N, Hm * Wm))
 
 
@@ -863,7 +886,7 @@ def conv_igemm_f16x3_qkv(seg: Seg, w3: X6Weight, bias: Optional[torch.Tensor], q
     ex = (ctypes.c_int * 3)(*[int(e) for e in exps])  # host array, read during the call
     pro = 0 if seg.scale is None else (2 if seg.silu else 1)
     _timed(f'conv_igemm_x6_kernel<128, 128, {pro}, true, 0, true> (qkv pre-split)', 'wc_conv_igemm_f16x3_qkv',
-           _flops([seg], Hm, Wm, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w3.data.data_ptr(),
+           _flops([seg], Hm, Wm, w3.N) if _measuring() else 0.0, ctypes.byref(a), w3.data.data_ptr(),
            w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), qkv3.data_ptr(), C, heads,
            ctypes.cast(ex, ctypes.c_void_p), _stream())
 
@@ -889,17 +912,16 @@ def split_f16x3_tiled(v: View, a_exp: int, scale: Optional[torch.Tensor] = None,
         _req(scale.shape == (v.B, v.C) and shift.shape == (v.B, v.C) and scale.is_contiguous()
              and shift.is_contiguous() and scale.dtype == torch.float32, 'GN affine [B][C]')
     a3 = torch.empty(2 * v.B * v.H * v.W * v.C, dtype=torch.int16, device=v.t.device)
-    _timed('split_tiled_kernel', 'wc_split_f16x3_tiled', 8.0 * v.B * v.H * v.W * v.C if PROFILE is not None or REPLAY is not None else 0.0,
+    _timed('split_tiled_kernel', 'wc_split_f16x3_tiled', 8.0 * v.B * v.H * v.W * v.C if _measuring() else 0.0,
            v.ptr, v.ldc, v.B, v.H * v.W, v.C, _ptr(scale), _ptr(shift), int(silu), int(a_exp), a3.data_ptr(),
            a3.numel() * 2, _stream())
     return a3
 
 
 def set_proj_tile(rows: int) -> int:
-    """wc_proj_set_tile: form of the pre-split projection GEMMs (0 the measured default, 256 or 128 rows
-    with LDS-DMA B, -128 = 128 rows with B in registers, -129 = A and B in registers); returns the
-    previous setting."""
-    prev = _native.set_selector('wc_proj_set_tile', int(rows), lambda v: v in (0, 128, 256, -128, -129))
+    """wc_proj_set_tile: form of the pre-split projection GEMMs (0 the measured default, 256 or 128 rows);
+    returns the previous setting."""
+    prev = _native.set_selector('wc_proj_set_tile', int(rows), lambda v: v in (0, 128, 256))
     return prev
 
 
@@ -912,7 +934,7 @@ def proj_f16x3(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[torch.T
     seg = Seg(v, [(0, 0)])
     a = _conv_args([seg], w3.N, bias, out, v.H, v.W, None, 0, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
     _timed('conv_igemm_x6_kernel<128, 128, 0, true, 0, true> (pre-split A)', 'wc_proj_f16x3',
-           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
+           _flops([seg], v.H, v.W, w3.N) if _measuring() else 0.0, ctypes.byref(a), a3.data_ptr(),
            a3.numel() * 2, w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(), _stream())
 
 
@@ -927,7 +949,7 @@ def proj_f16x3_qkv(v: View, a3: torch.Tensor, w3: 'X6Weight', bias: Optional[tor
     a = _conv_args([seg], w3.N, bias, None, v.H, v.W, None, 0, None, (1, 1, 0, 0), None, 0, out_dummy=True)
     ex = (ctypes.c_int * 3)(*[int(e) for e in exps])  # host array, read during the call
     _timed('conv_igemm_x6_kernel<128, 128, 0, true, 0, true> (qkv pre-split, pre-split A)', 'wc_proj_f16x3_qkv',
-           _flops([seg], v.H, v.W, w3.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), a3.data_ptr(),
+           _flops([seg], v.H, v.W, w3.N) if _measuring() else 0.0, ctypes.byref(a), a3.data_ptr(),
            a3.numel() * 2, w3.data.data_ptr(), w3.data.numel() * 2, int(a_exp), w3.wsinv.data_ptr(),
            qkv3.data_ptr(), C, heads, ctypes.cast(ex, ctypes.c_void_p), _stream())
 
@@ -983,7 +1005,7 @@ def conv3x3_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor], 
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     res_seg = 'true' if len(segs) == 2 else 'false'
     _timed(f'conv3x3_x6_kernel<{TH}, {BN}, {pro}, {res_seg}, false, false>', 'wc_conv3x3_x6',
-           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
+           _flops(segs, Hm, Wm, w6.N) if _measuring() else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 
 
@@ -1001,7 +1023,7 @@ def conv_igemm_x6(segs: Sequence[Seg], w6: X6Weight, bias: Optional[torch.Tensor
     pro = 0 if s0.scale is None else (2 if s0.silu else 1)
     unib = 'true' if (Hm * Wm) % bm == 0 else 'false'
     _timed(f'conv_igemm_x6_kernel<{bm}, {bn}, {pro}, {unib}, {act}, false>', 'wc_conv_igemm_x6',
-           _flops(segs, Hm, Wm, w6.N) if PROFILE is not None or REPLAY is not None else 0.0, ctypes.byref(a), w6.data.data_ptr(),
+           _flops(segs, Hm, Wm, w6.N) if _measuring() else 0.0, ctypes.byref(a), w6.data.data_ptr(),
            w6.data.numel() * 2, _stream())
 
 
@@ -1152,7 +1174,7 @@ def head_conv(x: View, scale: torch.Tensor, shift: torch.Tensor, w_packed: torch
     B, NO = out.shape[0], out.shape[1]
     _req(out.is_contiguous() and out.shape == (x.B, NO, x.H, x.W) and bias.numel() >= NO, 'head output shape')
     _req(w_packed.shape == (x.C // 16, 9, 16, 4), 'head weight layout')
-    _timed('head_conv_kernel', 'wc_head_conv', 2.0 * x.B * x.H * x.W * NO * 9 * x.C if PROFILE is not None or REPLAY is not None else 0.0,
+    _timed('head_conv_kernel', 'wc_head_conv', 2.0 * x.B * x.H * x.W * NO * 9 * x.C if _measuring() else 0.0,
            x.ptr, x.ldc, scale.data_ptr(), shift.data_ptr(), x.B, x.H, x.W, x.C, w_packed.data_ptr(),
            bias.data_ptr(), NO, out.data_ptr(), _stream())
 

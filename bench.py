@@ -255,6 +255,8 @@ def roofline_leg(model, x, t_dev, groups: int = 1):
                            + (f'; algorithmic {rec["algorithmic_bytes"] / 1e9:.3f}' if 'algorithmic_bytes' in rec
                               else ''))
     rn = rei.get(name)
+    if not abytes and rn and rn[3]:  # the stamped launches carry no byte count: the re-issue table's, per launch
+        abytes = rn[3] / rn[0] * n
     # what a bare f16 MFMA stream sustains on this power-capped chip: the MAXIMUM over the committed
     # waves-per-SIMD sweep (tools/probes/mfma_peak.hip, median of each point's three launches; the
     # best point is one wave per SIMD issuing back to back), the split-precision kernels' work

@@ -665,6 +665,7 @@ extern "C" int wc_sgg_update(const float* grad, const float* mu, const float* si
     if (!grad || !mu || !sigma || !xt_out) return WC_E_ARG;
     if (nb < 1 || S < 1) return WC_E_SHAPE;
     long total = (long)S * S;
+    wc_last_kernel = "sgg_kernel";
     hipLaunchKernelGGL(sgg_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), grad, mu, sigma, xt_out, mag_out, nb,
                        S, lambda_, std0, std1, std2, sum_batch ? 1 : 0);

@@ -68,8 +68,11 @@ __global__ __launch_bounds__(DW_NT) void dwconv_kernel(const float* __restrict__
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = bv;
     // torch order: for each output, taps ky-major, kx-minor.  Iterating ky outermost keeps that order
-    // per output while each halo row is read once per (ky, kx) for all R rows.
-#pragma unroll
+    // per output while each halo row is read once per (ky, kx) for all R rows.  K = 9 keeps the ky loop
+    // rolled: fully unrolled, the 9 x 9 x R halo reads were hoisted into 512 registers and spilled (346
+    // VGPR spills, 4.96 ms for the 1024^2 64-channel head of the SRGAN)
+    constexpr int KY_UNROLL = K <= 3 ? K : 1;
+#pragma unroll KY_UNROLL
     for (int ky = 0; ky < K; ++ky) {
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) {
@@ -98,9 +101,11 @@ int launch_dw(const float* x, int ldx, float* out, int ldo, const float* w, cons
     const long ntiles = (long)B * tiles_x * tiles_y;
     if (ntiles >= (1L << 31)) return WC_E_SHAPE;
     if (C >= 16) {
+        wc_last_kernel = K == 3 ? "dwconv_kernel<3, 4>" : "dwconv_kernel<9, 4>";
         hipLaunchKernelGGL((dwconv_kernel<K, 4>), dim3((unsigned)ntiles, (C + 15) / 16), dim3(DW_NT), 0, s, x, ldx,
                            out, ldo, w, bias, H, W, C, tiles_x, tiles_y);
     } else {
+        wc_last_kernel = K == 3 ? "dwconv_kernel<3, 1>" : "dwconv_kernel<9, 1>";
         hipLaunchKernelGGL((dwconv_kernel<K, 1>), dim3((unsigned)ntiles, C / 4), dim3(DW_NT), 0, s, x, ldx, out, ldo,
                            w, bias, H, W, C, tiles_x, tiles_y);
     }

@@ -32,6 +32,8 @@ def profile_conv(enable: bool):
     """Record (name, algorithmic work, start event, end event, algorithmic bytes, issued MFMA FLOPs or
     None) for every conv / attention / GN launch until disabled."""
     global PROFILE
+    if enable:
+        _native.last_kernel_name()  # drop a name left by a launch outside the measurement
     PROFILE = [] if enable else None
     return PROFILE
 STAMPS = None  # {'slots': int64 device tensor, 'launches': [(name, flops, nbytes, mfma)]}: see stamp_timing
@@ -47,6 +49,7 @@ def stamp_timing(slots: Optional[torch.Tensor]):
         STAMPS = None
     else:
         _req(slots.is_cuda and slots.dtype == torch.int64 and slots.is_contiguous(), 'stamp slots: int64 device tensor')
+        _native.last_kernel_name()  # drop a name left by a launch outside the measurement
         STAMPS = {'slots': slots, 'launches': []}
     return STAMPS
 
@@ -69,6 +72,8 @@ def replay_timing(name: Optional[str], reps: int = 5):
     event gaps; operands alive, the results rewritten unchanged).  Returns the state dict; the
     mean launch duration is sum(elapsed) / (reps * len(events))."""
     global REPLAY
+    if name is not None:
+        _native.last_kernel_name()  # drop a name left by a launch outside the measurement
     REPLAY = {'name': name, 'reps': reps, 'events': []} if name is not None else None
     return REPLAY
 
@@ -298,7 +303,7 @@ def _flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int) -> float:
 def _abytes(segs: Sequence[Seg], N: int, out_pixels: int, res: Optional[View] = None) -> float:
     """Algorithmic HBM bytes of a conv launch: every input element of every segment, the output and
     the residual view once (fp32)."""
-    if REPLAY is None:
+    if not _measuring():
         return 0.0
     b = sum(4.0 * sg.view.B * sg.view.H * sg.view.W * sg.view.C for sg in segs)
     b += 4.0 * segs[0].view.B * out_pixels * N * (2 if res is not None else 1)
@@ -1248,8 +1253,11 @@ def sgg_update(grad: torch.Tensor, mu: torch.Tensor, sigma: torch.Tensor, lam: f
     grad, mu, sigma = grad.contiguous(), mu.contiguous(), sigma.contiguous()
     xt = torch.empty_like(mu)
     mag = torch.empty((3 if batch_axis_sum else nb, S, S), dtype=torch.float32, device=mu.device)
-    _native.call('wc_sgg_update', grad.data_ptr(), mu.data_ptr(), sigma.data_ptr(), xt.data_ptr(), mag.data_ptr(),
-                 nb, S, float(lam), float(std[0]), float(std[1]), float(std[2]), int(batch_axis_sum), _stream())
+    # algorithmic bytes: the (nb, 3, 4S, 4S) gradient, mu, sigma and xt (nb, 3, S, S), the magnitude (S, S) per plane
+    nbytes = 4.0 * nb * S * S * (48 + 9) + 4.0 * mag.numel()
+    _timed('sgg_kernel', 'wc_sgg_update', 0.0, grad.data_ptr(), mu.data_ptr(), sigma.data_ptr(), xt.data_ptr(),
+           mag.data_ptr(), nb, S, float(lam), float(std[0]), float(std[1]), float(std[2]), int(batch_axis_sum),
+           _stream(), nbytes=nbytes)
     return xt, mag
 
 
@@ -1259,8 +1267,9 @@ def dwconv(x: View, w: torch.Tensor, bias: Optional[torch.Tensor], out: View, K:
     out.check()
     _req(out.B == x.B and out.H == x.H and out.W == x.W and out.C == x.C, 'dwconv shapes')
     w = w.reshape(x.C, K * K).contiguous()
-    _native.call('wc_dwconv', x.ptr, x.ldc, out.ptr, out.ldc, w.data_ptr(), _ptr(bias), x.B, x.H, x.W, x.C, K,
-                 _stream())
+    px = x.B * x.H * x.W
+    _timed(f'dwconv_kernel<{K}>', 'wc_dwconv', 2.0 * px * x.C * K * K, x.ptr, x.ldc, out.ptr, out.ldc, w.data_ptr(),
+           _ptr(bias), x.B, x.H, x.W, x.C, K, _stream(), nbytes=8.0 * px * x.C)
 
 
 def avgpool2x2(x: View, out: View):

@@ -62,8 +62,9 @@ def parse(argv=None):
     ap.add_argument('--timesteps', type=int, default=1000)
     ap.add_argument('--seed', type=int, default=3455)
     ap.add_argument('--graph', type=int, default=1, help='replay the UNet forward from a HIP graph')
-    ap.add_argument('--split', type=int, default=int(os.environ.get('WC_GRAPH_SPLIT', '1')),
-                    help='image groups per GPU run concurrently on their own streams inside the graph')
+    ap.add_argument('--split', type=int, default=None,
+                    help='image groups per GPU run concurrently on their own streams inside the graph '
+                         '(default: _GraphStep\'s, 2 at >= 16 images per GPU; WC_GRAPH_SPLIT)')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=None, help='CPU baseline batch (default: --batch)')

@@ -79,13 +79,15 @@ class _GraphStep:
         self.x_in = x.clone()
         self.t_in = torch.zeros(1, dtype=torch.long, device=x.device)
         # split > 1: the batch runs as `split` independent image groups on their own streams inside
-        # the one graph (every UNet op is per image: bit-identical result); concurrent groups fill
-        # each other's launch tails.  Same-box A/B at 256 px B=16: 30.53 (1) / 29.83 (2) / 30.20 (4)
-        # ms/step, within box-to-box spread, and the concurrent launches no longer time one kernel
-        # in isolation (rocprof vs roofline), so the default stays 1.  WC_GRAPH_SPLIT overrides.
-        if split is None:
-            split = int(os.environ.get('WC_GRAPH_SPLIT', '1'))
+        # the one graph (every UNet op is per image: bit-identical result, tests/test_gpu_unet.py);
+        # concurrent groups fill each other's launch tails and hide the small launches (GroupNorm
+        # finalize, scheduler) under the other group's convs.  Same-box A/B at 256 px B=16, 60-step
+        # bench, two rounds (profiles/r06_graph_split_ab.txt): 23.74 / 23.73 (1), 23.34 / 23.39 (2),
+        # 24.09 / 24.14 (4) ms/step -- two groups by default where each keeps >= 8 images (rounds 1-5
+        # measured 1 vs 2 within box spread on slower kernels).  WC_GRAPH_SPLIT overrides.
         B = x.shape[0]
+        if split is None:
+            split = int(os.environ.get('WC_GRAPH_SPLIT', '2' if B >= 16 and B % 2 == 0 else '1'))
         self.split = split if split > 1 and B % split == 0 else 1
         self.streams = [torch.cuda.Stream(device=x.device) for _ in range(self.split - 1)]
         s = torch.cuda.Stream()

@@ -601,6 +601,26 @@ int wc_nchw_to_nhwc(const float* src, int B, int C, int H, int W, float* dst, in
 int wc_dwconv(const float* x, int ldx, float* out, int ldo, const float* w, const float* bias, int B,
               int H, int W, int C, int K, void* stream);
 
+/* Training ends (train_ddpm.py:94-114 loss.backward() through unet_base.py:400 conv_in and
+ * :448-449,483-485 norm_out -> SiLU -> conv_out): fp32 VALU kernels for the two 3-channel convs, whose
+ * MFMA tiles would be 20x padding.
+ * wc_head_dgrad: dz (NHWC view, row stride ldz) = the transposed 3x3 conv of g (NCHW (B, NO, H, W), the
+ *   loss gradient of conv_out) with w_p = conv_out.weight re-laid [NO][9 taps][C] (C % 4 == 0, NO <= 4).
+ * wc_head_wgrad: dw [NO][C][3][3] (=) sum over pixels of g times SiLU(x*scale[b,c] + shift[b,c]) (the
+ *   forward's prologue on the NHWC view x, zero padding after it) at each tap; NO = 3, C in {32, 64}.
+ * wc_stem_wgrad: dw [N][CI][3][3] (=) sum over pixels of g (NHWC, N in {32, 64} channels, row stride
+ *   ldg) times the NCHW input x (CI = 3) at each tap.
+ * The weight gradients take a workspace of wc_small_wgrad_workspace(B, H, W, dw elements) floats (per-
+ * band partials, summed in a fixed order: deterministic); accumulate = 1 adds into dw. */
+int64_t wc_small_wgrad_workspace(int B, int H, int W, int L);
+int wc_head_dgrad(const float* g, int B, int NO, int H, int W, const float* w_p, int C, float* dz, int ldz,
+                  void* stream);
+int wc_head_wgrad(const float* x, int ldx, const float* scale, const float* shift, const float* g, int B,
+                  int NO, int H, int W, int C, float* work, int64_t work_floats, float* dw, int accumulate,
+                  void* stream);
+int wc_stem_wgrad(const float* x_nchw, int CI, const float* g, int ldg, int B, int H, int W, int N,
+                  float* work, int64_t work_floats, float* dw, int accumulate, void* stream);
+
 /* Library identification: "weatherconverter_amd 0.1 gfx950 src:<digest>", where the digest (also alone
  * from wc_source_hash) is the one weatherconverter_amd/_build.py source_hash() computed over the kernel
  * sources, this header and the compiler flags the library was built from.  The Python loader refuses a

@@ -28,7 +28,8 @@ EXPORTS = [
     'wc_gn_bwd_finalize', 'wc_bsum', 'wc_bsum_batch', 'wc_gn_bwd_apply', 'wc_attention_fwd_lse', 'wc_attention_bwd', 'wc_gemm_small',
     'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name', 'wc_stamp', 'wc_wall_clock_khz',
     'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse',
-    'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_dkdv192', 'wc_attention_bwd_prep', 'wc_pack_split'
+    'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_dkdv192', 'wc_attention_bwd_prep', 'wc_pack_split',
+    'wc_small_wgrad_workspace', 'wc_head_dgrad', 'wc_head_wgrad', 'wc_stem_wgrad'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
@@ -122,6 +123,10 @@ _SIGS = {
     'wc_mse_workspace_doubles': [],
     'wc_mse_loss': [_P, _P, _L, _P, _F, _P, _P, _P],
     'wc_dwconv': [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
+    'wc_small_wgrad_workspace': [_I, _I, _I, _I],
+    'wc_head_dgrad': [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P],
+    'wc_head_wgrad': [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P],
+    'wc_stem_wgrad': [_P, _I, _P, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P],
     'wc_conv_wgrad': [ctypes.POINTER(WgradArgs), _P, _I, _P],
     'wc_conv_wgrad_x6': [ctypes.POINTER(WgradArgs), _P, _I, _P],
     'wc_conv_wgrad_f16x3': [ctypes.POINTER(WgradArgs), _P, _I, _P, _I, _P, _P, _P],
@@ -205,6 +210,8 @@ def load(build_if_missing: bool = True):
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
+    if hasattr(lib, 'wc_small_wgrad_workspace'):
+        lib.wc_small_wgrad_workspace.restype = ctypes.c_int64
     lib.wc_version.argtypes = []
     lib.wc_version.restype = ctypes.c_char_p
     lib.wc_last_kernel_name.argtypes = []

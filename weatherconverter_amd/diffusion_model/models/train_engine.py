@@ -310,10 +310,18 @@ class TrainEngine:
             self.res_rows = rows
             co = m.conv_out.weight.detach()  # [NO][C][3][3]
             NO, C = co.shape[0], co.shape[1]
-            self.head_pk = self._pk(pack_conv(co), C, 9)
-            wt = torch.zeros((C, 32, 3, 3), dtype=torch.float32, device=self.device)
-            wt[:, :NO] = co.flip([2, 3]).transpose(0, 1)
-            self.head_T = self._pk(pack_conv(wt), 32, 9)  # dgrad over the 32-channel padded loss gradient
+            # the 3-channel head on its fp32 VALU kernels (wc_head_conv forward, wc_head_wgrad /
+            # wc_head_dgrad backward): an MFMA tile pads its 3 channels 20x (WC_TRAIN_SMALLCONV=0: the
+            # generic implicit GEMMs, kept for A/B)
+            self.head_small = K.smallconv_enabled() and NO == 3 and C in (32, 64)
+            if self.head_small:
+                self.head_wp = K.pack_head(co)
+                self.head_T = None
+            else:
+                self.head_pk = self._pk(pack_conv(co), C, 9)
+                wt = torch.zeros((C, 32, 3, 3), dtype=torch.float32, device=self.device)
+                wt[:, :NO] = co.flip([2, 3]).transpose(0, 1)
+                self.head_T = self._pk(pack_conv(wt), 32, 9)  # dgrad over the 32-channel padded loss gradient
 
     # ------------------------------------------------------------------ helpers
     def _new(self, B, H, W, C) -> torch.Tensor:
@@ -543,8 +551,11 @@ class TrainEngine:
         sc, sh, a0, o0 = K.gn_stats_pair(cur, gn.weight.detach().float(), gn.bias.detach().float(),
                                          part=getattr(cur, '_wc_gn_done', None))
         out = torch.empty((B, mc.im_channels, S, S2), dtype=torch.float32, device=self.device)
-        self._conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.head_pk,
-                   m.conv_out.bias.detach().float().contiguous(), None, S, S2, out_nchw=out)
+        if self.head_small:
+            K.head_conv(cur, sc, sh, self.head_wp, m.conv_out.bias.detach().float().contiguous(), out)
+        else:
+            self._conv([Seg(cur, TAPS3, scale=sc, shift=sh, silu=True)], self.head_pk,
+                       m.conv_out.bias.detach().float().contiguous(), None, S, S2, out_nchw=out)
         self.tape.append(('head', cur, (sc, sh, a0, o0)))
         self.last_tape = Tape(self)
         self.tape = []
@@ -702,6 +713,18 @@ class TrainEngine:
         _, cur, (sc, sh, a0, o0) = rec
         B, NO, S, S2 = gout.shape
         C = cur.C
+        if self.head_small:
+            g = gout.contiguous().float()
+            K.head_wgrad(cur, sc, sh, g, self._pgrad(m.conv_out.weight))
+            self._pgrad(m.conv_out.bias).copy_(g.sum((0, 2, 3)))
+            dz = View.full(self._new(B, S, S2, C))
+            K.head_dgrad(g, m.conv_out.weight, dz)
+            gn = m.norm_out
+            gcur, ow = self._grad_w(cur)
+            K.gn_backward(dz, cur, a0, o0, gn.weight.detach().float(), gn.bias.detach().float(), True, gcur,
+                          dgamma=self._pgrad(gn.weight), dbeta=self._pgrad(gn.bias), accumulate=not ow,
+                          absmax=self._gb(cur))
+            return
         g32 = K.nchw_to_nhwc(gout, 32)
         g4 = View(g32, 0, 4)
         wtmp = torch.zeros((4, C, 3, 3), dtype=torch.float32, device=self.device)
@@ -870,8 +893,11 @@ class TrainEngine:
         _, cur = rec
         g = self._grad(cur)
         self._bias_grad(g, m.conv_in.bias)
-        xn = K.nchw_to_nhwc(self.x, 4)
         w = m.conv_in.weight
+        if K.smallconv_enabled() and w.shape[1] == 3 and g.C in (32, 64) and self.x.is_contiguous():
+            K.stem_wgrad(self.x, g, self._pgrad(w))  # fp32 VALU, the 3 input channels unpadded
+            return
+        xn = K.nchw_to_nhwc(self.x, 4)
         self._wgrad(g, [Seg(View.full(xn), TAPS3)], self._pgrad(w), (w.shape[1] * 9, 9, 1), Cw=w.shape[1])
 
     def _temb_bwd(self):

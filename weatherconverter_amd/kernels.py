@@ -1184,6 +1184,59 @@ def head_conv(x: View, scale: torch.Tensor, shift: torch.Tensor, w_packed: torch
            bias.data_ptr(), NO, out.data_ptr(), _stream())
 
 
+def smallconv_enabled() -> bool:
+    """Training's 3-channel convs (the head's forward / weight / data gradient, the stem's weight
+    gradient) on their fp32 VALU kernels (WC_TRAIN_SMALLCONV=0: the generic implicit GEMMs, for A/B)."""
+    return os.environ.get('WC_TRAIN_SMALLCONV', '1') != '0'
+
+
+def head_dgrad(g: torch.Tensor, w: torch.Tensor, dz: View):
+    """Data gradient of conv_out (unet_base.py:485) from the NCHW loss gradient g (B, NO, H, W): the
+    transposed 3x3 conv into the NHWC view dz (C = conv_out.in_channels), fp32 (wc_head_dgrad)."""
+    dz.check()
+    B, NO, H, W = g.shape
+    _req(g.is_cuda and g.dtype == torch.float32 and g.is_contiguous(), 'head_dgrad: contiguous fp32 NCHW gradient')
+    _req(tuple(w.shape) == (NO, dz.C, 3, 3) and dz.B == B and dz.H == H and dz.W == W, 'head_dgrad shapes')
+    wp = w.detach().float().permute(0, 2, 3, 1).contiguous()  # [NO][ky][kx][C]
+    _timed(f'head_dgrad_kernel<{NO}>', 'wc_head_dgrad', 2.0 * B * H * W * NO * 9 * dz.C, g.data_ptr(), B, NO, H, W,
+           wp.data_ptr(), dz.C, dz.ptr, dz.ldc, _stream(), nbytes=4.0 * B * H * W * (NO + dz.C))
+
+
+def _small_work(B: int, H: int, W: int, L: int, dev) -> torch.Tensor:
+    n = _native.load().wc_small_wgrad_workspace(B, H, W, L)
+    _req(n > 0, 'small wgrad workspace')
+    return torch.empty(n, dtype=torch.float32, device=dev)
+
+
+def head_wgrad(x: View, scale: torch.Tensor, shift: torch.Tensor, g: torch.Tensor, dw: torch.Tensor,
+               accumulate: bool = False):
+    """Weight gradient of conv_out: dw [NO][C][3][3] (+)= sum over pixels of g (NCHW) times the forward's
+    SiLU(x*scale + shift) at each tap, fp32, fixed-order reduction (wc_head_wgrad)."""
+    x.check()
+    B, NO, H, W = g.shape
+    _req(g.is_cuda and g.dtype == torch.float32 and g.is_contiguous(), 'head_wgrad: contiguous fp32 NCHW gradient')
+    _req(x.B == B and x.H == H and x.W == W and tuple(dw.shape) == (NO, x.C, 3, 3) and dw.is_contiguous()
+         and dw.dtype == torch.float32, 'head_wgrad shapes')
+    work = _small_work(B, H, W, dw.numel(), dw.device)
+    _timed('head_wgrad_kernel', 'wc_head_wgrad', 2.0 * B * H * W * NO * 9 * x.C, x.ptr, x.ldc, scale.data_ptr(),
+           shift.data_ptr(), g.data_ptr(), B, NO, H, W, x.C, work.data_ptr(), work.numel(), dw.data_ptr(),
+           int(accumulate), _stream(), nbytes=4.0 * B * H * W * (NO + x.C))
+
+
+def stem_wgrad(x: torch.Tensor, g: View, dw: torch.Tensor, accumulate: bool = False):
+    """Weight gradient of conv_in (unet_base.py:400): dw [N][3][3][3] (+)= sum over pixels of g (NHWC
+    view, N channels) times the NCHW input x at each tap, fp32, fixed-order reduction (wc_stem_wgrad)."""
+    g.check()
+    B, CI, H, W = x.shape
+    _req(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(), 'stem_wgrad: contiguous fp32 NCHW input')
+    _req(g.B == B and g.H == H and g.W == W and tuple(dw.shape) == (g.C, CI, 3, 3) and dw.is_contiguous()
+         and dw.dtype == torch.float32, 'stem_wgrad shapes')
+    work = _small_work(B, H, W, dw.numel(), dw.device)
+    _timed('stem_wgrad_kernel', 'wc_stem_wgrad', 2.0 * B * H * W * CI * 9 * g.C, x.data_ptr(), CI, g.ptr, g.ldc, B, H,
+           W, g.C, work.data_ptr(), work.numel(), dw.data_ptr(), int(accumulate), _stream(),
+           nbytes=4.0 * B * H * W * (CI + g.C))
+
+
 def ddpm_step(x: torch.Tensor, eps: torch.Tensor, out: torch.Tensor, beta: float, s1m: float, sqrt_alpha: float,
               sigma: float, *, z: Optional[torch.Tensor] = None, mode: int = _native.NOISE_NONE, seed: int = 0,
               sample0: int = 0, step: int = 0, sz_out: Optional[torch.Tensor] = None):

@@ -300,13 +300,13 @@ def _flops(segs: Sequence[Seg], Hm: int, Wm: int, N: int) -> float:
     return 2.0 * segs[0].view.B * Hm * Wm * N * sum(len(sg.taps) * sg.view.C for sg in segs)
 
 
-def _abytes(segs: Sequence[Seg], N: int, out_pixels: int, res: Optional[View] = None) -> float:
+def _abytes(segs: Sequence[Seg], N: int, out_pixels: int, res: Optional[View] = None, B: int = 0) -> float:
     """Algorithmic HBM bytes of a conv launch: every input element of every segment, the output and
-    the residual view once (fp32)."""
+    the residual view once (fp32).  (B: the batch when segs may be empty.)"""
     if not _measuring():
         return 0.0
     b = sum(4.0 * sg.view.B * sg.view.H * sg.view.W * sg.view.C for sg in segs)
-    b += 4.0 * segs[0].view.B * out_pixels * N * (2 if res is not None else 1)
+    b += 4.0 * (segs[0].view.B if segs else B) * out_pixels * N * (2 if res is not None else 1)
     return b
 
 
@@ -724,7 +724,8 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
         _timed(f'conv3x3_wino_kernel<{TH}, {BN}, 3, {"true" if len(segs) == 2 else "false"}>',
                'wc_conv3x3_wino_f16x3_vp', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
                ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(), ab,
-               vbuf.data_ptr(), nb.value, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res),
+               vbuf.data_ptr(), nb.value, _stream(),
+               nbytes=(nb.value + _abytes(segs[1:], w.N, Hm * Wm, res, B=v.B)) if prof else 0.0,
                mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
         return
     _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {0 if raw else 2}, {"true" if len(segs) == 2 else "false"}>',

@@ -601,23 +601,6 @@ int wc_nchw_to_nhwc(const float* src, int B, int C, int H, int W, float* dst, in
 int wc_dwconv(const float* x, int ldx, float* out, int ldo, const float* w, const float* bias, int B,
               int H, int W, int C, int K, void* stream);
 
-/* ResBlock 3x3 conv through the 2D Winograd transform F(2x2, 3x3), position-major (wc_wino2d.hip): the
- * wide GN+SiLU convs (unet_base.py:87-109,146-150) with C0 % 32 == 0, an optional raw 1x1 residual
- * (C1 % 32 == 0, under the per-image bound a_bound, as wc_conv3x3_wino_f16x3), H % 16 == W % 16 == 0.
- * wc_wino2d_bytes: bytes of the segment-0 planes (16 per input element) and of the residual planes (4).
- * wc_wino2d_vsplit_f16x3: GN+SiLU x 2^(a_exp - 2) (capped by the residual bound), V = B^T d B per 2x2
- *   tile, two fp16 pieces: planes [b][C0/16][piece][16 positions][k-half][H/2][W/2] x 16 B; the
- *   residual input x the same power of two: [b][C1/16][piece][4 pixels][k-half][H/2][W/2] x 16 B.
- * wc_conv3x3_wino2d_f16x3: the conv from those planes with a kernels.pack_wino2d weight (U = G g G^T,
- *   per-channel power of two w_inv_scale = 2^-sW[n]); epilogue as wc_conv3x3_wino_f16x3 (bias, temb,
- *   residual view, absmax, GroupNorm tile partials). */
-int wc_wino2d_bytes(int B, int C0, int C1, int H, int W, int64_t* v_bytes, int64_t* r_bytes);
-int wc_wino2d_vsplit_f16x3(const wc_conv_args* args, int a_exp, const float* a_bound, void* v, int64_t v_bytes,
-                           void* vr, int64_t r_bytes, void* stream);
-int wc_conv3x3_wino2d_f16x3(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
-                            const float* w_inv_scale, const float* a_bound, const void* v, int64_t v_bytes,
-                            const void* vr, int64_t r_bytes, void* stream);
-
 /* Training ends (train_ddpm.py:94-114 loss.backward() through unet_base.py:400 conv_in and
  * :448-449,483-485 norm_out -> SiLU -> conv_out): fp32 VALU kernels for the two 3-channel convs, whose
  * MFMA tiles would be 20x padding.

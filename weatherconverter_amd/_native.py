@@ -29,8 +29,7 @@ EXPORTS = [
     'wc_silu', 'wc_colsum', 'wc_time_embedding', 'wc_nchw_to_nhwc', 'wc_last_kernel_name', 'wc_stamp', 'wc_wall_clock_khz',
     'wc_attention_fwd_f16x3_lse', 'wc_attention_fwd_x6_lse',
     'wc_conv_wgrad3', 'wc_conv_wgrad3_f16x3', 'wc_conv_wgrad3_splits', 'wc_absmax_images', 'wc_attention_bwd6', 'wc_attention_bwd_f16x3', 'wc_attention_bwd_dkdv192', 'wc_attention_bwd_prep', 'wc_pack_split',
-    'wc_small_wgrad_workspace', 'wc_head_dgrad', 'wc_head_wgrad', 'wc_stem_wgrad',
-    'wc_wino2d_bytes', 'wc_wino2d_vsplit_f16x3', 'wc_conv3x3_wino2d_f16x3'
+    'wc_small_wgrad_workspace', 'wc_head_dgrad', 'wc_head_wgrad', 'wc_stem_wgrad'
 ]
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_PRELU, ACT_TANH01 = 0, 1, 2, 3, 4
 
@@ -125,9 +124,6 @@ _SIGS = {
     'wc_mse_loss': [_P, _P, _L, _P, _F, _P, _P, _P],
     'wc_dwconv': [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
     'wc_small_wgrad_workspace': [_I, _I, _I, _I],
-    'wc_wino2d_bytes': [_I, _I, _I, _I, _I, _P, _P],
-    'wc_wino2d_vsplit_f16x3': [ctypes.POINTER(ConvArgs), _I, _P, _P, _L, _P, _L, _P],
-    'wc_conv3x3_wino2d_f16x3': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P, _L, _P, _L, _P],
     'wc_head_dgrad': [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P],
     'wc_head_wgrad': [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P],
     'wc_stem_wgrad': [_P, _I, _P, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P],

@@ -98,8 +98,6 @@ class ResPack:
     gb2: Tuple[float, float] = (0.0, 0.0)
     w1wn: Optional[K.X6Weight] = None  # Winograd F(2,3) packs (precision 'f16x3', kernels.wino_enabled())
     w2wn: Optional[K.X6Weight] = None
-    w1w2d: Optional[K.X6Weight] = None  # 2D Winograd F(2x2, 3x3) packs of the wide convs (kernels.wino2d_enabled())
-    w2w2d: Optional[K.X6Weight] = None
 
 
 @dataclass
@@ -214,9 +212,6 @@ class UnetEngine:
                 if K.wino_enabled():
                     p.w1wn = K.pack_wino(p.w1, ci)
                     p.w2wn = K.pack_wino(p.w2, co, ci)
-                    if K.wino2d_enabled() and co > 3 * 128 and ci % 32 == 0 and co % 32 == 0:
-                        p.w1w2d = K.pack_wino2d(p.w1, ci)
-                        p.w2w2d = K.pack_wino2d(p.w2, co, ci)
                 p.gb1 = (float(p.g1.abs().max()), float(p.be1.abs().max()))
                 p.gb2 = (float(p.g2.abs().max()), float(p.be2.abs().max()))
         self.temb_rows_w.append(tl.weight.detach().float())
@@ -344,22 +339,13 @@ class UnetEngine:
 
     def conv3(self, segs, w: torch.Tensor, w6, w3: Optional[K.X6Weight], gb: Tuple[float, float], bias, out: View,
               H: int, W: int, a_bound: Optional[torch.Tensor] = None, absmax: Optional[torch.Tensor] = None,
-              wn: Optional[K.X6Weight] = None, w2d: Optional[K.X6Weight] = None, **kw) -> bool:
+              wn: Optional[K.X6Weight] = None, **kw) -> bool:
         """A ResBlock 3x3 stride-1 conv (GN+SiLU prologue): the halo-tiled kernel in f16x3 (bound
         from the GroupNorm affine gb and the group size) or bf16x6 when the grid tiles, else the
         bf16x6 implicit GEMM (or fp32 MFMA in fp32 mode).  GN partials of `out` are emitted by the
         split-precision epilogues where they can be, else filled by a stats pass.  Returns whether
         the absmax was emitted."""
         gp = K.GnPart.of(out)
-        if (w2d is not None and K.wino2d_enabled() and K.wino2d_eligible(segs, w2d.N, H, W)
-                and (len(segs) == 1 or a_bound is not None)):
-            # the 2D Winograd F(2x2, 3x3) position-major form (2/3 of the 1D form's MFMA work)
-            n_group = H * W * segs[0].view.C // 8
-            fused = K.gn_conv_ok(out, gp, w2d.N, H, W)
-            K.conv3x3_wino2d(segs, w2d, bias, out, Hm=H, Wm=W, a_exp=K.f16x3_a_exp(gb[0], gb[1], n_group),
-                             a_bound=a_bound, absmax=absmax, gn=gp if fused else None, **kw)
-            self._gn_fill(out, fused)
-            return absmax is not None
         if (wn is not None and K.wino_eligible(segs, wn.N, H, W) and (len(segs) == 1 or a_bound is not None)
                 and (w3 is None or K.x6_eligible(segs, w3.N, H, W))):
             # the Winograd F(2,3)-along-x form of the same f16x3 conv (1.5x fewer MFMAs)
@@ -393,11 +379,11 @@ class UnetEngine:
             sc1, sh1 = self._gn(X, p.g1, p.be1)
         h = View.full(self._new(B, H, W, p.co, gn_sw=self._sw(p.co)))
         self.conv3([Seg(X, TAPS3, scale=sc1, shift=sh1, silu=True)], p.w1, p.w1x6, p.w1f3, p.gb1, p.b1, h, H, W,
-                   temb=temb[:, p.temb_off:], temb_ld=temb_ld, wn=p.w1wn, w2d=p.w1w2d)
+                   temb=temb[:, p.temb_off:], temb_ld=temb_ld, wn=p.w1wn)
         sc2, sh2 = self._gn(h, p.g2, p.be2)
         return self.conv3([Seg(h, TAPS3, scale=sc2, shift=sh2, silu=True),
                            Seg(X, TAPS1, kbase=9 * p.co)], p.w2, p.w2x6, p.w2f3, p.gb2, p.b2, Y, H, W, a_bound=xb,
-                          absmax=absmax, wn=p.w2wn, w2d=p.w2w2d)
+                          absmax=absmax, wn=p.w2wn)
 
     def attention(self, Y: View, p: AttnPack, absmax: Optional[torch.Tensor] = None) -> bool:
         B, H, W, C = Y.B, Y.H, Y.W, Y.C

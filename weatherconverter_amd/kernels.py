@@ -735,108 +735,6 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
            mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
 
 
-_G2 = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
-
-
-def pack_wino2d(w: torch.Tensor, C0: int, C1: int = 0) -> X6Weight:
-    """Pack a [N][9*C0 + C1] ResBlock conv weight (engine.pack_conv order) for wc_conv3x3_wino2d_f16x3: the
-    F(2x2, 3x3) filter transform U = G g G^T in float64, a per-output-channel power-of-two scale 2^sW[n]
-    with max |U|, |w_res| * 2^sW <= 2^14 (pack_wino's rule), each value rounded once to fp32 and split into
-    two round-to-nearest fp16 pieces; layout [N tile][K-step][piece][k-half][128][8] with the K-steps
-    position-major, (P = 4 p + q, 16-channel chunk c) -> P * C0/16 + c, then the residual chunks."""
-    N, K = w.shape
-    _req(K == 9 * C0 + C1 and C0 % 32 == 0 and C1 % 32 == 0, 'wino2d weight shape')
-    BN = 128
-    Np = -(-N // BN) * BN
-    T = Np // BN
-    wd = torch.zeros((Np, K), dtype=torch.float64, device=w.device)
-    wd[:N] = w.double()
-    g = wd[:, :9 * C0].reshape(Np, 3, 3, C0)
-    Gm = torch.tensor(_G2, dtype=torch.float64, device=w.device)
-    U = torch.einsum('pk,nklc,ql->npqc', Gm, g, Gm)  # [Np][4][4][C0]
-    r = wd[:, 9 * C0:]
-    amax = U.abs().reshape(Np, -1).amax(1)
-    if C1:
-        amax = torch.maximum(amax, r.abs().amax(1))
-    m, e = torch.frexp(amax)
-    sw = torch.where(amax > 0, torch.where(m == 0.5, 15 - e, 14 - e).double(), torch.zeros_like(amax))
-    sw = sw.clamp(-60, 60)
-    scale = torch.ldexp(torch.ones_like(sw), sw)
-
-    def pieces(v):  # exact power-of-two scaling, one rounding to fp32, two fp16 pieces
-        v32 = (v * scale.reshape((-1, ) + (1, ) * (v.dim() - 1))).float()
-        return torch.stack(_split2(v32)).view(torch.int16)
-
-    nc0 = C0 // 16
-    p0 = pieces(U).view(2, T, BN, 16, nc0, 2, 8).permute(1, 3, 4, 0, 5, 2, 6).reshape(T, -1)
-    parts = [p0]
-    if C1:
-        parts.append(pieces(r).view(2, T, BN, C1 // 16, 2, 8).permute(1, 3, 0, 4, 2, 5).reshape(T, -1))
-    data = torch.cat(parts, 1).contiguous()
-    wsinv = torch.ldexp(torch.ones(Np, dtype=torch.float32, device=w.device), (-sw).float()).contiguous()
-    return X6Weight(data, N, BN, C0, C1, 'wino2d', wsinv, bool(C1))
-
-
-def wino2d_enabled() -> bool:
-    """The wide pre-split convs through the 2D F(2x2, 3x3) position-major kernel (WC_WINO2D=0: the 1D
-    pre-split form, kept for A/B and as its test reference)."""
-    return os.environ.get('WC_WINO2D', '1') != '0'
-
-
-def wino2d_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
-    """The 2D form's constraints (wc_conv3x3_wino2d_f16x3's checks): a GN+SiLU 3x3 segment 0 with C0 % 32 == 0
-    (+ a raw 1x1 residual with C1 % 32 == 0), the grid in 16 x 16-pixel blocks, at least 4 output tiles
-    of 128 (the pre-split threshold: the planes are read once per output tile)."""
-    s0 = segs[0]
-    v = s0.view
-    if not (s0.silu and s0.scale is not None and len(s0.taps) == 9 and s0.stride == 1 and v.C % 32 == 0
-            and v.H == Hm and v.W == Wm and Hm % 16 == 0 and Wm % 16 == 0 and v.ldc % 4 == 0 and v.ptr % 16 == 0):
-        return False
-    if list(s0.taps) != [(ky - 1, kx - 1) for ky in range(3) for kx in range(3)]:
-        return False
-    if len(segs) == 2:
-        r = segs[1].view
-        if not (r.C % 32 == 0 and r.ldc % 4 == 0 and r.ptr % 16 == 0 and r.H == Hm and r.W == Wm):
-            return False
-    return _WINO_VP_MIN_TILES > 0 and -(-N // 128) >= _WINO_VP_MIN_TILES
-
-
-def conv3x3_wino2d(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
-                   a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
-                   temb_ld: int = 0, res: Optional[View] = None, absmax: Optional[torch.Tensor] = None,
-                   gn: Optional[GnPart] = None):
-    """The ResBlock 3x3 conv through the 2D Winograd F(2x2, 3x3) position-major kernel: segment 0 (GN+SiLU,
-    a_exp = f16x3_a_exp of that GroupNorm) transformed and split once into planes (wc_wino2d_vsplit_f16x3,
-    with the optional 1x1 residual's input under its per-image bound a_bound), then
-    wc_conv3x3_wino2d_f16x3."""
-    _req(w.data.is_cuda and w.data.is_contiguous() and w.order == 'wino2d', 'wino2d weight')
-    _req(w.C0 == segs[0].view.C and w.C1 == (segs[1].view.C if len(segs) == 2 else 0), 'wino2d weight segments')
-    _req(len(segs) == 1 or a_bound is not None, 'a residual wino2d segment needs a per-image A bound')
-    if a_bound is not None:
-        _req(a_bound.is_cuda and a_bound.dtype == torch.float32 and a_bound.numel() == segs[0].view.B, 'A bound')
-    a = _conv_args(segs, w.N, bias, out, Hm, Wm, temb, temb_ld, res, (1, 1, 0, 0), None, 0, absmax, gn=gn)
-    v = segs[0].view
-    C1 = segs[1].view.C if len(segs) == 2 else 0
-    vb, rb = ctypes.c_int64(), ctypes.c_int64()
-    _native.call('wc_wino2d_bytes', v.B, v.C, C1, Hm, Wm, ctypes.byref(vb), ctypes.byref(rb))
-    vbuf = torch.empty(vb.value, dtype=torch.uint8, device=v.t.device)
-    rbuf = torch.empty(max(rb.value, 16), dtype=torch.uint8, device=v.t.device)
-    ab = _ptr(a_bound) if len(segs) == 2 else None
-    prof = _measuring()
-    _timed('wino2d_vsplit_kernel', 'wc_wino2d_vsplit_f16x3', 0.0, ctypes.byref(a), int(a_exp), ab, vbuf.data_ptr(),
-           vb.value, rbuf.data_ptr(), rb.value, _stream(),
-           nbytes=(4.0 * v.B * Hm * Wm * (v.C + C1) + vb.value + rb.value) if prof else 0.0)
-    # issued f16 MFMA work: 16 products per 2x2 tile and input channel on segment 0, 1 per pixel on the
-    # residual, 3 pieces each, N padded to the 128-channel tile
-    Np = -(-w.N // 128) * 128
-    mfma = 3 * 2.0 * v.B * Hm * Wm * Np * (4 * v.C + C1)
-    _timed(f'conv3x3_wino2d_kernel<{"true" if len(segs) == 2 else "false"}>', 'wc_conv3x3_wino2d_f16x3',
-           _flops(segs, Hm, Wm, w.N) if prof else 0.0, ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2,
-           int(a_exp), w.wsinv.data_ptr(), ab, vbuf.data_ptr(), vb.value, rbuf.data_ptr(), rb.value, _stream(),
-           nbytes=(vb.value + rb.value + 4.0 * v.B * Hm * Wm * w.N * (2 if res is not None else 1)) if prof else 0.0,
-           mfma=mfma)
-
-
 # Pre-split Winograd segment 0 (wc_wino_vsplit_f16x3) for convs with at least this many 128-channel
 # output tiles (the redundancy the in-conv prologue pays: every output tile re-transforms the halo);
 # 0 = never.  WC_WINO_VP sets it (A/B runs); set_wino_vsplit at run time.

@@ -386,9 +386,10 @@ def test_old_unet_helper_kernels(K):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('B,H,W,C,NO', [(2, 32, 48, 64, 3), (1, 20, 13, 32, 4), (3, 16, 16, 128, 1), (1, 45, 30, 32, 4),
-                                        (2, 64, 40, 64, 3)])
+                                        (2, 64, 40, 64, 3), (1, 24, 40, 48, 3), (2, 16, 32, 16, 3)])
 def test_head_conv_vs_float64(B, H, W, C, NO):
-    """norm_out -> SiLU -> conv_out on wc_head_conv (ragged tiles, strided view) vs float64."""
+    """norm_out -> SiLU -> conv_out on wc_head_conv (ragged tiles, strided view, a 16-channel tail chunk
+    after the 32-channel ones) vs float64."""
     from weatherconverter_amd import kernels as K
     g = torch.Generator().manual_seed(B * 100 + C)
     buf = torch.randn((B, H, W, C + 32), generator=g) * 2 + 0.5

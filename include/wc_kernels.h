@@ -153,7 +153,8 @@ int wc_conv3x3_wino_tile_n(int N);
  * GroupNorm-affine'd, SiLU'd, scaled by 2^s (s = a_exp - 1, per image clamped to 13 - e(a_bound[b]) when
  * args has a residual segment -- the conv's own exponent), Winograd input-transformed (V0..V3 of every
  * output pair) and split into two fp16 pieces, stored in the conv's LDS image order:
- * vout[b][C/16][plane 16][H][W/2] x 16 bytes (wc_wino_vsplit_bytes).  Bit for bit what the conv's own
+ * vout[b][C/16][plane 16][H][W/2] x 16 bytes (wc_wino_vsplit_bytes; the single-piece training builds
+ * store the high piece's 8 planes only, their low piece being zero).  Bit for bit what the conv's own
  * prologue computes. */
 int wc_wino_vsplit_bytes(int B, int C, int H, int W, int64_t* bytes);
 int wc_wino_vsplit_f16x3(const wc_conv_args* args, int a_exp, const float* a_bound, void* vout, int64_t v_bytes,

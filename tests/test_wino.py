@@ -8,6 +8,8 @@ GPU: the kernel against a float64 direct conv (reference ResBlock convs unet_bas
 segment (chunk counts equal and unequal), the epilogue residual view, per-image absmax and GroupNorm
 tile partials.
 """
+import ctypes
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -273,6 +275,22 @@ def test_conv3x3_wino_presplit_bit_identical(B, H, W, Ci, Co, Cr):
     and as a tail, per-image residual exponents."""
     _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0),
                    lambda K, v: K.set_wino_vsplit(v))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('line', ['single16', 'bf16'])
+@pytest.mark.parametrize('B,H,W,Ci,Co,Cr', [(2, 16, 32, 64, 128, 0), (1, 32, 16, 48, 256, 48), (1, 8, 16, 32, 512, 512),
+                                            (2, 8, 96, 32, 256, 64), (1, 16, 80, 32, 128, 0)])
+def test_conv3x3_wino_presplit_bit_identical_single_piece_lines(line, B, H, W, Ci, Co, Cr):
+    """The single-piece training builds store only the high piece's 8 planes per chunk (their low piece is
+    zero) and the conv copies only those: still bit-identical to the in-conv prologue of the same build."""
+    from weatherconverter_amd import _native
+    with _native.variant(line):
+        _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0),
+                       lambda K, v: K.set_wino_vsplit(v))
+        n = ctypes.c_int64()
+        _native.call('wc_wino_vsplit_bytes', B, Ci, H, W, ctypes.byref(n))
+        assert n.value == B * (Ci // 16) * 8 * H * (W // 2) * 16
 
 
 def _compare_forms(B, H, W, Ci, Co, Cr, raw, select, restore):

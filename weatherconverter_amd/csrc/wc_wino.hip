@@ -103,6 +103,11 @@ struct WDev {
 // transform / split VALU and loads feed twice the MFMA work -- BN = 256 channels over 8 rows, or BN = 128
 // over 16 rows).  The weights stay packed in 128-channel tiles (wc_conv3x3_wino_tile_n): a 256-channel
 // workgroup reads two of them.
+// Planes of the pre-split layout per 16-channel chunk: (piece 2) x (position 4) x (k-half 2), or in the
+// single-piece builds (WC_SINGLE16: the 16-bit training lines, one piece per operand) the high piece's 8
+// planes only -- the low piece is zero there, so the pass writes and the conv copies half the bytes.
+constexpr int VPL = WC_SINGLE16 ? 8 : 16;
+
 template <int TH, int BN, int MB = 2, int NW = 4, bool VP = false>
 struct WTile {
     static constexpr int NT = 64 * NW;
@@ -115,8 +120,11 @@ struct WTile {
     // the k-half stride 16 mod 128 so the item writes of a 16-lane group hit 16 distinct 8-byte slots
     // (VP, PRO 3: the planes arrive by LDS-DMA in 1-KiB pieces, no item writes: no pad, planes contiguous)
     static constexpr int PSTR = HR * 128 + (VP ? 0 : 16);
-    static constexpr int DPW = 16 * HR * 8 / 64 / NW;  // VP: 1-KiB LDS-DMA pieces per wave per chunk
-    static_assert(!VP || 16 * HR * 8 == DPW * 64 * NW, "VP: the halo stage is a whole number of pieces per wave");
+    // VP: the chunk's VPL planes of HR rows x 8 tiles arrive as 1-KiB LDS-DMA pieces, piece i of wave w is
+    // w + NW i (the last round partial when the count is not a multiple of NW)
+    static constexpr int DPIECES = VPL * HR * 8 / 64;
+    static_assert(!VP || VPL * HR * 8 == DPIECES * 64, "VP: the halo stage is a whole number of 1-KiB pieces");
+    static constexpr int DPW = (DPIECES + NW - 1) / NW;
     static constexpr int HSTAGE = 16 * PSTR;     // planes (piece 2) x (position 4) x (k-half 2)
     static constexpr int CPSTR = TH * 128 + 16;  // residual centre plane ([row][tile])
     static constexpr int CSTAGE = 8 * CPSTR;     // (piece 2) x (position 0 / 3) x (k-half 2)
@@ -199,7 +207,7 @@ void conv3x3_wino_kernel(WDev p) {
     const __amdgpu_buffer_rsrc_t srdw = make_srd(p.w);
     const __amdgpu_buffer_rsrc_t srdsc = make_srd(PRO == 2 ? p.scale : p.src0);
     const __amdgpu_buffer_rsrc_t srdsh = make_srd(PRO == 2 ? p.shift : p.src0);
-    // VP: this image's pre-split planes [chunk][plane 16][row H][tile W/2] x 16 B; per-lane byte offsets
+    // VP: this image's pre-split planes [chunk][plane VPL][row H][tile W/2] x 16 B; per-lane byte offsets
     // of this wave's LDS-DMA pieces (chunk 0; a chunk is a scalar offset), OOB for halo rows outside
     // the image (the load returns zeros: the padding rows' V)
     const __amdgpu_buffer_rsrc_t srdv = make_srd(VP ? (const void*)(p.vpre + (long)b * p.vimg) : (const void*)p.src0);
@@ -207,18 +215,20 @@ void conv3x3_wino_kernel(WDev p) {
     if constexpr (VP) {
 #pragma unroll
         for (int i = 0; i < T::DPW; ++i) {
-            const int f = (wave * T::DPW + i) * 64 + lane;  // 16-byte fragment of the stage
+            const int f = (wave + NW * i) * 64 + lane;  // 16-byte fragment of the stage
             const int P = f / (T::HR * 8), r = (f >> 3) % T::HR, tl = f & 7;
             const int y = y0 - 1 + r;
             voff[i] = (unsigned)y < (unsigned)p.H ? (unsigned)(((P * p.H + y) * (p.W / 2) + (x0 >> 1) + tl) * 16) : OOB;
         }
     }
-    const int vchunk = 16 * p.H * (p.W / 2) * 16;  // bytes of one 16-channel chunk's planes
+    const int vchunk = VPL * p.H * (p.W / 2) * 16;  // bytes of one 16-channel chunk's planes
     auto dma_halo = [&](int c, int hs) {
         if constexpr (VP) {
-            unsigned char* dst = smem + hs * T::HSTAGE + wave * T::DPW * 1024;
+            unsigned char* dst = smem + hs * T::HSTAGE + wave * 1024;
 #pragma unroll
-            for (int i = 0; i < T::DPW; ++i) wino_lds16(srdv, dst + i * 1024, voff[i], c * vchunk);
+            for (int i = 0; i < T::DPW; ++i)
+                if (T::DPIECES % NW == 0 || wave + NW * i < T::DPIECES)  // wave-uniform: the partial last round
+                    wino_lds16(srdv, dst + i * NW * 1024, voff[i], c * vchunk);
         }
     };
 
@@ -760,8 +770,8 @@ int wino_setup(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
     return WC_OK;
 }
 
-// bytes of one image's pre-split planes: [chunk C/16][plane 16][row H][tile W/2] x 16 B
-long wino_vimg(int C, int H, int W) { return (long)(C / 16) * 16 * H * (W / 2) * 16; }
+// bytes of one image's pre-split planes: [chunk C/16][plane VPL][row H][tile W/2] x 16 B
+long wino_vimg(int C, int H, int W) { return (long)(C / 16) * VPL * H * (W / 2) * 16; }
 
 // ---- wino_vsplit_kernel: segment 0 of a GN+SiLU Winograd conv, transformed and split once ----
 // Workgroup = R = 256 / W image rows of one image and NCK 16-channel chunks (NCK = 2 where C % 32 == 0:
@@ -836,7 +846,7 @@ __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restric
     const long frag = ((long)y * T2 + t) * 16;
 #pragma unroll
     for (int ck = 0; ck < NCK; ++ck) {
-        unsigned char* vb = vout + (long)b * vimg + (long)(kg * NCK + ck) * 16 * H * T2 * 16;
+        unsigned char* vb = vout + (long)b * vimg + (long)(kg * NCK + ck) * VPL * H * T2 * 16;
         u32x2 pc[2][4][2];  // [quad of the octet][position][piece]
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
@@ -849,7 +859,7 @@ __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restric
 #pragma unroll
         for (int pos = 0; pos < 4; ++pos)
 #pragma unroll
-            for (int piece = 0; piece < 2; ++piece)
+            for (int piece = 0; piece < VPL / 8; ++piece)  // (single-piece builds: the high piece only)
                 *reinterpret_cast<u32x4*>(vb + (piece * 8 + pos * 2 + h) * plane + frag) =
                     u32x4{pc[0][pos][piece].x, pc[0][pos][piece].y, pc[1][pos][piece].x, pc[1][pos][piece].y};
     }

@@ -1,5 +1,6 @@
 """The halo 3x3 weight-gradient kernel (wc_conv_wgrad3_f16x3) alone on the ResBlock shapes of the 256-px
-UNet at B=16 (GN+SiLU prologue), for timing and PMC passes.  usage: wgrad3_probe.py [--only i]"""
+UNet (GN+SiLU prologue), for timing and PMC passes.  usage: wgrad3_probe.py [--only i] [--batch B]
+[--line f16x3|bf16|f16] (bf16 / f16: the single-piece training builds' library)"""
 import argparse
 import os
 import sys
@@ -31,13 +32,18 @@ def case(B, S, C, M):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', type=int, default=-1)
+    ap.add_argument('--batch', type=int, default=0)
+    ap.add_argument('--line', default='f16x3', choices=['f16x3', 'bf16', 'f16'])
     a = ap.parse_args()
-    K._native.load()
-    for i, (B, S, C, M) in enumerate(SHAPES):
-        if a.only >= 0 and i != a.only:
-            continue
-        t, tf = case(B, S, C, M)
-        print(f'wgrad3 B={B} S={S:3d} C={C} M={M}: {t * 1e3:8.3f} ms  {tf:6.1f} TF/s', flush=True)
+    var = {'f16x3': '', 'bf16': 'bf16', 'f16': 'single16'}[a.line]
+    with K._native.variant(var):
+        K._native.load()
+        for i, (B, S, C, M) in enumerate(SHAPES):
+            if a.only >= 0 and i != a.only:
+                continue
+            B = a.batch or B
+            t, tf = case(B, S, C, M)
+            print(f'wgrad3 {a.line} B={B} S={S:3d} C={C} M={M}: {t * 1e3:8.3f} ms  {tf:6.1f} TF/s', flush=True)
 
 
 if __name__ == '__main__':

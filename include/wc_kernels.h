@@ -164,6 +164,26 @@ int wc_wino_vsplit_f16x3(const wc_conv_args* args, int a_exp, const float* a_bou
 int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
                              const float* w_inv_scale, const float* a_bound, const void* vpre, int64_t v_bytes,
                              void* stream);
+/* wc_conv3x3_wino_f16x3 on one raw segment (a training data gradient dz, under a_bound) whose epilogue
+ * also forms the GroupNorm(+SiLU) backward's sums of the values it writes (the pass wc_gn_bwd_reduce
+ * makes over dz, without re-reading dz): with xhat = x*sc0 + sh0 at the same pixel and channel and
+ * dy = dz * SiLU'(gamma*xhat + beta) (silu) or dz, part[B][splits][N][2] = (sum dy, sum dy*xhat) and
+ * part3[B][splits][N] (optional) = sum xhat per (image, 8- or 16-row x 16-column tile, wave row);
+ * splits = wc_conv3x3_wino_gnb_splits(N, H, W).  wc_gn_bwd_finalize takes them as the reduce's. */
+typedef struct wc_gnb_epi {
+    const float* x;
+    int ldx, silu;
+    const float* sc0;
+    const float* sh0;
+    const float* gamma;
+    const float* beta;
+    float* part;
+    float* part3;
+    int splits, pad;
+} wc_gnb_epi;
+int wc_conv3x3_wino_gnb_splits(int N, int H, int W);
+int wc_conv3x3_wino_f16x3_gnb(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
+                              const float* w_inv_scale, const float* a_bound, const wc_gnb_epi* g, void* stream);
 /* Device re-pack of a [N][9*C0 + C1] fp32 ResBlock conv weight (K = (ky*3 + kx, c), then the 1x1
  * residual columns) into wc_conv3x3_wino_f16x3's layout and w_inv_scale[ceil(N/BN)*BN]: the F(2,3)
  * filter transform in float64, the per-channel power-of-two scale, one rounding to fp32, two fp16

@@ -332,3 +332,43 @@ def _compare_forms(B, H, W, Ci, Co, Cr, raw, select, restore):
         restore(K, prev)
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b), ((a - b).abs().max(), names)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,H,W,Cg,Co', [(2, 16, 32, 128, 128), (2, 32, 16, 64, 64), (1, 8, 48, 256, 192),
+                                         (3, 16, 16, 64, 128)])
+def test_dgrad_epilogue_gn_backward_sums(B, H, W, Cg, Co):
+    """The training data-gradient conv (raw segment under the per-image bound) forming the GroupNorm+SiLU
+    backward's sums of what it writes (wc_conv3x3_wino_f16x3_gnb) instead of a wc_gn_bwd_reduce pass
+    over dz: the written dz bit-identical to the plain conv's, and gn_backward's dx, dgamma, dbeta and
+    closed-form dx sums equal to the reduce path's to fp32 summation order (rel-L2 <= 1e-6); 64- and
+    128-channel tiles (one and two wave rows per tile), several output-channel tiles."""
+    from weatherconverter_amd import kernels as K
+    g = torch.Generator().manual_seed(61)
+    gy = (torch.randn((B, H, W, Cg), generator=g) * 1e-2).cuda()
+    w = (torch.randn((Co, 9 * Cg), generator=g) / (9 * Cg)**0.5).cuda()
+    x = (torch.randn((B, H, W, Co), generator=g) * 2 + 0.5).cuda()
+    sc0 = (torch.rand((B, Co), generator=g) + 0.5).cuda()
+    sh0 = (torch.randn((B, Co), generator=g) * 0.3).cuda()
+    ga = (torch.rand(Co, generator=g) + 0.5).cuda()
+    be = (torch.randn(Co, generator=g) * 0.1).cuda()
+    bound = gy.abs().reshape(B, -1).amax(1).contiguous()
+    segs = [K.Seg(K.View.full(gy), TAPS3)]
+    assert K.wino_eligible(segs, Co, H, W)
+    wp = K.pack_wino(w, Cg)
+    xv = K.View.full(x)
+    res = {}
+    for mode in ('reduce', 'epilogue'):
+        dz = torch.empty((B, H, W, Co), device='cuda')
+        pre = K.GnbSums.make(xv, sc0, sh0, ga, be, True, dx_sums=True) if mode == 'epilogue' else None
+        assert mode == 'reduce' or pre is not None
+        K.conv3x3_wino(segs, wp, None, K.View.full(dz), Hm=H, Wm=W, a_exp=60, a_bound=bound, gnb=pre)
+        dx = torch.empty((B, H, W, Co), device='cuda')
+        dgam, dbet = torch.zeros(Co, device='cuda'), torch.zeros(Co, device='cuda')
+        dsum = K.gn_backward(K.View.full(dz), xv, sc0, sh0, ga, be, True, K.View.full(dx), dgamma=dgam, dbeta=dbet,
+                             accumulate=False, dx_sums=True, pre=pre)
+        torch.cuda.synchronize()
+        res[mode] = [t.cpu() for t in (dz, dx, dgam, dbet, dsum[..., 0])]
+    assert torch.equal(res['reduce'][0], res['epilogue'][0])  # the conv's output is unchanged
+    for a, b in zip(res['reduce'][1:], res['epilogue'][1:]):
+        assert rel_l2(b, a) <= 1e-6, rel_l2(b, a)

@@ -17,7 +17,7 @@ MAX_TAPS = 16
 NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 
 EXPORTS = [
-    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
+    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_conv3x3_wino_gnb_splits', 'wc_conv3x3_wino_f16x3_gnb', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
     'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
@@ -41,6 +41,13 @@ class ConvSeg(ctypes.Structure):
         ('dy', ctypes.c_int * MAX_TAPS), ('dx', ctypes.c_int * MAX_TAPS), ('scale', ctypes.c_void_p),
         ('shift', ctypes.c_void_p), ('silu', ctypes.c_int), ('kbase', ctypes.c_int)
     ]
+
+
+class GnbEpi(ctypes.Structure):
+    """wc_gnb_epi (include/wc_kernels.h): the GroupNorm-backward sums a data-gradient conv's epilogue forms."""
+    _fields_ = [('x', ctypes.c_void_p), ('ldx', ctypes.c_int), ('silu', ctypes.c_int), ('sc0', ctypes.c_void_p),
+                ('sh0', ctypes.c_void_p), ('gamma', ctypes.c_void_p), ('beta', ctypes.c_void_p),
+                ('part', ctypes.c_void_p), ('part3', ctypes.c_void_p), ('splits', ctypes.c_int), ('pad', ctypes.c_int)]
 
 
 class ConvArgs(ctypes.Structure):
@@ -82,6 +89,8 @@ _SIGS = {
     'wc_wino_vsplit_f16x3': [ctypes.POINTER(ConvArgs), _I, _P, _P, _L, _P],
     'wc_conv3x3_wino_f16x3_vp': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P, _L, _P],
     'wc_conv3x3_wino_tile_n': [_I],
+    'wc_conv3x3_wino_gnb_splits': [_I, _I, _I],
+    'wc_conv3x3_wino_f16x3_gnb': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, ctypes.POINTER(GnbEpi), _P],
     'wc_pack_wino': [_P, _I, _I, _I, _P, _L, _P, _P],
     'wc_pack_wino_raw': [_P, _P, _I, _I, _I, _I, _P, _L, _P, _P],
     'wc_pack_wino_batch': [_P, _I, _I, _I, _P],

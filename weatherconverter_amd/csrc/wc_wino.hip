@@ -94,7 +94,23 @@ struct WDev {
     int tiles_x, tiles_y, ntiles_n;
     const unsigned char* vpre;  // PRO 3: segment 0 pre-transformed and split (wino_vsplit_kernel layout)
     long vimg;                  // PRO 3: bytes of one image's V
+    // PRO 0 (a training data gradient dz of a GroupNorm(+SiLU) input x): the GroupNorm backward's
+    // per-channel sums of the written values (wc_conv3x3_wino_f16x3_gnb), gnb_reduce_kernel's
+    // (sum dy, sum dy xhat) [, sum xhat] with xhat = x sc0 + sh0, dy = dz SiLU'(gamma xhat + beta)
+    const float* gb_x;
+    int gb_ldx, gb_silu;
+    const float* gb_sc0;
+    const float* gb_sh0;
+    const float* gb_gamma;
+    const float* gb_beta;
+    float* gb_part;   // [B][splits][N][2], split = (tile, wave row)
+    float* gb_part3;  // [B][splits][N] or NULL
 };
+
+WC_DEVICE float wino_silu_grad(float y) {  // d/dy [y sigmoid(y)], as wc_backward.hip's silu_grad
+    const float s = 1.0f / (1.0f + __expf(-y));
+    return s * (1.0f + y * (1.0f - s));
+}
 
 // MB: 32-tile MFMA row blocks per wave (4 image rows x 8 tiles each): 2 (two waves per SIMD) or 4 (one
 // wave per SIMD, 512 registers: each weight fragment feeds twice the MFMAs, halving the vector-memory
@@ -614,6 +630,7 @@ void conv3x3_wino_kernel(WDev p) {
     if (nok && p.temb) eadd += p.temb[b * p.temb_ld + n];
     const float emul = nok ? p.wsinv[n] * ainv : 0.f;
     float vmax = 0.f;
+    float gs1 = 0.f, gs2 = 0.f, gs3 = 0.f;  // GroupNorm-backward sums of this lane's channel (PRO 0)
     // accumulator register r of block mb is MFMA row (r & 3) + 8 (r >> 2) + 4 half: the four registers of
     // a group j = r >> 2 are four consecutive tiles of one image row.  One per-lane byte offset per
     // (mb, j) and the tile steps (r & 3) x 2 pixels as wave-uniform scalar offsets: no per-store VALU.
@@ -650,6 +667,37 @@ void conv3x3_wino_kernel(WDev p) {
             acc[1][mb][r] = yb;
             vmax = fmaxf(vmax, fmaxf(fabsf(ya), fabsf(yb)));
         }
+        if constexpr (PRO == 0) {
+            if (p.gb_part) {  // the same 32 values against x at the same pixels (loads issued first)
+                const __amdgpu_buffer_rsrc_t srd_x = make_srd(p.gb_x + img_px * p.gb_ldx);
+                const int so_x = 4 * p.gb_ldx;
+                float xv[2][16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int j = r >> 2;
+                    const int row = 8 * j + 4 * half;
+                    const int pix = (y0 + 4 * MB * wm + 4 * mb + wg_row(row)) * p.W + x0 + 2 * wg_tile(row);
+                    const unsigned vx = nok ? (unsigned)(pix * p.gb_ldx + n) * 4u : OOB;
+                    xv[0][r] = bload_f1s(srd_x, vx, (r & 3) * 2 * so_x);
+                    xv[1][r] = bload_f1s(srd_x, vx, ((r & 3) * 2 + 1) * so_x);
+                }
+                const long bn = (long)b * p.N + (nok ? n : 0);
+                const float sc0 = p.gb_sc0[bn], sh0 = p.gb_sh0[bn];
+                const float ga = p.gb_gamma ? p.gb_gamma[nok ? n : 0] : 1.f;
+                const float be = p.gb_beta ? p.gb_beta[nok ? n : 0] : 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const float xh = xv[e][r] * sc0 + sh0;
+                        float d = acc[e][mb][r];
+                        if (p.gb_silu) d *= wino_silu_grad(ga * xh + be);
+                        gs1 += d;
+                        gs2 += d * xh;
+                        gs3 += xh;
+                    }
+            }
+        }
         if (nok) {
             if constexpr (WC_ABL & 128) {  // ablation: no output stores (one store only if a sum hits a magic value)
                 float sum = 0.f;
@@ -667,6 +715,20 @@ void conv3x3_wino_kernel(WDev p) {
     }
     if (!nok) vmax = 0.f;
     if (p.absmax) block_absmax_atomic(p.absmax, b, vmax);
+    if constexpr (PRO == 0) {
+        if (p.gb_part) {  // the two lanes of a channel (rows 0-3 / 4-7 of each block) add, lane half 0 writes
+            gs1 += __shfl_xor(gs1, 32, 64);
+            gs2 += __shfl_xor(gs2, 32, 64);
+            gs3 += __shfl_xor(gs3, 32, 64);
+            const int splits = p.tiles_y * p.tiles_x * T::WAVES_M;
+            const long sp = (long)b * splits + ((long)tyi * p.tiles_x + txi) * T::WAVES_M + wm;
+            if (nok && half == 0) {
+                p.gb_part[(sp * p.N + n) * 2] = gs1;
+                p.gb_part[(sp * p.N + n) * 2 + 1] = gs2;
+                if (p.gb_part3) p.gb_part3[sp * p.N + n] = gs3;
+            }
+        }
+    }
     if (p.gn_part) {
         // this wave's 64-pixel blocks (4 rows x 16 px each), numbered by pixel position alone (image 4-row
         // block r4 -> ((r4 / 2) * tiles_x + tile x) * 2 + r4 % 2), so every tile height / wave form writes the
@@ -878,6 +940,31 @@ extern "C" int wc_conv3x3_wino_f16x3(const wc_conv_args* a, const void* w, int64
     if (pro == 0) return BN == 64 ? launch_wino<16, 64, 0, false>(d, s) : launch_wino<8, 128, 0, false>(d, s);
     if (BN == 64) return res ? launch_wino<16, 64, 2, true>(d, s) : launch_wino<16, 64, 2, false>(d, s);
     return res ? launch_wino<8, 128, 2, true>(d, s) : launch_wino<8, 128, 2, false>(d, s);
+}
+
+extern "C" int wc_conv3x3_wino_gnb_splits(int N, int H, int W) {
+    const int BN = wc_conv3x3_wino_tile_n(N), TH = BN == 64 ? 16 : 8;
+    if (N <= 0 || H <= 0 || W <= 0 || H % TH || W % 16) return -1;
+    const int waves_m = 4 / (BN / 32);
+    return (H / TH) * (W / 16) * waves_m;
+}
+
+extern "C" int wc_conv3x3_wino_f16x3_gnb(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
+                                         const float* w_inv_scale, const float* a_bound, const wc_gnb_epi* g,
+                                         void* stream) {
+    WDev d;
+    int pro, BN;
+    bool res;
+    const int st = wino_setup(a, w, w_bytes, a_exp, w_inv_scale, a_bound, d, pro, res, BN);
+    if (st != WC_OK) return st;
+    if (pro != 0 || !g || !g->x || !g->sc0 || !g->sh0 || !g->part) return WC_E_ARG;
+    if (g->ldx < d.N || g->splits != wc_conv3x3_wino_gnb_splits(d.N, d.H, d.W)) return WC_E_SHAPE;
+    if ((long)d.B * d.H * d.W * g->ldx * 4 >= (1L << 31)) return WC_E_SHAPE;
+    d.gb_x = g->x; d.gb_ldx = g->ldx; d.gb_silu = g->silu ? 1 : 0;
+    d.gb_sc0 = g->sc0; d.gb_sh0 = g->sh0; d.gb_gamma = g->gamma; d.gb_beta = g->beta;
+    d.gb_part = g->part; d.gb_part3 = g->part3;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return BN == 64 ? launch_wino<16, 64, 0, false>(d, s) : launch_wino<8, 128, 0, false>(d, s);
 }
 
 extern "C" int wc_wino_vsplit_bytes(int B, int C, int H, int W, int64_t* bytes) {

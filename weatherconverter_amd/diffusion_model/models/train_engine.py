@@ -756,9 +756,18 @@ class TrainEngine:
                     self._pgrad(rp['conv2'].weight), (co * 9, 9, 1), dw1=self._pgrad(rp['resc'].weight), s1=ci,
                     f3=K.F3Bounds(bY, K.f16x3_a_exp(*rp['gb2'], H * W * co // 8), None, bXf) if f3Y else None)
         dz2 = View.full(self._new(B, H, W, co))
+        g2 = rp['gn2']
+        ga2, be2 = g2.weight.detach().float(), g2.bias.detach().float()
+        # dh's per-(image, channel) sums (conv1's bias / time-embedding gradients) in closed form from the
+        # GN backward's own sums (WC_TRAIN_DH_SUMS=0: a channel_sums pass over dh)
+        dh_sums = os.environ.get('WC_TRAIN_DH_SUMS', '1') != '0'
+        pre2 = None
         if f3Y:
             if rp.has('wn_2T') and K.wino_eligible([Seg(gY, TAPS3)], co, H, W):
-                K.conv3x3_wino([Seg(gY, TAPS3)], rp['wn_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
+                # GN2's backward sums of dz2 formed in the data-gradient conv's epilogue (no pass over dz2)
+                if K.gnb_epilogue_enabled():
+                    pre2 = K.GnbSums.make(h, st2[2], st2[3], ga2, be2, True, dx_sums=dh_sums)
+                K.conv3x3_wino([Seg(gY, TAPS3)], rp['wn_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY, gnb=pre2)
             else:
                 K.conv3x3_f16x3([Seg(gY, TAPS3)], rp['f3_2T'], None, dz2, Hm=H, Wm=W, a_exp=60, a_bound=bY)
             gX, ow = self._grad_w(X)
@@ -772,14 +781,10 @@ class TrainEngine:
             self._conv([Seg(gY, TAPS3)], rp['pk2T'], None, dz2, H, W)
             gX, ow = self._grad_w(X)
             self._conv([Seg(gY, TAPS1)], rp['pkrT'], None, gX, H, W, res=None if ow else gX, absmax=bX)
-        g2 = rp['gn2']
         dh = View.full(self._new(B, H, W, co))
         bdh = self._zrow(B) if self.f3d else None
-        # dh's per-(image, channel) sums (conv1's bias / time-embedding gradients) in closed form from the
-        # GN backward's own sums (WC_TRAIN_DH_SUMS=0: a channel_sums pass over dh)
-        sums = K.gn_backward(dz2, h, st2[2], st2[3], g2.weight.detach().float(), g2.bias.detach().float(), True, dh,
-                             dgamma=self._pgrad(g2.weight), dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh,
-                             dx_sums=os.environ.get('WC_TRAIN_DH_SUMS', '1') != '0')
+        sums = K.gn_backward(dz2, h, st2[2], st2[3], ga2, be2, True, dh, dgamma=self._pgrad(g2.weight),
+                             dbeta=self._pgrad(g2.bias), accumulate=False, absmax=bdh, dx_sums=dh_sums, pre=pre2)
         if sums is None:
             sums = K.channel_sums(dh)
         K.bsum(sums, 0, self._pgrad(rp['conv1'].bias), accumulate=True)
@@ -789,16 +794,20 @@ class TrainEngine:
         self._wgrad(dh, [Seg(X, TAPS3, scale=st1[0], shift=st1[1], silu=True)], self._pgrad(rp['conv1'].weight),
                     (ci * 9, 9, 1), f3=K.F3Bounds(bh, K.f16x3_a_exp(*rp['gb1'], H * W * ci // 8)) if f3h else None)
         dz1 = View.full(self._new(B, H, W, ci))
+        g1 = rp['gn1']
+        ga1, be1 = g1.weight.detach().float(), g1.bias.detach().float()
+        pre1 = None
         if f3h:
             if rp.has('wn_1T') and K.wino_eligible([Seg(dh, TAPS3)], ci, H, W):
-                K.conv3x3_wino([Seg(dh, TAPS3)], rp['wn_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
+                if K.gnb_epilogue_enabled():
+                    pre1 = K.GnbSums.make(X, st1[2], st1[3], ga1, be1, True)
+                K.conv3x3_wino([Seg(dh, TAPS3)], rp['wn_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh, gnb=pre1)
             else:
                 K.conv3x3_f16x3([Seg(dh, TAPS3)], rp['f3_1T'], None, dz1, Hm=H, Wm=W, a_exp=60, a_bound=bh)
         else:
             self._conv([Seg(dh, TAPS3)], rp['pk1T'], None, dz1, H, W)
-        g1 = rp['gn1']
-        K.gn_backward(dz1, X, st1[2], st1[3], g1.weight.detach().float(), g1.bias.detach().float(), True, gX,
-                      dgamma=self._pgrad(g1.weight), dbeta=self._pgrad(g1.bias), accumulate=True, absmax=bX)
+        K.gn_backward(dz1, X, st1[2], st1[3], ga1, be1, True, gX, dgamma=self._pgrad(g1.weight),
+                      dbeta=self._pgrad(g1.bias), accumulate=True, absmax=bX, pre=pre1)
 
     def _bwd_attn(self, rec, gout):
         _, Ypre, Yout, qkv, o, lse, st, ap = rec

@@ -694,10 +694,50 @@ def wino_eligible(segs: Sequence[Seg], N: int, Hm: int, Wm: int) -> bool:
     return s0.silu and (len(segs) == 1 or (segs[1].view.C % 16 == 0 and TH == 8))
 
 
+@dataclass
+class GnbSums:
+    """The GroupNorm(+SiLU) backward's per-channel sums of a data gradient dz, formed by the epilogue of
+    the Winograd conv that writes dz (conv3x3_wino(..., gnb=)) instead of a wc_gn_bwd_reduce pass over
+    it: part [B][splits][C][2] = (sum dy, sum dy*xhat), part3 [B][splits][C] = sum xhat (dx_sums), one
+    split per (image, conv tile, wave row).  gn_backward(..., pre=) takes them."""
+    x: 'View'
+    sc0: torch.Tensor
+    sh0: torch.Tensor
+    gamma: Optional[torch.Tensor]
+    beta: Optional[torch.Tensor]
+    silu: bool
+    part: torch.Tensor
+    part3: Optional[torch.Tensor]
+    splits: int
+
+    @staticmethod
+    def make(x: 'View', sc0: torch.Tensor, sh0: torch.Tensor, gamma: Optional[torch.Tensor],
+             beta: Optional[torch.Tensor], silu: bool, dx_sums: bool = False) -> Optional['GnbSums']:
+        """Buffers for the sums of a dz shaped like x (None where the Winograd tiling does not cover x)."""
+        sp = _native.load().wc_conv3x3_wino_gnb_splits(x.C, x.H, x.W)
+        if sp <= 0:
+            return None
+        dev = x.t.device
+        return GnbSums(x, sc0, sh0, gamma, beta, silu,
+                       torch.empty(x.B * sp * x.C * 2, dtype=torch.float32, device=dev),
+                       torch.empty(x.B * sp * x.C, dtype=torch.float32, device=dev) if dx_sums else None, sp)
+
+    def epi(self) -> '_native.GnbEpi':
+        x = self.x
+        return _native.GnbEpi(x.ptr, x.ldc, int(self.silu), self.sc0.data_ptr(), self.sh0.data_ptr(), _ptr(self.gamma),
+                              _ptr(self.beta), self.part.data_ptr(), _ptr(self.part3), self.splits, 0)
+
+
+def gnb_epilogue_enabled() -> bool:
+    """The training backward forms the GroupNorm-backward sums in the data-gradient conv's epilogue
+    (WC_TRAIN_GNB_EPI=0: a wc_gn_bwd_reduce pass over dz, A/B)."""
+    return os.environ.get('WC_TRAIN_GNB_EPI', '1') != '0'
+
+
 def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor], out: View, *, Hm: int, Wm: int,
                  a_exp: int, a_bound: Optional[torch.Tensor] = None, temb: Optional[torch.Tensor] = None,
                  temb_ld: int = 0, res: Optional[View] = None, absmax: Optional[torch.Tensor] = None,
-                 gn: Optional[GnPart] = None):
+                 gn: Optional[GnPart] = None, gnb: Optional[GnbSums] = None):
     """The ResBlock 3x3 conv through the Winograd F(2,3)-along-x kernel (wc_conv3x3_wino_f16x3): segment 0
     with the GN+SiLU prologue (a_exp = f16x3_a_exp of that GroupNorm) and an optional fused 1x1
     residual under the per-image bound a_bound, or one raw segment under a_bound (a_exp = 60: the
@@ -712,6 +752,18 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
     TH, BN = wino_tile(w.N)
     prof = _measuring()
     ab = _ptr(a_bound) if (len(segs) == 2 or raw) else None
+    if gnb is not None:
+        # the data gradient dz of a GroupNorm(+SiLU): its backward sums formed in the epilogue
+        xv = gnb.x
+        _req(raw and len(segs) == 1 and xv.B == segs[0].view.B and xv.H == Hm and xv.W == Wm and xv.C == w.N
+             and gnb.sc0.numel() == xv.B * w.N, 'GN-backward sums: the raw data-gradient conv of x')
+        e = gnb.epi()
+        _timed(f'conv3x3_wino_kernel<{TH}, {BN}, 0, false>', 'wc_conv3x3_wino_f16x3_gnb',
+               _flops(segs, Hm, Wm, w.N) if prof else 0.0, ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2,
+               int(a_exp), w.wsinv.data_ptr(), ab, ctypes.byref(e), _stream(),
+               nbytes=(_abytes(segs, w.N, Hm * Wm, res) + 4.0 * xv.B * Hm * Wm * w.N) if prof else 0.0,
+               mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
+        return
     if not raw and wino_vsplit_wanted(segs, w.N, Hm, Wm):
         # segment 0 GN+SiLU'd, transformed and split once (not once per output-channel tile), then the
         # conv copies its halo planes by LDS-DMA (wc_wino_vsplit_f16x3 + wc_conv3x3_wino_f16x3_vp)
@@ -1603,28 +1655,35 @@ def bsum_flush():
 def gn_backward(dz: View, x: View, sc0: torch.Tensor, sh0: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
                 silu: bool, dx: View, *, dgamma: Optional[torch.Tensor] = None, dbeta: Optional[torch.Tensor] = None,
                 accumulate: bool = True, groups: int = 8, absmax: Optional[torch.Tensor] = None,
-                dx_sums: bool = False) -> Optional[torch.Tensor]:
+                dx_sums: bool = False, pre: Optional[GnbSums] = None) -> Optional[torch.Tensor]:
     """Backward of SiLU(GroupNorm(x)) (silu) or GroupNorm(x): dx (+)= d/dx given dz = d/d output;
     dgamma / dbeta (+)= their gradients.  absmax: optional float32[B] raised to the max |dx| written
     per image.  dx_sums (accumulate off): also return float32 [B][C][2] whose [..., 0] is each image's
     per-channel sum of dx (channel_sums(dx)'s layout, from the reduce's sums in closed form instead of
-    a pass over dx)."""
+    a pass over dx).  pre: the sums of dz already formed by the epilogue of the conv that wrote it
+    (GnbSums for this x, sc0, sh0, gamma, beta, silu; part3 present when dx_sums): no reduce pass."""
     for v in (dz, x, dx):
         v.check()
     B, HW, C = x.B, x.H * x.W, x.C
     _req(dz.C == C and dx.C == C and dz.B == B and dx.B == B, 'GN backward view shapes')
     _req(not (dx_sums and accumulate), 'dx_sums needs accumulate=False (the sums are of the written values)')
     lib = _native.load()
-    splits = lib.wc_gn_bwd_splits(B, HW)
     dev = x.t.device
-    part = torch.empty(B * splits * C * 2, dtype=torch.float32, device=dev)
-    part3 = torch.empty(B * splits * C, dtype=torch.float32, device=dev) if dx_sums else None
     dsum = torch.empty((B, C, 2), dtype=torch.float32, device=dev) if dx_sums else None
     sums = torch.empty((B, C, 2), dtype=torch.float32, device=dev)
     coef = torch.empty((B, C, 4), dtype=torch.float32, device=dev)
     s = _stream()
-    _timed('gnb_reduce_kernel', 'wc_gn_bwd_reduce', 8.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc, sc0.data_ptr(),
-           sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), B, HW, C, splits, part.data_ptr(), _ptr(part3), s)
+    if pre is not None:
+        _req(pre.x.ptr == x.ptr and pre.x.C == C and pre.silu == bool(silu) and pre.sc0 is sc0 and pre.sh0 is sh0
+             and (pre.part3 is not None or not dx_sums), 'GN backward: sums formed for another GroupNorm')
+        splits, part, part3 = pre.splits, pre.part, (pre.part3 if dx_sums else None)
+    else:
+        splits = lib.wc_gn_bwd_splits(B, HW)
+        part = torch.empty(B * splits * C * 2, dtype=torch.float32, device=dev)
+        part3 = torch.empty(B * splits * C, dtype=torch.float32, device=dev) if dx_sums else None
+        _timed('gnb_reduce_kernel', 'wc_gn_bwd_reduce', 8.0 * B * HW * C, dz.ptr, dz.ldc, x.ptr, x.ldc,
+               sc0.data_ptr(), sh0.data_ptr(), _ptr(gamma), _ptr(beta), int(silu), B, HW, C, splits, part.data_ptr(),
+               _ptr(part3), s)
     _native.call('wc_gn_bwd_finalize', part.data_ptr(), B, splits, C, groups, HW, sc0.data_ptr(), _ptr(gamma),
                  sums.data_ptr(), coef.data_ptr(), _ptr(part3), _ptr(dsum), s)
     if dbeta is not None:

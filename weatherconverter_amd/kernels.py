@@ -752,6 +752,7 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
     TH, BN = wino_tile(w.N)
     prof = _measuring()
     ab = _ptr(a_bound) if (len(segs) == 2 or raw) else None
+    wbytes = float(w.data.numel() * w.data.element_size())  # the packed filter: read at least once as well
     if gnb is not None:
         # the data gradient dz of a GroupNorm(+SiLU): its backward sums formed in the epilogue
         xv = gnb.x
@@ -761,7 +762,7 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
         _timed(f'conv3x3_wino_kernel<{TH}, {BN}, 0, false>', 'wc_conv3x3_wino_f16x3_gnb',
                _flops(segs, Hm, Wm, w.N) if prof else 0.0, ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2,
                int(a_exp), w.wsinv.data_ptr(), ab, ctypes.byref(e), _stream(),
-               nbytes=(_abytes(segs, w.N, Hm * Wm, res) + 4.0 * xv.B * Hm * Wm * w.N) if prof else 0.0,
+               nbytes=(_abytes(segs, w.N, Hm * Wm, res) + 4.0 * xv.B * Hm * Wm * w.N + wbytes) if prof else 0.0,
                mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
         return
     if not raw and wino_vsplit_wanted(segs, w.N, Hm, Wm):
@@ -777,13 +778,13 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
                'wc_conv3x3_wino_f16x3_vp', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
                ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(), ab,
                vbuf.data_ptr(), nb.value, _stream(),
-               nbytes=(nb.value + _abytes(segs[1:], w.N, Hm * Wm, res, B=v.B)) if prof else 0.0,
+               nbytes=(nb.value + _abytes(segs[1:], w.N, Hm * Wm, res, B=v.B) + wbytes) if prof else 0.0,
                mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
         return
     _timed(f'conv3x3_wino_kernel<{TH}, {BN}, {0 if raw else 2}, {"true" if len(segs) == 2 else "false"}>',
            'wc_conv3x3_wino_f16x3', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
            ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(),
-           ab, _stream(), nbytes=_abytes(segs, w.N, Hm * Wm, res),
+           ab, _stream(), nbytes=(_abytes(segs, w.N, Hm * Wm, res) + wbytes) if prof else 0.0,
            mfma=wino_mfma_flops(segs, Hm, Wm, w.N))
 
 

@@ -699,7 +699,9 @@ def main():
             if not args.no_roofline:
                 # the dominant kernel as the timed graph launches it: one image group
                 g = runner.split if runner is not None else 1
-                result['roofline'] = roofline_leg(model, x[:B // g], ts[500:501], groups=g)
+                from weatherconverter_amd.kernels import wino_vp_wide
+                with wino_vp_wide(g > 1):  # the same instantiations as the timed graph (its groups' form)
+                    result['roofline'] = roofline_leg(model, x[:B // g], ts[500:501], groups=g)
             if not args.no_parity and args.size == 256:
                 result['parity'] = parity_leg(model, dev)
     if rank == 0:

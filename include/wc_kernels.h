@@ -164,6 +164,12 @@ int wc_wino_vsplit_f16x3(const wc_conv_args* args, int a_exp, const float* a_bou
 int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
                              const float* w_inv_scale, const float* a_bound, const void* vpre, int64_t v_bytes,
                              void* stream);
+/* wc_conv3x3_wino_f16x3_vp with 8-wave workgroups of 256 output channels (N % 256 == 0; same results bit
+ * for bit): each halo plane copy feeds twice the MFMAs.  Slower alone, faster beside a concurrent
+ * stream of launches (the two-group sampling graph picks it). */
+int wc_conv3x3_wino_f16x3_vp8(const wc_conv_args* args, const void* w, int64_t w_bytes, int a_exp,
+                              const float* w_inv_scale, const float* a_bound, const void* vpre, int64_t v_bytes,
+                              void* stream);
 /* wc_conv3x3_wino_f16x3 on one raw segment (a training data gradient dz, under a_bound) whose epilogue
  * also forms the GroupNorm(+SiLU) backward's sums of the values it writes (the pass wc_gn_bwd_reduce
  * makes over dz, without re-reading dz): with xhat = x*sc0 + sh0 at the same pixel and channel and

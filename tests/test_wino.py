@@ -272,9 +272,16 @@ def test_conv3x3_wino_presplit_bit_identical(B, H, W, Ci, Co, Cr):
     """The pre-split form (wc_wino_vsplit_f16x3 once per input, then wc_conv3x3_wino_f16x3_vp copying the
     halo planes by LDS-DMA) against the in-conv prologue: bit-identical output, absmax and GroupNorm
     partials (the same arithmetic in a separate pass); 64- and 128-channel tiles, residual interleaved
-    and as a tail, per-image residual exponents."""
+    and as a tail, per-image residual exponents.  N % 256 == 0: also the 8-wave 256-channel form
+    (wc_conv3x3_wino_f16x3_vp8, kernels.wino_vp_wide)."""
+    from weatherconverter_amd import kernels as K
     _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0),
                    lambda K, v: K.set_wino_vsplit(v))
+    if Co % 256 == 0:
+        with K.wino_vp_wide():
+            names = _compare_forms(B, H, W, Ci, Co, Cr, False, lambda K, m: K.set_wino_vsplit(1 if m else 0),
+                                   lambda K, v: K.set_wino_vsplit(v))
+        assert names[1].startswith('conv3x3_wino_kernel<8, 256, 3'), names
 
 
 @pytest.mark.gpu
@@ -332,6 +339,7 @@ def _compare_forms(B, H, W, Ci, Co, Cr, raw, select, restore):
         restore(K, prev)
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b), ((a - b).abs().max(), names)
+    return names
 
 
 @pytest.mark.gpu

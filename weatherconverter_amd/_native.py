@@ -17,7 +17,7 @@ MAX_TAPS = 16
 NOISE_NONE, NOISE_TENSOR, NOISE_PHILOX = 0, 1, 2
 
 EXPORTS = [
-    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_conv3x3_wino_gnb_splits', 'wc_conv3x3_wino_f16x3_gnb', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
+    'wc_conv_igemm', 'wc_conv3x3_x6', 'wc_conv3x3_f16x3', 'wc_conv3x3_wino_f16x3', 'wc_conv3x3_wino_tile_n', 'wc_wino_vsplit_bytes', 'wc_wino_vsplit_f16x3', 'wc_conv3x3_wino_f16x3_vp', 'wc_conv3x3_wino_f16x3_vp8', 'wc_conv3x3_wino_gnb_splits', 'wc_conv3x3_wino_f16x3_gnb', 'wc_pack_wino', 'wc_pack_wino_raw', 'wc_pack_wino_batch', 'wc_conv3x3_x6_tile_n', 'wc_conv_igemm_x6',
     'wc_conv_igemm_f16x3', 'wc_conv4x4s2_f16x3', 'wc_convtr4x4s2_f16x3', 'wc_conv_igemm_f16x3_qkv', 'wc_split_f16x3_tiled', 'wc_attention_fwd_f16x3_presplit_a3', 'wc_proj_f16x3', 'wc_proj_f16x3_qkv', 'wc_proj_set_tile', 'wc_attention_fwd_f16x3_presplit',
     'wc_gn_num_splits',
     'wc_gn_stats', 'wc_gn_finalize', 'wc_gn_finalize_bound', 'wc_gn_partials', 'wc_gn_finalize_part', 'wc_attention_fwd', 'wc_attention_fwd_x6', 'wc_attention_fwd_f16x3',
@@ -88,6 +88,7 @@ _SIGS = {
     'wc_wino_vsplit_bytes': [_I, _I, _I, _I, _P],
     'wc_wino_vsplit_f16x3': [ctypes.POINTER(ConvArgs), _I, _P, _P, _L, _P],
     'wc_conv3x3_wino_f16x3_vp': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P, _L, _P],
+    'wc_conv3x3_wino_f16x3_vp8': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, _P, _L, _P],
     'wc_conv3x3_wino_tile_n': [_I],
     'wc_conv3x3_wino_gnb_splits': [_I, _I, _I],
     'wc_conv3x3_wino_f16x3_gnb': [ctypes.POINTER(ConvArgs), _P, _L, _I, _P, _P, ctypes.POINTER(GnbEpi), _P],

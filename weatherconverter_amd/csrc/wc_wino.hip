@@ -1024,6 +1024,27 @@ extern "C" int wc_conv3x3_wino_f16x3_vp(const wc_conv_args* a, const void* w, in
     return res ? launch_wino<8, 128, 3, true>(d, s) : launch_wino<8, 128, 3, false>(d, s);
 }
 
+// The same with 8-wave workgroups of 256 output channels (N % 256 == 0): each halo plane copy feeds
+// twice the MFMAs, one workgroup per CU.  Measured slower alone at every batch (B = 2..16: +3..17 %)
+// but faster beside a concurrent launch stream (the two-group sampling graph: 23.36-23.37 vs
+// 23.52-23.53 ms/step), so the caller picks it (profiles/r06_wino_vp8_ab.txt).
+extern "C" int wc_conv3x3_wino_f16x3_vp8(const wc_conv_args* a, const void* w, int64_t w_bytes, int a_exp,
+                                         const float* w_inv_scale, const float* a_bound, const void* vpre,
+                                         int64_t v_bytes, void* stream) {
+    WDev d;
+    int pro, BN;
+    bool res;
+    const int st = wino_setup(a, w, w_bytes, a_exp, w_inv_scale, a_bound, d, pro, res, BN);
+    if (st != WC_OK) return st;
+    if (pro != 2 || !vpre || (reinterpret_cast<uintptr_t>(vpre) & 15)) return WC_E_ARG;
+    if (BN != 128 || d.N % 256) return WC_E_SHAPE;
+    d.vimg = wino_vimg(d.C0, d.H, d.W);
+    if (v_bytes != (int64_t)d.B * d.vimg || d.vimg >= (1L << 31)) return WC_E_SHAPE;
+    d.vpre = reinterpret_cast<const unsigned char*>(vpre);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return res ? launch_wino<8, 256, 3, true, 2, 8>(d, s) : launch_wino<8, 256, 3, false, 2, 8>(d, s);
+}
+
 // ---- device re-pack for wc_conv3x3_wino_f16x3 (training: the weights change every step) ----
 // One workgroup per output channel n (of the N-tile-padded count): max |U|, |w_res| over the row, the
 // power-of-two scale 2^sW with max * 2^sW <= 2^14 (sW from the exponent: exact, no log2), then every

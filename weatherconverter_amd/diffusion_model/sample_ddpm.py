@@ -90,15 +90,19 @@ class _GraphStep:
             split = int(os.environ.get('WC_GRAPH_SPLIT', '2' if B >= 16 and B % 2 == 0 else '1'))
         self.split = split if split > 1 and B % split == 0 else 1
         self.streams = [torch.cuda.Stream(device=x.device) for _ in range(self.split - 1)]
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):  # warm the allocator / engine pack outside capture
+        # concurrent groups: the pre-split convs with N % 256 == 0 on 8-wave workgroups, the form that
+        # measured faster beside the other group's launches (slower alone: kernels.wino_vp_wide)
+        from ..kernels import wino_vp_wide
+        with wino_vp_wide(self.split > 1):
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm the allocator / engine pack outside capture
+                    self.eps = self._forward()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
                 self.eps = self._forward()
-        torch.cuda.current_stream().wait_stream(s)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.eps = self._forward()
 
     def _forward(self) -> torch.Tensor:
         if self.split == 1:

@@ -5,6 +5,7 @@ All launches go on the current torch stream (so torch ops, HIP graphs captured t
 ever reaches a kernel; the C layer re-validates and returns a status that is turned into a
 RuntimeError.
 """
+import contextlib
 import ctypes
 import functools
 import os
@@ -774,8 +775,9 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
         vbuf = torch.empty(nb.value, dtype=torch.uint8, device=v.t.device)
         _timed('wino_vsplit_kernel', 'wc_wino_vsplit_f16x3', 0.0, ctypes.byref(a), int(a_exp), ab,
                vbuf.data_ptr(), nb.value, _stream(), nbytes=4.0 * v.B * Hm * Wm * v.C + nb.value)
-        _timed(f'conv3x3_wino_kernel<{TH}, {BN}, 3, {"true" if len(segs) == 2 else "false"}>',
-               'wc_conv3x3_wino_f16x3_vp', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
+        wide = _WINO_VP_WIDE and BN == 128 and w.N % 256 == 0
+        _timed(f'conv3x3_wino_kernel<{TH}, {256 if wide else BN}, 3, {"true" if len(segs) == 2 else "false"}>',
+               'wc_conv3x3_wino_f16x3_vp8' if wide else 'wc_conv3x3_wino_f16x3_vp', _flops(segs, Hm, Wm, w.N) if prof else 0.0,
                ctypes.byref(a), w.data.data_ptr(), w.data.numel() * 2, int(a_exp), w.wsinv.data_ptr(), ab,
                vbuf.data_ptr(), nb.value, _stream(),
                nbytes=(nb.value + _abytes(segs[1:], w.N, Hm * Wm, res, B=v.B) + wbytes) if prof else 0.0,
@@ -792,6 +794,24 @@ def conv3x3_wino(segs: Sequence[Seg], w: X6Weight, bias: Optional[torch.Tensor],
 # output tiles (the redundancy the in-conv prologue pays: every output tile re-transforms the halo);
 # 0 = never.  WC_WINO_VP sets it (A/B runs); set_wino_vsplit at run time.
 _WINO_VP_MIN_TILES = int(os.environ.get('WC_WINO_VP', '4'))
+
+
+# The pre-split convs with N % 256 == 0 on 8-wave 256-channel workgroups (wc_conv3x3_wino_f16x3_vp8):
+# set while a forward is captured beside another concurrent one (the two-group sampling graph), where
+# that form measured faster; alone the 4-wave form is (profiles/r06_wino_vp8_ab.txt).
+_WINO_VP_WIDE = False
+
+
+@contextlib.contextmanager
+def wino_vp_wide(on: bool = True):
+    """Inside the block the pre-split Winograd convs with N % 256 == 0 take the 8-wave form
+    (WC_WINO_VP8=0: never, A/B runs)."""
+    global _WINO_VP_WIDE
+    prev, _WINO_VP_WIDE = _WINO_VP_WIDE, bool(on) and os.environ.get('WC_WINO_VP8', '1') != '0'
+    try:
+        yield
+    finally:
+        _WINO_VP_WIDE = prev
 
 
 def set_wino_vsplit(min_tiles: int) -> int:

@@ -65,6 +65,9 @@ def parse(argv=None):
     ap.add_argument('--split', type=int, default=None,
                     help='image groups per GPU run concurrently on their own streams inside the graph '
                          '(default: _GraphStep\'s, 2 at >= 16 images per GPU; WC_GRAPH_SPLIT)')
+    ap.add_argument('--vp-wide', type=int, default=0,
+                    help='eager runs (--graph 0): the pre-split convs in the form the two-group graph uses '
+                         '(kernels.wino_vp_wide), so a PMC pass at --batch B/2 sees the timed instantiations')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=None, help='CPU baseline batch (default: --batch)')
@@ -600,7 +603,12 @@ def main():
     with torch.no_grad():
         x = kernels.philox_normal(shape, dev, args.seed, sample0=sample0, step=T)
         runner = _GraphStep(model, x, split=args.split) if args.graph else None
-        fwd = runner if runner is not None else (lambda xx, tt: model(xx, tt))
+        if runner is not None:
+            fwd = runner
+        else:  # eager (PMC passes): --vp-wide 1 launches the kernel forms the two-group graph captures
+            def fwd(xx, tt):
+                with kernels.wino_vp_wide(bool(args.vp_wide)):
+                    return model(xx, tt)
         nxt = torch.empty_like(x)
         # untimed warmup: W steps from a scratch copy
         xw = x.clone()

@@ -433,6 +433,48 @@ def test_split_attention_lse_matches_float64(precision, C, heads, N):
     assert rel_l2(dqkv.cpu()[:N], q_.grad.reshape(B * N, 3 * C)[:N]) < 1e-5
 
 
+@pytest.mark.parametrize('C,heads,N', [(768, 4, 64), (768, 4, 1024), (512, 4, 160)])
+def test_attention_backward_bf16_line_vs_float64(C, heads, N):
+    """The bf16 training line's attention backward (libwc_kernels_bf16.so, one bf16 piece per operand):
+    at D = 192 the whole head width runs in one workgroup (rows as pieces, no output-dim split:
+    attn_bwd6_dq_kernel<192, true, 1> and the V-rows-in-LDS dK / dV at DS = 1), at D = 128 the generic
+    pair; against float64 autograd within bf16 operand rounding (2^-9 relative per operand)."""
+    from weatherconverter_amd import _native
+    from weatherconverter_amd import kernels as K
+    g = _gen(16)
+    B, d = 2, C // heads
+    qkv = torch.randn((B * N, 3 * C), generator=g)
+    do = torch.randn((B * N, C), generator=g)
+    do[:N] *= 1e-3
+    exps = (10, 10, 10)
+    with _native.variant('bf16'):
+        o = torch.empty((B * N, C), device='cuda')
+        lse = torch.empty((B, heads, N), device='cuda')
+        K.attention_fwd_lse(qkv.cuda(), o, lse, B, N, C, heads, precision='f16x3', exps=exps)
+        dqkv = torch.empty((B * N, 3 * C), device='cuda')
+        dob = do.abs().reshape(B, -1).amax(1).cuda()
+        amx = torch.zeros(B, device='cuda')
+        prof = K.profile_conv(True)
+        raised = K.attention_bwd(qkv.cuda(), o, do.cuda(), lse, dqkv, B, N, C, heads, precision='f16x3', exps=exps,
+                                 dout_bound=dob, dqkv_absmax=amx)
+        torch.cuda.synchronize()
+        K.profile_conv(False)
+    assert raised and torch.equal(amx.cpu(), dqkv.cpu().abs().reshape(B, -1).amax(1))
+    names = [n for n, *_ in prof]
+    assert f'attn_bwd6_dq_kernel<{d}, true, 1>' in names, names
+    q_ = qkv.double().reshape(B, N, 3 * C).requires_grad_(True)
+    q, k, v = q_.split(C, dim=-1)
+    sh = lambda z: z.reshape(B, N, heads, d).transpose(1, 2)  # noqa: E731
+    sc = (sh(q) * d**-0.5) @ sh(k).transpose(-1, -2)
+    out = (torch.softmax(sc, -1) @ sh(v)).transpose(1, 2).reshape(B, N, C)
+    out.backward(do.double().reshape(B, N, C))
+    ref = q_.grad.reshape(B * N, 3 * C)
+    err = rel_l2(dqkv.cpu(), ref)
+    err_small = rel_l2(dqkv.cpu()[:N], ref[:N])  # the small-gradient image, its own dO exponent
+    print(f'bf16 line attention backward D={d} N={N}: rel-L2 {err:.3e} (small image {err_small:.3e})')
+    assert 1e-5 < err < 2e-2 and err_small < 2e-2
+
+
 @pytest.mark.parametrize('B,H,W,C,N', [(3, 16, 32, 128, 128), (2, 32, 16, 64, 64), (1, 8, 48, 256, 128)])
 def test_dgrad_f16x3_raw_segment_per_image_bound(B, H, W, C, N):
     """The training backward's 3x3 data gradient on f16x3: a raw (no GroupNorm) operand whose

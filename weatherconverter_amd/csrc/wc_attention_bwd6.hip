@@ -9,8 +9,9 @@
 // have none).  A 32x32x16 block costs 6 x 32 cycles here against 8 x 64 on fp32 MFMA.
 //
 //   attn_bwd6_dkdv_kernel  a wave owns 32 keys (K, V rows in registers as bf16 pieces; D <= 128 — at
-//       D = 192 the accumulators and rows spill, and that width stays on fp32 MFMA); 32-query tiles of Q and dO are staged once per tile as
-//       pieces in LDS ([piece][query][dim], shared by the 4 waves).
+//       D = 192 the two-piece forms keep the V rows in LDS and split the output dims over workgroups,
+//       the single-piece builds run the whole width in one); 32-query tiles of Q and dO are staged once
+//       per tile as pieces in LDS ([piece][query][dim], shared by the 4 waves).
 //         S = Q K^T, dP = dO V^T     rows = queries (A: ds_read_b128 from the tile), cols = keys (B: regs)
 //         P, dS in the accumulator registers (lane = key, register r = query (r&3)+8(r>>2)+4 half)
 //         dV^T += dO^T P, dK^T += Q^T dS   A: the tile read transposed (ds_read_b64_tr_b16) in the
@@ -50,7 +51,9 @@ struct B6Cfg {
     static constexpr int STAGE = 2 * TILE + 2 * 32 * 4;  // two tiles (Q, dO or K, V) + lse / Dv
     static constexpr int LDS = 2 * STAGE;                // double-buffered: tile t + 1 staged under tile t
     static constexpr int IPT = D / 32;                   // float4 items per thread of one 32 x D tile
-    static constexpr bool PRESPLIT = D <= 128;   // own rows kept as pieces (else fp32, split per use)
+    // own rows kept as pieces (else fp32, split per use); the single-piece builds hold one piece, so
+    // D = 192 rows fit as pieces there too (half the registers of the fp32 rows)
+    static constexpr bool PRESPLIT = D <= 128 || NPS == 1;
     static constexpr int VROWB = NCH * NPS * 64 * 16;  // one wave's own rows as pieces in get() order (VL)
     static constexpr int LDS_VL = STAGE + 4 * VROWB;  // VL: one Q / dO stage + the four waves' V rows
 };
@@ -241,7 +244,7 @@ WC_DEVICE BwdScales bwd_scales(int eq, int ek, int ev, const float* dobound, int
 // tiles are single-staged to make room (the next tile's global loads still fly under the MFMAs): at
 // D = 192 the K and V rows together would take 192 registers and the kernel spilled.
 template <int D, bool F3, int DS = 1, bool VL = false>
-__global__ __launch_bounds__(256, 1) void attn_bwd6_dkdv_kernel(
+__global__ __launch_bounds__(256, F3 && WC_SINGLE16 && D <= 64 ? 2 : 1) void attn_bwd6_dkdv_kernel(
     const float* __restrict__ qkv, int ldq, const float* __restrict__ dO, int lddo, const float* __restrict__ lse,
     const float* __restrict__ Dv, float* __restrict__ dqkv, int lddq, int N, int C, float scale_log2, float scale,
     int eq, int ek, int ev, const float* __restrict__ dobound, float* __restrict__ amx) {
@@ -600,6 +603,29 @@ static int attention_bwd_split(const float* qkv, int ld_qkv, const float* out, i
             if (!f3) return WC_E_SHAPE;
             using Cf = B6Cfg<192, true>;
             const bool fp32_dkdv = amx == nullptr;
+#if WC_SINGLE16
+            // single-piece builds: one piece per row and tile, so the whole width fits one wave (rows as
+            // pieces; dK / dV with the V rows in LDS): no output split, S and dP computed once per kernel
+            // instead of 2 (dK / dV) and 3 (dQ) times
+            if (!fp32_dkdv) {
+                st = launch_dkdv192<1>(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads, scale, eq,
+                                       ek, ev, dobound, amx, s);
+                if (st != WC_OK) return st;
+                static bool attr1 = false;
+                if (!attr1) {
+                    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd6_dq_kernel<192, true, 1>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+                    if (e != hipSuccess) return (int)e;
+                    attr1 = true;
+                }
+                WC_SET_NAME("attn_bwd6_dq_kernel", {WC_TI(192), WC_TB(true), WC_TI(1)});
+                hipLaunchKernelGGL((attn_bwd6_dq_kernel<192, true, 1>), dim3((N + 127) / 128, heads, B), dim3(256), Cf::LDS,
+                                   s, qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, N, C,
+                                   scale * 1.4426950408889634f, scale, eq, ek, ev, dobound, amx);
+                WC_CHECK_LAUNCH();
+                return WC_OK;
+            }
+#endif
             if (fp32_dkdv) {
                 st = wc_attention_bwd_dkdv192(qkv, ld_qkv, dout, ld_dout, lse, dv_work, dqkv, ld_dqkv, B, N, C, heads,
                                               scale, stream);

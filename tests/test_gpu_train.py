@@ -128,18 +128,26 @@ def test_conv_wgrad3_f16x3_vs_float64(pro, M, C0, B, H, W):
     assert rel_l2(dw.cpu(), w.grad) < 1e-5
 
 
+@pytest.mark.parametrize('variant', ['', 'bf16'])
 @pytest.mark.parametrize('form', ['3x3_gn_res', '4x4s2_raw', '1x1_raw'])
-def test_conv_wgrad_generic_f16x3_vs_float64(form):
+def test_conv_wgrad_generic_f16x3_vs_float64(form, variant):
     """The generic weight-gradient GEMM on f16x3 (wc_conv_wgrad_f16x3): a GroupNorm+SiLU 3x3 segment at
     its static exponent with a raw 1x1 residual segment under its per-image bound (a grid the halo
-    kernel does not take), a raw 4x4/s2 conv and a raw 1x1 under per-image bounds; gradients whose
-    images differ by 10^3 in scale; against float64 at rel-L2 <= 1e-5."""
+    kernel does not take), a raw 4x4/s2 conv and a raw 1x1 under per-image bounds (a pixel count that
+    ends in a partial K-step); gradients whose images differ by 10^3 in scale; against float64 at
+    rel-L2 <= 1e-5.  variant 'bf16': the bf16 training line's single-piece form (one LDS plane, 32
+    pixels per barrier) within bf16 operand rounding."""
+    import contextlib
+    from weatherconverter_amd import _native
     from weatherconverter_amd import kernels as K
     from weatherconverter_amd.kernels import Seg, View
     from weatherconverter_amd.diffusion_model.models.engine import TAPS1, TAPS3, TAPS4S2
+    lib = _native.variant(variant) if variant else contextlib.nullcontext()
+    tol = 1e-5 if not variant else 2e-2
+    ok = (lambda e: e < tol) if not variant else (lambda e: 1e-5 < e < tol)  # noqa: E731
     g = _gen(8)
     B, C0, C1, M = 2, 64, 32, 128
-    H, W = (12, 20) if form != '4x4s2_raw' else (16, 32)
+    H, W = {'3x3_gn_res': (12, 20), '4x4s2_raw': (16, 32), '1x1_raw': (11, 21)}[form]
     Hm, Wm = (H // 2, W // 2) if form == '4x4s2_raw' else (H, W)
     x = torch.randn((B, H, W, C0), generator=g) * torch.tensor([1.0, 30.0])[:, None, None, None]
     xr = torch.randn((B, H, W, C1), generator=g)
@@ -157,25 +165,31 @@ def test_conv_wgrad_generic_f16x3_vs_float64(form):
         assert not K.wgrad3_ok(View.full(dy.cuda()), segs[0])
         f3 = K.F3Bounds(gb, x_exp, None, xr.abs().amax((1, 2, 3)).cuda())
         dw = torch.zeros((M, C0, 3, 3), device='cuda')
-        K.conv_wgrad(View.full(dy.cuda()), segs, dw, (C0 * 9, 9, 1), dw1=dwr, s1=C1, x6=True, f3=f3)
+        with lib:
+            K.conv_wgrad(View.full(dy.cuda()), segs, dw, (C0 * 9, 9, 1), dw1=dwr, s1=C1, x6=True, f3=f3)
+            torch.cuda.synchronize()
         w = torch.zeros((M, C0, 3, 3), dtype=torch.float64, requires_grad=True)
         F.conv2d(a.permute(0, 3, 1, 2), w, padding=1).backward(dy.double().permute(0, 3, 1, 2))
         ref = torch.einsum('bhwm,bhwc->mc', dy.double(), xr.double())
-        assert rel_l2(dwr.cpu(), ref) < 1e-5
+        assert ok(rel_l2(dwr.cpu(), ref)), rel_l2(dwr.cpu(), ref)
     elif form == '4x4s2_raw':
         f3 = K.F3Bounds(gb, 60, x.abs().amax((1, 2, 3)).cuda())
         dw = torch.zeros((M, C0, 4, 4), device='cuda')
-        K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS4S2, stride=2)], dw, (C0 * 16, 16, 1),
-                     x6=True, f3=f3)
+        with lib:
+            K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS4S2, stride=2)], dw, (C0 * 16, 16, 1),
+                         x6=True, f3=f3)
+            torch.cuda.synchronize()
         w = torch.zeros((M, C0, 4, 4), dtype=torch.float64, requires_grad=True)
         F.conv2d(x.double().permute(0, 3, 1, 2), w, stride=2, padding=1).backward(dy.double().permute(0, 3, 1, 2))
     else:
         f3 = K.F3Bounds(gb, 60, x.abs().amax((1, 2, 3)).cuda())
         dw = torch.zeros((M, C0), device='cuda')
-        K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS1)], dw, (C0, 1, 0), x6=True, f3=f3)
+        with lib:
+            K.conv_wgrad(View.full(dy.cuda()), [Seg(View.full(x.cuda()), TAPS1)], dw, (C0, 1, 0), x6=True, f3=f3)
+            torch.cuda.synchronize()
         w = torch.zeros((M, C0), dtype=torch.float64, requires_grad=True)
         (torch.einsum('bhwc,mc->bhwm', x.double(), w) * dy.double()).sum().backward()
-    assert rel_l2(dw.cpu(), w.grad) < 1e-5
+    assert ok(rel_l2(dw.cpu(), w.grad)), rel_l2(dw.cpu(), w.grad)
 
 
 def test_wgrad_reduce_many_splits_two_level():

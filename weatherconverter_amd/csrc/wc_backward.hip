@@ -78,21 +78,30 @@ struct WgDev {
 // F3 (with X6): f16x3 instead — G x 2^sg, segment 0 x 2^sx0, segment 1 x 2^sx1 split into two fp16
 // pieces (products h*h + h*l + l*h), s = 13 - floor(log2 bound) from the batch max of the per-image
 // bounds (segment 0: at most its static exponent xe0); the epilogue removes 2^-(sg + sx) per column.
+// Pixels per K-step (per barrier): 16 for the split forms, 32 for fp32 (32 pixels per barrier measured
+// slower for the f16x3 tiles, 292 vs 264 us at the 1x1 shapes, and for the single-piece tiles, 392 vs
+// 352 us on the GroupNorm-affine 1x1 form: profiles/r06_train_wgrad_ab.txt).
+template <bool X6>
+constexpr int wg_kp() { return X6 ? 16 : WG_KP; }
+// LDS piece planes: the single-piece builds (WC_SINGLE16, one 16-bit piece per operand) stage the high
+// piece only (the low piece is zero there and mfma_f16c drops its products)
+template <bool X6, bool F3>
+constexpr int wg_nps() { return !X6 ? 0 : (F3 && WC_SINGLE16) ? 1 : F3 ? 2 : 3; }
+
 template <int BM, int BN, int PRO, bool X6, bool F3 = false>
 __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     static_assert(!F3 || X6, "F3 runs the X6 structure");
     constexpr int NP = F3 ? 2 : 3;
+    constexpr int NPS = wg_nps<X6, F3>();
     constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves of 64x64");
-    // pixels per K-step (per barrier): 16 for the split forms, 32 for fp32 (32 pixels per barrier for
-    // the f16x3 tiles measured slower: 292 vs 264 us at the 1x1 shapes)
-    constexpr int KP = X6 ? 16 : WG_KP;
+    constexpr int KP = wg_kp<X6>();
     constexpr int AS = BM + 32, BS = BN + 32;  // fp32 LDS row strides: lane halves on disjoint banks
     constexpr int ASB = BM * 2 + 64, BSB = BN * 2 + 64;  // X6 row bytes
     constexpr int APL = KP * ASB, BPL = KP * BSB;        // X6 bytes of one piece plane
     constexpr int A_PER_T = KP * BM / 4 / WG_THREADS;
     constexpr int B_PER_T = KP * BN / 4 / WG_THREADS;
-    constexpr int STAGE = X6 ? NP * (APL + BPL) : KP * (AS + BS) * 4;  // bytes
+    constexpr int STAGE = X6 ? NPS * (APL + BPL) : KP * (AS + BS) * 4;  // bytes
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
     const int tid = threadIdx.x;
@@ -101,7 +110,14 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int l32 = lane & 31, half = lane >> 5;
 
+    // XCD-aware bijective order: the ntm x ntn tiles of one pixel split (which all read that split's G
+    // and input rows) are consecutive logical blocks and land on one XCD, whose L2 then serves their
+    // re-reads (round-robin placement fetched the rows into every XCD's L2, once per tile)
     int t = blockIdx.x;
+    {
+        const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, xcd = t % 8;
+        t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + t / 8;
+    }
     const int tn = t % p.ntn;
     t /= p.ntn;
     const int tm = t % p.ntm;
@@ -231,7 +247,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
     };
     auto store = [&](int buf) {
         unsigned char* a = lds + buf * STAGE;
-        unsigned char* bb = a + (X6 ? NP * APL : KP * AS * 4);
+        unsigned char* bb = a + (X6 ? NPS * APL : KP * AS * 4);
 #pragma unroll
         for (int j = 0; j < A_PER_T; ++j) {
             if constexpr (F3) {
@@ -239,7 +255,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
                 wcx6::split2_f16(ra[j] * gsc, h, l);
                 unsigned char* d = a + arow[j] * ASB + acol[j] * 2;
                 *reinterpret_cast<wcx6::u32x2*>(d) = h;
-                *reinterpret_cast<wcx6::u32x2*>(d + APL) = l;
+                if constexpr (NPS > 1) *reinterpret_cast<wcx6::u32x2*>(d + APL) = l;
             } else if constexpr (X6) {
                 wcx6::u32x2 p0, p1, p2;
                 wcx6::split3(ra[j], p0, p1, p2);
@@ -268,7 +284,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
                 wcx6::split2_f16(v * (bseg[j] == 1 ? xsc1 : xsc0), h, l);
                 unsigned char* d = bb + brow[j] * BSB + bcol[j] * 2;
                 *reinterpret_cast<wcx6::u32x2*>(d) = h;
-                *reinterpret_cast<wcx6::u32x2*>(d + BPL) = l;
+                if constexpr (NPS > 1) *reinterpret_cast<wcx6::u32x2*>(d + BPL) = l;
             } else if constexpr (X6) {
                 wcx6::u32x2 p0, p1, p2;
                 wcx6::split3(v, p0, p1, p2);
@@ -314,10 +330,15 @@ __global__ __launch_bounds__(WG_THREADS, 2) void conv_wgrad_kernel(WgDev p) {
 #pragma unroll
             for (int ks = 0; ks < KP / 16; ++ks) {  // 16-pixel MFMA K-steps of the stage
                 const unsigned char* a = lds + buf * STAGE + tr_a + ks * 16 * ASB;
-                const unsigned char* bb = lds + buf * STAGE + 2 * APL + tr_b + ks * 16 * BSB;
+                const unsigned char* bb = lds + buf * STAGE + NPS * APL + tr_b + ks * 16 * BSB;
                 wcx6::u32x4 fa[2][2], fb[2][2];
 #pragma unroll
                 for (int pc = 0; pc < 2; ++pc) {
+                    if (pc >= NPS) {  // single-piece builds: the low piece is never read (mfma_f16c drops it)
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) fa[i][pc] = fb[i][pc] = wcx6::u32x4{0u, 0u, 0u, 0u};
+                        continue;
+                    }
 #pragma unroll
                     for (int mb = 0; mb < 2; ++mb) fa[mb][pc] = tr_frag(a + pc * APL + mb * 64, ASB);
 #pragma unroll
@@ -442,9 +463,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce_groups_kernel(float* __restr
 }
 template <int BM, int BN, int PRO, bool X6, bool F3 = false>
 int wgrad_launch(const WgDev& d, int grid, hipStream_t s) {
-    constexpr int KP = X6 ? 16 : WG_KP;
+    constexpr int KP = wg_kp<X6>();
     constexpr int bytes =
-        2 * (X6 ? (F3 ? 2 : 3) * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
+        2 * (X6 ? wg_nps<X6, F3>() * KP * ((BM * 2 + 64) + (BN * 2 + 64)) : KP * ((BM + 32) + (BN + 32)) * 4);
     static bool attr_set = false;
     if (!attr_set && bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_kernel<BM, BN, PRO, X6, F3>),

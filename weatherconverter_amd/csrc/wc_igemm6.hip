@@ -98,6 +98,29 @@ struct IgTile {
 // step s + 2 is issued while step s computes, one barrier per step.  (Measured and dropped: a 4-stage
 // ring walked in pairs of steps, one barrier per pair: 254 vs 274 TF/s at two instead of three
 // workgroups per CU -- the projections are not barrier-bound.)
+// Output-tile order of the GEMM grids.  XCD-aware bijection first (blocks b and b + 8 share an XCD:
+// consecutive logical tiles land on one XCD's L2), then, within the logical order, bands of WC_IG_GM
+// M-tiles walked N-tile by N-tile (M fastest inside a band): the ~64 workgroups an XCD runs at once
+// then hold about 8 A row-tiles and 8 B column-tiles instead of ~4 A tiles and every B tile -- the
+// qkv projections' B (C x 3C, up to 7 MB pre-split) does not fit a 4 MB L2 and was refetched for
+// every M-tile.  WC_IG_GM = 1 is the plain N-fastest order.
+#ifndef WC_IG_GM
+#define WC_IG_GM 8
+#endif
+WC_DEVICE void ig_tile_order(int ntn, int& tm, int& tn) {
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        const int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int ntm = nblk / ntn;
+    const int band = bid / (WC_IG_GM * ntn), rem = bid - band * (WC_IG_GM * ntn);
+    const int gm = min(WC_IG_GM, ntm - band * WC_IG_GM);  // the last band may be narrower
+    tn = rem / gm;
+    tm = band * WC_IG_GM + rem % gm;
+}
+
 template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false, bool P1 = false,
           bool PA = false>
 __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_kernel(IgDev p) {
@@ -117,14 +140,8 @@ __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_k
     const int wm = wave / T::WAVES_N;
     const int wn = wave % T::WAVES_N;
 
-    const int nblk = gridDim.x;
-    int bid = blockIdx.x;
-    {
-        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    }
-    const int tile_m = bid / p.ntiles_n;
-    const int tile_n = bid % p.ntiles_n;
+    int tile_m, tile_n;
+    ig_tile_order(p.ntiles_n, tile_m, tile_n);
     const int m0 = tile_m * BM;
     const int n0 = tile_n * BN;
     const int HWm = p.Hm * p.Wm;
@@ -1039,14 +1056,8 @@ __global__ __launch_bounds__(NT, H == 2 || DA ? 2 : 3) void proj_pa_kernel(IgDev
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int nblk = gridDim.x;
-    int bid = blockIdx.x;
-    {
-        int q = nblk / 8, r = nblk % 8, xcd = bid % 8;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    }
-    const int tile_m = bid / p.ntiles_n;
-    const int tile_n = bid % p.ntiles_n;
+    int tile_m, tile_n;
+    ig_tile_order(p.ntiles_n, tile_m, tile_n);
     const int m0 = tile_m * BM;
     const int n0 = tile_n * BN;
     const int HWm = p.Hm * p.Wm;

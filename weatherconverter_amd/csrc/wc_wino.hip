@@ -847,6 +847,9 @@ long wino_vimg(int C, int H, int W) { return (long)(C / 16) * VPL * H * (W / 2) 
 // consecutive tiles.  The same operations in the same order as the conv kernel's items (prologue /
 // transform, PRO 2): the planes are bit for bit the LDS image those items write.  s per image as the
 // conv: a_exp - 1, clamped to 13 - e(res_bound[b]) under a residual.
+#ifndef VS_IPT
+#define VS_IPT 4
+#endif
 template <int NCK>
 __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restrict__ src, int ldc, int B, int H,
                                                           int W, int C, const float* __restrict__ scale,
@@ -868,29 +871,31 @@ __global__ __launch_bounds__(256) void wino_vsplit_kernel(const float* __restric
         s_exp = max(s_exp, -100);
     }
     const float ascale = ldexpf(1.0f, s_exp);
-    // stage 1: item = (row, padded pixel, quad of the NCK x 16 channels); 4 items per thread in flight
+    // stage 1: item = (row, padded pixel, quad of the NCK x 16 channels); VS_IPT items per thread in
+    // flight.  256 % (4 NCK) == 0, so a thread's channel quad -- and its GN scale / shift -- is the same
+    // for every item it takes: loaded once
     const int W2 = W + 2, items = R * W2 * 4 * NCK, cstride = R * W2 * 5;
-    for (int i0 = tid; i0 < items; i0 += 4 * 256) {
-        f32x4 v[4], sc[4], sh[4];
-        bool inb[4];
-        int slot[4];
+    const int qt = tid % (4 * NCK), ct = kg * 16 * NCK + 4 * qt;
+    const f32x4 sct = *reinterpret_cast<const f32x4*>(scale + (long)b * C + ct);
+    const f32x4 sht = *reinterpret_cast<const f32x4*>(shift + (long)b * C + ct);
+    for (int i0 = tid; i0 < items; i0 += VS_IPT * 256) {
+        f32x4 v[VS_IPT];
+        bool inb[VS_IPT];
+        int slot[VS_IPT];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = min(i0 + u * 256, items - 1);
-            const int q = i % (4 * NCK), px = (i / (4 * NCK)) % W2 - 1, r = (i / (4 * NCK)) / W2;
+        for (int u = 0; u < VS_IPT; ++u) {
+            const int i = min(i0 + u * 256, items - 1);  // past the end: a repeat of the last item, not stored
+            const int px = (i / (4 * NCK)) % W2 - 1, r = (i / (4 * NCK)) / W2;
             const int y = y0 + r;
             inb[u] = (unsigned)px < (unsigned)W && y < H;
-            const int c = kg * 16 * NCK + 4 * q;
-            sc[u] = *reinterpret_cast<const f32x4*>(scale + (long)b * C + c);
-            sh[u] = *reinterpret_cast<const f32x4*>(shift + (long)b * C + c);
-            v[u] = *reinterpret_cast<const f32x4*>(src + ((long)(b * H + min(y, H - 1)) * W + min(max(px, 0), W - 1)) * ldc + c);
+            v[u] = *reinterpret_cast<const f32x4*>(src + ((long)(b * H + min(y, H - 1)) * W + min(max(px, 0), W - 1)) * ldc + ct);
             // a pixel is 5 slots (4 quads + pad): stage 2's lanes, two pixels apart, then read distinct banks
-            slot[u] = (q >> 2) * cstride + (r * W2 + px + 1) * 5 + (q & 3);
+            slot[u] = (qt >> 2) * cstride + (r * W2 + px + 1) * 5 + (qt & 3);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < VS_IPT; ++u) {
             if (i0 + u * 256 >= items) break;
-            f32x4 a = v[u] * sc[u] + sh[u];
+            f32x4 a = v[u] * sct + sht;
             a.x = silu_fast(a.x); a.y = silu_fast(a.y);
             a.z = silu_fast(a.z); a.w = silu_fast(a.w);
             act[slot[u]] = inb[u] ? a * ascale : f32x4{0.f, 0.f, 0.f, 0.f};

@@ -85,19 +85,6 @@ struct IgTile {
     static constexpr int B_FULL = BSTEP0 / 16 / NT;       // items j < B_FULL valid in every step
 };
 
-// PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU.  UNIB: tiles never straddle images.  ACT: epilogue
-// activation (template, see wc_conv.hip).  F3: segment 0 on f16x3 (caller bounds |a| 2^a_exp).
-// TR (the pre-split qkv epilogue only): accumulate the transposed block (lanes = pixels, rows =
-// channels; the same products, B and A fragments swapped in the MFMA).
-// The pre-split qkv form (TR, BN 128) is held to 3 waves per SIMD (174 -> 168 VGPRs, 5 spilled).
-// P1 (UNIB, f16x3 segment 0 only): a pointwise 1x1 stride-1 conv whose tiles are whole rows of one
-// image (the attention projections): no tap stepping, no bounds or padding logic per element.
-// PA (with P1): the A operand arrives pre-scaled and pre-split in the LDS stage order
-// (wc_split_f16x3_tiled), so both operands of a K-step are 16 KiB copied HBM/L2 -> LDS by
-// LDS-DMA (4 wave-instructions per wave, no registers, no VALU) into a 3-stage ring: the copy of
-// step s + 2 is issued while step s computes, one barrier per step.  (Measured and dropped: a 4-stage
-// ring walked in pairs of steps, one barrier per pair: 254 vs 274 TF/s at two instead of three
-// workgroups per CU -- the projections are not barrier-bound.)
 // Output-tile order of the GEMM grids.  XCD-aware bijection first (blocks b and b + 8 share an XCD:
 // consecutive logical tiles land on one XCD's L2), then, within the logical order, bands of WC_IG_GM
 // M-tiles walked N-tile by N-tile (M fastest inside a band): the ~64 workgroups an XCD runs at once
@@ -121,6 +108,19 @@ WC_DEVICE void ig_tile_order(int ntn, int& tm, int& tn) {
     tm = band * WC_IG_GM + rem % gm;
 }
 
+// PRO: 0 raw, 1 GN affine, 2 GN affine + SiLU.  UNIB: tiles never straddle images.  ACT: epilogue
+// activation (template, see wc_conv.hip).  F3: segment 0 on f16x3 (caller bounds |a| 2^a_exp).
+// TR (the pre-split qkv epilogue only): accumulate the transposed block (lanes = pixels, rows =
+// channels; the same products, B and A fragments swapped in the MFMA).
+// The pre-split qkv form (TR, BN 128) is held to 3 waves per SIMD (174 -> 168 VGPRs, 5 spilled).
+// P1 (UNIB, f16x3 segment 0 only): a pointwise 1x1 stride-1 conv whose tiles are whole rows of one
+// image (the attention projections): no tap stepping, no bounds or padding logic per element.
+// PA (with P1): the A operand arrives pre-scaled and pre-split in the LDS stage order
+// (wc_split_f16x3_tiled), so both operands of a K-step are 16 KiB copied HBM/L2 -> LDS by
+// LDS-DMA (4 wave-instructions per wave, no registers, no VALU) into a 3-stage ring: the copy of
+// step s + 2 is issued while step s computes, one barrier per step.  (Measured and dropped: a 4-stage
+// ring walked in pairs of steps, one barrier per pair: 254 vs 274 TF/s at two instead of three
+// workgroups per CU -- the projections are not barrier-bound.)
 template <int BM, int BN, int PRO, bool UNIB, int ACT, bool F3, int NPL, bool TR = false, bool P1 = false,
           bool PA = false>
 __global__ __launch_bounds__(NT, (TR && BN == 128) ? 3 : 2) void conv_igemm_x6_kernel(IgDev p) {
